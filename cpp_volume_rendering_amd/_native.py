@@ -1,0 +1,135 @@
+"""ctypes binding of the C-ABI in include/cvr.h (libcvr.so, built in-tree).
+
+The shared library is the product: HIP kernels for gfx950 plus the C-ABI.
+There is no fallback — if libcvr.so is missing or cannot be loaded the import
+fails loudly (run ``python -c "import __graft_entry__ as g; g.build()"``).
+
+torch is imported before the library is loaded so that libcvr.so binds to the
+HIP runtime torch already carries (both have SONAME libamdhip64.so.7); device
+pointers and streams can then be shared with torch tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen below, see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libcvr.so")
+
+CVR_OK, CVR_ERR_ARG, CVR_ERR_HIP, CVR_ERR_OOM, CVR_ERR_STATE, CVR_ERR_IO = range(6)
+GRADIENT_NONE, GRADIENT_FINITE_DIFFERENCES, GRADIENT_SOBEL_FELDMAN = 0, 1, 2
+
+# Every symbol include/cvr.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "cvr_abi_version", "cvr_status_string", "cvr_create", "cvr_destroy", "cvr_last_error",
+    "cvr_set_stream", "cvr_synchronize", "cvr_set_volume", "cvr_set_volume_device",
+    "cvr_set_transfer_function", "cvr_set_gradient", "cvr_device_bytes", "cvr_tiles_for_rank",
+    "cvr_render_rc1pass", "cvr_unpack_tiles_device", "cvr_camera_lookat", "cvr_default_step",
+    "cvr_tf1d_build_rgbt", "cvr_read_tf1d", "cvr_read_raw", "cvr_read_syn",
+    "cvr_read_camera_state", "cvr_read_light_position",
+)
+
+
+class CvrError(RuntimeError):
+    def __init__(self, status: int, where: str, detail: str = ""):
+        self.status = status
+        super().__init__(f"{where}: {_status_name(status)}" + (f" — {detail}" if detail else ""))
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("eye", ctypes.c_float * 3), ("center", ctypes.c_float * 3),
+                ("up", ctypes.c_float * 3), ("fovy_deg", ctypes.c_float),
+                ("aspect", ctypes.c_float)]
+
+
+class Frame(ctypes.Structure):
+    _fields_ = [("camera", Camera), ("width", ctypes.c_int), ("height", ctypes.c_int),
+                ("tile_size", ctypes.c_int), ("rank", ctypes.c_int), ("nranks", ctypes.c_int)]
+
+
+class Output(ctypes.Structure):
+    _fields_ = [("rgba", ctypes.c_void_p), ("samples", ctypes.c_void_p),
+                ("total", ctypes.c_void_p), ("on_device", ctypes.c_int)]
+
+
+class Rc1passParams(ctypes.Structure):
+    _fields_ = [("step", ctypes.c_float), ("apply_gradient_shading", ctypes.c_int),
+                ("ka", ctypes.c_float), ("kd", ctypes.c_float), ("ks", ctypes.c_float),
+                ("shininess", ctypes.c_float), ("ispecular", ctypes.c_float * 3),
+                ("light_pos", ctypes.c_float * 3)]
+
+
+_lib = None
+
+
+def _status_name(st: int) -> str:
+    names = {0: "CVR_OK", 1: "CVR_ERR_ARG", 2: "CVR_ERR_HIP", 3: "CVR_ERR_OOM",
+             4: "CVR_ERR_STATE", 5: "CVR_ERR_IO"}
+    return names.get(st, f"status {st}")
+
+
+def lib() -> ctypes.CDLL:
+    """Load libcvr.so (once) and declare the C signatures."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libcvr.so not built: {LIB_PATH} is missing "
+                          "(build with __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, F, V = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, None
+    FP = ctypes.POINTER(ctypes.c_float)
+    DP = ctypes.POINTER(ctypes.c_double)
+    IP = ctypes.POINTER(ctypes.c_int)
+    sig = {
+        "cvr_abi_version": ([], I),
+        "cvr_status_string": ([I], ctypes.c_char_p),
+        "cvr_create": ([I, ctypes.POINTER(P)], I),
+        "cvr_destroy": ([P], V),
+        "cvr_last_error": ([P], ctypes.c_char_p),
+        "cvr_set_stream": ([P, P], I),
+        "cvr_synchronize": ([P], I),
+        "cvr_set_volume": ([P, P, I, I, I, I, FP], I),
+        "cvr_set_volume_device": ([P, P, I, I, I, I, FP], I),
+        "cvr_set_transfer_function": ([P, FP, I], I),
+        "cvr_set_gradient": ([P, I], I),
+        "cvr_device_bytes": ([P], ctypes.c_size_t),
+        "cvr_tiles_for_rank": ([ctypes.POINTER(Frame), I], I),
+        "cvr_render_rc1pass": ([P, ctypes.POINTER(Frame), ctypes.POINTER(Rc1passParams),
+                                ctypes.POINTER(Output)], I),
+        "cvr_unpack_tiles_device": ([P, ctypes.POINTER(Frame), P, I, P], I),
+        "cvr_camera_lookat": ([ctypes.POINTER(Camera), FP, FP], I),
+        "cvr_default_step": ([FP], F),
+        "cvr_tf1d_build_rgbt": ([DP, I, DP, I, I, I, FP], I),
+        "cvr_read_tf1d": ([ctypes.c_char_p, FP, IP], I),
+        "cvr_read_raw": ([ctypes.c_char_p, P, ctypes.c_size_t, IP, IP, IP, IP], I),
+        "cvr_read_syn": ([ctypes.c_char_p, P, ctypes.c_size_t, IP, IP, IP], I),
+        "cvr_read_camera_state": ([ctypes.c_char_p, I, ctypes.POINTER(Camera), ctypes.c_char_p,
+                                   I, IP], I),
+        "cvr_read_light_position": ([ctypes.c_char_p, I, I, FP, IP], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def check(status: int, where: str, ctx=None) -> None:
+    if status != CVR_OK:
+        detail = ""
+        if ctx:
+            msg = lib().cvr_last_error(ctx)
+            detail = msg.decode(errors="replace") if msg else ""
+        raise CvrError(status, where, detail)
+
+
+def fptr(arr):
+    """ctypes float* of a C-contiguous float32 numpy array."""
+    return arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def dptr(arr):
+    return arr.ctypes.data_as(ctypes.POINTER(ctypes.c_double))

@@ -1,0 +1,438 @@
+// cvr_api.cpp — C-ABI implementation (include/cvr.h): context, device
+// resources, render dispatch, and the host-side camera / TF helpers.
+//
+// Compiled with -ffp-contract=off: the camera and TF arithmetic below feed the
+// kernels and must be bit-reproducible (CVR-SPEC).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "cvr_internal.h"
+
+using cvr::Ctx;
+
+namespace {
+
+cvr_status fail(Ctx* c, cvr_status st, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return st;
+}
+
+#define HIP_TRY(ctx, expr)                                                                    \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      return fail(ctx, _e == hipErrorOutOfMemory ? CVR_ERR_OOM : CVR_ERR_HIP, "%s: %s (%s:%d)", \
+                  #expr, hipGetErrorString(_e), __FILE__, __LINE__);                         \
+  } while (0)
+
+void free_dev(void*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+// float -> binary16 bits, round to nearest even (the GL driver's conversion of
+// GL_FLOAT client data to a 16F internal format).
+uint16_t to_half_bits(float f) {
+  _Float16 h = (_Float16)f;
+  uint16_t b;
+  std::memcpy(&b, &h, 2);
+  return b;
+}
+float half_round(float f) {
+  _Float16 h = (_Float16)f;
+  return (float)h;
+}
+
+struct V3 { float x, y, z; };
+inline V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 cross(V3 x, V3 y) {
+  return {x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y};
+}
+inline float gdot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline V3 gnormalize(V3 v) {
+  float inv = 1.0f / std::sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+  return {v.x * inv, v.y * inv, v.z * inv};
+}
+
+}  // namespace
+
+extern "C" {
+#pragma GCC visibility push(default)
+
+int cvr_abi_version(void) { return CVR_ABI_VERSION; }
+
+const char* cvr_status_string(cvr_status s) {
+  switch (s) {
+    case CVR_OK: return "CVR_OK";
+    case CVR_ERR_ARG: return "CVR_ERR_ARG";
+    case CVR_ERR_HIP: return "CVR_ERR_HIP";
+    case CVR_ERR_OOM: return "CVR_ERR_OOM";
+    case CVR_ERR_STATE: return "CVR_ERR_STATE";
+    case CVR_ERR_IO: return "CVR_ERR_IO";
+  }
+  return "CVR_ERR_UNKNOWN";
+}
+
+// glm::lookAt (glm 0.9.5, include/glm/gtc/matrix_transform.inl:403-428), float.
+cvr_status cvr_camera_lookat(const cvr_camera* cam, float out_view[16], float* out_tan) {
+  if (!cam || !out_view || !out_tan) return CVR_ERR_ARG;
+  V3 eye{cam->eye[0], cam->eye[1], cam->eye[2]};
+  V3 center{cam->center[0], cam->center[1], cam->center[2]};
+  V3 up{cam->up[0], cam->up[1], cam->up[2]};
+  V3 f = gnormalize(sub(center, eye));
+  V3 s = gnormalize(cross(f, up));
+  V3 u = cross(s, f);
+  float* R = out_view;
+  for (int i = 0; i < 16; i++) R[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+  R[0] = s.x; R[4] = s.y; R[8] = s.z;
+  R[1] = u.x; R[5] = u.y; R[9] = u.z;
+  R[2] = -f.x; R[6] = -f.y; R[10] = -f.z;
+  R[12] = -gdot(s, eye);
+  R[13] = -gdot(u, eye);
+  R[14] = gdot(f, eye);
+  // (float)tan(DEGREE_TO_RADIANS(fovy) / 2.0): rc1prenderer.cpp:97, math_utils/utils.h:13
+  double rad = (double)cam->fovy_deg * (3.14159265358979323846 / 180.0);
+  *out_tan = (float)std::tan(rad / 2.0);
+  return CVR_OK;
+}
+
+// rc1prenderer.cpp:62-63
+float cvr_default_step(const float scale[3]) {
+  double sx = scale[0], sy = scale[1], sz = scale[2];
+  return (float)((0.5f / std::sqrt(3.0f)) * std::sqrt(sx * sx + sy * sy + sz * sz));
+}
+
+// TransferFunction1D::BuildLinear + GenerateTexture_1D_RGBt
+// (transferfunction1d.cpp:319-358, 89-118; transferfunction.h:79-82).
+cvr_status cvr_tf1d_build_rgbt(const double* rgb_cp, int n_rgb, const double* a_cp, int n_a,
+                               int max_density, int extinction_input, float* out_rgbt) {
+  if (max_density < 1 || !out_rgbt || n_rgb < 0 || n_a < 0) return CVR_ERR_ARG;
+  if ((n_rgb > 0 && !rgb_cp) || (n_a > 0 && !a_cp)) return CVR_ERR_ARG;
+  const int n = max_density + 1;
+  std::vector<double> tab((size_t)n * 4, 0.0);   // glm 0.9.5 dvec4 zero-init
+  for (int i = 0; i + 1 < n_rgb; i++) {
+    // TransferControlPoint keeps its colour in a glm::vec4 (float)
+    float c0[3], c1[3];
+    for (int k = 0; k < 3; k++) {
+      c0[k] = (float)rgb_cp[i * 4 + k];
+      c1[k] = (float)rgb_cp[(i + 1) * 4 + k];
+    }
+    int i0 = (int)rgb_cp[i * 4 + 3], i1 = (int)rgb_cp[(i + 1) * 4 + 3];
+    double diff[3] = {(double)(c1[0] - c0[0]), (double)(c1[1] - c0[1]), (double)(c1[2] - c0[2])};
+    for (int x = i0; x <= i1; x++) {
+      if (x < 0 || x >= n) return CVR_ERR_ARG;
+      double k = (double)(x - i0) / (double)(i1 - i0);
+      for (int ch = 0; ch < 3; ch++) tab[(size_t)x * 4 + ch] = (double)c0[ch] + diff[ch] * k;
+    }
+  }
+  for (int i = 0; i + 1 < n_a; i++) {
+    float a0 = (float)a_cp[i * 2], a1 = (float)a_cp[(i + 1) * 2];
+    int i0 = (int)a_cp[i * 2 + 1], i1 = (int)a_cp[(i + 1) * 2 + 1];
+    double diff = (double)(a1 - a0);
+    for (int x = i0; x <= i1; x++) {
+      if (x < 0 || x >= n) return CVR_ERR_ARG;
+      double k = (double)(x - i0) / (double)(i1 - i0);
+      tab[(size_t)x * 4 + 3] = (double)a0 + diff * k;
+    }
+  }
+  for (int i = 0; i < n; i++) {
+    out_rgbt[i * 4 + 0] = (float)tab[(size_t)i * 4 + 0];
+    out_rgbt[i * 4 + 1] = (float)tab[(size_t)i * 4 + 1];
+    out_rgbt[i * 4 + 2] = (float)tab[(size_t)i * 4 + 2];
+    float v4 = (float)tab[(size_t)i * 4 + 3];
+    if (!extinction_input) v4 = (float)std::log(1.0 / (1.0 - (double)v4));
+    out_rgbt[i * 4 + 3] = v4;
+  }
+  return CVR_OK;
+}
+
+cvr_status cvr_create(int device, cvr_ctx** out_ctx) {
+  if (!out_ctx) return CVR_ERR_ARG;
+  *out_ctx = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return CVR_ERR_HIP;
+  if (device < 0 || device >= ndev) return CVR_ERR_ARG;
+  Ctx* c = new (std::nothrow) Ctx();
+  if (!c) return CVR_ERR_OOM;
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->d_total, sizeof(unsigned long long)) != hipSuccess) {
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return CVR_ERR_HIP;
+  }
+  c->stream = c->own_stream;
+  *out_ctx = reinterpret_cast<cvr_ctx*>(c);
+  return CVR_OK;
+}
+
+void cvr_destroy(cvr_ctx* ctx) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  free_dev(c->d_vox);
+  free_dev(c->d_cells);
+  void* p = c->d_tf; free_dev(p); c->d_tf = nullptr;
+  free_dev(c->d_grad);
+  p = c->d_total; free_dev(p); c->d_total = nullptr;
+  free_dev(c->d_scratch);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+const char* cvr_last_error(const cvr_ctx* ctx) {
+  const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+  return c ? c->err.c_str() : "null context";
+}
+
+cvr_status cvr_set_stream(cvr_ctx* ctx, void* stream) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  c->stream = stream ? (hipStream_t)stream : c->own_stream;
+  return CVR_OK;
+}
+
+cvr_status cvr_synchronize(cvr_ctx* ctx) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return CVR_OK;
+}
+
+size_t cvr_device_bytes(const cvr_ctx* ctx) {
+  const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+  if (!c) return 0;
+  return c->vox_bytes + c->cells_bytes + c->grad_bytes + (size_t)c->tf_n * 16 + c->scratch_bytes;
+}
+
+static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, int bpv, int w,
+                                    int h, int d, const float scale[3]) {
+  if (!src || (bpv != 1 && bpv != 2) || w < 1 || h < 1 || d < 1 || !scale)
+    return fail(c, CVR_ERR_ARG, "cvr_set_volume: bad arguments");
+  if (!(scale[0] > 0 && scale[1] > 0 && scale[2] > 0))
+    return fail(c, CVR_ERR_ARG, "cvr_set_volume: scale must be positive");
+  if ((size_t)(w + 4) * (h + 4) * (d + 4) >= (size_t)1 << 32)
+    return fail(c, CVR_ERR_ARG, "cvr_set_volume: volume too large for 32-bit cell indexing");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  free_dev(c->d_vox); c->vox_bytes = 0;
+  free_dev(c->d_cells); c->cells_bytes = 0;
+  free_dev(c->d_grad); c->grad_bytes = 0; c->grad_mode = 0;
+  c->N[0] = w; c->N[1] = h; c->N[2] = d;
+  for (int i = 0; i < 3; i++) c->scale[i] = scale[i];
+  c->bpv = bpv;
+  c->vox_bytes = (size_t)w * h * d * bpv;
+  HIP_TRY(c, hipMalloc(&c->d_vox, c->vox_bytes));
+  HIP_TRY(c, hipMemcpyAsync(c->d_vox, src, c->vox_bytes,
+                            src_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+  // GetNormalizedSample -> (GLfloat) -> GL_R16F, as a per-value table
+  const int nv = bpv == 1 ? 256 : 65536;
+  std::vector<uint16_t> lut(nv);
+  for (int v = 0; v < nv; v++)
+    lut[v] = to_half_bits((float)((double)v / (bpv == 1 ? (256.0 - 1.0) : (65536.0 - 1.0))));
+  uint16_t* d_lut = nullptr;
+  HIP_TRY(c, hipMalloc(&d_lut, nv * sizeof(uint16_t)));
+  hipError_t e = hipMemcpyAsync(d_lut, lut.data(), nv * sizeof(uint16_t), hipMemcpyHostToDevice,
+                                c->stream);
+  c->cells = cvr::make_cell_grid(c->N);
+  c->cells_bytes = cvr::cell_count(c->cells) * 16;
+  if (e == hipSuccess) e = hipMalloc(&c->d_cells, c->cells_bytes);
+  if (e == hipSuccess)
+    e = cvr::launch_build_cells_impl(c->d_vox, bpv, d_lut, c->N, c->cells, c->d_cells, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_lut);
+  if (e != hipSuccess) {
+    free_dev(c->d_cells); c->cells_bytes = 0;
+    return fail(c, e == hipErrorOutOfMemory ? CVR_ERR_OOM : CVR_ERR_HIP,
+                "cvr_set_volume: %s", hipGetErrorString(e));
+  }
+  return CVR_OK;
+}
+
+cvr_status cvr_set_volume(cvr_ctx* ctx, const void* voxels, int bpv, int w, int h, int d,
+                          const float scale[3]) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  return set_volume_common(c, voxels, false, bpv, w, h, d, scale);
+}
+
+cvr_status cvr_set_volume_device(cvr_ctx* ctx, const void* d_voxels, int bpv, int w, int h,
+                                 int d, const float scale[3]) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  return set_volume_common(c, d_voxels, true, bpv, w, h, d, scale);
+}
+
+cvr_status cvr_set_transfer_function(cvr_ctx* ctx, const float* rgbt, int n) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!rgbt || n < 2 || n > 4096)
+    return fail(c, CVR_ERR_ARG, "cvr_set_transfer_function: need 2 <= n <= 4096 entries");
+  std::vector<float> q((size_t)n * 4);
+  for (size_t i = 0; i < q.size(); i++) q[i] = half_round(rgbt[i]);   // GL_RGBA16F
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (n != c->tf_n) {
+    void* p = c->d_tf; free_dev(p); c->d_tf = nullptr;
+    HIP_TRY(c, hipMalloc((void**)&c->d_tf, (size_t)n * 16));
+    c->tf_n = n;
+  }
+  HIP_TRY(c, hipMemcpy(c->d_tf, q.data(), (size_t)n * 16, hipMemcpyHostToDevice));
+  return CVR_OK;
+}
+
+cvr_status cvr_set_gradient(cvr_ctx* ctx, int mode) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (mode < 0 || mode > 2) return fail(c, CVR_ERR_ARG, "cvr_set_gradient: bad mode %d", mode);
+  if (mode != 0 && !c->d_vox) return fail(c, CVR_ERR_STATE, "cvr_set_gradient: no volume");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  free_dev(c->d_grad); c->grad_bytes = 0; c->grad_mode = 0;
+  if (mode == 0) return CVR_OK;
+  c->grad_bytes = (size_t)c->N[0] * c->N[1] * c->N[2] * 8;
+  HIP_TRY(c, hipMalloc(&c->d_grad, c->grad_bytes));
+  HIP_TRY(c, cvr::launch_gradient(*c, mode, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->grad_mode = mode;
+  return CVR_OK;
+}
+
+int cvr_tiles_for_rank(const cvr_frame* f, int rank) {
+  if (!f || f->width < 1 || f->height < 1) return 0;
+  if (f->nranks <= 1) return 1;
+  if (f->tile_size < 16 || f->tile_size % 16 != 0 || rank < 0 || rank >= f->nranks) return 0;
+  int ntx = (f->width + f->tile_size - 1) / f->tile_size;
+  int nty = (f->height + f->tile_size - 1) / f->tile_size;
+  int nt = ntx * nty;
+  return nt > rank ? (nt - rank + f->nranks - 1) / f->nranks : 0;
+}
+
+static cvr_status ensure_scratch(Ctx* c, size_t bytes) {
+  if (c->scratch_bytes >= bytes) return CVR_OK;
+  free_dev(c->d_scratch);
+  c->scratch_bytes = 0;
+  HIP_TRY(c, hipMalloc(&c->d_scratch, bytes));
+  c->scratch_bytes = bytes;
+  return CVR_OK;
+}
+
+cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pass_params* p,
+                              const cvr_output* o) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: null argument");
+  if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
+    return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: bad viewport %dx%d", f->width, f->height);
+  if (!c->d_cells) return fail(c, CVR_ERR_STATE, "cvr_render_rc1pass: no volume set");
+  if (!c->d_tf) return fail(c, CVR_ERR_STATE, "cvr_render_rc1pass: no transfer function set");
+  const bool phong = p->apply_gradient_shading != 0;
+  if (phong && !c->d_grad)
+    return fail(c, CVR_ERR_STATE, "cvr_render_rc1pass: gradient shading needs cvr_set_gradient");
+  const bool packed = f->nranks > 1;
+  if (packed && (f->tile_size < 16 || f->tile_size % 16 != 0 || f->rank < 0 || f->rank >= f->nranks))
+    return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: bad tiling (tile %d, rank %d/%d)",
+                f->tile_size, f->rank, f->nranks);
+
+  cvr::Rc1passArgs A{};
+  float V[16], tanh;
+  cvr_camera_lookat(&f->camera, V, &tanh);
+  for (int i = 0; i < 3; i++) {
+    A.eye[i] = f->camera.eye[i];
+    A.col0[i] = V[0 * 4 + i];
+    A.col1[i] = V[1 * 4 + i];
+    A.col2[i] = V[2 * 4 + i];
+  }
+  A.tan_half_fovy = tanh;
+  A.aspect = f->camera.aspect > 0 ? f->camera.aspect : (float)f->width / (float)f->height;
+  A.W = f->width;
+  A.H = f->height;
+  for (int i = 0; i < 3; i++) {
+    float G = (float)c->N[i] * c->scale[i];     // VolumeGridSize, rc1prenderer.cpp:241
+    A.half_grid[i] = G * 0.5f;
+    A.n_over_g[i] = (float)c->N[i] / G;
+    A.nm1[i] = (float)(c->N[i] - 1);
+    A.N[i] = c->N[i];
+  }
+  A.cells = c->cells;
+  A.step = p->step > 0 ? p->step : cvr_default_step(c->scale);
+  A.tf_n = c->tf_n;
+  A.ka = p->ka; A.kd = p->kd; A.ks = p->ks; A.shininess = p->shininess;
+  for (int i = 0; i < 3; i++) { A.ispec[i] = p->ispecular[i]; A.light[i] = p->light_pos[i]; }
+  int nblocks;
+  size_t npix;
+  if (!packed) {
+    A.packed = 0;
+    nblocks = ((f->width + 15) / 16) * ((f->height + 15) / 16);
+    npix = (size_t)f->width * f->height;
+  } else {
+    A.packed = 1;
+    A.tile = f->tile_size; A.rank = f->rank; A.nranks = f->nranks;
+    A.ntx = (f->width + f->tile_size - 1) / f->tile_size;
+    A.my_tiles = cvr_tiles_for_rank(f, f->rank);
+    nblocks = A.my_tiles * (f->tile_size / 16) * (f->tile_size / 16);
+    npix = (size_t)A.my_tiles * f->tile_size * f->tile_size;
+  }
+  A.xcd_remap = 1;
+
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  float4* d_out;
+  uint32_t* d_samples;
+  unsigned long long* d_total;
+  size_t rgba_bytes = npix * 16, smp_bytes = npix * 4;
+  if (o->on_device) {
+    d_out = (float4*)o->rgba;
+    d_samples = (uint32_t*)o->samples;
+    d_total = (unsigned long long*)o->total;
+  } else {
+    cvr_status st = ensure_scratch(c, rgba_bytes + (o->samples ? smp_bytes : 0));
+    if (st != CVR_OK) return st;
+    d_out = (float4*)c->d_scratch;
+    d_samples = o->samples ? (uint32_t*)((char*)c->d_scratch + rgba_bytes) : nullptr;
+    d_total = o->total ? c->d_total : nullptr;
+  }
+  // device outputs: the kernel ADDS to *total (the caller zeroes it); host
+  // outputs: the context's own counter is reset here.
+  if (d_total && !o->on_device) HIP_TRY(c, hipMemsetAsync(d_total, 0, sizeof(unsigned long long), s));
+  HIP_TRY(c, cvr::launch_rc1pass(*c, A, phong, d_out, d_samples, d_total, nblocks, s));
+  if (!o->on_device) {
+    HIP_TRY(c, hipMemcpyAsync(o->rgba, d_out, rgba_bytes, hipMemcpyDeviceToHost, s));
+    if (o->samples) HIP_TRY(c, hipMemcpyAsync(o->samples, d_samples, smp_bytes, hipMemcpyDeviceToHost, s));
+    if (o->total) HIP_TRY(c, hipMemcpyAsync(o->total, d_total, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return CVR_OK;
+}
+
+cvr_status cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* f, const void* d_packed,
+                                   int tpr_max, void* d_rgba) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!f || !d_packed || !d_rgba || f->nranks < 1 || f->tile_size < 16 || tpr_max < 0)
+    return fail(c, CVR_ERR_ARG, "cvr_unpack_tiles_device: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, cvr::launch_unpack_tiles((const float4*)d_packed, (float4*)d_rgba, f->width, f->height,
+                                      f->tile_size, f->nranks, tpr_max, c->stream));
+  return CVR_OK;
+}
+
+#pragma GCC visibility pop
+}  // extern "C"

@@ -1,0 +1,101 @@
+// cvr_internal.h — context state and kernel launch parameters shared by the
+// C-ABI implementation (cvr_api.cpp) and the gfx950 kernels (raymarch.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+
+#include "../../include/cvr.h"
+
+namespace cvr {
+
+// Padded-cell volume layout ("cell8"): cell (a,b,c), a in [0, N], holds the 8
+// corner values that GL trilinear filtering reads for texel coordinate
+// x in [a-1, a): corners clamp(a-1) and clamp(a) per axis (CLAMP_TO_EDGE).
+// One sample = one 16-byte (fp16 corners) load.  Cells are grouped in 4x4x4
+// bricks (1 KiB) so that a wave's 8x8 ray tile hits few cache lines.
+constexpr int kBrick = 4;
+
+struct CellGrid {
+  int cx, cy, cz;        // cells per axis = N + 1
+  int bx, by, bz;        // bricks per axis = ceil(cells / 4)
+};
+
+// Per-frame constants of the rc1pass kernel (passed by value).
+struct Rc1passArgs {
+  // ray generation (ray_marching_1p.comp:87-99)
+  float eye[3];
+  float col0[3], col1[3], col2[3];   // columns of mat3(View)
+  float tan_half_fovy, aspect;
+  float inv_w, inv_h;                // unused: exact division by W/H is used
+  int W, H;
+  // volume grid (rc1prenderer.cpp:233-258)
+  float half_grid[3];                // VolumeGridSize / 2
+  float n_over_g[3];                 // N / VolumeGridSize  (texel space)
+  float nm1[3];                      // N - 1 (float)
+  int N[3];
+  CellGrid cells;
+  float step;
+  int tf_n;
+  // Blinn-Phong (ray_marching_1p.comp:48-81)
+  float ka, kd, ks, shininess;
+  float ispec[3];
+  float light[3];
+  // screen-tile split (cvr_frame)
+  int tile, rank, nranks, ntx, my_tiles, sub_per_tile_x;
+  int packed;
+  int xcd_remap;
+};
+
+struct Ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // volume
+  int N[3] = {0, 0, 0};
+  float scale[3] = {1, 1, 1};
+  int bpv = 0;
+  void* d_vox = nullptr;          // raw voxels (u8/u16), kept for gradient/precompute
+  size_t vox_bytes = 0;
+  void* d_cells = nullptr;        // cell8 fp16 layout
+  size_t cells_bytes = 0;
+  CellGrid cells{};
+  // transfer function (RGBA16F values as float)
+  float* d_tf = nullptr;
+  int tf_n = 0;
+  // gradient (4 x fp16 per voxel, x-fastest)
+  void* d_grad = nullptr;
+  size_t grad_bytes = 0;
+  int grad_mode = 0;
+  // scratch
+  unsigned long long* d_total = nullptr;
+  void* d_scratch = nullptr;      // host-output staging
+  size_t scratch_bytes = 0;
+};
+
+// kernels / launchers (raymarch.hip)
+hipError_t launch_build_cells_impl(const void* vox, int bpv, const uint16_t* lut, const int N[3],
+                                   const CellGrid& g, void* cells, hipStream_t s);
+hipError_t launch_gradient(const Ctx& c, int mode, hipStream_t s);
+hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
+                          uint32_t* samples, unsigned long long* total, int nwavetiles,
+                          hipStream_t s);
+hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
+                               int nranks, int tiles_per_rank_max, hipStream_t s);
+
+inline CellGrid make_cell_grid(const int N[3]) {
+  CellGrid g;
+  g.cx = N[0] + 1; g.cy = N[1] + 1; g.cz = N[2] + 1;
+  g.bx = (g.cx + kBrick - 1) / kBrick;
+  g.by = (g.cy + kBrick - 1) / kBrick;
+  g.bz = (g.cz + kBrick - 1) / kBrick;
+  return g;
+}
+
+inline size_t cell_count(const CellGrid& g) {
+  return (size_t)g.bx * g.by * g.bz * (kBrick * kBrick * kBrick);
+}
+
+}  // namespace cvr

@@ -1,0 +1,207 @@
+// cvr_io.cpp — native readers for the reference's input formats.  The
+// reference readers are MSVC-only (fopen_s, sscanf_s, `unsigned char(v)` casts:
+// libs/file_utils/rawloader.cpp:16, libs/volvis_utils/reader.cpp:317,352), so
+// they are re-implemented here with the same grammar and semantics.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/cvr.h"
+
+namespace {
+
+std::string basename_of(const std::string& p) {
+  size_t a = p.find_last_of("/\\");
+  return a == std::string::npos ? p : p.substr(a + 1);
+}
+
+}  // namespace
+
+extern "C" {
+#pragma GCC visibility push(default)
+
+// TransferFunctionReader::readtf1d (reader.cpp:744-814)
+cvr_status cvr_read_tf1d(const char* path, float* out_rgbt, int* out_n) {
+  if (!path || !out_n) return CVR_ERR_ARG;
+  std::ifstream f(path);
+  if (!f.is_open()) return CVR_ERR_IO;
+  std::string interpolation;
+  std::getline(f, interpolation);     // "linear" (cubic is never implemented)
+  int init = 0;
+  if (!(f >> init)) return CVR_ERR_IO;
+  int max_density = 255, extuse = 0;
+  if (init == 2) {
+    if (!(f >> max_density >> extuse)) return CVR_ERR_IO;
+  } else if (init == 1) {
+    if (!(f >> max_density)) return CVR_ERR_IO;
+  }
+  int n_rgb = 0;
+  if (!(f >> n_rgb) || n_rgb < 0) return CVR_ERR_IO;
+  std::vector<double> rgb((size_t)n_rgb * 4);
+  for (int i = 0; i < n_rgb; i++) {
+    double r, g, b;
+    int iso;
+    if (!(f >> r >> g >> b >> iso)) return CVR_ERR_IO;
+    rgb[i * 4 + 0] = r; rgb[i * 4 + 1] = g; rgb[i * 4 + 2] = b; rgb[i * 4 + 3] = iso;
+  }
+  int n_a = 0;
+  if (!(f >> n_a) || n_a < 0) return CVR_ERR_IO;
+  std::vector<double> a((size_t)n_a * 2);
+  for (int i = 0; i < n_a; i++) {
+    double av;
+    int iso;
+    if (!(f >> av >> iso)) return CVR_ERR_IO;
+    a[i * 2 + 0] = av; a[i * 2 + 1] = iso;
+  }
+  *out_n = max_density + 1;
+  if (!out_rgbt) return CVR_OK;
+  return cvr_tf1d_build_rgbt(rgb.data(), n_rgb, a.data(), n_a, max_density, extuse == 1,
+                             out_rgbt);
+}
+
+// VolumeReader::readraw (reader.cpp:162-225): "name.<bytes>.<W>x<H>x<D>.raw"
+cvr_status cvr_read_raw(const char* path, void* voxels, size_t capacity, int* out_w, int* out_h,
+                        int* out_d, int* out_bpv) {
+  if (!path || !out_w || !out_h || !out_d || !out_bpv) return CVR_ERR_ARG;
+  std::string name = basename_of(path);
+  size_t ext = name.find_last_of('.');
+  if (ext == std::string::npos) return CVR_ERR_IO;
+  name = name.substr(0, ext);
+  size_t ds = name.find_last_of('.');
+  if (ds == std::string::npos) return CVR_ERR_IO;
+  std::string sizes = name.substr(ds + 1);
+  name = name.substr(0, ds);
+  size_t db = name.find_last_of('.');
+  std::string bytes = db == std::string::npos ? name : name.substr(db + 1);
+  int w = 0, h = 0, d = 0;
+  if (std::sscanf(sizes.c_str(), "%dx%dx%d", &w, &h, &d) != 3) return CVR_ERR_IO;
+  int bpv = std::atoi(bytes.c_str());
+  if (w < 1 || h < 1 || d < 1 || (bpv != 1 && bpv != 2)) return CVR_ERR_IO;
+  *out_w = w; *out_h = h; *out_d = d; *out_bpv = bpv;
+  if (!voxels) return CVR_OK;
+  size_t need = (size_t)w * h * d * bpv;
+  if (capacity < need) return CVR_ERR_ARG;
+  FILE* fp = std::fopen(path, "rb");
+  if (!fp) return CVR_ERR_IO;
+  size_t got = std::fread(voxels, 1, need, fp);
+  std::fclose(fp);
+  return got == need ? CVR_OK : CVR_ERR_IO;
+}
+
+// VolumeReader::readsyn (reader.cpp:283-371).  The reference leaves unlisted
+// voxels uninitialised (:301); here they are zero.
+cvr_status cvr_read_syn(const char* path, uint8_t* voxels, size_t capacity, int* out_w,
+                        int* out_h, int* out_d) {
+  if (!path || !out_w || !out_h || !out_d) return CVR_ERR_ARG;
+  std::ifstream f(path);
+  if (!f.is_open()) return CVR_ERR_IO;
+  int w, h, d;
+  if (!(f >> w >> h >> d) || w < 1 || h < 1 || d < 1) return CVR_ERR_IO;
+  *out_w = w; *out_h = h; *out_d = d;
+  if (!voxels) return CVR_OK;
+  size_t need = (size_t)w * h * d;
+  if (capacity < need) return CVR_ERR_ARG;
+  std::memset(voxels, 0, need);
+  int kind;
+  while (f >> kind) {
+    if (kind == 1) {
+      int x0, y0, z0, x1, y1, z1, v;
+      if (!(f >> x0 >> y0 >> z0 >> x1 >> y1 >> z1 >> v)) return CVR_ERR_IO;
+      for (int x = x0; x < x1; x++)
+        for (int y = y0; y < y1; y++)
+          for (int z = z0; z < z1; z++) {
+            if (x < 0 || y < 0 || z < 0 || x >= w || y >= h || z >= d) return CVR_ERR_IO;
+            voxels[(size_t)x + (size_t)w * y + (size_t)w * h * z] = (uint8_t)v;
+          }
+    } else {
+      int x, y, z, v;
+      if (!(f >> x >> y >> z >> v)) return CVR_ERR_IO;
+      if (x < 0 || y < 0 || z < 0 || x >= w || y >= h || z >= d) return CVR_ERR_IO;
+      voxels[(size_t)x + (size_t)w * y + (size_t)w * h * z] = (uint8_t)v;
+    }
+  }
+  return CVR_OK;
+}
+
+// CameraStateList::ReadCameraStates (camerastatelist.cpp:26-87)
+cvr_status cvr_read_camera_state(const char* path, int index, cvr_camera* out_cam, char* out_name,
+                                 int name_capacity, int* out_count) {
+  if (!path) return CVR_ERR_ARG;
+  std::ifstream f(path);
+  if (!f.is_open()) return CVR_ERR_IO;
+  struct State { std::string name; float eye[3], center[3], up[3]; };
+  std::vector<State> states;
+  std::string line;
+  while (!f.eof()) {
+    State s{};
+    line.clear();
+    std::getline(f, line);
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    s.name = line;
+    line.clear();
+    std::getline(f, line);
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    if (line == "ARCBALL") {
+      f >> s.eye[0] >> s.eye[1] >> s.eye[2];
+      f >> s.center[0] >> s.center[1] >> s.center[2];
+      f >> s.up[0] >> s.up[1] >> s.up[2];
+      std::getline(f, line);
+    }
+    states.push_back(s);
+  }
+  if (out_count) *out_count = (int)states.size();
+  if (!out_cam) return CVR_OK;
+  if (index < 0 || index >= (int)states.size()) return CVR_ERR_ARG;
+  const State& s = states[index];
+  for (int i = 0; i < 3; i++) {
+    out_cam->eye[i] = s.eye[i];
+    out_cam->center[i] = s.center[i];
+    out_cam->up[i] = s.up[i];
+  }
+  out_cam->fovy_deg = 45.0f;   // CameraData default, camera.cpp:25,44
+  out_cam->aspect = 0.0f;      // derived from the viewport
+  if (out_name && name_capacity > 0) {
+    std::strncpy(out_name, s.name.c_str(), (size_t)name_capacity - 1);
+    out_name[name_capacity - 1] = 0;
+  }
+  return CVR_OK;
+}
+
+// LightSourceList::ReadLightSourceLists (lightsourcelist.cpp:81-148)
+cvr_status cvr_read_light_position(const char* path, int list, int light, float out_pos[3],
+                                   int* out_count) {
+  if (!path) return CVR_ERR_ARG;
+  std::ifstream f(path);
+  if (!f.is_open()) return CVR_ERR_IO;
+  std::vector<std::vector<std::vector<float>>> lists;
+  std::string line;
+  while (!f.eof()) {
+    line.clear();
+    std::getline(f, line);
+    int n = 0;
+    std::vector<std::vector<float>> lights;
+    if (f >> n) {
+      for (int i = 0; i < n; i++) {
+        std::vector<float> v(13);
+        for (int k = 0; k < 13; k++) f >> v[k];
+        line.clear();
+        std::getline(f, line);
+        lights.push_back(v);
+      }
+    }
+    lists.push_back(lights);
+  }
+  if (out_count) *out_count = (int)lists.size();
+  if (!out_pos) return CVR_OK;
+  if (list < 0 || list >= (int)lists.size() || light < 0 || light >= (int)lists[list].size())
+    return CVR_ERR_ARG;
+  for (int i = 0; i < 3; i++) out_pos[i] = lists[list][light][i];
+  return CVR_OK;
+}
+
+#pragma GCC visibility pop
+}  // extern "C"

@@ -1,0 +1,380 @@
+"""Host-side mirror of cppvolrend's renderer-plugin API over the C-ABI.
+
+The classes follow the reference names and call sequence so that code (and
+tests) read like the reference:
+
+    RenderingManager::InitData  -> DataManager.read_* / RenderingParameters
+    BaseVolumeRenderer          -> BaseVolumeRenderer   (cppvolrend/volrenderbase.h:25-96)
+    RayCasting1Pass             -> RayCasting1Pass      (cppvolrend/structured/rc1pass/rc1prenderer.*)
+
+Per frame: ``PrepareRender(camera)`` (calls ``Update`` when outdated) then
+``Redraw()``, exactly as RenderingManager::Display does
+(cppvolrend/renderingmanager.cpp:199-208).  Every call goes to libcvr.so; the
+image lives in device memory (a torch tensor on the renderer's device).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+STRUCTURED = "STRUCTURED"   # vis::GRID_VOLUME_DATA_TYPE::STRUCTURED
+
+
+@dataclass
+class Camera:
+    """vis::CameraData subset used by the ray generator (libs/vis_utils/camera.cpp)."""
+    eye: tuple = (256.0, 256.0, 512.0)       # data/#list_camera_states "Initial State"
+    center: tuple = (0.0, 0.0, 0.0)
+    up: tuple = (0.0, 1.0, 0.0)
+    fovy_deg: float = 45.0                   # camera.cpp:25
+    aspect: float = 0.0                      # 0: width / height (Camera::UpdateAspectRatio)
+
+    def to_c(self) -> N.Camera:
+        c = N.Camera()
+        c.eye[:] = [float(v) for v in self.eye]
+        c.center[:] = [float(v) for v in self.center]
+        c.up[:] = [float(v) for v in self.up]
+        c.fovy_deg = float(self.fovy_deg)
+        c.aspect = float(self.aspect)
+        return c
+
+    def GetEye(self):
+        return self.eye
+
+
+@dataclass
+class RenderingParameters:
+    """vis::RenderingParameters defaults (libs/volvis_utils/renderingparameters.cpp:17-32)."""
+    screen_width: int = 768
+    screen_height: int = 768
+    blinnphong_ka: float = 0.5
+    blinnphong_kd: float = 0.5
+    blinnphong_ks: float = 0.8
+    blinnphong_shininess: float = 30.0
+    light_position: tuple = (-206.873, -51.0699, 557.011)   # data/#list_light_sources list 0
+    light_specular: tuple = (1.0, 1.0, 1.0)                 # lightsourcelist.cpp:24
+    camera: Camera = field(default_factory=Camera)
+
+    def GetScreenWidth(self): return self.screen_width
+    def GetScreenHeight(self): return self.screen_height
+    def GetCamera(self): return self.camera
+    def GetBlinnPhongLightingPosition(self): return self.light_position
+    def GetLightSourceSpecular(self): return self.light_specular
+
+
+class DataManager:
+    """vis::DataManager subset: the current structured volume, its TF and gradient type."""
+
+    def __init__(self):
+        self.volume: Optional[np.ndarray] = None    # (D, H, W) u8/u16, x fastest
+        self.scale = (1.0, 1.0, 1.0)
+        self.tf_rgbt: Optional[np.ndarray] = None  # (n, 4) float32: r, g, b, extinction
+        self.gradient_type = N.GRADIENT_NONE        # datamanager.cpp:27 (NONE by default)
+        self.name = ""
+
+    # -- inputs --------------------------------------------------------------
+    def SetVolume(self, voxels: np.ndarray, scale=(1.0, 1.0, 1.0), name: str = ""):
+        if voxels.ndim != 3 or voxels.dtype not in (np.uint8, np.uint16):
+            raise ValueError("volume must be a (D, H, W) uint8/uint16 array")
+        self.volume = np.ascontiguousarray(voxels)
+        self.scale = tuple(float(s) for s in scale)
+        self.name = name
+
+    def SetTransferFunction(self, rgbt: np.ndarray):
+        rgbt = np.ascontiguousarray(rgbt, dtype=np.float32)
+        if rgbt.ndim != 2 or rgbt.shape[1] != 4:
+            raise ValueError("transfer function must be (n, 4) r, g, b, extinction")
+        self.tf_rgbt = rgbt
+
+    def ReadVolume(self, path: str, scale=None):
+        """.raw (name.<bytes>.<W>x<H>x<D>.raw) or .syn, like VolumeReader::ReadStructuredVolume."""
+        L = N.lib()
+        w, h, d, b = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        bp = path.encode()
+        if path.endswith(".raw"):
+            N.check(L.cvr_read_raw(bp, None, 0, w, h, d, b), "cvr_read_raw")
+            dt = np.uint8 if b.value == 1 else np.uint16
+            vox = np.empty((d.value, h.value, w.value), dtype=dt)
+            N.check(L.cvr_read_raw(bp, vox.ctypes.data, vox.nbytes, w, h, d, b), "cvr_read_raw")
+        elif path.endswith(".syn"):
+            N.check(L.cvr_read_syn(bp, None, 0, w, h, d), "cvr_read_syn")
+            vox = np.empty((d.value, h.value, w.value), dtype=np.uint8)
+            N.check(L.cvr_read_syn(bp, vox.ctypes.data, vox.nbytes, w, h, d), "cvr_read_syn")
+        else:
+            raise ValueError(f"unsupported volume format: {path}")
+        self.SetVolume(vox, scale or (1.0, 1.0, 1.0), name=path)
+
+    def ReadTransferFunction(self, path: str):
+        self.SetTransferFunction(read_tf1d(path))
+
+    # -- accessors (reference names) -----------------------------------------
+    def GetCurrentStructuredVolume(self): return self.volume
+    def GetCurrentTransferFunction(self): return self.tf_rgbt
+
+    def SetGradientType(self, gtype: int):
+        self.gradient_type = int(gtype)
+
+
+def read_tf1d(path: str) -> np.ndarray:
+    L = N.lib()
+    n = ctypes.c_int()
+    N.check(L.cvr_read_tf1d(path.encode(), None, n), "cvr_read_tf1d")
+    out = np.empty((n.value, 4), dtype=np.float32)
+    N.check(L.cvr_read_tf1d(path.encode(), N.fptr(out), n), "cvr_read_tf1d")
+    return out
+
+
+def build_tf_rgbt(rgb_cp, alpha_cp, max_density: int = 255, extinction_input: bool = False):
+    """TransferFunction1D control points -> GenerateTexture_1D_RGBt data (float, pre-fp16)."""
+    rgb = np.ascontiguousarray(np.asarray(rgb_cp, dtype=np.float64).reshape(-1, 4))
+    a = np.ascontiguousarray(np.asarray(alpha_cp, dtype=np.float64).reshape(-1, 2))
+    out = np.empty((max_density + 1, 4), dtype=np.float32)
+    N.check(N.lib().cvr_tf1d_build_rgbt(N.dptr(rgb), rgb.shape[0], N.dptr(a), a.shape[0],
+                                        max_density, int(extinction_input), N.fptr(out)),
+            "cvr_tf1d_build_rgbt")
+    return out
+
+
+def read_camera_state(path: str, index: int = 0) -> Camera:
+    c = N.Camera()
+    name = ctypes.create_string_buffer(256)
+    cnt = ctypes.c_int()
+    N.check(N.lib().cvr_read_camera_state(path.encode(), index, c, name, 256, cnt),
+            "cvr_read_camera_state")
+    return Camera(tuple(c.eye), tuple(c.center), tuple(c.up), c.fovy_deg, 0.0)
+
+
+def read_light_position(path: str, list_index: int = 0, light: int = 0):
+    pos = (ctypes.c_float * 3)()
+    cnt = ctypes.c_int()
+    N.check(N.lib().cvr_read_light_position(path.encode(), list_index, light, pos, cnt),
+            "cvr_read_light_position")
+    return tuple(pos)
+
+
+class Device:
+    """One libcvr context (cvr_ctx) bound to a HIP device; owns all device data."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self._h = ctypes.c_void_p()
+        N.check(N.lib().cvr_create(device, ctypes.byref(self._h)), "cvr_create")
+
+    @property
+    def handle(self):
+        if not self._h:
+            raise N.CvrError(N.CVR_ERR_STATE, "Device", "context destroyed")
+        return self._h
+
+    def close(self):
+        if self._h:
+            N.lib().cvr_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream: Optional[int]):
+        N.check(N.lib().cvr_set_stream(self.handle, stream), "cvr_set_stream", self.handle)
+
+    def synchronize(self):
+        N.check(N.lib().cvr_synchronize(self.handle), "cvr_synchronize", self.handle)
+
+    def set_volume(self, voxels: np.ndarray, scale):
+        vox = np.ascontiguousarray(voxels)
+        d, h, w = vox.shape
+        sc = np.asarray(scale, dtype=np.float32)
+        N.check(N.lib().cvr_set_volume(self.handle, vox.ctypes.data, vox.dtype.itemsize, w, h, d,
+                                       N.fptr(sc)), "cvr_set_volume", self.handle)
+
+    def set_volume_device(self, voxels: torch.Tensor, scale):
+        if not voxels.is_cuda or not voxels.is_contiguous():
+            raise ValueError("expected a contiguous device tensor")
+        d, h, w = voxels.shape
+        sc = np.asarray(scale, dtype=np.float32)
+        N.check(N.lib().cvr_set_volume_device(self.handle, voxels.data_ptr(),
+                                              voxels.element_size(), w, h, d, N.fptr(sc)),
+                "cvr_set_volume_device", self.handle)
+
+    def set_transfer_function(self, rgbt: np.ndarray):
+        t = np.ascontiguousarray(rgbt, dtype=np.float32)
+        N.check(N.lib().cvr_set_transfer_function(self.handle, N.fptr(t), t.shape[0]),
+                "cvr_set_transfer_function", self.handle)
+
+    def set_gradient(self, mode: int):
+        N.check(N.lib().cvr_set_gradient(self.handle, int(mode)), "cvr_set_gradient", self.handle)
+
+    def device_bytes(self) -> int:
+        return int(N.lib().cvr_device_bytes(self.handle))
+
+
+def make_frame(camera: Camera, width: int, height: int, tile_size: int = 0, rank: int = 0,
+               nranks: int = 1) -> N.Frame:
+    f = N.Frame()
+    f.camera = camera.to_c()
+    f.width, f.height = int(width), int(height)
+    f.tile_size, f.rank, f.nranks = int(tile_size), int(rank), int(nranks)
+    return f
+
+
+def tiles_for_rank(frame: N.Frame, rank: int) -> int:
+    return int(N.lib().cvr_tiles_for_rank(ctypes.byref(frame), rank))
+
+
+class BaseVolumeRenderer:
+    """cppvolrend/volrenderbase.h:25-96 (GL-free)."""
+
+    SINGLE_RAY_PER_PIXEL = 0
+
+    def __init__(self):
+        self.vr_built = False
+        self.vr_outdated = True
+        self.m_ext_data_manager: Optional[DataManager] = None
+        self.m_ext_rendering_parameters: Optional[RenderingParameters] = None
+
+    # non-virtual API
+    def SetExternalResources(self, data_mgr: DataManager, rdr_prm: RenderingParameters):
+        self.m_ext_data_manager = data_mgr
+        self.m_ext_rendering_parameters = rdr_prm
+
+    def PrepareRender(self, camera: Camera):
+        if self.IsOutdated():
+            self.Update(camera)
+            self.vr_outdated = False
+
+    def SetOutdated(self): self.vr_outdated = True
+    def IsOutdated(self): return self.vr_outdated
+    def IsBuilt(self): return self.vr_built
+    def SetBuilt(self, b: bool): self.vr_built = bool(b)
+    def IsPixelMultiScalingSupported(self): return False
+    def GetCurrentMultiScalingMode(self): return self.SINGLE_RAY_PER_PIXEL
+
+    # virtual API
+    def GetName(self) -> str: raise NotImplementedError
+    def GetAbbreviationName(self) -> str: raise NotImplementedError
+    def GetDataTypeSupport(self) -> str: raise NotImplementedError
+    def Init(self, swidth: int, sheight: int) -> bool: raise NotImplementedError
+    def Update(self, camera: Camera) -> bool: raise NotImplementedError
+    def Redraw(self): pass
+    def ReloadShaders(self): pass
+    def FillParameterSpace(self, pspace: dict): pspace.clear()
+
+    def Reshape(self, w: int, h: int):
+        self.SetOutdated()
+
+    def Clean(self):
+        self.SetBuilt(False)
+
+
+class RayCasting1Pass(BaseVolumeRenderer):
+    """HIP implementation of RayCasting1Pass (cppvolrend/structured/rc1pass/rc1prenderer.cpp)."""
+
+    def __init__(self, device: int = 0):
+        super().__init__()
+        self.m_u_step_size = 0.5                    # rc1prenderer.cpp:21
+        self.m_apply_gradient_shading = False       # :22
+        self._device_index = device
+        self._dev: Optional[Device] = None
+        self._frame: Optional[N.Frame] = None
+        self._params = N.Rc1passParams()
+        self.width = self.height = 0
+        self.rgba: Optional[torch.Tensor] = None    # (H, W, 4) float32, device
+        self.samples: Optional[torch.Tensor] = None  # (H, W) int32 iteration counts
+        self.total: Optional[torch.Tensor] = None   # (1,) int64 sum of samples
+
+    def GetName(self): return "1-Pass - Ray Casting"
+    def GetAbbreviationName(self): return "s_1rc"
+    def GetDataTypeSupport(self): return STRUCTURED
+
+    @property
+    def device(self) -> Device:
+        if self._dev is None:
+            raise N.CvrError(N.CVR_ERR_STATE, "RayCasting1Pass", "Init() not called")
+        return self._dev
+
+    def Init(self, swidth: int, sheight: int) -> bool:
+        if self.IsBuilt():
+            self.Clean()
+        dm = self.m_ext_data_manager
+        if dm is None or dm.volume is None or dm.tf_rgbt is None:
+            return False                            # rc1prenderer.cpp:54
+        self._dev = Device(self._device_index)
+        self._dev.set_volume(dm.volume, dm.scale)
+        self._dev.set_transfer_function(dm.tf_rgbt)
+        if dm.gradient_type != N.GRADIENT_NONE:
+            self._dev.set_gradient(dm.gradient_type)
+        sc = np.asarray(dm.scale, dtype=np.float32)
+        self.m_u_step_size = float(N.lib().cvr_default_step(N.fptr(sc)))   # :62-63
+        self.Reshape(swidth, sheight)
+        self.SetBuilt(True)
+        self.SetOutdated()
+        return True
+
+    def Reshape(self, w: int, h: int):
+        self.width, self.height = int(w), int(h)
+        dev = torch.device("cuda", self._device_index)
+        self.rgba = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
+        self.samples = torch.zeros((h, w), dtype=torch.int32, device=dev)
+        self.total = torch.zeros((1,), dtype=torch.int64, device=dev)
+        super().Reshape(w, h)
+
+    def Update(self, camera: Camera) -> bool:
+        rp = self.m_ext_rendering_parameters or RenderingParameters()
+        self._frame = make_frame(camera, self.width, self.height)
+        p = self._params
+        p.step = float(self.m_u_step_size)
+        p.apply_gradient_shading = int(bool(self.m_apply_gradient_shading) and
+                                       self.m_ext_data_manager.gradient_type != N.GRADIENT_NONE)
+        p.ka, p.kd = rp.blinnphong_ka, rp.blinnphong_kd
+        p.ks, p.shininess = rp.blinnphong_ks, rp.blinnphong_shininess
+        p.ispecular[:] = [float(v) for v in rp.light_specular]
+        p.light_pos[:] = [float(v) for v in rp.light_position]
+        return True
+
+    def Redraw(self, stream: Optional[torch.cuda.Stream] = None, count_samples: bool = True):
+        """Dispatch the ray-march into self.rgba (asynchronous on `stream`)."""
+        if self._frame is None:
+            raise N.CvrError(N.CVR_ERR_STATE, "RayCasting1Pass.Redraw", "Update() not called")
+        s = stream if stream is not None else torch.cuda.current_stream(self._device_index)
+        self.device.set_stream(s.cuda_stream)
+        if count_samples:
+            with torch.cuda.stream(s):
+                self.total.zero_()                  # the kernel accumulates into it
+        out = N.Output(self.rgba.data_ptr(),
+                       self.samples.data_ptr() if count_samples else None,
+                       self.total.data_ptr() if count_samples else None, 1)
+        N.check(N.lib().cvr_render_rc1pass(self.device.handle, ctypes.byref(self._frame),
+                                           ctypes.byref(self._params), ctypes.byref(out)),
+                "cvr_render_rc1pass", self.device.handle)
+
+    def FillParameterSpace(self, pspace: dict):
+        pspace.clear()
+        pspace["StepSize"] = (0.2, 2.0, 0.1)        # rc1prenderer.cpp:225-229
+
+    def Clean(self):
+        if self._dev is not None:
+            self._dev.close()
+            self._dev = None
+        super().Clean()
+
+
+def composite_over_white(rgba: np.ndarray) -> np.ndarray:
+    """Screen image as RenderFrameToScreen::Draw blends it over the white clear colour
+    with SRC_ALPHA / ONE_MINUS_SRC_ALPHA (renderingmanager.cpp:103-112), as RGB8."""
+    rgb = rgba[..., :3] * rgba[..., 3:4] + (1.0 - rgba[..., 3:4])
+    return np.clip(np.floor(rgb * 255.0 + 0.5), 0, 255).astype(np.uint8)
+
+
+def default_step(scale) -> float:
+    sx, sy, sz = (float(s) for s in scale)
+    return float(np.float32((0.5 / math.sqrt(3.0)) * math.sqrt(sx * sx + sy * sy + sz * sz)))

@@ -1,0 +1,215 @@
+/*
+ * cvr.h — C-ABI of the MI355X-native structured volume ray-caster.
+ *
+ * This is the drop-in boundary for cppvolrend's renderer-plugin path
+ * (k2683/cpp_volume_rendering).  A reference-side adapter class
+ * (`HipRayCasting1Pass : BaseVolumeRenderer`) forwards the
+ * plugin calls to these functions; no GL object and no torch type crosses the
+ * boundary, only plain pointers, sizes and POD structs.
+ *
+ * Mapping to the reference interface (paths relative to the reference root):
+ *
+ *   cvr_create / cvr_destroy     <- BaseVolumeRenderer ctor / Clean()
+ *                                   cppvolrend/volrenderbase.cpp:5-29
+ *   cvr_set_volume               <- DataManager::GenerateStructuredVolumeTexture +
+ *                                   vis::GenerateRTexture (u8/255 -> float -> GL_R16F)
+ *                                   libs/volvis_utils/datamanager.cpp:311-330,
+ *                                   libs/volvis_utils/utils.cpp:20-56
+ *   cvr_set_transfer_function    <- TransferFunction1D::GenerateTexture_1D_RGBt
+ *                                   (256 x RGBA16F, alpha already converted to extinction)
+ *                                   libs/volvis_utils/transferfunction1d.cpp:89-118
+ *   cvr_set_gradient             <- DataManager::GenerateStructuredGradientTexture
+ *                                   libs/volvis_utils/datamanager.cpp:332-352,
+ *                                   libs/volvis_utils/utils.cpp:146-284 (finite differences)
+ *   cvr_render_rc1pass           <- RayCasting1Pass::Update + Redraw
+ *                                   cppvolrend/structured/rc1pass/rc1prenderer.cpp:72-151
+ *                                   (the dispatch of ray_marching_1p.comp:85-179)
+ *   cvr_render_dosct             <- RC1PConeTracingDirOcclusionShading::Update + Redraw
+ *                                   cppvolrend/structured/rc1pdosct/dosrcrenderer.cpp:134-260
+ *   cvr_render_extbsd            <- RC1PExtinctionBasedShading::Update + Redraw
+ *                                   cppvolrend/structured/rc1pextbsd/ebsrenderer.cpp:125-260
+ *   cvr_status (never exit())    <- gl::ExitOnGLError  libs/gl_utils/utils.cpp:11-30
+ *
+ * Threading: one context per device, externally synchronised (the reference
+ * renderer runs on the single GLUT thread, app_freeglut.cpp:172-175).
+ * Ownership: the context owns every device allocation; no caller pointer is
+ * retained after a call returns.
+ */
+#ifndef CVR_H
+#define CVR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CVR_ABI_VERSION 1
+
+typedef enum cvr_status {
+  CVR_OK = 0,
+  CVR_ERR_ARG = 1,    /* invalid argument (null pointer, bad size, bad enum)   */
+  CVR_ERR_HIP = 2,    /* a HIP runtime call failed                              */
+  CVR_ERR_OOM = 3,    /* device allocation failed                               */
+  CVR_ERR_STATE = 4,  /* call out of order (e.g. render before set_volume);
+                         mirrors RayCasting1Pass::Init returning false when the
+                         volume texture is missing, rc1prenderer.cpp:54          */
+  CVR_ERR_IO = 5      /* a reader could not open / parse its file              */
+} cvr_status;
+
+typedef struct cvr_ctx cvr_ctx;
+
+/* ----------------------------------------------------------------------------
+ * Frame description: vis::Camera state + viewport + optional screen-tile split.
+ * -------------------------------------------------------------------------- */
+typedef struct cvr_camera {
+  float eye[3];     /* Camera::GetEye                       camera.cpp:340   */
+  float center[3];  /* look-at target                       camera.cpp:281   */
+  float up[3];      /* up vector                            camera.cpp:281   */
+  float fovy_deg;   /* 45 by default                        camera.cpp:25,44 */
+  float aspect;     /* <= 0: width / height                 camera.cpp:307   */
+} cvr_camera;
+
+typedef struct cvr_frame {
+  cvr_camera camera;
+  int width;        /* viewport (RenderingParameters::GetScreenWidth)         */
+  int height;
+  /* Screen-tile split (multi-GPU): nranks <= 1 renders the whole W x H image
+   * row-major.  nranks > 1: the image is cut into tile_size^2 tiles, global
+   * tile t (row-major over tiles) belongs to rank t % nranks, and this rank
+   * writes its k-th tile (t = rank + k*nranks) packed at offset
+   * k*tile_size*tile_size pixels, row-major inside the tile.               */
+  int tile_size;
+  int rank;
+  int nranks;
+} cvr_frame;
+
+/* Output buffers.  rgba: float RGBA, premultiplied, W*H*4 floats (or the
+ * packed tile buffer).  samples (optional): per-pixel loop-iteration count of
+ * ray_marching_1p.comp:124-172 (transparent samples included, stopping at the
+ * ERT break).  total (optional): the sum of all iteration counts (uint64).
+ * on_device = 1: all three are device pointers and the call is asynchronous
+ * on the context stream; the frame's count is atomically ADDED to *total, so
+ * the caller zeroes it (one counter can accumulate many frames).
+ * on_device = 0: host pointers, *total is overwritten, the call blocks.      */
+typedef struct cvr_output {
+  void* rgba;
+  void* samples;
+  void* total;
+  int on_device;
+} cvr_output;
+
+/* ----------------------------------------------------------------------------
+ * Renderer parameters
+ * -------------------------------------------------------------------------- */
+
+/* RayCasting1Pass ("1-Pass - Ray Casting", s_1rc): rc1prenderer.cpp:18-138. */
+typedef struct cvr_rc1pass_params {
+  float step;                  /* <= 0: 0.5/sqrt(3)*|scale|, rc1prenderer.cpp:62-63 */
+  int   apply_gradient_shading;/* Blinn-Phong with the gradient volume, :112        */
+  float ka, kd, ks, shininess; /* renderingparameters.cpp:23-26 (0.5,0.5,0.8,30)     */
+  float ispecular[3];          /* light specular colour, lightsourcelist.cpp:24      */
+  float light_pos[3];          /* RenderingParameters::GetBlinnPhongLightingPosition */
+} cvr_rc1pass_params;
+
+/* ----------------------------------------------------------------------------
+ * Context
+ * -------------------------------------------------------------------------- */
+int         cvr_abi_version(void);
+const char* cvr_status_string(cvr_status s);
+cvr_status  cvr_create(int device, cvr_ctx** out_ctx);
+void        cvr_destroy(cvr_ctx* ctx);
+const char* cvr_last_error(const cvr_ctx* ctx);
+/* Launch stream (a hipStream_t); NULL = the context's own stream. */
+cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
+cvr_status  cvr_synchronize(cvr_ctx* ctx);
+
+/* Volume: x-fastest voxels (i + j*w + k*w*h), 1 byte (u8) or 2 bytes (u16)
+ * per voxel, normalised as v/255 or v/65535 (structuredgridvolume.cpp:121-151)
+ * and stored with GL_R16F semantics.  The data is copied (host pointer). */
+cvr_status  cvr_set_volume(cvr_ctx* ctx, const void* voxels, int bytes_per_voxel,
+                           int w, int h, int d, const float scale[3]);
+/* Same, from a device pointer that stays owned by the caller. */
+cvr_status  cvr_set_volume_device(cvr_ctx* ctx, const void* d_voxels, int bytes_per_voxel,
+                                  int w, int h, int d, const float scale[3]);
+
+/* Transfer function as n entries of (r, g, b, extinction) floats, i.e. the
+ * data GenerateTexture_1D_RGBt uploads; stored with GL_RGBA16F semantics and
+ * sampled linearly at x = v*n - 0.5, clamp-to-edge. */
+cvr_status  cvr_set_transfer_function(cvr_ctx* ctx, const float* rgbt, int n);
+
+/* Gradient volume for Blinn-Phong.  0 = none, 1 = finite differences
+ * (GenerateGradientTexture defaults: sample size 1, no filter, normalised),
+ * 2 = Sobel-Feldman (GenerateSobelFeldmanGradientTexture, unnormalised). */
+#define CVR_GRADIENT_NONE 0
+#define CVR_GRADIENT_FINITE_DIFFERENCES 1
+#define CVR_GRADIENT_SOBEL_FELDMAN 2
+cvr_status  cvr_set_gradient(cvr_ctx* ctx, int mode);
+
+/* Device bytes held by the context (volume layouts, TF, gradient, ...). */
+size_t      cvr_device_bytes(const cvr_ctx* ctx);
+
+/* ----------------------------------------------------------------------------
+ * Rendering
+ * -------------------------------------------------------------------------- */
+/* Number of tiles rank `rank` owns under the split described by `frame`. */
+int         cvr_tiles_for_rank(const cvr_frame* frame, int rank);
+
+cvr_status  cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* frame,
+                               const cvr_rc1pass_params* params, const cvr_output* out);
+
+/* Rank-0 side of the screen-tile split: `d_packed` holds nranks consecutive
+ * blocks of `tiles_per_rank_max` packed tiles (rank r's block at offset
+ * r*tiles_per_rank_max*tile_size^2 pixels); scatter them into the W x H
+ * device image `d_rgba`.  Asynchronous on the context stream. */
+cvr_status  cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* frame,
+                                    const void* d_packed, int tiles_per_rank_max,
+                                    void* d_rgba);
+
+/* ----------------------------------------------------------------------------
+ * Host-side helpers (native replacements for the reference's MSVC-only
+ * readers and its CPU table builders).  They touch no device.
+ * -------------------------------------------------------------------------- */
+/* Derived render constants, exposed for testing: the view matrix the ray
+ * generator uses (glm::lookAt, column-major 4x4) and tan(fovy/2). */
+cvr_status  cvr_camera_lookat(const cvr_camera* cam, float out_view[16], float* out_tan_half_fovy);
+/* Default integration step for a voxel scale: 0.5/sqrt(3)*|scale|. */
+float       cvr_default_step(const float scale[3]);
+
+/* TransferFunction1D built from control points (BuildLinear,
+ * transferfunction1d.cpp:319-358) and converted like GenerateTexture_1D_RGBt
+ * (:89-118).  rgb_cp: n_rgb x (r, g, b, isovalue); a_cp: n_a x (a, isovalue).
+ * out_rgbt receives (max_density+1) x 4 floats. */
+cvr_status  cvr_tf1d_build_rgbt(const double* rgb_cp, int n_rgb, const double* a_cp, int n_a,
+                                int max_density, int extinction_input, float* out_rgbt);
+
+/* .tf1d reader (TransferFunctionReader::readtf1d, reader.cpp:744-814) and the
+ * built table.  out_rgbt must hold 4*(max_density+1) floats; pass NULL to
+ * query *out_n first. */
+cvr_status  cvr_read_tf1d(const char* path, float* out_rgbt, int* out_n);
+
+/* .raw reader: dims and bytes per voxel parsed from "name.<bytes>.<W>x<H>x<D>.raw"
+ * (VolumeReader::readraw, reader.cpp:162-225).  Pass voxels = NULL to query. */
+cvr_status  cvr_read_raw(const char* path, void* voxels, size_t capacity,
+                         int* out_w, int* out_h, int* out_d, int* out_bytes_per_voxel);
+
+/* .syn reader (VolumeReader::readsyn, reader.cpp:283-371); u8 voxels. */
+cvr_status  cvr_read_syn(const char* path, uint8_t* voxels, size_t capacity,
+                         int* out_w, int* out_h, int* out_d);
+
+/* #list_camera_states (CameraStateList::ReadCameraStates, camerastatelist.cpp:26-87):
+ * returns the index-th ARCBALL state. */
+cvr_status  cvr_read_camera_state(const char* path, int index, cvr_camera* out_cam,
+                                  char* out_name, int name_capacity, int* out_count);
+
+/* #list_light_sources (LightSourceList::ReadLightSourceLists, lightsourcelist.cpp:81-148):
+ * position of light `light` of list `list`. */
+cvr_status  cvr_read_light_position(const char* path, int list, int light, float out_pos[3],
+                                    int* out_count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CVR_H */

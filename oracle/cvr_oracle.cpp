@@ -1,0 +1,529 @@
+/*
+ * cvr_oracle.cpp — CPU restatement of cppvolrend's structured single-pass
+ * ray-march (rc1pass) and its inputs.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this library, and only as the checker / the timed CPU baseline.  The product
+ * (cpp_volume_rendering_amd, libcvr.so) never links or calls it.
+ *
+ * Reference (paths relative to the reference root, read-only):
+ *   ray generation .............. cppvolrend/structured/rc1pass/ray_marching_1p.comp:87-99
+ *   ray/AABB slab test .......... cppvolrend/structured/_common_shaders/ray_bbox_intersection.comp:18-52
+ *   march + FTB composite + ERT . ray_marching_1p.comp:106-176
+ *   Blinn-Phong ................. ray_marching_1p.comp:48-81 (applied at :145-146)
+ *   step size ................... cppvolrend/structured/rc1pass/rc1prenderer.cpp:62-63
+ *   volume texture (R16F) ....... libs/volvis_utils/utils.cpp:20-56, structuredgridvolume.cpp:121-151
+ *   TF table (RGBA16F, a->tau) .. libs/volvis_utils/transferfunction1d.cpp:89-130, 319-358;
+ *                                 transferfunction.h:74-82
+ *   TF CPU lookup (Get) ......... transferfunction1d.cpp:132-157
+ *   FD gradient (RGB16F) ........ libs/volvis_utils/utils.cpp:146-284
+ *   Sobel-Feldman gradient ...... libs/volvis_utils/utils.cpp:287-350
+ *   camera ...................... libs/vis_utils/camera.cpp:281-284 (glm 0.9.5 lookAt,
+ *                                 include/glm/gtc/matrix_transform.inl:403-428)
+ *
+ * Parity status: the GLSL shaders cannot execute in this image (Windows/GL-only
+ * app, no headless GL), so this restatement follows them by reading.  Its CPU
+ * table builders are pinned against golden vectors emitted by the reference's own
+ * C++ compiled under oracle/ref (TransferFunction1D, SummedAreaTable3D); the
+ * shader arithmetic itself (GL hardware texture filtering) is "parity unpinned"
+ * at the level of the vendor's fixed-point filter weights — see DESIGN.md §Parity.
+ *
+ * Arithmetic contract ("CVR-SPEC", shared with the HIP kernels):
+ *   - compiled with -ffp-contract=off; every fused multiply-add is an explicit fmaf;
+ *   - division and sqrt are IEEE correctly rounded;
+ *   - exp/pow use the polynomial cvr_expf/cvr_powf below (fma/rint/ldexp only);
+ *   - fp16 storage is emulated with round-to-nearest-even float->half.
+ * With that contract the GPU kernels reproduce this file bit for bit.
+ */
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <cstdio>
+#include <vector>
+#include <algorithm>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORACLE_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// fp16 emulation (GL_R16F / GL_RGBA16F / GL_RGB16F internal formats)
+// ---------------------------------------------------------------------------
+inline uint32_t f2u(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+inline float u2f(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+
+// float -> IEEE binary16, round to nearest even (what a GL driver does when it
+// converts GL_FLOAT client data to a 16F internal format).
+uint16_t float_to_half(float f) {
+  uint32_t x = f2u(f);
+  uint32_t sign = (x >> 16) & 0x8000u;
+  uint32_t absx = x & 0x7fffffffu;
+  if (absx >= 0x7f800000u) {                 // inf / nan
+    return (uint16_t)(sign | 0x7c00u | (absx > 0x7f800000u ? 0x200u : 0u));
+  }
+  if (absx >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // rounds to inf
+  if (absx < 0x38800000u) {                  // half subnormal or zero
+    if (absx < 0x33000000u) return (uint16_t)sign;             // < 2^-25 -> 0
+    uint32_t mant = (absx & 0x7fffffu) | 0x800000u;
+    int e = (int)(absx >> 23);               // 102..112
+    int shift = 126 - e;                     // 14..24
+    uint32_t hm = mant >> shift;
+    uint32_t rem = mant & ((1u << shift) - 1u);
+    uint32_t halfway = 1u << (shift - 1);
+    if (rem > halfway || (rem == halfway && (hm & 1u))) hm++;
+    return (uint16_t)(sign | hm);
+  }
+  uint32_t e = (absx >> 23) - 112u;          // rebias 127 -> 15
+  uint32_t m = absx & 0x7fffffu;
+  uint32_t h = (e << 10) | (m >> 13);
+  uint32_t rem = m & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+  return (uint16_t)(sign | h);
+}
+
+float half_to_float(uint16_t h) {
+  uint32_t sign = ((uint32_t)h & 0x8000u) << 16;
+  uint32_t e = (h >> 10) & 0x1fu;
+  uint32_t m = h & 0x3ffu;
+  if (e == 0) {
+    if (m == 0) return u2f(sign);
+    float v = (float)m * 5.9604644775390625e-8f;   // m * 2^-24, exact
+    return sign ? -v : v;
+  }
+  if (e == 31) return u2f(sign | 0x7f800000u | (m << 13));
+  return u2f(sign | ((e + 112u) << 23) | (m << 13));
+}
+
+inline float q16(float f) { return half_to_float(float_to_half(f)); }
+
+// ---------------------------------------------------------------------------
+// CVR-SPEC math helpers
+// ---------------------------------------------------------------------------
+struct v3 { float x, y, z; };
+inline v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+inline float dot3(v3 a, v3 b) { return std::fmaf(a.z, b.z, std::fmaf(a.y, b.y, a.x * b.x)); }
+inline v3 normalize3(v3 v) {
+  float inv = 1.0f / std::sqrt(dot3(v, v));
+  return mk(v.x * inv, v.y * inv, v.z * inv);
+}
+inline float lerpf(float a, float b, float t) { return std::fmaf(t, b - a, a); }
+
+// exp(x): Cody-Waite reduction + degree-6 polynomial (Cephes expf coefficients).
+float cvr_expf(float x) {
+  if (x != x) return x;
+  if (x < -86.0f) return 0.0f;
+  if (x > 88.5f) return INFINITY;
+  float n = std::rint(x * 1.44269504088896341f);
+  float r = std::fmaf(n, -0.693359375f, x);
+  r = std::fmaf(n, 2.12194440e-4f, r);
+  float p = 1.9875691500e-4f;
+  p = std::fmaf(p, r, 1.3981999507e-3f);
+  p = std::fmaf(p, r, 8.3334519073e-3f);
+  p = std::fmaf(p, r, 4.1665795894e-2f);
+  p = std::fmaf(p, r, 1.6666665459e-1f);
+  p = std::fmaf(p, r, 5.0000001201e-1f);
+  float r2 = r * r;
+  float y = std::fmaf(p, r2, r) + 1.0f;
+  return std::ldexp(y, (int)n);
+}
+
+// pow(x, y) for x >= 0: exp(y * ln x), ln by Cephes logf polynomial.
+float cvr_powf(float x, float y) {
+  if (x != x || y != y) return x + y;
+  if (!(x > 0.0f) || x < 1.17549435e-38f) {
+    if (y > 0.0f) return 0.0f;
+    if (y == 0.0f) return 1.0f;
+    return INFINITY;
+  }
+  if (x == INFINITY) return y > 0.0f ? INFINITY : (y == 0.0f ? 1.0f : 0.0f);
+  uint32_t bits = f2u(x);
+  int e = (int)((bits >> 23) & 0xffu) - 126;
+  float m = u2f((bits & 0x007fffffu) | 0x3f000000u);       // [0.5, 1)
+  if (m < 0.70710678118654752f) { m = m + m; e = e - 1; }
+  float f = m - 1.0f;
+  float z = f * f;
+  float p = 7.0376836292e-2f;
+  p = std::fmaf(p, f, -1.1514610310e-1f);
+  p = std::fmaf(p, f, 1.1676998740e-1f);
+  p = std::fmaf(p, f, -1.2420140846e-1f);
+  p = std::fmaf(p, f, 1.4249322787e-1f);
+  p = std::fmaf(p, f, -1.6668057665e-1f);
+  p = std::fmaf(p, f, 2.0000714765e-1f);
+  p = std::fmaf(p, f, -2.4999993993e-1f);
+  p = std::fmaf(p, f, 3.3333331174e-1f);
+  float r = (p * f) * z;
+  float fe = (float)e;
+  r = std::fmaf(fe, -2.12194440e-4f, r);
+  r = std::fmaf(-0.5f, z, r);
+  float lnx = f + r;
+  lnx = std::fmaf(fe, 0.693359375f, lnx);
+  return cvr_expf(y * lnx);
+}
+
+// ---------------------------------------------------------------------------
+// Camera: glm 0.9.5 lookAt (float), tan(fovy/2) via DEGREE_TO_RADIANS in double
+// ---------------------------------------------------------------------------
+inline v3 cross3(v3 x, v3 y) {   // glm::cross: x.y*y.z - y.y*x.z, ...
+  return mk(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y);
+}
+inline float glm_dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline v3 glm_normalize(v3 v) {
+  float sqr = v.x * v.x + v.y * v.y + v.z * v.z;
+  float inv = 1.0f / std::sqrt(sqr);
+  return mk(v.x * inv, v.y * inv, v.z * inv);
+}
+
+}  // namespace
+
+// ===========================================================================
+// Exported oracle API
+// ===========================================================================
+
+ORACLE_API float oracle_q16(float f) { return q16(f); }
+ORACLE_API uint16_t oracle_float_to_half(float f) { return float_to_half(f); }
+ORACLE_API float oracle_half_to_float(uint16_t h) { return half_to_float(h); }
+ORACLE_API float oracle_expf(float x) { return cvr_expf(x); }
+ORACLE_API float oracle_powf(float x, float y) { return cvr_powf(x, y); }
+
+// glm::lookAt (column-major, out[col*4+row]) and tan(fovy/2).
+ORACLE_API void oracle_lookat(const float eye_[3], const float center_[3], const float up_[3],
+                              float fovy_deg, float out_view[16], float* out_tan) {
+  v3 eye = mk(eye_[0], eye_[1], eye_[2]);
+  v3 center = mk(center_[0], center_[1], center_[2]);
+  v3 up = mk(up_[0], up_[1], up_[2]);
+  v3 f = glm_normalize(mk(center.x - eye.x, center.y - eye.y, center.z - eye.z));
+  v3 s = glm_normalize(cross3(f, up));
+  v3 u = cross3(s, f);
+  float R[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  R[0 * 4 + 0] = s.x; R[1 * 4 + 0] = s.y; R[2 * 4 + 0] = s.z;
+  R[0 * 4 + 1] = u.x; R[1 * 4 + 1] = u.y; R[2 * 4 + 1] = u.z;
+  R[0 * 4 + 2] = -f.x; R[1 * 4 + 2] = -f.y; R[2 * 4 + 2] = -f.z;
+  R[3 * 4 + 0] = -glm_dot(s, eye);
+  R[3 * 4 + 1] = -glm_dot(u, eye);
+  R[3 * 4 + 2] = glm_dot(f, eye);
+  std::memcpy(out_view, R, sizeof(R));
+  // (float)tan(DEGREE_TO_RADIANS(fovy) / 2.0), rc1prenderer.cpp:97, math_utils/utils.h:13
+  double rad = (double)fovy_deg * (3.14159265358979323846264338327950288 / 180.0);
+  *out_tan = (float)std::tan(rad / 2.0);
+}
+
+// Default integration step (rc1prenderer.cpp:62-63).
+ORACLE_API float oracle_default_step(const float scale[3]) {
+  double sx = scale[0], sy = scale[1], sz = scale[2];
+  return (float)((0.5f / std::sqrt(3.0f)) * std::sqrt(sx * sx + sy * sy + sz * sz));
+}
+
+// TransferFunction1D::BuildLinear (transferfunction1d.cpp:319-358) into a
+// double table of (max_density+1) x 4, zero where no control segment covers
+// an isovalue (glm 0.9.5 zero-initialises dvec4).
+ORACLE_API void oracle_tf_build_double(const double* rgb_cp, int n_rgb, const double* a_cp,
+                                       int n_a, int max_density, double* out_table) {
+  int n = max_density + 1;
+  for (int i = 0; i < 4 * n; i++) out_table[i] = 0.0;
+  for (int i = 0; i < n_rgb - 1; i++) {
+    // TransferControlPoint stores its colour as glm::vec4 (float)
+    int i0 = (int)rgb_cp[i * 4 + 3], i1 = (int)rgb_cp[(i + 1) * 4 + 3];
+    float c0[3], c1[3];
+    for (int c = 0; c < 3; c++) { c0[c] = (float)rgb_cp[i * 4 + c]; c1[c] = (float)rgb_cp[(i + 1) * 4 + c]; }
+    double diff[3];
+    for (int c = 0; c < 3; c++) diff[c] = (double)(c1[c] - c0[c]);
+    for (int x = i0; x <= i1; x++) {
+      double k = (double)(x - i0) / (double)(i1 - i0);
+      if (x < 0 || x >= n) continue;
+      for (int c = 0; c < 3; c++) out_table[x * 4 + c] = (double)c0[c] + diff[c] * k;
+    }
+  }
+  for (int i = 0; i < n_a - 1; i++) {
+    int i0 = (int)a_cp[i * 2 + 1], i1 = (int)a_cp[(i + 1) * 2 + 1];
+    float a0 = (float)a_cp[i * 2], a1 = (float)a_cp[(i + 1) * 2];
+    double diff = (double)(a1 - a0);
+    for (int x = i0; x <= i1; x++) {
+      double k = (double)(x - i0) / (double)(i1 - i0);
+      if (x < 0 || x >= n) continue;
+      out_table[x * 4 + 3] = (double)a0 + diff * k;
+    }
+  }
+}
+
+// GenerateTexture_1D_RGBt (transferfunction1d.cpp:89-118): rgb as float,
+// alpha -> extinction tau = log(1/(1-a)) (transferfunction.h:79-82) unless the
+// TF already holds extinction; the GL upload rounds to RGBA16F.
+ORACLE_API void oracle_tf_rgbt(const double* table, int n, int extinction_input, int round16,
+                               float* out_rgbt) {
+  for (int i = 0; i < n; i++) {
+    float r = (float)table[i * 4 + 0], g = (float)table[i * 4 + 1], b = (float)table[i * 4 + 2];
+    float v4 = (float)table[i * 4 + 3];
+    if (!extinction_input) v4 = (float)std::log(1.0 / (1.0 - (double)v4));
+    float o[4] = {r, g, b, v4};
+    for (int c = 0; c < 4; c++) out_rgbt[i * 4 + c] = round16 ? q16(o[c]) : o[c];
+  }
+}
+
+// TransferFunction1D::Get(value, max) (transferfunction1d.cpp:132-157): the
+// CPU mapping used by the EBS SAT build (no half-texel skew).
+ORACLE_API void oracle_tf_get(const double* table, int max_density, double value,
+                              double max_data_value, float out[4]) {
+  if (max_data_value >= 0) value = value * ((double)max_density / max_data_value);
+  if (value < 0.0f || value > (float)max_density) { out[0] = out[1] = out[2] = out[3] = 0; return; }
+  if (std::fabs(value - (float)max_density) < 0.000001) {
+    for (int c = 0; c < 4; c++) out[c] = (float)table[max_density * 4 + c];
+    return;
+  }
+  int iv = (int)value;
+  double t = value - iv;
+  for (int c = 0; c < 4; c++) out[c] = (float)((1.0 - t) * table[iv * 4 + c] + t * table[(iv + 1) * 4 + c]);
+}
+
+// GetNormalizedSample (structuredgridvolume.cpp:121-151) -> (GLfloat) ->
+// GL_R16F (utils.cpp:20-56).  out[i] = float value of the stored half.
+ORACLE_API void oracle_volume_r16f(const void* voxels, int bytes_per_voxel, int64_t count,
+                                   float* out) {
+  if (bytes_per_voxel == 1) {
+    const uint8_t* v = (const uint8_t*)voxels;
+    for (int64_t i = 0; i < count; i++) out[i] = q16((float)((double)v[i] / (256.0 - 1.0)));
+  } else {
+    const uint16_t* v = (const uint16_t*)voxels;
+    for (int64_t i = 0; i < count; i++) out[i] = q16((float)((double)v[i] / (65536.0 - 1.0)));
+  }
+}
+
+namespace {
+inline double norm_sample(const void* vox, int bpv, int w, int h, int d, int x, int y, int z) {
+  if (x < 0 || y < 0 || z < 0 || x >= w || y >= h || z >= d) return 0.0;
+  int64_t i = (int64_t)x + (int64_t)y * w + (int64_t)z * w * h;
+  if (bpv == 1) return (double)((const uint8_t*)vox)[i] / (256.0 - 1.0);
+  return (double)((const uint16_t*)vox)[i] / (65536.0 - 1.0);
+}
+}  // namespace
+
+// GenerateGradientTexture with its defaults (gradient_sample_size 1, no filter,
+// normalised; utils.cpp:146-190, 245-284): xyz per voxel, RGB16F-rounded.
+ORACLE_API void oracle_gradient_fd(const void* vox, int bpv, int w, int h, int d, float* out_xyz) {
+#pragma omp parallel for schedule(static)
+  for (int z = 0; z < d; z++)
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++) {
+        double gx = norm_sample(vox, bpv, w, h, d, x + 1, y, z) - norm_sample(vox, bpv, w, h, d, x - 1, y, z);
+        double gy = norm_sample(vox, bpv, w, h, d, x, y + 1, z) - norm_sample(vox, bpv, w, h, d, x, y - 1, z);
+        double gz = norm_sample(vox, bpv, w, h, d, x, y, z + 1) - norm_sample(vox, bpv, w, h, d, x, y, z - 1);
+        // glm::normalize<double>: v * inversesqrt(dot(v,v)), inversesqrt = 1/sqrt
+        double sqr = gx * gx + gy * gy + gz * gz;
+        double inv = 1.0 / std::sqrt(sqr);
+        gx *= inv; gy *= inv; gz *= inv;
+        if (gx != gx) { gx = gy = gz = 0.0; }
+        int64_t i = ((int64_t)z * h + y) * w + x;
+        out_xyz[i * 3 + 0] = q16((float)gx);
+        out_xyz[i * 3 + 1] = q16((float)gy);
+        out_xyz[i * 3 + 2] = q16((float)gz);
+      }
+}
+
+// GenerateSobelFeldmanGradientTexture (utils.cpp:287-350), unnormalised, RGB16F.
+ORACLE_API void oracle_gradient_sobel(const void* vox, int bpv, int w, int h, int d, float* out_xyz) {
+#pragma omp parallel for schedule(static)
+  for (int z = 0; z < d; z++)
+    for (int y = 0; y < h; y++)
+      for (int x = 0; x < w; x++) {
+        double sx = 0, sy = 0, sz = 0;
+        for (int v1 = -1; v1 <= 1; v1++)
+          for (int v2 = -1; v2 <= 1; v2++) {
+            double wgt = std::pow(2.0, std::abs(v1) + std::abs(v2));
+            sz += norm_sample(vox, bpv, w, h, d, x + v1, y + v2, z - 1) * (4.0 / wgt)
+                + norm_sample(vox, bpv, w, h, d, x + v1, y + v2, z + 1) * (-4.0 / wgt);
+            sy += norm_sample(vox, bpv, w, h, d, x + v1, y - 1, z + v2) * (4.0 / wgt)
+                + norm_sample(vox, bpv, w, h, d, x + v1, y + 1, z + v2) * (-4.0 / wgt);
+            sx += norm_sample(vox, bpv, w, h, d, x - 1, y + v2, z + v1) * (4.0 / wgt)
+                + norm_sample(vox, bpv, w, h, d, x + 1, y + v2, z + v1) * (-4.0 / wgt);
+          }
+        int64_t i = ((int64_t)z * h + y) * w + x;
+        out_xyz[i * 3 + 0] = q16((float)sx);
+        out_xyz[i * 3 + 1] = q16((float)sy);
+        out_xyz[i * 3 + 2] = q16((float)sz);
+      }
+}
+
+// ---------------------------------------------------------------------------
+// rc1pass ray-march
+// ---------------------------------------------------------------------------
+struct OracleRc1pass {
+  // volume (float values of the stored halves), x-fastest
+  const float* vol; int N[3]; float scale[3];
+  const float* tf; int tf_n;           // tf_n x (r,g,b,tau), half-rounded
+  const float* grad;                   // N voxels x 3, or null
+  // camera
+  float eye[3], center[3], up[3], fovy_deg, aspect;
+  int W, H;
+  float step;
+  int phong; float ka, kd, ks, shininess; float ispec[3]; float light[3];
+};
+
+namespace {
+
+struct Tex {
+  const float* v; int N[3]; int comps;
+  // trilinear, clamp-to-edge, texel-centre convention; x,y,z already in texel space
+  inline void sample(float x, float y, float z, float* out) const {
+    float cx = std::fmin(std::fmax(x, -1.0f), (float)(N[0] - 1));
+    float cy = std::fmin(std::fmax(y, -1.0f), (float)(N[1] - 1));
+    float cz = std::fmin(std::fmax(z, -1.0f), (float)(N[2] - 1));
+    float flx = std::floor(cx), fly = std::floor(cy), flz = std::floor(cz);
+    float ax = cx - flx, ay = cy - fly, az = cz - flz;
+    int ix = (int)flx, iy = (int)fly, iz = (int)flz;
+    int x0 = std::max(ix, 0), x1 = std::min(ix + 1, N[0] - 1);
+    int y0 = std::max(iy, 0), y1 = std::min(iy + 1, N[1] - 1);
+    int z0 = std::max(iz, 0), z1 = std::min(iz + 1, N[2] - 1);
+    auto at = [&](int i, int j, int k, int c) {
+      return v[(((int64_t)k * N[1] + j) * N[0] + i) * comps + c];
+    };
+    for (int c = 0; c < comps; c++) {
+      float c00 = lerpf(at(x0, y0, z0, c), at(x1, y0, z0, c), ax);
+      float c10 = lerpf(at(x0, y1, z0, c), at(x1, y1, z0, c), ax);
+      float c01 = lerpf(at(x0, y0, z1, c), at(x1, y0, z1, c), ax);
+      float c11 = lerpf(at(x0, y1, z1, c), at(x1, y1, z1, c), ax);
+      float c0 = lerpf(c00, c10, ay);
+      float c1 = lerpf(c01, c11, ay);
+      out[c] = lerpf(c0, c1, az);
+    }
+  }
+};
+
+// texture(TexTransferFunc, density): 1D linear, clamp-to-edge, x = u*n - 0.5
+inline void tf_lookup(const float* tf, int n, float density, float out[4]) {
+  float x = std::fmaf(density, (float)n, -0.5f);
+  x = std::fmin(std::fmax(x, -1.0f), (float)(n - 1));
+  float fl = std::floor(x);
+  float a = x - fl;
+  int i = (int)fl;
+  int i0 = std::max(i, 0), i1 = std::min(i + 1, n - 1);
+  for (int c = 0; c < 4; c++) out[c] = lerpf(tf[i0 * 4 + c], tf[i1 * 4 + c], a);
+}
+
+}  // namespace
+
+// Renders rows [y0, y1) of the full frame.  out: W*H*4 floats, counts: W*H.
+static void rc1pass_rows(const OracleRc1pass& P, int y0, int y1, float* out, uint32_t* counts,
+                         int nthreads) {
+  float V[16], tanf;
+  oracle_lookat(P.eye, P.center, P.up, P.fovy_deg, V, &tanf);
+  const float aspect = P.aspect > 0 ? P.aspect : (float)P.W / (float)P.H;
+  const v3 eye = mk(P.eye[0], P.eye[1], P.eye[2]);
+  // VolumeGridSize = resolution * voxel size (rc1prenderer.cpp:233-241)
+  const v3 G = mk((float)P.N[0] * P.scale[0], (float)P.N[1] * P.scale[1], (float)P.N[2] * P.scale[2]);
+  const v3 half = mk(G.x * 0.5f, G.y * 0.5f, G.z * 0.5f);
+  const v3 NoG = mk((float)P.N[0] / G.x, (float)P.N[1] / G.y, (float)P.N[2] / G.z);
+  const v3 light = mk(P.light[0], P.light[1], P.light[2]);
+  Tex vol{P.vol, {P.N[0], P.N[1], P.N[2]}, 1};
+  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3};
+  const float step = P.step;
+  const int W = P.W, H = P.H;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int py = y0; py < y1; py++) {
+    for (int px = 0; px < W; px++) {
+      int64_t pix = (int64_t)py * W + px;
+      float dst[4] = {0, 0, 0, 0};
+      uint32_t cnt = 0;
+      // ray generation (ray_marching_1p.comp:93-99)
+      float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+      float vx = std::fmaf(fx / (float)W, 2.0f, -1.0f);
+      float vy = std::fmaf(fy / (float)H, 2.0f, -1.0f);
+      v3 c = mk((vx * tanf) * aspect, vy * tanf, -1.0f);
+      // vec3 * mat3(View): component j = dot(c, column j)
+      v3 d = mk(dot3(c, mk(V[0], V[1], V[2])), dot3(c, mk(V[4], V[5], V[6])),
+                dot3(c, mk(V[8], V[9], V[10])));
+      v3 dir = normalize3(d);
+      dir = normalize3(dir);   // RayAABBIntersection normalises again (:219)
+      // slab test (ray_bbox_intersection.comp:18-30)
+      v3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+      v3 ta = mk(inv.x * (-half.x - eye.x), inv.y * (-half.y - eye.y), inv.z * (-half.z - eye.z));
+      v3 tb = mk(inv.x * (half.x - eye.x), inv.y * (half.y - eye.y), inv.z * (half.z - eye.z));
+      float tnear = std::fmax(std::fmax(std::fmin(ta.x, tb.x), std::fmin(ta.y, tb.y)), std::fmin(ta.z, tb.z));
+      float tfar = std::fmin(std::fmin(std::fmax(ta.x, tb.x), std::fmax(ta.y, tb.y)), std::fmax(ta.z, tb.z));
+      bool hit = tfar > tnear;
+      tnear = std::fmax(tnear, 0.0f);
+      if (hit) {
+        float D = std::fabs(tfar - tnear);
+        v3 tpos = mk(std::fmaf(dir.x, tnear, eye.x) + half.x, std::fmaf(dir.y, tnear, eye.y) + half.y,
+                     std::fmaf(dir.z, tnear, eye.z) + half.z);
+        // texel-space ray: x_tex = (p / G) * N - 0.5 = p * (N/G) - 0.5
+        v3 o = mk(std::fmaf(tpos.x, NoG.x, -0.5f), std::fmaf(tpos.y, NoG.y, -0.5f), std::fmaf(tpos.z, NoG.z, -0.5f));
+        v3 dt = mk(dir.x * NoG.x, dir.y * NoG.y, dir.z * NoG.z);
+        float s = 0.0f;
+        while (s < D) {
+          float h = std::fmin(step, D - s);
+          float t = std::fmaf(h, 0.5f, s);
+          float x = std::fmaf(dt.x, t, o.x), y = std::fmaf(dt.y, t, o.y), z = std::fmaf(dt.z, t, o.z);
+          float dens;
+          vol.sample(x, y, z, &dens);
+          float src[4];
+          tf_lookup(P.tf, P.tf_n, dens, src);
+          cnt++;
+          if (src[3] > 0.0f) {
+            if (P.phong && P.grad) {
+              float g[3];
+              grd.sample(x, y, z, g);
+              if (g[0] != 0.0f || g[1] != 0.0f || g[2] != 0.0f) {
+                // world position of the sample: Tpos - G/2 (ray_marching_1p.comp:56)
+                v3 wp = mk(std::fmaf(dir.x, t, tpos.x) - half.x, std::fmaf(dir.y, t, tpos.y) - half.y,
+                           std::fmaf(dir.z, t, tpos.z) - half.z);
+                v3 n = normalize3(mk(g[0], g[1], g[2]));
+                v3 L = normalize3(mk(light.x - wp.x, light.y - wp.y, light.z - wp.z));
+                v3 Ve = normalize3(mk(eye.x - wp.x, eye.y - wp.y, eye.z - wp.z));
+                v3 Hv = normalize3(mk(Ve.x + L.x, Ve.y + L.y, Ve.z + L.z));
+                float dd = std::fmax(0.0f, dot3(n, L));
+                float ds = std::fmax(0.0f, dot3(Hv, n));
+                float pw = cvr_powf(ds, P.shininess);
+                float f = std::fmaf(P.kd, dd, P.ka);
+                for (int k = 0; k < 3; k++) src[k] = std::fmaf(P.ispec[k] * P.ks, pw, src[k] * f);
+              }
+            }
+            float a = 1.0f - cvr_expf(-(src[3] * h));
+            float om = 1.0f - dst[3];
+            dst[0] = std::fmaf(om, src[0] * a, dst[0]);
+            dst[1] = std::fmaf(om, src[1] * a, dst[1]);
+            dst[2] = std::fmaf(om, src[2] * a, dst[2]);
+            dst[3] = std::fmaf(om, a, dst[3]);
+            if (dst[3] > 0.99f) break;
+          }
+          s = s + h;
+        }
+      }
+      if (out) for (int k = 0; k < 4; k++) out[pix * 4 + k] = dst[k];
+      if (counts) counts[pix] = cnt;
+    }
+  }
+}
+
+// Full-frame render. Returns the total iteration count S.
+ORACLE_API uint64_t oracle_render_rc1pass(const OracleRc1pass* P, float* out_rgba,
+                                          uint32_t* out_counts, int nthreads) {
+  std::vector<uint32_t> tmp;
+  uint32_t* counts = out_counts;
+  if (!counts) { tmp.resize((size_t)P->W * P->H); counts = tmp.data(); }
+  rc1pass_rows(*P, 0, P->H, out_rgba, counts, nthreads);
+  uint64_t total = 0;
+  for (int64_t i = 0; i < (int64_t)P->W * P->H; i++) total += counts[i];
+  return total;
+}
+
+// Bounded-sample render for the CPU baseline: rows [y0, y1) only.
+ORACLE_API uint64_t oracle_render_rc1pass_rows(const OracleRc1pass* P, int y0, int y1,
+                                               float* out_rgba, uint32_t* out_counts, int nthreads) {
+  rc1pass_rows(*P, y0, y1, out_rgba, out_counts, nthreads);
+  uint64_t total = 0;
+  for (int64_t i = (int64_t)y0 * P->W; i < (int64_t)y1 * P->W; i++) total += out_counts[i];
+  return total;
+}
+
+ORACLE_API int oracle_num_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}

@@ -1,0 +1,173 @@
+"""ctypes wrapper of oracle/build/liboracle.so — the CPU restatement of the
+reference's rc1pass path (see cvr_oracle.cpp for the file:line map).
+TEST INFRASTRUCTURE ONLY."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+_lib = None
+
+
+class OracleRc1pass(ctypes.Structure):
+    _fields_ = [("vol", ctypes.c_void_p), ("N", ctypes.c_int * 3), ("scale", ctypes.c_float * 3),
+                ("tf", ctypes.c_void_p), ("tf_n", ctypes.c_int), ("grad", ctypes.c_void_p),
+                ("eye", ctypes.c_float * 3), ("center", ctypes.c_float * 3),
+                ("up", ctypes.c_float * 3), ("fovy_deg", ctypes.c_float),
+                ("aspect", ctypes.c_float), ("W", ctypes.c_int), ("H", ctypes.c_int),
+                ("step", ctypes.c_float), ("phong", ctypes.c_int), ("ka", ctypes.c_float),
+                ("kd", ctypes.c_float), ("ks", ctypes.c_float), ("shininess", ctypes.c_float),
+                ("ispec", ctypes.c_float * 3), ("light", ctypes.c_float * 3)]
+
+
+def build() -> None:
+    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        F, P, I = ctypes.c_float, ctypes.c_void_p, ctypes.c_int
+        L.oracle_q16.argtypes, L.oracle_q16.restype = [F], F
+        L.oracle_expf.argtypes, L.oracle_expf.restype = [F], F
+        L.oracle_powf.argtypes, L.oracle_powf.restype = [F, F], F
+        L.oracle_lookat.argtypes = [P, P, P, F, P, P]
+        L.oracle_default_step.argtypes, L.oracle_default_step.restype = [P], F
+        L.oracle_tf_build_double.argtypes = [P, I, P, I, I, P]
+        L.oracle_tf_rgbt.argtypes = [P, I, I, I, P]
+        L.oracle_tf_get.argtypes = [P, I, ctypes.c_double, ctypes.c_double, P]
+        L.oracle_volume_r16f.argtypes = [P, I, ctypes.c_int64, P]
+        L.oracle_gradient_fd.argtypes = [P, I, I, I, I, P]
+        L.oracle_gradient_sobel.argtypes = [P, I, I, I, I, P]
+        L.oracle_render_rc1pass.argtypes = [ctypes.POINTER(OracleRc1pass), P, P, I]
+        L.oracle_render_rc1pass.restype = ctypes.c_uint64
+        L.oracle_render_rc1pass_rows.argtypes = [ctypes.POINTER(OracleRc1pass), I, I, P, P, I]
+        L.oracle_render_rc1pass_rows.restype = ctypes.c_uint64
+        L.oracle_num_threads.restype = I
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data
+
+
+def q16(x: float) -> float:
+    return lib().oracle_q16(x)
+
+
+def expf(x: float) -> float:
+    return lib().oracle_expf(x)
+
+
+def powf(x: float, y: float) -> float:
+    return lib().oracle_powf(x, y)
+
+
+def lookat(eye, center, up, fovy_deg=45.0):
+    e = np.asarray(eye, np.float32); c = np.asarray(center, np.float32)
+    u = np.asarray(up, np.float32)
+    out = np.zeros(16, np.float32); t = np.zeros(1, np.float32)
+    lib().oracle_lookat(_p(e), _p(c), _p(u), fovy_deg, _p(out), _p(t))
+    return out, float(t[0])
+
+
+def default_step(scale) -> float:
+    s = np.asarray(scale, np.float32)
+    return float(lib().oracle_default_step(_p(s)))
+
+
+def tf_table_double(rgb_cp, alpha_cp, max_density=255) -> np.ndarray:
+    rgb = np.ascontiguousarray(np.asarray(rgb_cp, np.float64).reshape(-1, 4))
+    a = np.ascontiguousarray(np.asarray(alpha_cp, np.float64).reshape(-1, 2))
+    out = np.zeros((max_density + 1, 4), np.float64)
+    lib().oracle_tf_build_double(_p(rgb), rgb.shape[0], _p(a), a.shape[0], max_density, _p(out))
+    return out
+
+
+def tf_rgbt(table: np.ndarray, extinction_input=False, round16=True) -> np.ndarray:
+    t = np.ascontiguousarray(table, np.float64)
+    out = np.zeros((t.shape[0], 4), np.float32)
+    lib().oracle_tf_rgbt(_p(t), t.shape[0], int(extinction_input), int(round16), _p(out))
+    return out
+
+
+def tf_get(table: np.ndarray, value: float, max_data_value: float = -1.0) -> np.ndarray:
+    t = np.ascontiguousarray(table, np.float64)
+    out = np.zeros(4, np.float32)
+    lib().oracle_tf_get(_p(t), t.shape[0] - 1, value, max_data_value, _p(out))
+    return out
+
+
+def volume_r16f(vox: np.ndarray) -> np.ndarray:
+    v = np.ascontiguousarray(vox)
+    out = np.empty(v.shape, np.float32)
+    lib().oracle_volume_r16f(_p(v), v.dtype.itemsize, v.size, _p(out))
+    return out
+
+
+def gradient(vox: np.ndarray, mode: str = "fd") -> np.ndarray:
+    v = np.ascontiguousarray(vox)
+    d, h, w = v.shape
+    out = np.empty((d, h, w, 3), np.float32)
+    fn = lib().oracle_gradient_fd if mode == "fd" else lib().oracle_gradient_sobel
+    fn(_p(v), v.dtype.itemsize, w, h, d, _p(out))
+    return out
+
+
+def _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shininess, ispec,
+            light, aspect=0.0):
+    P = OracleRc1pass()
+    d, h, w = vol16.shape
+    P.vol = _p(vol16)
+    P.N[:] = [w, h, d]
+    P.scale[:] = [float(s) for s in scale]
+    P.tf = _p(tf)
+    P.tf_n = tf.shape[0]
+    P.grad = _p(grad) if grad is not None else None
+    P.eye[:] = [float(v) for v in camera["eye"]]
+    P.center[:] = [float(v) for v in camera["center"]]
+    P.up[:] = [float(v) for v in camera["up"]]
+    P.fovy_deg = float(camera.get("fovy_deg", 45.0))
+    P.aspect = float(aspect)
+    P.W, P.H = int(W), int(H)
+    P.step = float(step)
+    P.phong = int(phong)
+    P.ka, P.kd, P.ks, P.shininess = ka, kd, ks, shininess
+    P.ispec[:] = [float(v) for v in ispec]
+    P.light[:] = [float(v) for v in light]
+    return P
+
+
+def render_rc1pass(vol16: np.ndarray, scale, tf: np.ndarray, camera: dict, W: int, H: int,
+                   step: float, grad: np.ndarray | None = None, phong: bool = False,
+                   ka=0.5, kd=0.5, ks=0.8, shininess=30.0, ispec=(1.0, 1.0, 1.0),
+                   light=(0.0, 0.0, 0.0), threads: int = 0, rows=None):
+    """Full frame (or rows=(y0,y1)) of ray_marching_1p.comp. Returns (rgba HxWx4, counts HxW, S)."""
+    vol16 = np.ascontiguousarray(vol16, np.float32)
+    tf = np.ascontiguousarray(tf, np.float32)
+    if grad is not None:
+        grad = np.ascontiguousarray(grad, np.float32)
+    P = _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shininess, ispec,
+                light)
+    rgba = np.zeros((H, W, 4), np.float32)
+    cnt = np.zeros((H, W), np.uint32)
+    if rows is None:
+        S = lib().oracle_render_rc1pass(ctypes.byref(P), _p(rgba), _p(cnt), int(threads))
+    else:
+        S = lib().oracle_render_rc1pass_rows(ctypes.byref(P), int(rows[0]), int(rows[1]),
+                                             _p(rgba), _p(cnt), int(threads))
+    return rgba, cnt, int(S)
+
+
+def num_threads() -> int:
+    return int(lib().oracle_num_threads())
