@@ -23,7 +23,7 @@ GRADIENT_NONE, GRADIENT_FINITE_DIFFERENCES, GRADIENT_SOBEL_FELDMAN = 0, 1, 2
 # Every symbol include/cvr.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "cvr_abi_version", "cvr_status_string", "cvr_create", "cvr_destroy", "cvr_last_error",
-    "cvr_set_stream", "cvr_synchronize", "cvr_set_volume", "cvr_set_volume_device",
+    "cvr_set_stream", "cvr_set_option", "cvr_get_option", "cvr_synchronize", "cvr_set_volume", "cvr_set_volume_device",
     "cvr_set_transfer_function", "cvr_set_gradient", "cvr_device_bytes", "cvr_tiles_for_rank",
     "cvr_render_rc1pass", "cvr_unpack_tiles_device", "cvr_camera_lookat", "cvr_default_step",
     "cvr_tf1d_build_rgbt", "cvr_read_tf1d", "cvr_read_raw", "cvr_read_syn",
@@ -90,6 +90,8 @@ def lib() -> ctypes.CDLL:
         "cvr_last_error": ([P], ctypes.c_char_p),
         "cvr_set_stream": ([P, P], I),
         "cvr_synchronize": ([P], I),
+        "cvr_set_option": ([P, ctypes.c_char_p, I], I),
+        "cvr_get_option": ([P, ctypes.c_char_p], I),
         "cvr_set_volume": ([P, P, I, I, I, I, FP], I),
         "cvr_set_volume_device": ([P, P, I, I, I, I, FP], I),
         "cvr_set_transfer_function": ([P, FP, I], I),

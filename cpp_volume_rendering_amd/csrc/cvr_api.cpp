@@ -192,6 +192,8 @@ void cvr_destroy(cvr_ctx* ctx) {
   free_dev(c->d_grad);
   p = c->d_total; free_dev(p); c->d_total = nullptr;
   free_dev(c->d_scratch);
+  p = c->d_order; free_dev(p); c->d_order = nullptr;
+  p = c->d_wave_cost; free_dev(p); c->d_wave_cost = nullptr;
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -204,8 +206,34 @@ const char* cvr_last_error(const cvr_ctx* ctx) {
 cvr_status cvr_set_stream(cvr_ctx* ctx, void* stream) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
-  c->stream = stream ? (hipStream_t)stream : c->own_stream;
+  c->stream = (hipStream_t)stream;     // NULL = the legacy default stream
   return CVR_OK;
+}
+
+cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c || !key) return CVR_ERR_ARG;
+  if (!std::strcmp(key, "batch")) {
+    if (value != 1 && value != 2 && value != 4 && value != 8)
+      return fail(c, CVR_ERR_ARG, "batch must be 1, 2, 4 or 8");
+    c->batch = value;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "tile_order")) {
+    if (value < 0 || value > 2) return fail(c, CVR_ERR_ARG, "tile_order must be 0, 1 or 2");
+    c->use_order = value;
+    c->order_valid = 0;
+    return CVR_OK;
+  }
+  return fail(c, CVR_ERR_ARG, "unknown option '%s'", key);
+}
+
+int cvr_get_option(const cvr_ctx* ctx, const char* key) {
+  const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+  if (!c || !key) return -1;
+  if (!std::strcmp(key, "batch")) return c->batch;
+  if (!std::strcmp(key, "tile_order")) return c->use_order;
+  return -1;
 }
 
 cvr_status cvr_synchronize(cvr_ctx* ctx) {
@@ -412,7 +440,28 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   // device outputs: the kernel ADDS to *total (the caller zeroes it); host
   // outputs: the context's own counter is reset here.
   if (d_total && !o->on_device) HIP_TRY(c, hipMemsetAsync(d_total, 0, sizeof(unsigned long long), s));
-  HIP_TRY(c, cvr::launch_rc1pass(*c, A, phong, d_out, d_samples, d_total, nblocks, s));
+  // Longest-first block order learned from the previous frame (tile_order option).
+  const int* order = nullptr;
+  uint32_t* wave_cost = nullptr;
+  int nseg = c->use_order == 2 ? 8 : 1;
+  if (c->use_order && nblocks % nseg == 0 && nblocks / nseg <= 16384) {
+    if (c->order_len != nblocks) {
+      void* p = c->d_order; free_dev(p); c->d_order = nullptr;
+      p = c->d_wave_cost; free_dev(p); c->d_wave_cost = nullptr;
+      c->order_len = 0; c->order_valid = 0;
+      HIP_TRY(c, hipMalloc((void**)&c->d_order, (size_t)nblocks * sizeof(int)));
+      HIP_TRY(c, hipMalloc((void**)&c->d_wave_cost, (size_t)nblocks * 4 * sizeof(uint32_t)));
+      c->order_len = nblocks;
+    }
+    order = c->order_valid ? c->d_order : nullptr;
+    wave_cost = c->d_wave_cost;
+  }
+  HIP_TRY(c, cvr::launch_rc1pass(*c, A, phong, d_out, d_samples, d_total, order, wave_cost,
+                                 nblocks, s));
+  if (wave_cost) {
+    HIP_TRY(c, cvr::launch_tile_order(wave_cost, nblocks, nseg, c->d_order, s));
+    c->order_valid = 1;
+  }
   if (!o->on_device) {
     HIP_TRY(c, hipMemcpyAsync(o->rgba, d_out, rgba_bytes, hipMemcpyDeviceToHost, s));
     if (o->samples) HIP_TRY(c, hipMemcpyAsync(o->samples, d_samples, smp_bytes, hipMemcpyDeviceToHost, s));

@@ -69,6 +69,13 @@ struct Ctx {
   void* d_grad = nullptr;
   size_t grad_bytes = 0;
   int grad_mode = 0;
+  // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
+  int batch = 4;
+  int use_order = 0;              // 0 off, 1 global LPT, 2 LPT per XCD band
+  int* d_order = nullptr;          // block permutation for the next frame
+  uint32_t* d_wave_cost = nullptr; // per-wave max iterations of the last frame
+  int order_len = 0;               // nblocks the buffers are sized for
+  int order_valid = 0;             // d_order holds a permutation for order_len blocks
   // scratch
   unsigned long long* d_total = nullptr;
   void* d_scratch = nullptr;      // host-output staging
@@ -80,8 +87,10 @@ hipError_t launch_build_cells_impl(const void* vox, int bpv, const uint16_t* lut
                                    const CellGrid& g, void* cells, hipStream_t s);
 hipError_t launch_gradient(const Ctx& c, int mode, hipStream_t s);
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
-                          uint32_t* samples, unsigned long long* total, int nwavetiles,
-                          hipStream_t s);
+                          uint32_t* samples, unsigned long long* total, const int* order,
+                          uint32_t* wave_cost, int nblocks, hipStream_t s);
+hipError_t launch_tile_order(const uint32_t* wave_cost, int nblocks, int nseg, int* order,
+                             hipStream_t s);
 hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
                                int nranks, int tiles_per_rank_max, hipStream_t s);
 

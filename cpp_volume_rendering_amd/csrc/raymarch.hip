@@ -185,7 +185,27 @@ __device__ __forceinline__ float4 tf_lookup(const float4* __restrict__ tf, int n
 
 constexpr int kMaxTfLds = 4096;
 
-// Pixel assignment of lane `lane` in wave `wave` of (remapped) block `L`.
+// Branch-free CVR-SPEC exp: same values as cvr_expf (selects instead of the
+// early returns, so a wave never splits on the special cases).
+__device__ __forceinline__ float cvr_expf_nb(float x) {
+  float xc = fminf(fmaxf(x, -86.0f), 88.5f);
+  float n = rintf(xc * 1.44269504088896341f);
+  float r = fmaf(n, -0.693359375f, xc);
+  r = fmaf(n, 2.12194440e-4f, r);
+  float p = 1.9875691500e-4f;
+  p = fmaf(p, r, 1.3981999507e-3f);
+  p = fmaf(p, r, 8.3334519073e-3f);
+  p = fmaf(p, r, 4.1665795894e-2f);
+  p = fmaf(p, r, 1.6666665459e-1f);
+  p = fmaf(p, r, 5.0000001201e-1f);
+  float r2 = r * r;
+  float y = ldexpf(fmaf(p, r2, r) + 1.0f, (int)n);
+  y = x < -86.0f ? 0.0f : y;
+  y = x > 88.5f ? __builtin_inff() : y;
+  return x != x ? x : y;
+}
+
+// Pixel assignment of lane `lane` in wave `wave` of logical block `L`.
 __device__ __forceinline__ void pixel_of(const Rc1passArgs& A, int L, int wave, int lane, int& px,
                                          int& py, long long& out_idx) {
   int lx = ((wave & 1) << 3) | (lane & 7);
@@ -208,21 +228,91 @@ __device__ __forceinline__ void pixel_of(const Rc1passArgs& A, int L, int wave, 
   }
 }
 
-template <bool PHONG>
+// One sample's cell address + weights (stage 1 of the batched march).
+struct SamplePos { uint32_t idx; float ax, ay, az; int ix, iy, iz; };
+
+__device__ __forceinline__ SamplePos sample_pos(float x, float y, float z, const Rc1passArgs& A,
+                                                uint32_t bxby) {
+  // GL_LINEAR texel-centre convention; positions are inside [-0.5, N-0.5] for
+  // every hit ray, so the CLAMP_TO_EDGE corner clamp is folded into the padded
+  // cell grid (cell = floor(x)+1 in [0, N]; the integer clamp only guards memory).
+  float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+  SamplePos p;
+  p.ax = x - fx; p.ay = y - fy; p.az = z - fz;
+  p.ix = (int)fx; p.iy = (int)fy; p.iz = (int)fz;
+  uint32_t cx = (uint32_t)min(max(p.ix + 1, 0), A.N[0]);
+  uint32_t cy = (uint32_t)min(max(p.iy + 1, 0), A.N[1]);
+  uint32_t cz = (uint32_t)min(max(p.iz + 1, 0), A.N[2]);
+  uint32_t brick = __umul24(cz >> 2, bxby) + __umul24(cy >> 2, (uint32_t)A.cells.bx) + (cx >> 2);
+  p.idx = (brick << 6) | ((cz & 3u) << 4) | ((cy & 3u) << 2) | (cx & 3u);
+  return p;
+}
+
+__device__ __forceinline__ float trilerp_cell(uint4 raw, float ax, float ay, float az) {
+  float v000, v100, v010, v110, v001, v101, v011, v111;
+  h2f2(raw.x, v000, v100);
+  h2f2(raw.y, v010, v110);
+  h2f2(raw.z, v001, v101);
+  h2f2(raw.w, v011, v111);
+  float c00 = lerpf(v000, v100, ax);
+  float c10 = lerpf(v010, v110, ax);
+  float c01 = lerpf(v001, v101, ax);
+  float c11 = lerpf(v011, v111, ax);
+  float c0 = lerpf(c00, c10, ay);
+  float c1 = lerpf(c01, c11, ay);
+  return lerpf(c0, c1, az);
+}
+
+// Blinn-Phong (ray_marching_1p.comp:48-81), CVR-SPEC arithmetic.
+__device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint2* __restrict__ grad,
+                                            const SamplePos& sp, f3 dir, float t, f3 tpos, f3 hg,
+                                            f3 eye, float4& src) {
+  Texel tx;
+  tx.ix = sp.ix; tx.iy = sp.iy; tx.iz = sp.iz;
+  tx.ax = sp.ax; tx.ay = sp.ay; tx.az = sp.az;
+  f3 g = sample_gradient(grad, A.N, tx);
+  if (g.x != 0.0f || g.y != 0.0f || g.z != 0.0f) {
+    f3 wp{fmaf(dir.x, t, tpos.x) - hg.x, fmaf(dir.y, t, tpos.y) - hg.y, fmaf(dir.z, t, tpos.z) - hg.z};
+    f3 n = normalize3(g);
+    f3 Ld = normalize3(f3{A.light[0] - wp.x, A.light[1] - wp.y, A.light[2] - wp.z});
+    f3 Ve = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
+    f3 Hv = normalize3(f3{Ve.x + Ld.x, Ve.y + Ld.y, Ve.z + Ld.z});
+    float dd = fmaxf(0.0f, dot3(n, Ld));
+    float ds = fmaxf(0.0f, dot3(Hv, n));
+    float pw = cvr_powf(ds, A.shininess);
+    float f = fmaf(A.kd, dd, A.ka);
+    src.x = fmaf(A.ispec[0] * A.ks, pw, src.x * f);
+    src.y = fmaf(A.ispec[1] * A.ks, pw, src.y * f);
+    src.z = fmaf(A.ispec[2] * A.ks, pw, src.z * f);
+  }
+}
+
+// The ray-march.  K samples are addressed and fetched per batch (K 16-byte
+// loads in flight per lane), then their densities are classified through the
+// LDS transfer function, then composited front to back in order with the
+// per-lane ERT exit.  The arithmetic per sample is exactly the sequential loop
+// of ray_marching_1p.comp:124-172 (s accumulates h one step at a time).
+template <int K, bool PHONG>
 __global__ void __launch_bounds__(256)
 rc1pass_kernel(Rc1passArgs A, const uint4* __restrict__ cells, const uint2* __restrict__ grad,
                const float4* __restrict__ tf_g, float4* __restrict__ out,
                uint32_t* __restrict__ samples, unsigned long long* __restrict__ total,
-               int nblocks) {
-  extern __shared__ float4 tf[];   // tf_n entries (dynamic LDS, 16-B aligned base)
-  for (int i = threadIdx.x; i < A.tf_n; i += blockDim.x) tf[i] = tf_g[i];
+               const int* __restrict__ order, uint32_t* __restrict__ wave_cost, int nblocks) {
+  // Padded TF: tfp[k] = T[clamp(k-1, 0, n-1)], k in [0, n+1]; a lookup at
+  // x = d*n - 0.5 reads the two adjacent entries tfp[floor(x)+1], tfp[floor(x)+2].
+  extern __shared__ float4 tfp[];
+  const int n = A.tf_n;
+  for (int i = threadIdx.x; i < n + 2; i += blockDim.x) tfp[i] = tf_g[min(max(i - 1, 0), n - 1)];
   __syncthreads();
 
-  // XCD-aware remap: blocks b and b+8 share an XCD, so give XCD (b % 8) the
-  // contiguous range of logical blocks [ (b%8)*nblocks/8, ... ).
-  int b = blockIdx.x;
-  int L = b;
-  if (A.xcd_remap && (nblocks & 7) == 0) L = (b & 7) * (nblocks >> 3) + (b >> 3);
+  // Block -> screen tile: a cost-ordered permutation (longest tiles first) when
+  // given, else an XCD-aware remap (blocks b and b+8 share an XCD; XCD b%8 gets
+  // one contiguous band of logical blocks).
+  const int b = blockIdx.x;
+  int L;
+  if (order) L = order[b];
+  else if (A.xcd_remap && (nblocks & 7) == 0) L = (b & 7) * (nblocks >> 3) + (b >> 3);
+  else L = b;
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -254,48 +344,70 @@ rc1pass_kernel(Rc1passArgs A, const uint4* __restrict__ cells, const uint2* __re
     tnear = fmaxf(tnear, 0.0f);
     if (hit) {
       const float D = fabsf(tfar - tnear);
-      f3 tpos{fmaf(dir.x, tnear, eye.x) + hg.x, fmaf(dir.y, tnear, eye.y) + hg.y,
-              fmaf(dir.z, tnear, eye.z) + hg.z};
-      f3 o{fmaf(tpos.x, A.n_over_g[0], -0.5f), fmaf(tpos.y, A.n_over_g[1], -0.5f),
-           fmaf(tpos.z, A.n_over_g[2], -0.5f)};
-      f3 dt{dir.x * A.n_over_g[0], dir.y * A.n_over_g[1], dir.z * A.n_over_g[2]};
+      const f3 tpos{fmaf(dir.x, tnear, eye.x) + hg.x, fmaf(dir.y, tnear, eye.y) + hg.y,
+                    fmaf(dir.z, tnear, eye.z) + hg.z};
+      const f3 o{fmaf(tpos.x, A.n_over_g[0], -0.5f), fmaf(tpos.y, A.n_over_g[1], -0.5f),
+                 fmaf(tpos.z, A.n_over_g[2], -0.5f)};
+      const f3 dt{dir.x * A.n_over_g[0], dir.y * A.n_over_g[1], dir.z * A.n_over_g[2]};
       const float step = A.step;
+      const uint32_t bxby = (uint32_t)A.cells.bx * (uint32_t)A.cells.by;
+      const float fn = (float)n;
       float s = 0.0f;
-      while (s < D) {
-        float h = fminf(step, D - s);
-        float t = fmaf(h, 0.5f, s);
-        Texel tx = texel(fmaf(dt.x, t, o.x), fmaf(dt.y, t, o.y), fmaf(dt.z, t, o.z), A.nm1);
-        float dens = sample_cells(cells, A.cells, tx);
-        float4 src = tf_lookup(tf, A.tf_n, dens);
-        cnt++;
-        if (src.w > 0.0f) {
-          if (PHONG) {
-            f3 g = sample_gradient(grad, A.N, tx);
-            if (g.x != 0.0f || g.y != 0.0f || g.z != 0.0f) {
-              f3 wp{fmaf(dir.x, t, tpos.x) - hg.x, fmaf(dir.y, t, tpos.y) - hg.y,
-                    fmaf(dir.z, t, tpos.z) - hg.z};
-              f3 n = normalize3(g);
-              f3 Ld = normalize3(f3{A.light[0] - wp.x, A.light[1] - wp.y, A.light[2] - wp.z});
-              f3 Ve = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
-              f3 Hv = normalize3(f3{Ve.x + Ld.x, Ve.y + Ld.y, Ve.z + Ld.z});
-              float dd = fmaxf(0.0f, dot3(n, Ld));
-              float ds = fmaxf(0.0f, dot3(Hv, n));
-              float pw = cvr_powf(ds, A.shininess);
-              float f = fmaf(A.kd, dd, A.ka);
-              src.x = fmaf(A.ispec[0] * A.ks, pw, src.x * f);
-              src.y = fmaf(A.ispec[1] * A.ks, pw, src.y * f);
-              src.z = fmaf(A.ispec[2] * A.ks, pw, src.z * f);
+      bool done = !(s < D);
+      while (!done) {
+        // stage 1: the next K sample positions (sequential s += h) and their loads
+        float hj[K], tj[K];
+        bool vj[K];
+        SamplePos sp[K];
+        uint4 raw[K];
+        float ss = s;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+          vj[j] = ss < D;
+          hj[j] = fminf(step, D - ss);
+          tj[j] = fmaf(hj[j], 0.5f, ss);
+          ss = ss + hj[j];
+          sp[j] = sample_pos(fmaf(dt.x, tj[j], o.x), fmaf(dt.y, tj[j], o.y), fmaf(dt.z, tj[j], o.z),
+                             A, bxby);
+          raw[j] = cells[sp[j].idx];
+        }
+        // stage 2: density and transfer-function classification
+        float4 src[K];
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+          float dens = trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az);
+          float x = fmaf(dens, fn, -0.5f);
+          float fl = floorf(x);
+          float a = x - fl;
+          int i = min(max((int)fl + 1, 0), n);
+          float4 t0 = tfp[i], t1 = tfp[i + 1];
+          src[j] = make_float4(lerpf(t0.x, t1.x, a), lerpf(t0.y, t1.y, a), lerpf(t0.z, t1.z, a),
+                               lerpf(t0.w, t1.w, a));
+        }
+        // stage 3: front-to-back composite + ERT, in sample order
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+          if (!done) {
+            if (!vj[j]) {
+              done = true;
+            } else {
+              cnt++;
+              float4 sc = src[j];
+              if (sc.w > 0.0f) {
+                if (PHONG) shade_phong(A, grad, sp[j], dir, tj[j], tpos, hg, eye, sc);
+                float a = 1.0f - cvr_expf_nb(-(sc.w * hj[j]));
+                float om = 1.0f - dst.w;
+                dst.x = fmaf(om, sc.x * a, dst.x);
+                dst.y = fmaf(om, sc.y * a, dst.y);
+                dst.z = fmaf(om, sc.z * a, dst.z);
+                dst.w = fmaf(om, a, dst.w);
+                if (dst.w > 0.99f) done = true;
+              }
             }
           }
-          float a = 1.0f - cvr_expf(-(src.w * h));
-          float om = 1.0f - dst.w;
-          dst.x = fmaf(om, src.x * a, dst.x);
-          dst.y = fmaf(om, src.y * a, dst.y);
-          dst.z = fmaf(om, src.z * a, dst.z);
-          dst.w = fmaf(om, a, dst.w);
-          if (dst.w > 0.99f) break;
         }
-        s = s + h;
+        s = ss;
+        if (!(s < D)) done = true;
       }
     }
     out[oidx] = dst;   // misses store the cleared (0,0,0,0), renderoutputframe.cpp:187-190
@@ -310,22 +422,94 @@ rc1pass_kernel(Rc1passArgs A, const uint4* __restrict__ cells, const uint2* __re
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if (lane == 0 && v) atomicAdd(total, v);
   }
+  if (wave_cost) {   // the wave's critical path (its longest ray) for the next frame's order
+    uint32_t m = cnt;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+    if (lane == 0) wave_cost[L * 4 + wave] = m;
+  }
+}
+
+// Longest-processing-time-first block order from the previous frame's wave
+// costs: segment s (one workgroup) sorts logical blocks [s*seg, (s+1)*seg) by
+// descending cost (bitonic sort in LDS) and assigns them to physical blocks
+// s, s+nseg, s+2*nseg, ... (nseg = 8: one XCD band per segment; nseg = 1: global).
+__global__ void __launch_bounds__(1024)
+tile_order_kernel(const uint32_t* __restrict__ wave_cost, int nblocks, int nseg,
+                  int* __restrict__ order) {
+  extern __shared__ unsigned long long keys[];
+  const int seg = nblocks / nseg;
+  const int base = blockIdx.x * seg;
+  int P = 1;
+  while (P < seg) P <<= 1;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    unsigned long long k = 0;
+    if (i < seg) {
+      uint32_t L = (uint32_t)(base + i);
+      uint32_t c = wave_cost[L * 4] + wave_cost[L * 4 + 1] + wave_cost[L * 4 + 2] + wave_cost[L * 4 + 3];
+      k = ((unsigned long long)c << 32) | (0xffffffffu - L);
+    }
+    keys[i] = k;
+  }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        int j = i ^ stride;
+        if (j > i) {
+          bool desc = (i & size) == 0;
+          unsigned long long a = keys[i], b = keys[j];
+          if ((a < b) == desc) { keys[i] = b; keys[j] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < seg; i += blockDim.x) {
+    int L = (int)(0xffffffffu - (uint32_t)keys[i]);
+    order[nseg == 1 ? i : (blockIdx.x + nseg * i)] = L;
+  }
+}
+
+hipError_t launch_tile_order(const uint32_t* wave_cost, int nblocks, int nseg, int* order,
+                             hipStream_t s) {
+  if (nblocks % nseg) return hipErrorInvalidValue;
+  int seg = nblocks / nseg, P = 1;
+  while (P < seg) P <<= 1;
+  if (P > 16384) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tile_order_kernel, dim3(nseg), dim3(1024), (size_t)P * 8, s, wave_cost,
+                     nblocks, nseg, order);
+  return hipGetLastError();
+}
+
+template <int K>
+static hipError_t launch_k(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
+                           uint32_t* samples, unsigned long long* total, const int* order,
+                           uint32_t* wave_cost, int nblocks, hipStream_t s) {
+  dim3 grid(nblocks), block(256);
+  size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
+  if (phong)
+    hipLaunchKernelGGL((rc1pass_kernel<K, true>), grid, block, lds, s, a, (const uint4*)c.d_cells,
+                       (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, total, order,
+                       wave_cost, nblocks);
+  else
+    hipLaunchKernelGGL((rc1pass_kernel<K, false>), grid, block, lds, s, a, (const uint4*)c.d_cells,
+                       (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, total, order,
+                       wave_cost, nblocks);
+  return hipGetLastError();
 }
 
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
-                          uint32_t* samples, unsigned long long* total, int nblocks,
-                          hipStream_t s) {
+                          uint32_t* samples, unsigned long long* total, const int* order,
+                          uint32_t* wave_cost, int nblocks, hipStream_t s) {
   if (nblocks <= 0) return hipSuccess;
-  dim3 grid(nblocks), block(256);
-  size_t lds = (size_t)a.tf_n * sizeof(float4);
   if (a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
-  if (phong)
-    hipLaunchKernelGGL(rc1pass_kernel<true>, grid, block, lds, s, a, (const uint4*)c.d_cells,
-                       (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, total, nblocks);
-  else
-    hipLaunchKernelGGL(rc1pass_kernel<false>, grid, block, lds, s, a, (const uint4*)c.d_cells,
-                       (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, total, nblocks);
-  return hipGetLastError();
+  switch (c.batch) {
+    case 1: return launch_k<1>(c, a, phong, out, samples, total, order, wave_cost, nblocks, s);
+    case 2: return launch_k<2>(c, a, phong, out, samples, total, order, wave_cost, nblocks, s);
+    case 8: return launch_k<8>(c, a, phong, out, samples, total, order, wave_cost, nblocks, s);
+    default: return launch_k<4>(c, a, phong, out, samples, total, order, wave_cost, nblocks, s);
+  }
 }
 
 // ---------------------------------------------------------------------------

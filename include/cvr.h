@@ -121,8 +121,15 @@ const char* cvr_status_string(cvr_status s);
 cvr_status  cvr_create(int device, cvr_ctx** out_ctx);
 void        cvr_destroy(cvr_ctx* ctx);
 const char* cvr_last_error(const cvr_ctx* ctx);
-/* Launch stream (a hipStream_t); NULL = the context's own stream. */
+/* Launch stream (a hipStream_t); NULL = the legacy default (null) stream.
+ * A new context starts on a private non-blocking stream of its own. */
 cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
+/* Tuning options (results are identical for every setting):
+ *   "batch"      samples addressed + fetched per batch of the march (1, 2, 4, 8; default 4)
+ *   "tile_order" 1/2: launch screen tiles longest-first using the previous frame's
+ *                per-wave costs (LPT; 2 = within each XCD band); 0: XCD-banded order (default) */
+cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
+int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);
 
 /* Volume: x-fastest voxels (i + j*w + k*w*h), 1 byte (u8) or 2 bytes (u16)

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""A/B timing of rc1pass kernel variants (batch size, tile order) in ONE process,
+interleaved rounds (methodology rule 24).  Every variant's image is checked bit-equal
+to the first variant's.  Usage: python tools/ab_rc1pass.py [--size 512] [--res 1024]"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cpp_volume_rendering_amd import _native as N  # noqa: E402
+from cpp_volume_rendering_amd import datasets as D  # noqa: E402
+from cpp_volume_rendering_amd.renderer import Camera, Device, build_tf_rgbt, make_frame  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--field", default="ml")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--variants", default="b1o0,b2o0,b4o0,b8o0,b4o1,b4o2,b2o1,b2o2")
+    ap.add_argument("--phong", action="store_true")
+    a = ap.parse_args()
+    n, W = a.size, a.res
+    vol = D.marschner_lobb_u8(n) if a.field == "ml" else D.blobs_u8(n)
+    dev = Device(0)
+    dev.set_volume(vol, D.voxel_scale(n))
+    dev.set_transfer_function(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
+    if a.phong:
+        dev.set_gradient(1)
+    s = torch.cuda.Stream()
+    dev.set_stream(s.cuda_stream)
+    frame = make_frame(Camera(**D.INITIAL_STATE_CAMERA), W, W)
+    p = N.Rc1passParams()
+    p.apply_gradient_shading = int(a.phong)
+    p.ka, p.kd, p.ks, p.shininess = 0.5, 0.5, 0.8, 30.0
+    p.ispecular[:] = [1, 1, 1]
+    p.light_pos[:] = list(D.LIGHT_LIST0_POSITION)
+    img = torch.zeros((W, W, 4), dtype=torch.float32, device="cuda")
+    tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out = N.Output(img.data_ptr(), None, tot.data_ptr(), 1)
+    L = N.lib()
+
+    def run(frames):
+        for _ in range(frames):
+            N.check(L.cvr_render_rc1pass(dev.handle, ctypes.byref(frame), ctypes.byref(p),
+                                         ctypes.byref(out)), "render", dev.handle)
+
+    variants = a.variants.split(",")
+    res = {v: [] for v in variants}
+    ref_img = None
+    S = None
+    for rnd in range(a.rounds):
+        for v in variants:
+            b, o = int(v[1:v.index("o")]), int(v[v.index("o") + 1:])
+            N.check(L.cvr_set_option(dev.handle, b"batch", b), "opt")
+            N.check(L.cvr_set_option(dev.handle, b"tile_order", o), "opt")
+            with torch.cuda.stream(s):
+                run(3)   # warm up + learn the order
+                tot.zero_()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                run(a.frames)
+                e1.record(s)
+            s.synchronize()
+            ms = e0.elapsed_time(e1) / a.frames
+            res[v].append(ms)
+            cur = img.cpu().numpy()
+            if ref_img is None:
+                ref_img = cur
+                S = int(tot.item()) // a.frames
+            else:
+                assert np.array_equal(cur.view(np.uint32), ref_img.view(np.uint32)), f"{v} differs"
+    out_rows = []
+    for v in variants:
+        med = float(np.median(res[v]))
+        out_rows.append({"variant": v, "median_ms": round(med, 4), "min_ms": round(min(res[v]), 4),
+                         "gsamples_s": round(S / med / 1e6, 1)})
+    print(json.dumps({"size": n, "res": W, "field": a.field, "phong": a.phong,
+                      "samples_per_frame": S, "rows": out_rows}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
