@@ -177,6 +177,10 @@ cvr_status cvr_create(int device, cvr_ctx** out_ctx) {
     return CVR_ERR_HIP;
   }
   c->stream = c->own_stream;
+  {
+    hipDeviceProp_t prop;
+    c->num_cus = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
   *out_ctx = reinterpret_cast<cvr_ctx*>(c);
   return CVR_OK;
 }
@@ -193,7 +197,8 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_total; free_dev(p); c->d_total = nullptr;
   free_dev(c->d_scratch);
   p = c->d_order; free_dev(p); c->d_order = nullptr;
-  p = c->d_wave_cost; free_dev(p); c->d_wave_cost = nullptr;
+  p = c->d_tile_cost; free_dev(p); c->d_tile_cost = nullptr;
+  p = c->d_heads; free_dev(p); c->d_heads = nullptr;
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -220,8 +225,14 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     return CVR_OK;
   }
   if (!std::strcmp(key, "tile_order")) {
-    if (value < 0 || value > 2) return fail(c, CVR_ERR_ARG, "tile_order must be 0, 1 or 2");
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "tile_order must be 0 or 1");
     c->use_order = value;
+    c->order_valid = 0;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "schedule")) {
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "schedule must be 0 or 1");
+    c->schedule = value;
     c->order_valid = 0;
     return CVR_OK;
   }
@@ -233,6 +244,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!c || !key) return -1;
   if (!std::strcmp(key, "batch")) return c->batch;
   if (!std::strcmp(key, "tile_order")) return c->use_order;
+  if (!std::strcmp(key, "schedule")) return c->schedule;
   return -1;
 }
 
@@ -404,21 +416,29 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   A.tf_n = c->tf_n;
   A.ka = p->ka; A.kd = p->kd; A.ks = p->ks; A.shininess = p->shininess;
   for (int i = 0; i < 3; i++) { A.ispec[i] = p->ispecular[i]; A.light[i] = p->light_pos[i]; }
-  int nblocks;
+  cvr::RenderPlan plan{};
   size_t npix;
   if (!packed) {
     A.packed = 0;
-    nblocks = ((f->width + 15) / 16) * ((f->height + 15) / 16);
+    plan.ntile_x = (f->width + 7) / 8;
+    plan.ntile_y = (f->height + 7) / 8;
+    plan.ntiles = plan.ntile_x * plan.ntile_y;
+    plan.nbx = (f->width + 15) / 16;
+    plan.nblocks = plan.nbx * ((f->height + 15) / 16);
     npix = (size_t)f->width * f->height;
   } else {
     A.packed = 1;
     A.tile = f->tile_size; A.rank = f->rank; A.nranks = f->nranks;
     A.ntx = (f->width + f->tile_size - 1) / f->tile_size;
     A.my_tiles = cvr_tiles_for_rank(f, f->rank);
-    nblocks = A.my_tiles * (f->tile_size / 16) * (f->tile_size / 16);
+    const int s8 = f->tile_size / 8;
+    plan.ntiles = A.my_tiles * s8 * s8;
+    plan.nbx = f->tile_size / 16;
+    plan.nblocks = A.my_tiles * plan.nbx * plan.nbx;
     npix = (size_t)A.my_tiles * f->tile_size * f->tile_size;
   }
-  A.xcd_remap = 1;
+  A.ntiles = plan.ntiles;
+  plan.queue = c->schedule == 1;
 
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
@@ -440,27 +460,36 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   // device outputs: the kernel ADDS to *total (the caller zeroes it); host
   // outputs: the context's own counter is reset here.
   if (d_total && !o->on_device) HIP_TRY(c, hipMemsetAsync(d_total, 0, sizeof(unsigned long long), s));
-  // Longest-first block order learned from the previous frame (tile_order option).
+
+  // Longest-first (LPT) order learned from the previous frame of the same plan:
+  // the kernel records each wave tile's critical path, tile_order_kernel sorts
+  // every XCD band by it (and re-arms the queue heads) for the next frame.
+  const int units = plan.queue ? plan.ntiles : plan.nblocks;
+  const bool can_order = c->use_order && (plan.queue || !packed) && (units + 7) / 8 <= 16384;
+  const int key = (plan.queue ? 1 : 2) ^ (plan.ntiles << 2) ^ (plan.nblocks << 20) ^
+                  (packed ? (f->rank << 8) ^ (f->nranks << 12) : 0);
   const int* order = nullptr;
-  uint32_t* wave_cost = nullptr;
-  int nseg = c->use_order == 2 ? 8 : 1;
-  if (c->use_order && nblocks % nseg == 0 && nblocks / nseg <= 16384) {
-    if (c->order_len != nblocks) {
+  uint32_t* tile_cost = nullptr;
+  if (can_order) {
+    if (c->order_units < units || !c->d_tile_cost) {
       void* p = c->d_order; free_dev(p); c->d_order = nullptr;
-      p = c->d_wave_cost; free_dev(p); c->d_wave_cost = nullptr;
-      c->order_len = 0; c->order_valid = 0;
-      HIP_TRY(c, hipMalloc((void**)&c->d_order, (size_t)nblocks * sizeof(int)));
-      HIP_TRY(c, hipMalloc((void**)&c->d_wave_cost, (size_t)nblocks * 4 * sizeof(uint32_t)));
-      c->order_len = nblocks;
+      p = c->d_tile_cost; free_dev(p); c->d_tile_cost = nullptr;
+      c->order_units = 0;
+      HIP_TRY(c, hipMalloc((void**)&c->d_order, (size_t)units * sizeof(int)));
+      HIP_TRY(c, hipMalloc((void**)&c->d_tile_cost, (size_t)plan.ntiles * sizeof(uint32_t) + 64));
+      c->order_units = units;
+      c->order_valid = 0;
     }
+    if (c->order_key != key) c->order_valid = 0;
     order = c->order_valid ? c->d_order : nullptr;
-    wave_cost = c->d_wave_cost;
+    tile_cost = c->d_tile_cost;
   }
-  HIP_TRY(c, cvr::launch_rc1pass(*c, A, phong, d_out, d_samples, d_total, order, wave_cost,
-                                 nblocks, s));
-  if (wave_cost) {
-    HIP_TRY(c, cvr::launch_tile_order(wave_cost, nblocks, nseg, c->d_order, s));
+  if (plan.queue && !c->d_heads) HIP_TRY(c, hipMalloc((void**)&c->d_heads, 64));
+  HIP_TRY(c, cvr::launch_rc1pass(*c, A, phong, d_out, d_samples, d_total, order, tile_cost, plan, s));
+  if (tile_cost) {
+    HIP_TRY(c, cvr::launch_tile_order(tile_cost, plan, c->d_order, c->d_heads, s));
     c->order_valid = 1;
+    c->order_key = key;
   }
   if (!o->on_device) {
     HIP_TRY(c, hipMemcpyAsync(o->rgba, d_out, rgba_bytes, hipMemcpyDeviceToHost, s));

@@ -1,0 +1,149 @@
+// cvr_device.h — device helpers of the gfx950 ray-marching kernels
+// (CVR-SPEC arithmetic; see DESIGN.md and oracle/cvr_oracle.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "cvr_internal.h"
+
+namespace cvr {
+
+
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float lerpf(float a, float b, float t) { return fmaf(t, b - a, a); }
+
+__device__ __forceinline__ void h2f2(uint32_t w, float& lo, float& hi) {
+  half2_t p = __builtin_bit_cast(half2_t, w);
+  lo = (float)p.x;
+  hi = (float)p.y;
+}
+
+// exp(x), CVR-SPEC (identical to oracle cvr_expf)
+__device__ __forceinline__ float cvr_expf(float x) {
+  if (x != x) return x;
+  if (x < -86.0f) return 0.0f;
+  if (x > 88.5f) return __builtin_inff();
+  float n = rintf(x * 1.44269504088896341f);
+  float r = fmaf(n, -0.693359375f, x);
+  r = fmaf(n, 2.12194440e-4f, r);
+  float p = 1.9875691500e-4f;
+  p = fmaf(p, r, 1.3981999507e-3f);
+  p = fmaf(p, r, 8.3334519073e-3f);
+  p = fmaf(p, r, 4.1665795894e-2f);
+  p = fmaf(p, r, 1.6666665459e-1f);
+  p = fmaf(p, r, 5.0000001201e-1f);
+  float r2 = r * r;
+  float y = fmaf(p, r2, r) + 1.0f;
+  return ldexpf(y, (int)n);
+}
+
+// pow(x, y) for x >= 0, CVR-SPEC (identical to oracle cvr_powf)
+__device__ __forceinline__ float cvr_powf(float x, float y) {
+  if (x != x || y != y) return x + y;
+  if (!(x > 0.0f) || x < 1.17549435e-38f) {
+    if (y > 0.0f) return 0.0f;
+    if (y == 0.0f) return 1.0f;
+    return __builtin_inff();
+  }
+  if (x == __builtin_inff()) return y > 0.0f ? __builtin_inff() : (y == 0.0f ? 1.0f : 0.0f);
+  uint32_t bits = __float_as_uint(x);
+  int e = (int)((bits >> 23) & 0xffu) - 126;
+  float m = __uint_as_float((bits & 0x007fffffu) | 0x3f000000u);
+  if (m < 0.70710678118654752f) { m = m + m; e = e - 1; }
+  float f = m - 1.0f;
+  float z = f * f;
+  float p = 7.0376836292e-2f;
+  p = fmaf(p, f, -1.1514610310e-1f);
+  p = fmaf(p, f, 1.1676998740e-1f);
+  p = fmaf(p, f, -1.2420140846e-1f);
+  p = fmaf(p, f, 1.4249322787e-1f);
+  p = fmaf(p, f, -1.6668057665e-1f);
+  p = fmaf(p, f, 2.0000714765e-1f);
+  p = fmaf(p, f, -2.4999993993e-1f);
+  p = fmaf(p, f, 3.3333331174e-1f);
+  float r = (p * f) * z;
+  float fe = (float)e;
+  r = fmaf(fe, -2.12194440e-4f, r);
+  r = fmaf(-0.5f, z, r);
+  float lnx = f + r;
+  lnx = fmaf(fe, 0.693359375f, lnx);
+  return cvr_expf(y * lnx);
+}
+
+struct f3 { float x, y, z; };
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+__device__ __forceinline__ f3 normalize3(f3 v) {
+  float inv = 1.0f / sqrtf(dot3(v, v));
+  return f3{v.x * inv, v.y * inv, v.z * inv};
+}
+
+// Corner indices + weights of one trilinear sample (texel space).
+struct Texel { int ix, iy, iz; float ax, ay, az; };
+
+// Gradient: 4 x fp16 (x, y, z, 0) per voxel, x-fastest, trilinear per channel.
+__device__ __forceinline__ f3 sample_gradient(const uint2* __restrict__ grad, const int N[3],
+                                              const Texel& t) {
+  int x0 = max(t.ix, 0), x1 = min(t.ix + 1, N[0] - 1);
+  int y0 = max(t.iy, 0), y1 = min(t.iy + 1, N[1] - 1);
+  int z0 = max(t.iz, 0), z1 = min(t.iz + 1, N[2] - 1);
+  size_t sx = 1, sy = (size_t)N[0], sz = (size_t)N[0] * N[1];
+  uint2 q[8];
+  q[0] = grad[x0 * sx + y0 * sy + z0 * sz];
+  q[1] = grad[x1 * sx + y0 * sy + z0 * sz];
+  q[2] = grad[x0 * sx + y1 * sy + z0 * sz];
+  q[3] = grad[x1 * sx + y1 * sy + z0 * sz];
+  q[4] = grad[x0 * sx + y0 * sy + z1 * sz];
+  q[5] = grad[x1 * sx + y0 * sy + z1 * sz];
+  q[6] = grad[x0 * sx + y1 * sy + z1 * sz];
+  q[7] = grad[x1 * sx + y1 * sy + z1 * sz];
+  float vx[8], vy[8], vz[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    float dummy;
+    h2f2(q[i].x, vx[i], vy[i]);
+    h2f2(q[i].y, vz[i], dummy);
+  }
+  f3 r;
+  {
+    float c00 = lerpf(vx[0], vx[1], t.ax), c10 = lerpf(vx[2], vx[3], t.ax);
+    float c01 = lerpf(vx[4], vx[5], t.ax), c11 = lerpf(vx[6], vx[7], t.ax);
+    r.x = lerpf(lerpf(c00, c10, t.ay), lerpf(c01, c11, t.ay), t.az);
+  }
+  {
+    float c00 = lerpf(vy[0], vy[1], t.ax), c10 = lerpf(vy[2], vy[3], t.ax);
+    float c01 = lerpf(vy[4], vy[5], t.ax), c11 = lerpf(vy[6], vy[7], t.ax);
+    r.y = lerpf(lerpf(c00, c10, t.ay), lerpf(c01, c11, t.ay), t.az);
+  }
+  {
+    float c00 = lerpf(vz[0], vz[1], t.ax), c10 = lerpf(vz[2], vz[3], t.ax);
+    float c01 = lerpf(vz[4], vz[5], t.ax), c11 = lerpf(vz[6], vz[7], t.ax);
+    r.z = lerpf(lerpf(c00, c10, t.ay), lerpf(c01, c11, t.ay), t.az);
+  }
+  return r;
+}
+
+
+// Branch-free CVR-SPEC exp: same values as cvr_expf (selects instead of the
+// early returns, so a wave never splits on the special cases).
+__device__ __forceinline__ float cvr_expf_nb(float x) {
+  float xc = fminf(fmaxf(x, -86.0f), 88.5f);
+  float n = rintf(xc * 1.44269504088896341f);
+  float r = fmaf(n, -0.693359375f, xc);
+  r = fmaf(n, 2.12194440e-4f, r);
+  float p = 1.9875691500e-4f;
+  p = fmaf(p, r, 1.3981999507e-3f);
+  p = fmaf(p, r, 8.3334519073e-3f);
+  p = fmaf(p, r, 4.1665795894e-2f);
+  p = fmaf(p, r, 1.6666665459e-1f);
+  p = fmaf(p, r, 5.0000001201e-1f);
+  float r2 = r * r;
+  float y = ldexpf(fmaf(p, r2, r) + 1.0f, (int)n);
+  y = x < -86.0f ? 0.0f : y;
+  y = x > 88.5f ? __builtin_inff() : y;
+  return x != x ? x : y;
+}
+
+
+}  // namespace cvr

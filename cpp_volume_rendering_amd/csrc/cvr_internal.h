@@ -43,9 +43,18 @@ struct Rc1passArgs {
   float ispec[3];
   float light[3];
   // screen-tile split (cvr_frame)
-  int tile, rank, nranks, ntx, my_tiles, sub_per_tile_x;
+  int tile, rank, nranks, ntx, my_tiles;
   int packed;
-  int xcd_remap;
+  int ntiles;                        // 8x8 wave tiles of this launch
+};
+
+// How one frame is cut into work (block schedule or persistent tile queue).
+struct RenderPlan {
+  int queue;                         // 1: persistent waves + per-band tile queues
+  int nblocks;                       // 16x16 blocks (block schedule)
+  int nbx;                           // blocks per row (unpacked) / per tile row (packed)
+  int ntiles;                        // 8x8 wave tiles
+  int ntile_x, ntile_y;              // wave-tile grid (unpacked)
 };
 
 struct Ctx {
@@ -71,11 +80,15 @@ struct Ctx {
   int grad_mode = 0;
   // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
   int batch = 4;
-  int use_order = 0;              // 0 off, 1 global LPT, 2 LPT per XCD band
-  int* d_order = nullptr;          // block permutation for the next frame
-  uint32_t* d_wave_cost = nullptr; // per-wave max iterations of the last frame
-  int order_len = 0;               // nblocks the buffers are sized for
-  int order_valid = 0;             // d_order holds a permutation for order_len blocks
+  int schedule = 1;                // 0: one 16x16 block per workgroup, 1: persistent tile queues
+  int use_order = 1;               // 1: longest-first (LPT) from the previous frame's costs
+  int* d_order = nullptr;          // unit permutation for the next frame
+  uint32_t* d_tile_cost = nullptr; // per-wave-tile critical path of the last frame
+  int order_units = 0;             // units the order buffer is sized for
+  int order_key = -1;              // plan signature the order was learned for
+  int order_valid = 0;
+  unsigned* d_heads = nullptr;     // 8 queue heads (persistent schedule)
+  int num_cus = 0;
   // scratch
   unsigned long long* d_total = nullptr;
   void* d_scratch = nullptr;      // host-output staging
@@ -88,9 +101,9 @@ hipError_t launch_build_cells_impl(const void* vox, int bpv, const uint16_t* lut
 hipError_t launch_gradient(const Ctx& c, int mode, hipStream_t s);
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
                           uint32_t* samples, unsigned long long* total, const int* order,
-                          uint32_t* wave_cost, int nblocks, hipStream_t s);
-hipError_t launch_tile_order(const uint32_t* wave_cost, int nblocks, int nseg, int* order,
-                             hipStream_t s);
+                          uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s);
+hipError_t launch_tile_order(const uint32_t* tile_cost, const RenderPlan& plan, int* order,
+                             unsigned* heads, hipStream_t s);
 hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
                                int nranks, int tiles_per_rank_max, hipStream_t s);
 

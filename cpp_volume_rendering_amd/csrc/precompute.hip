@@ -1,0 +1,153 @@
+// precompute.hip — one-time device precompute of the ray-caster's inputs:
+// the padded/bricked cell8 volume layout (GL_R16F semantics), the gradient
+// volume (finite differences / Sobel-Feldman, RGB16F), and the rank-0 tile
+// unpack of the screen-tile split.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "cvr_internal.h"
+
+namespace cvr {
+
+// Build the padded, bricked cell8 layout from raw voxels using the host-made
+// value table lut[v] = half(float(v / 255.0)) (GL_R16F upload of
+// GetNormalizedSample, utils.cpp:20-56).
+template <typename VT>
+__global__ void build_cells_kernel(const VT* __restrict__ vox, const uint16_t* __restrict__ lut,
+                                   int nx, int ny, int nz, CellGrid g, uint4* __restrict__ cells,
+                                   size_t ncells) {
+  size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= ncells) return;
+  uint32_t i = (uint32_t)idx;
+  uint32_t inner = i & 63u, brick = i >> 6;
+  int a = (int)(inner & 3u), b = (int)((inner >> 2) & 3u), c = (int)(inner >> 4);
+  int bxi = (int)(brick % (uint32_t)g.bx);
+  uint32_t rest = brick / (uint32_t)g.bx;
+  int byi = (int)(rest % (uint32_t)g.by), bzi = (int)(rest / (uint32_t)g.by);
+  a += bxi * 4; b += byi * 4; c += bzi * 4;
+  uint4 r = make_uint4(0, 0, 0, 0);
+  if (a < g.cx && b < g.cy && c < g.cz) {
+    int x0 = max(a - 1, 0), x1 = min(a, nx - 1);
+    int y0 = max(b - 1, 0), y1 = min(b, ny - 1);
+    int z0 = max(c - 1, 0), z1 = min(c, nz - 1);
+    auto q = [&](int x, int y, int z) -> uint32_t {
+      return lut[vox[(size_t)x + (size_t)y * nx + (size_t)z * nx * ny]];
+    };
+    r.x = q(x0, y0, z0) | (q(x1, y0, z0) << 16);
+    r.y = q(x0, y1, z0) | (q(x1, y1, z0) << 16);
+    r.z = q(x0, y0, z1) | (q(x1, y0, z1) << 16);
+    r.w = q(x0, y1, z1) | (q(x1, y1, z1) << 16);
+  }
+  cells[idx] = r;
+}
+
+hipError_t launch_build_cells_impl(const void* vox, int bpv, const uint16_t* lut, const int N[3],
+                                   const CellGrid& g, void* cells, hipStream_t s) {
+  size_t n = cell_count(g);
+  int bs = 256;
+  size_t nb = (n + bs - 1) / bs;
+  if (bpv == 1)
+    hipLaunchKernelGGL(build_cells_kernel<uint8_t>, dim3((unsigned)nb), dim3(bs), 0, s,
+                       (const uint8_t*)vox, lut, N[0], N[1], N[2], g, (uint4*)cells, n);
+  else
+    hipLaunchKernelGGL(build_cells_kernel<uint16_t>, dim3((unsigned)nb), dim3(bs), 0, s,
+                       (const uint16_t*)vox, lut, N[0], N[1], N[2], g, (uint4*)cells, n);
+  return hipGetLastError();
+}
+
+// GetNormalizedSample in double (structuredgridvolume.cpp:121-151), 0 outside.
+template <typename VT>
+__device__ __forceinline__ double norm_sample(const VT* vox, int nx, int ny, int nz, int x, int y,
+                                              int z, double inv_max) {
+  if (x < 0 || y < 0 || z < 0 || x >= nx || y >= ny || z >= nz) return 0.0;
+  return (double)vox[(size_t)x + (size_t)y * nx + (size_t)z * nx * ny] / inv_max;
+}
+
+__device__ __forceinline__ uint32_t f2h_bits(float f) {
+  _Float16 h = (_Float16)f;
+  return (uint32_t)__builtin_bit_cast(uint16_t, h);
+}
+
+// GenerateGradientTexture (utils.cpp:146-190) with its defaults, and
+// GenerateSobelFeldmanGradientTexture (utils.cpp:287-333); stored RGB16F.
+template <typename VT>
+__global__ void gradient_kernel(const VT* __restrict__ vox, int nx, int ny, int nz, int mode,
+                                double maxv, uint2* __restrict__ grad) {
+  size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t n = (size_t)nx * ny * nz;
+  if (idx >= n) return;
+  int x = (int)(idx % (size_t)nx);
+  size_t r = idx / (size_t)nx;
+  int y = (int)(r % (size_t)ny), z = (int)(r / (size_t)ny);
+  double gx = 0, gy = 0, gz = 0;
+  if (mode == CVR_GRADIENT_FINITE_DIFFERENCES) {
+    gx = norm_sample(vox, nx, ny, nz, x + 1, y, z, maxv) - norm_sample(vox, nx, ny, nz, x - 1, y, z, maxv);
+    gy = norm_sample(vox, nx, ny, nz, x, y + 1, z, maxv) - norm_sample(vox, nx, ny, nz, x, y - 1, z, maxv);
+    gz = norm_sample(vox, nx, ny, nz, x, y, z + 1, maxv) - norm_sample(vox, nx, ny, nz, x, y, z - 1, maxv);
+    double sqr = gx * gx + gy * gy + gz * gz;
+    double inv = 1.0 / sqrt(sqr);
+    gx *= inv; gy *= inv; gz *= inv;
+    if (gx != gx) { gx = 0.0; gy = 0.0; gz = 0.0; }
+  } else {
+    for (int v1 = -1; v1 <= 1; v1++)
+      for (int v2 = -1; v2 <= 1; v2++) {
+        int m = abs(v1) + abs(v2);
+        double wgt = m == 0 ? 1.0 : (m == 1 ? 2.0 : 4.0);   // pow(2, |v1|+|v2|)
+        gz += norm_sample(vox, nx, ny, nz, x + v1, y + v2, z - 1, maxv) * (4.0 / wgt)
+            + norm_sample(vox, nx, ny, nz, x + v1, y + v2, z + 1, maxv) * (-4.0 / wgt);
+        gy += norm_sample(vox, nx, ny, nz, x + v1, y - 1, z + v2, maxv) * (4.0 / wgt)
+            + norm_sample(vox, nx, ny, nz, x + v1, y + 1, z + v2, maxv) * (-4.0 / wgt);
+        gx += norm_sample(vox, nx, ny, nz, x - 1, y + v2, z + v1, maxv) * (4.0 / wgt)
+            + norm_sample(vox, nx, ny, nz, x + 1, y + v2, z + v1, maxv) * (-4.0 / wgt);
+      }
+  }
+  uint2 o;
+  o.x = f2h_bits((float)gx) | (f2h_bits((float)gy) << 16);
+  o.y = f2h_bits((float)gz);
+  grad[idx] = o;
+}
+
+hipError_t launch_gradient(const Ctx& c, int mode, hipStream_t s) {
+  size_t n = (size_t)c.N[0] * c.N[1] * c.N[2];
+  int bs = 256;
+  size_t nb = (n + bs - 1) / bs;
+  if (c.bpv == 1)
+    hipLaunchKernelGGL(gradient_kernel<uint8_t>, dim3((unsigned)nb), dim3(bs), 0, s,
+                       (const uint8_t*)c.d_vox, c.N[0], c.N[1], c.N[2], mode, 255.0,
+                       (uint2*)c.d_grad);
+  else
+    hipLaunchKernelGGL(gradient_kernel<uint16_t>, dim3((unsigned)nb), dim3(bs), 0, s,
+                       (const uint16_t*)c.d_vox, c.N[0], c.N[1], c.N[2], mode, 65535.0,
+                       (uint2*)c.d_grad);
+  return hipGetLastError();
+}
+
+// Scatter packed per-rank tiles (screen-tile split) into the W x H image.
+__global__ void unpack_tiles_kernel(const float4* __restrict__ packed, float4* __restrict__ out,
+                                    int W, int H, int tile, int nranks, int tpr_max, int ntx,
+                                    size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  size_t tt = (size_t)tile * tile;
+  size_t slot = i / tt;                     // rank * tpr_max + k
+  int inner = (int)(i - slot * tt);
+  int r = (int)(slot / (size_t)tpr_max), k = (int)(slot % (size_t)tpr_max);
+  int t = r + k * nranks;
+  int tx = t % ntx, ty = t / ntx;
+  int px = tx * tile + inner % tile, py = ty * tile + inner / tile;
+  if (px < W && py < H && ty * tile < H) out[(size_t)py * W + px] = packed[i];
+}
+
+hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
+                               int nranks, int tpr_max, hipStream_t s) {
+  int ntx = (W + tile - 1) / tile;
+  size_t n = (size_t)nranks * tpr_max * tile * tile;
+  int bs = 256;
+  size_t nb = (n + bs - 1) / bs;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(unpack_tiles_kernel, dim3((unsigned)nb), dim3(bs), 0, s, packed, out, W, H,
+                     tile, nranks, tpr_max, ntx, n);
+  return hipGetLastError();
+}
+
+}  // namespace cvr

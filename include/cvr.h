@@ -126,8 +126,10 @@ const char* cvr_last_error(const cvr_ctx* ctx);
 cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
 /* Tuning options (results are identical for every setting):
  *   "batch"      samples addressed + fetched per batch of the march (1, 2, 4, 8; default 4)
- *   "tile_order" 1/2: launch screen tiles longest-first using the previous frame's
- *                per-wave costs (LPT; 2 = within each XCD band); 0: XCD-banded order (default) */
+ *   "schedule"   1: persistent waves dequeue 8x8 tiles from one queue per XCD
+ *                band, stealing across bands (default); 0: one 16x16 block per workgroup
+ *   "tile_order" 1: take tiles longest-first (LPT) using the previous frame's per-tile
+ *                critical paths, per XCD band (default); 0: screen order */
 cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
 int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--field", default="ml")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=20)
-    ap.add_argument("--variants", default="b1o0,b2o0,b4o0,b8o0,b4o1,b4o2,b2o1,b2o2")
+    ap.add_argument("--variants", default="s0b4o0,s0b4o1,s1b4o0,s1b4o1,s1b2o1,s1b8o1,s1b1o1")
     ap.add_argument("--phong", action="store_true")
     a = ap.parse_args()
     n, W = a.size, a.res
@@ -58,7 +58,9 @@ def main():
     S = None
     for rnd in range(a.rounds):
         for v in variants:
-            b, o = int(v[1:v.index("o")]), int(v[v.index("o") + 1:])
+            sch = int(v[1:v.index("b")])
+            b, o = int(v[v.index("b") + 1:v.index("o")]), int(v[v.index("o") + 1:])
+            N.check(L.cvr_set_option(dev.handle, b"schedule", sch), "opt")
             N.check(L.cvr_set_option(dev.handle, b"batch", b), "opt")
             N.check(L.cvr_set_option(dev.handle, b"tile_order", o), "opt")
             with torch.cuda.stream(s):
