@@ -230,6 +230,11 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->order_valid = 0;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "queue_blocks_per_cu")) {
+    if (value < 0 || value > 32) return fail(c, CVR_ERR_ARG, "queue_blocks_per_cu in [0, 32]");
+    c->queue_blocks_per_cu = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "schedule")) {
     if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "schedule must be 0 or 1");
     c->schedule = value;
@@ -245,6 +250,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "batch")) return c->batch;
   if (!std::strcmp(key, "tile_order")) return c->use_order;
   if (!std::strcmp(key, "schedule")) return c->schedule;
+  if (!std::strcmp(key, "queue_blocks_per_cu")) return c->queue_blocks_per_cu;
   return -1;
 }
 

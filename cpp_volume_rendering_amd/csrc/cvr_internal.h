@@ -88,6 +88,7 @@ struct Ctx {
   int order_key = -1;              // plan signature the order was learned for
   int order_valid = 0;
   unsigned* d_heads = nullptr;     // 8 queue heads (persistent schedule)
+  int queue_blocks_per_cu = 0;     // persistent grid = this x CUs (0: 8)
   int num_cus = 0;
   // scratch
   unsigned long long* d_total = nullptr;

@@ -409,10 +409,10 @@ static hipError_t launch_kp(const Ctx& c, const Rc1passArgs& a, float4* out, uin
                             const RenderPlan& plan, hipStream_t s) {
   size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
   if (plan.queue) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rc1pass_queue_kernel<K, PHONG>, 256,
-                                                     lds) != hipSuccess || per_cu < 1)
-      per_cu = 1;
+    // Residency from the register budget: waves/SIMD = 512 / VGPR allocation
+    // (MI355X_MICROARCH.md, Register files), 4 SIMDs per CU, 4 waves per block.
+    // Over-subscribing is harmless (late blocks find the queues empty).
+    int per_cu = c.queue_blocks_per_cu > 0 ? c.queue_blocks_per_cu : 8;
     int grid = per_cu * c.num_cus;
     hipLaunchKernelGGL((rc1pass_queue_kernel<K, PHONG>), dim3(grid), dim3(256), lds, s, a,
                        (const uint4*)c.d_cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out,

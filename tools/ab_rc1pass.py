@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--field", default="ml")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=20)
-    ap.add_argument("--variants", default="s0b4o0,s0b4o1,s1b4o0,s1b4o1,s1b2o1,s1b8o1,s1b1o1")
+    ap.add_argument("--variants", default="s0b4o1,s1b4o1q2,s1b4o1q4,s1b4o1q5,s1b4o1q8,s1b4o1q16,s1b4o0q5")
     ap.add_argument("--phong", action="store_true")
     a = ap.parse_args()
     n, W = a.size, a.res
@@ -58,8 +58,15 @@ def main():
     S = None
     for rnd in range(a.rounds):
         for v in variants:
-            sch = int(v[1:v.index("b")])
-            b, o = int(v[v.index("b") + 1:v.index("o")]), int(v[v.index("o") + 1:])
+            qb = 0
+            if "q" in v:
+                qb = int(v[v.index("q") + 1:])
+                v_ = v[:v.index("q")]
+            else:
+                v_ = v
+            sch = int(v_[1:v_.index("b")])
+            N.check(L.cvr_set_option(dev.handle, b"queue_blocks_per_cu", qb), "opt")
+            b, o = int(v_[v_.index("b") + 1:v_.index("o")]), int(v_[v_.index("o") + 1:])
             N.check(L.cvr_set_option(dev.handle, b"schedule", sch), "opt")
             N.check(L.cvr_set_option(dev.handle, b"batch", b), "opt")
             N.check(L.cvr_set_option(dev.handle, b"tile_order", o), "opt")
