@@ -324,7 +324,12 @@ rc1pass_queue_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   for (int tried = 0; tried < 8;) {
     const int b0 = (band * nt) >> 3, b1 = ((band + 1) * nt) >> 3;
     unsigned q = 0;
-    if (lane == 0) q = atomicAdd(&heads[band], 1u);
+    if (lane == 0) {
+      // a plain (L2) read first: an exhausted band costs no atomic (one word
+      // serialises ~90 atomics/us, and every exiting wave probes all 8 bands)
+      q = __hip_atomic_load(&heads[band], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int)q < b1 - b0) q = atomicAdd(&heads[band], 1u);
+    }
     q = __builtin_amdgcn_readfirstlane(q);
     if ((int)q >= b1 - b0) {          // band exhausted: steal from the next one
       band = (band + 1) & 7;
