@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
-VAR=${1:-b4o2}
+VAR=${1:-s0b4o1}
 EXTRA=${2:-}
 mkdir -p gpurun_out/pmc
 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
@@ -14,4 +14,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_INS
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d gpurun_out/pmc/g$i -o pmc --output-format csv -- python3 tools/ab_rc1pass.py --variants $VAR --rounds 1 --frames 5 $EXTRA > gpurun_out/pmc/g$i.log 2>&1 || { echo "group $grp failed"; tail -5 gpurun_out/pmc/g$i.log; }
 done
-python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.json && cat gpurun_out/pmc/summary.json
+python3 tools/pmc_summary.py gpurun_out/pmc ${KERNEL:-rc1pass} > gpurun_out/pmc/summary.json && cat gpurun_out/pmc/summary.json
