@@ -198,7 +198,6 @@ void cvr_destroy(cvr_ctx* ctx) {
   free_dev(c->d_scratch);
   p = c->d_order; free_dev(p); c->d_order = nullptr;
   p = c->d_tile_cost; free_dev(p); c->d_tile_cost = nullptr;
-  p = c->d_heads; free_dev(p); c->d_heads = nullptr;
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -230,11 +229,6 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->order_valid = 0;
     return CVR_OK;
   }
-  if (!std::strcmp(key, "queue_blocks_per_cu")) {
-    if (value < 0 || value > 32) return fail(c, CVR_ERR_ARG, "queue_blocks_per_cu in [0, 32]");
-    c->queue_blocks_per_cu = value;
-    return CVR_OK;
-  }
   if (!std::strcmp(key, "schedule")) {
     if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "schedule must be 0 or 1");
     c->schedule = value;
@@ -250,7 +244,6 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "batch")) return c->batch;
   if (!std::strcmp(key, "tile_order")) return c->use_order;
   if (!std::strcmp(key, "schedule")) return c->schedule;
-  if (!std::strcmp(key, "queue_blocks_per_cu")) return c->queue_blocks_per_cu;
   return -1;
 }
 
@@ -444,7 +437,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     npix = (size_t)A.my_tiles * f->tile_size * f->tile_size;
   }
   A.ntiles = plan.ntiles;
-  plan.queue = c->schedule == 1;
+  plan.wave_blocks = c->schedule == 1;
 
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
@@ -470,9 +463,9 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   // Longest-first (LPT) order learned from the previous frame of the same plan:
   // the kernel records each wave tile's critical path, tile_order_kernel sorts
   // every XCD band by it (and re-arms the queue heads) for the next frame.
-  const int units = plan.queue ? plan.ntiles : plan.nblocks;
-  const bool can_order = c->use_order && (plan.queue || !packed) && (units + 7) / 8 <= 16384;
-  const int key = (plan.queue ? 1 : 2) ^ (plan.ntiles << 2) ^ (plan.nblocks << 20) ^
+  const int units = plan.wave_blocks ? plan.ntiles : plan.nblocks;
+  const bool can_order = c->use_order && (plan.wave_blocks || !packed) && (units + 7) / 8 <= 16384;
+  const int key = (plan.wave_blocks ? 1 : 2) ^ (plan.ntiles << 2) ^ (plan.nblocks << 20) ^
                   (packed ? (f->rank << 8) ^ (f->nranks << 12) : 0);
   const int* order = nullptr;
   uint32_t* tile_cost = nullptr;
@@ -490,10 +483,9 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     order = c->order_valid ? c->d_order : nullptr;
     tile_cost = c->d_tile_cost;
   }
-  if (plan.queue && !c->d_heads) HIP_TRY(c, hipMalloc((void**)&c->d_heads, 64));
   HIP_TRY(c, cvr::launch_rc1pass(*c, A, phong, d_out, d_samples, d_total, order, tile_cost, plan, s));
   if (tile_cost) {
-    HIP_TRY(c, cvr::launch_tile_order(tile_cost, plan, c->d_order, c->d_heads, s));
+    HIP_TRY(c, cvr::launch_tile_order(tile_cost, plan, c->d_order, s));
     c->order_valid = 1;
     c->order_key = key;
   }

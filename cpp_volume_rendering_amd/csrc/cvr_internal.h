@@ -50,7 +50,7 @@ struct Rc1passArgs {
 
 // How one frame is cut into work (block schedule or persistent tile queue).
 struct RenderPlan {
-  int queue;                         // 1: persistent waves + per-band tile queues
+  int wave_blocks;                   // 1: one wave tile per workgroup, 0: 2x2 tiles
   int nblocks;                       // 16x16 blocks (block schedule)
   int nbx;                           // blocks per row (unpacked) / per tile row (packed)
   int ntiles;                        // 8x8 wave tiles
@@ -80,15 +80,13 @@ struct Ctx {
   int grad_mode = 0;
   // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
   int batch = 4;
-  int schedule = 1;                // 0: one 16x16 block per workgroup, 1: persistent tile queues
+  int schedule = 1;                // 0: 2x2 wave tiles per workgroup, 1: one wave tile per workgroup
   int use_order = 1;               // 1: longest-first (LPT) from the previous frame's costs
   int* d_order = nullptr;          // unit permutation for the next frame
   uint32_t* d_tile_cost = nullptr; // per-wave-tile critical path of the last frame
   int order_units = 0;             // units the order buffer is sized for
   int order_key = -1;              // plan signature the order was learned for
   int order_valid = 0;
-  unsigned* d_heads = nullptr;     // 8 queue heads (persistent schedule)
-  int queue_blocks_per_cu = 0;     // persistent grid = this x CUs (0: 8)
   int num_cus = 0;
   // scratch
   unsigned long long* d_total = nullptr;
@@ -104,7 +102,7 @@ hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4
                           uint32_t* samples, unsigned long long* total, const int* order,
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s);
 hipError_t launch_tile_order(const uint32_t* tile_cost, const RenderPlan& plan, int* order,
-                             unsigned* heads, hipStream_t s);
+                             hipStream_t s);
 hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
                                int nranks, int tiles_per_rank_max, hipStream_t s);
 

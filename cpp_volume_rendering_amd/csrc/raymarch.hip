@@ -11,10 +11,9 @@
 //   * per-ray state in registers; K samples addressed and fetched per batch
 //     (K x 16 B in flight per lane), classified, then composited in order with
 //     the per-lane early ray termination (dst.a > 0.99);
-//   * scheduling: either one 16x16 block per workgroup (XCD-banded), or
-//     persistent waves that dequeue 8x8 tiles from one queue per XCD band
-//     (longest tiles first when the previous frame's costs are known) and steal
-//     from the other bands when their own runs dry.
+//   * scheduling: one wave tile (or 2x2 of them) per workgroup, each XCD owns
+//     one horizontal band of the screen (L2 locality) and receives its tiles
+//     longest-first when the previous frame's per-tile costs are known (LPT).
 //
 // Arithmetic follows CVR-SPEC: explicit fmaf, IEEE div/sqrt, the
 // polynomial cvr_expf / cvr_powf.  The file is compiled with -ffp-contract=off
@@ -253,40 +252,43 @@ __device__ __forceinline__ void finish_tile(const Rc1passArgs& A, int t, int lan
 // Kernels
 // ---------------------------------------------------------------------------
 
-// Block schedule: workgroup = 2x2 wave tiles (16x16 px).  Logical block L comes
-// from the LPT order when given, else from the XCD-banded remap (blocks b and
-// b+8 share an XCD, so XCD b%8 gets one contiguous band of blocks).
-template <int K, bool PHONG>
-__global__ void __launch_bounds__(256)
+// Block schedule.  WPB = 4: a workgroup is 2x2 wave tiles (16x16 px); WPB = 1:
+// a workgroup is one wave tile (8x8 px), so a long ray only holds its own wave
+// slot.  Logical unit L comes from the LPT order when given, else from the
+// XCD-banded remap (units b and b+8 share an XCD, so XCD b%8 gets one
+// contiguous band of the screen).
+template <int K, bool PHONG, int WPB>
+__global__ void __launch_bounds__(64 * WPB)
 rc1pass_blocks_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                       const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
                       float4* __restrict__ out, uint32_t* __restrict__ samples,
                       unsigned long long* __restrict__ total, const int* __restrict__ order,
-                      uint32_t* __restrict__ tile_cost, int nblocks, int nbx) {
+                      uint32_t* __restrict__ tile_cost, int nunits, int nbx) {
   extern __shared__ float4 tfp[];
   load_tf_lds(tfp, tf_g, A.tf_n);
   const int b = blockIdx.x;
   int L;
   if (order) L = order[b];
-  else if ((nblocks & 7) == 0) L = (b & 7) * (nblocks >> 3) + (b >> 3);
+  else if ((nunits & 7) == 0) L = (b & 7) * (nunits >> 3) + (b >> 3);
   else L = b;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = WPB == 1 ? 0 : (threadIdx.x >> 6);
   int t;
-  bool tile_ok;
-  if (!A.packed) {   // block L = (bx, by) in 16x16 units -> wave tile (2bx + w&1, 2by + w>>1)
+  bool tile_ok = true;
+  if (WPB == 1) {
+    t = L;
+  } else if (!A.packed) {   // block L = (bx, by) in 16x16 units -> wave tile (2bx + w&1, 2by + w>>1)
     const int by = L / nbx, bx = L - by * nbx;
     const int ntile_x = (A.W + 7) >> 3, ntile_y = (A.H + 7) >> 3;
     const int ty = (by << 1) + (wave >> 1), tx = (bx << 1) + (wave & 1);
     tile_ok = tx < ntile_x && ty < ntile_y;
     t = ty * ntile_x + tx;
-  } else {           // packed: block = 2x2 sub-tiles of one rank tile; nbx = blocks per tile row
+  } else {                  // packed: block = 2x2 sub-tiles of one rank tile; nbx = blocks per tile row
     const int s = A.tile >> 3, bpt = nbx * nbx;
     const int k = L / bpt, j = L - k * bpt;
     const int sy = ((j / nbx) << 1) + (wave >> 1), sx = ((j % nbx) << 1) + (wave & 1);
     t = k * s * s + sy * s + sx;
-    tile_ok = true;
   }
-  if (!tile_ok) return;   // wave-uniform: a wave tile past the image edge
+  if (!tile_ok) return;     // wave-uniform: a wave tile past the image edge
   int px, py;
   long long oidx;
   tile_pixel(A, t, lane, px, py, oidx);
@@ -297,66 +299,15 @@ rc1pass_blocks_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   finish_tile(A, t, lane, inside, oidx, dst, cnt, out, samples, total, tile_cost);
 }
 
-__device__ __forceinline__ int xcc_id() {
-  unsigned x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-  return (int)(x & 7u);
-}
-
-// Persistent schedule: every wave loops, dequeuing 8x8 tiles.  Tile ids are cut
-// into 8 contiguous bands (horizontal screen bands), one queue per band; a wave
-// starts on its XCD's band (L2 locality) and steals from the next bands when it
-// runs dry.  With `order` the tiles of each band are taken longest first (LPT
-// from the previous frame's per-tile critical paths).  Every wave reaches the
-// exit once all 8 queues are exhausted.
-template <int K, bool PHONG>
-__global__ void __launch_bounds__(256)
-rc1pass_queue_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
-                     const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
-                     float4* __restrict__ out, uint32_t* __restrict__ samples,
-                     unsigned long long* __restrict__ total, const int* __restrict__ order,
-                     uint32_t* __restrict__ tile_cost, unsigned* __restrict__ heads) {
-  extern __shared__ float4 tfp[];
-  load_tf_lds(tfp, tf_g, A.tf_n);
-  const int lane = threadIdx.x & 63;
-  const int nt = A.ntiles;
-  int band = xcc_id();
-  for (int tried = 0; tried < 8;) {
-    const int b0 = (band * nt) >> 3, b1 = ((band + 1) * nt) >> 3;
-    unsigned q = 0;
-    if (lane == 0) {
-      // a plain (L2) read first: an exhausted band costs no atomic (one word
-      // serialises ~90 atomics/us, and every exiting wave probes all 8 bands)
-      q = __hip_atomic_load(&heads[band], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((int)q < b1 - b0) q = atomicAdd(&heads[band], 1u);
-    }
-    q = __builtin_amdgcn_readfirstlane(q);
-    if ((int)q >= b1 - b0) {          // band exhausted: steal from the next one
-      band = (band + 1) & 7;
-      tried++;
-      continue;
-    }
-    const int t = order ? order[b0 + (int)q] : b0 + (int)q;
-    int px, py;
-    long long oidx;
-    tile_pixel(A, t, lane, px, py, oidx);
-    const bool inside = px < A.W && py < A.H;
-    float4 dst = make_float4(0.f, 0.f, 0.f, 0.f);
-    uint32_t cnt = 0;
-    if (inside) march_ray<K, PHONG>(A, cells, grad, tfp, px, py, dst, cnt);
-    finish_tile(A, t, lane, inside, oidx, dst, cnt, out, samples, total, tile_cost);
-  }
-}
-
 // LPT order from the previous frame's per-tile costs: workgroup `seg` sorts the
-// units of band seg (bitonic sort in LDS, descending cost, ties by index) and
-// writes them either in place (queue schedule: order[band_start + i]) or
-// interleaved over XCDs (block schedule: physical block seg + 8*i).  The block
-// schedule sums the 4 wave tiles of each 16x16 block.  Also re-arms the queue
-// heads for the next frame.
+// units of XCD band seg (bitonic sort in LDS, descending cost, ties by index)
+// and deals them to physical blocks seg, seg+8, seg+16, ... (the blocks XCD
+// seg receives), so every XCD keeps its screen band and starts with its
+// longest units.  A unit is one wave tile, or (blocks_mode) a 16x16 block whose
+// cost sums its 4 wave tiles.
 __global__ void __launch_bounds__(1024)
 tile_order_kernel(const uint32_t* __restrict__ tile_cost, int nunits, int blocks_mode, int nbx,
-                  int ntile_x, int ntile_y, int* __restrict__ order, unsigned* __restrict__ heads) {
+                  int ntile_x, int ntile_y, int* __restrict__ order) {
   extern __shared__ unsigned long long keys[];
   const int b0 = (blockIdx.x * nunits) >> 3, b1 = ((blockIdx.x + 1) * nunits) >> 3;
   const int seg = b1 - b0;
@@ -395,13 +346,8 @@ tile_order_kernel(const uint32_t* __restrict__ tile_cost, int nunits, int blocks
   }
   for (int i = threadIdx.x; i < seg; i += blockDim.x) {
     int u = (int)(0xffffffffu - (uint32_t)keys[i]);
-    order[blocks_mode ? (blockIdx.x + 8 * i) : (b0 + i)] = u;
+    order[blockIdx.x + 8 * i] = u;
   }
-  if (threadIdx.x == 0 && heads) heads[blockIdx.x] = 0u;
-}
-
-__global__ void reset_heads_kernel(unsigned* heads) {
-  if (threadIdx.x < 8) heads[threadIdx.x] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -413,20 +359,14 @@ static hipError_t launch_kp(const Ctx& c, const Rc1passArgs& a, float4* out, uin
                             unsigned long long* total, const int* order, uint32_t* tile_cost,
                             const RenderPlan& plan, hipStream_t s) {
   size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
-  if (plan.queue) {
-    // Residency from the register budget: waves/SIMD = 512 / VGPR allocation
-    // (MI355X_MICROARCH.md, Register files), 4 SIMDs per CU, 4 waves per block.
-    // Over-subscribing is harmless (late blocks find the queues empty).
-    int per_cu = c.queue_blocks_per_cu > 0 ? c.queue_blocks_per_cu : 8;
-    int grid = per_cu * c.num_cus;
-    hipLaunchKernelGGL((rc1pass_queue_kernel<K, PHONG>), dim3(grid), dim3(256), lds, s, a,
-                       (const uint4*)c.d_cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out,
-                       samples, total, order, tile_cost, c.d_heads);
-  } else {
-    hipLaunchKernelGGL((rc1pass_blocks_kernel<K, PHONG>), dim3(plan.nblocks), dim3(256), lds, s,
+  if (plan.wave_blocks)
+    hipLaunchKernelGGL((rc1pass_blocks_kernel<K, PHONG, 1>), dim3(plan.ntiles), dim3(64), lds, s,
+                       a, (const uint4*)c.d_cells, (const uint2*)c.d_grad, (const float4*)c.d_tf,
+                       out, samples, total, order, tile_cost, plan.ntiles, 0);
+  else
+    hipLaunchKernelGGL((rc1pass_blocks_kernel<K, PHONG, 4>), dim3(plan.nblocks), dim3(256), lds, s,
                        a, (const uint4*)c.d_cells, (const uint2*)c.d_grad, (const float4*)c.d_tf,
                        out, samples, total, order, tile_cost, plan.nblocks, plan.nbx);
-  }
   return hipGetLastError();
 }
 
@@ -443,9 +383,6 @@ hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
   if (plan.nblocks <= 0 || a.ntiles <= 0) return hipSuccess;
   if (a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
-  if (plan.queue && !order) {   // queue heads must start at zero
-    hipLaunchKernelGGL(reset_heads_kernel, dim3(1), dim3(64), 0, s, c.d_heads);
-  }
   switch (c.batch) {
     case 1: return launch_k<1>(c, a, phong, out, samples, total, order, tile_cost, plan, s);
     case 2: return launch_k<2>(c, a, phong, out, samples, total, order, tile_cost, plan, s);
@@ -455,15 +392,14 @@ hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4
 }
 
 hipError_t launch_tile_order(const uint32_t* tile_cost, const RenderPlan& plan, int* order,
-                             unsigned* heads, hipStream_t s) {
-  const int nunits = plan.queue ? plan.ntiles : plan.nblocks;
+                             hipStream_t s) {
+  const int nunits = plan.wave_blocks ? plan.ntiles : plan.nblocks;
   const int seg = (nunits + 7) >> 3;
   int P = 1;
   while (P < seg) P <<= 1;
   if (P > 16384) return hipErrorInvalidValue;
   hipLaunchKernelGGL(tile_order_kernel, dim3(8), dim3(1024), (size_t)P * 8, s, tile_cost, nunits,
-                     plan.queue ? 0 : 1, plan.nbx, plan.ntile_x, plan.ntile_y, order,
-                     plan.queue ? heads : nullptr);
+                     plan.wave_blocks ? 0 : 1, plan.nbx, plan.ntile_x, plan.ntile_y, order);
   return hipGetLastError();
 }
 

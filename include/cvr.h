@@ -126,11 +126,10 @@ const char* cvr_last_error(const cvr_ctx* ctx);
 cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
 /* Tuning options (results are identical for every setting):
  *   "batch"      samples addressed + fetched per batch of the march (1, 2, 4, 8; default 4)
- *   "schedule"   1: persistent waves dequeue 8x8 tiles from one queue per XCD
- *                band, stealing across bands (default); 0: one 16x16 block per workgroup
- *   "queue_blocks_per_cu" persistent grid size in 256-thread blocks per CU (0: 8)
- *   "tile_order" 1: take tiles longest-first (LPT) using the previous frame's per-tile
- *                critical paths, per XCD band (default); 0: screen order */
+ *   "schedule"   1: one 8x8 wave tile per workgroup (default); 0: 2x2 wave tiles
+ *   "tile_order" 1: each XCD takes the tiles of its screen band longest-first (LPT),
+ *                using the previous frame's per-tile critical paths (default);
+ *                0: screen order */
 cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
 int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);
