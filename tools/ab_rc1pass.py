@@ -65,7 +65,6 @@ def main():
             else:
                 v_ = v
             sch = int(v_[1:v_.index("b")])
-            N.check(L.cvr_set_option(dev.handle, b"queue_blocks_per_cu", qb), "opt")
             b, o = int(v_[v_.index("b") + 1:v_.index("o")]), int(v_[v_.index("o") + 1:])
             N.check(L.cvr_set_option(dev.handle, b"schedule", sch), "opt")
             N.check(L.cvr_set_option(dev.handle, b"batch", b), "opt")
