@@ -218,8 +218,8 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c || !key) return CVR_ERR_ARG;
   if (!std::strcmp(key, "batch")) {
-    if (value != 1 && value != 2 && value != 4 && value != 8)
-      return fail(c, CVR_ERR_ARG, "batch must be 1, 2, 4 or 8");
+    if (value != 2 && value != 4 && value != 8)
+      return fail(c, CVR_ERR_ARG, "batch must be 2, 4 or 8");
     c->batch = value;
     return CVR_OK;
   }
@@ -229,10 +229,15 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->order_valid = 0;
     return CVR_OK;
   }
-  if (!std::strcmp(key, "schedule")) {
-    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "schedule must be 0 or 1");
-    c->schedule = value;
-    c->order_valid = 0;
+  if (!std::strcmp(key, "layout")) {
+    if (value != cvr::kLayoutBrick && value != cvr::kLayoutLinear)
+      return fail(c, CVR_ERR_ARG, "layout must be 0 (bricked) or 1 (linear)");
+    c->layout = value;   // takes effect at the next cvr_set_volume
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "boost")) {
+    if (value < 0 || value > 100) return fail(c, CVR_ERR_ARG, "boost must be a percentage");
+    c->boost_pct = value;
     return CVR_OK;
   }
   return fail(c, CVR_ERR_ARG, "unknown option '%s'", key);
@@ -243,7 +248,8 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!c || !key) return -1;
   if (!std::strcmp(key, "batch")) return c->batch;
   if (!std::strcmp(key, "tile_order")) return c->use_order;
-  if (!std::strcmp(key, "schedule")) return c->schedule;
+  if (!std::strcmp(key, "layout")) return c->layout;
+  if (!std::strcmp(key, "boost")) return c->boost_pct;
   return -1;
 }
 
@@ -290,7 +296,7 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
   HIP_TRY(c, hipMalloc(&d_lut, nv * sizeof(uint16_t)));
   hipError_t e = hipMemcpyAsync(d_lut, lut.data(), nv * sizeof(uint16_t), hipMemcpyHostToDevice,
                                 c->stream);
-  c->cells = cvr::make_cell_grid(c->N);
+  c->cells = cvr::make_cell_grid(c->N, c->layout);
   c->cells_bytes = cvr::cell_count(c->cells) * 16;
   if (e == hipSuccess) e = hipMalloc(&c->d_cells, c->cells_bytes);
   if (e == hipSuccess)
@@ -419,11 +425,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   size_t npix;
   if (!packed) {
     A.packed = 0;
-    plan.ntile_x = (f->width + 7) / 8;
-    plan.ntile_y = (f->height + 7) / 8;
-    plan.ntiles = plan.ntile_x * plan.ntile_y;
-    plan.nbx = (f->width + 15) / 16;
-    plan.nblocks = plan.nbx * ((f->height + 15) / 16);
+    plan.ntiles = ((f->width + 7) / 8) * ((f->height + 7) / 8);
     npix = (size_t)f->width * f->height;
   } else {
     A.packed = 1;
@@ -432,12 +434,11 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     A.my_tiles = cvr_tiles_for_rank(f, f->rank);
     const int s8 = f->tile_size / 8;
     plan.ntiles = A.my_tiles * s8 * s8;
-    plan.nbx = f->tile_size / 16;
-    plan.nblocks = A.my_tiles * plan.nbx * plan.nbx;
     npix = (size_t)A.my_tiles * f->tile_size * f->tile_size;
   }
   A.ntiles = plan.ntiles;
-  plan.wave_blocks = c->schedule == 1;
+  plan.order_slots = 8 * ((plan.ntiles + 7) / 8);
+  plan.boost = (int)(((long long)(plan.ntiles / 8) * c->boost_pct) / 100);
 
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
@@ -463,10 +464,9 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   // Longest-first (LPT) order learned from the previous frame of the same plan:
   // the kernel records each wave tile's critical path, tile_order_kernel sorts
   // every XCD band by it (and re-arms the queue heads) for the next frame.
-  const int units = plan.wave_blocks ? plan.ntiles : plan.nblocks;
-  const bool can_order = c->use_order && (plan.wave_blocks || !packed) && (units + 7) / 8 <= 16384;
-  const int key = (plan.wave_blocks ? 1 : 2) ^ (plan.ntiles << 2) ^ (plan.nblocks << 20) ^
-                  (packed ? (f->rank << 8) ^ (f->nranks << 12) : 0);
+  const int units = plan.order_slots;
+  const bool can_order = c->use_order && (units + 7) / 8 <= 16384;
+  const int key = (plan.ntiles << 2) ^ (packed ? (f->rank << 8) ^ (f->nranks << 12) ^ 1 : 0);
   const int* order = nullptr;
   uint32_t* tile_cost = nullptr;
   if (can_order) {

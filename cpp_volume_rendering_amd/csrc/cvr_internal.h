@@ -16,10 +16,15 @@ namespace cvr {
 // One sample = one 16-byte (fp16 corners) load.  Cells are grouped in 4x4x4
 // bricks (1 KiB) so that a wave's 8x8 ray tile hits few cache lines.
 constexpr int kBrick = 4;
+constexpr int kLayoutBrick = 0;   // 4x4x4-cell bricks (1 KiB), bricks x-fastest
+constexpr int kLayoutLinear = 1;  // (N+1)^3 cells, x-fastest
 
 struct CellGrid {
+  int layout;
   int cx, cy, cz;        // cells per axis = N + 1
-  int bx, by, bz;        // bricks per axis = ceil(cells / 4)
+  int bx, by, bz;        // bricks per axis = ceil(cells / 4)        (brick layout)
+  int pitch_y, pitch_z;  // cx, cx*cy                                (linear layout)
+  long long linear_origin;  // index of cell (1,1,1) = texel (0,0,0) (linear layout)
 };
 
 // Per-frame constants of the rc1pass kernel (passed by value).
@@ -48,13 +53,11 @@ struct Rc1passArgs {
   int ntiles;                        // 8x8 wave tiles of this launch
 };
 
-// How one frame is cut into work (block schedule or persistent tile queue).
+// How one frame is cut into work: one 8x8 wave tile per workgroup.
 struct RenderPlan {
-  int wave_blocks;                   // 1: one wave tile per workgroup, 0: 2x2 tiles
-  int nblocks;                       // 16x16 blocks (block schedule)
-  int nbx;                           // blocks per row (unpacked) / per tile row (packed)
-  int ntiles;                        // 8x8 wave tiles
-  int ntile_x, ntile_y;              // wave-tile grid (unpacked)
+  int ntiles;                        // 8x8 wave tiles (one workgroup each)
+  int order_slots;                   // 8 * ceil(ntiles / 8): grid size under an LPT order
+  int boost;                         // per band, the first `boost` tiles run at priority 2
 };
 
 struct Ctx {
@@ -80,7 +83,8 @@ struct Ctx {
   int grad_mode = 0;
   // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
   int batch = 4;
-  int schedule = 1;                // 0: 2x2 wave tiles per workgroup, 1: one wave tile per workgroup
+  int layout = kLayoutBrick;       // cell layout used by the next cvr_set_volume
+  int boost_pct = 5;               // % of every band's longest tiles run at raised priority
   int use_order = 1;               // 1: longest-first (LPT) from the previous frame's costs
   int* d_order = nullptr;          // unit permutation for the next frame
   uint32_t* d_tile_cost = nullptr; // per-wave-tile critical path of the last frame
@@ -106,16 +110,21 @@ hipError_t launch_tile_order(const uint32_t* tile_cost, const RenderPlan& plan, 
 hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
                                int nranks, int tiles_per_rank_max, hipStream_t s);
 
-inline CellGrid make_cell_grid(const int N[3]) {
+inline CellGrid make_cell_grid(const int N[3], int layout) {
   CellGrid g;
+  g.layout = layout;
   g.cx = N[0] + 1; g.cy = N[1] + 1; g.cz = N[2] + 1;
   g.bx = (g.cx + kBrick - 1) / kBrick;
   g.by = (g.cy + kBrick - 1) / kBrick;
   g.bz = (g.cz + kBrick - 1) / kBrick;
+  g.pitch_y = g.cx;
+  g.pitch_z = g.cx * g.cy;
+  g.linear_origin = 1 + (long long)g.pitch_y + (long long)g.pitch_z;
   return g;
 }
 
 inline size_t cell_count(const CellGrid& g) {
+  if (g.layout == kLayoutLinear) return (size_t)g.cx * g.cy * g.cz;
   return (size_t)g.bx * g.by * g.bz * (kBrick * kBrick * kBrick);
 }
 

@@ -19,12 +19,20 @@ __global__ void build_cells_kernel(const VT* __restrict__ vox, const uint16_t* _
   size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= ncells) return;
   uint32_t i = (uint32_t)idx;
-  uint32_t inner = i & 63u, brick = i >> 6;
-  int a = (int)(inner & 3u), b = (int)((inner >> 2) & 3u), c = (int)(inner >> 4);
-  int bxi = (int)(brick % (uint32_t)g.bx);
-  uint32_t rest = brick / (uint32_t)g.bx;
-  int byi = (int)(rest % (uint32_t)g.by), bzi = (int)(rest / (uint32_t)g.by);
-  a += bxi * 4; b += byi * 4; c += bzi * 4;
+  int a, b, c;
+  if (g.layout == kLayoutLinear) {
+    a = (int)(i % (uint32_t)g.cx);
+    uint32_t r = i / (uint32_t)g.cx;
+    b = (int)(r % (uint32_t)g.cy);
+    c = (int)(r / (uint32_t)g.cy);
+  } else {
+    uint32_t inner = i & 63u, brick = i >> 6;
+    a = (int)(inner & 3u); b = (int)((inner >> 2) & 3u); c = (int)(inner >> 4);
+    int bxi = (int)(brick % (uint32_t)g.bx);
+    uint32_t rest = brick / (uint32_t)g.bx;
+    int byi = (int)(rest % (uint32_t)g.by), bzi = (int)(rest / (uint32_t)g.by);
+    a += bxi * 4; b += byi * 4; c += bzi * 4;
+  }
   uint4 r = make_uint4(0, 0, 0, 0);
   if (a < g.cx && b < g.cy && c < g.cz) {
     int x0 = max(a - 1, 0), x1 = min(a, nx - 1);

@@ -11,9 +11,10 @@
 //   * per-ray state in registers; K samples addressed and fetched per batch
 //     (K x 16 B in flight per lane), classified, then composited in order with
 //     the per-lane early ray termination (dst.a > 0.99);
-//   * scheduling: one wave tile (or 2x2 of them) per workgroup, each XCD owns
-//     one horizontal band of the screen (L2 locality) and receives its tiles
-//     longest-first when the previous frame's per-tile costs are known (LPT).
+//   * scheduling: one wave tile per workgroup; each XCD owns one horizontal
+//     band of the screen (L2 locality) and receives its tiles longest-first
+//     when the previous frame's per-tile costs are known (LPT), the longest
+//     ones at raised wave priority.
 //
 // Arithmetic follows CVR-SPEC: explicit fmaf, IEEE div/sqrt, the
 // polynomial cvr_expf / cvr_powf.  The file is compiled with -ffp-contract=off
@@ -60,35 +61,52 @@ __device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lane
 // ---------------------------------------------------------------------------
 
 // One sample's cell address + weights (stage 1 of the batched march).
-struct SamplePos { uint32_t idx; float ax, ay, az; int ix, iy, iz; };
+struct SamplePos { int idx; float ax, ay, az; int ix, iy, iz; };   // idx may be < 0 (linear: origin-relative)
 
+template <int LAYOUT>
 __device__ __forceinline__ SamplePos sample_pos(float x, float y, float z, const Rc1passArgs& A,
                                                 uint32_t bxby) {
-  // GL_LINEAR texel-centre convention; positions are inside [-0.5, N-0.5] for
-  // every hit ray, so the CLAMP_TO_EDGE corner clamp is folded into the padded
-  // cell grid (cell = floor(x)+1 in [0, N]; the integer clamp only guards memory).
+  // GL_LINEAR texel-centre convention.  Clamping to [-1, N-1] (one v_med3) is
+  // value-neutral under CLAMP_TO_EDGE and keeps the padded cell index
+  // floor(x)+1 inside [0, N].
+  x = __builtin_amdgcn_fmed3f(x, -1.0f, A.nm1[0]);
+  y = __builtin_amdgcn_fmed3f(y, -1.0f, A.nm1[1]);
+  z = __builtin_amdgcn_fmed3f(z, -1.0f, A.nm1[2]);
   float fx = floorf(x), fy = floorf(y), fz = floorf(z);
   SamplePos p;
   p.ax = x - fx; p.ay = y - fy; p.az = z - fz;
   p.ix = (int)fx; p.iy = (int)fy; p.iz = (int)fz;
-  uint32_t cx = (uint32_t)min(max(p.ix + 1, 0), A.N[0]);
-  uint32_t cy = (uint32_t)min(max(p.iy + 1, 0), A.N[1]);
-  uint32_t cz = (uint32_t)min(max(p.iz + 1, 0), A.N[2]);
-  uint32_t brick = __umul24(cz >> 2, bxby) + __umul24(cy >> 2, (uint32_t)A.cells.bx) + (cx >> 2);
-  p.idx = (brick << 6) | ((cz & 3u) << 4) | ((cy & 3u) << 2) | (cx & 3u);
+  if (LAYOUT == kLayoutLinear) {
+    // cell (ix+1, iy+1, iz+1) of the (N+1)^3 grid; the +1 offsets live in the base pointer
+    p.idx = __mul24(p.iz, A.cells.pitch_z) + __mul24(p.iy, A.cells.pitch_y) + p.ix;
+  } else {
+    uint32_t cx = (uint32_t)(p.ix + 1), cy = (uint32_t)(p.iy + 1), cz = (uint32_t)(p.iz + 1);
+    uint32_t brick = __umul24(cz >> 2, bxby) + __umul24(cy >> 2, (uint32_t)A.cells.bx) + (cx >> 2);
+    p.idx = (int)((brick << 6) | ((cz & 3u) << 4) | ((cy & 3u) << 2) | (cx & 3u));
+  }
   return p;
 }
 
+// (float)hi - (float)lo of a packed fp16 pair, in ONE mixed-precision FMA
+// (hi * 1.0 + (-lo), computed exactly then rounded once = the fp32 subtraction
+// of the two exactly-converted halves).
+__device__ __forceinline__ float pair_diff(uint32_t w) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%1 op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(w));
+  return d;
+}
+
+// lerp(lo, hi, t) of a packed fp16 pair = fmaf(t, hi - lo, lo): two v_fma_mix_f32.
+__device__ __forceinline__ float pair_lerp(uint32_t w, float t) {
+  half2_t p = __builtin_bit_cast(half2_t, w);
+  return fmaf(t, pair_diff(w), (float)p.x);
+}
+
 __device__ __forceinline__ float trilerp_cell(uint4 raw, float ax, float ay, float az) {
-  float v000, v100, v010, v110, v001, v101, v011, v111;
-  h2f2(raw.x, v000, v100);
-  h2f2(raw.y, v010, v110);
-  h2f2(raw.z, v001, v101);
-  h2f2(raw.w, v011, v111);
-  float c00 = lerpf(v000, v100, ax);
-  float c10 = lerpf(v010, v110, ax);
-  float c01 = lerpf(v001, v101, ax);
-  float c11 = lerpf(v011, v111, ax);
+  float c00 = pair_lerp(raw.x, ax);    // (v000, v100)
+  float c10 = pair_lerp(raw.y, ax);    // (v010, v110)
+  float c01 = pair_lerp(raw.z, ax);    // (v001, v101)
+  float c11 = pair_lerp(raw.w, ax);    // (v011, v111)
   float c0 = lerpf(c00, c10, ay);
   float c1 = lerpf(c01, c11, ay);
   return lerpf(c0, c1, az);
@@ -121,7 +139,7 @@ __device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint2* _
 // One ray of ray_marching_1p.comp:87-176.  The arithmetic per sample is
 // exactly the reference's sequential loop (s accumulates h one step at a time);
 // the batching only changes when the loads are issued.
-template <int K, bool PHONG>
+template <int K, bool PHONG, int LAYOUT>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
                                           const uint2* __restrict__ grad,
                                           const float4* __restrict__ tfp, int px, int py,
@@ -172,8 +190,8 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       hj[j] = fminf(step, D - ss);
       tj[j] = fmaf(hj[j], 0.5f, ss);
       ss = ss + hj[j];
-      sp[j] = sample_pos(fmaf(dt.x, tj[j], o.x), fmaf(dt.y, tj[j], o.y), fmaf(dt.z, tj[j], o.z), A,
-                         bxby);
+      sp[j] = sample_pos<LAYOUT>(fmaf(dt.x, tj[j], o.x), fmaf(dt.y, tj[j], o.y),
+                                 fmaf(dt.z, tj[j], o.z), A, bxby);
       raw[j] = cells[sp[j].idx];
     }
     // stage 2: density and transfer-function classification (padded LDS table:
@@ -185,7 +203,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       float x = fmaf(dens, fn, -0.5f);
       float fl = floorf(x);
       float a = x - fl;
-      int i = min(max((int)fl + 1, 0), n);
+      int i = (int)fl + 1;   // dens in [0,1] (a lerp of [0,1] values) -> i in [0, n]
       float4 t0 = tfp[i], t1 = tfp[i + 1];
       src[j] = make_float4(lerpf(t0.x, t1.x, a), lerpf(t0.y, t1.y, a), lerpf(t0.z, t1.z, a),
                            lerpf(t0.w, t1.w, a));
@@ -252,62 +270,50 @@ __device__ __forceinline__ void finish_tile(const Rc1passArgs& A, int t, int lan
 // Kernels
 // ---------------------------------------------------------------------------
 
-// Block schedule.  WPB = 4: a workgroup is 2x2 wave tiles (16x16 px); WPB = 1:
-// a workgroup is one wave tile (8x8 px), so a long ray only holds its own wave
-// slot.  Logical unit L comes from the LPT order when given, else from the
-// XCD-banded remap (units b and b+8 share an XCD, so XCD b%8 gets one
-// contiguous band of the screen).
-template <int K, bool PHONG, int WPB>
-__global__ void __launch_bounds__(64 * WPB)
-rc1pass_blocks_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
-                      const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
-                      float4* __restrict__ out, uint32_t* __restrict__ samples,
-                      unsigned long long* __restrict__ total, const int* __restrict__ order,
-                      uint32_t* __restrict__ tile_cost, int nunits, int nbx) {
+// One workgroup = one wave = one 8x8 tile, so a long ray only ever holds its
+// own wave slot.  Tile t comes from the LPT order when given (each XCD gets its
+// screen band longest-first), else from the XCD-banded remap (blocks b and b+8
+// share an XCD, so XCD b%8 gets one contiguous band of the screen).  The first
+// `boost` tiles of every band (its longest, by the previous frame) raise their
+// wave priority so their long dependency chains issue ahead of short tiles.
+template <int K, bool PHONG, int LAYOUT>
+__global__ void __launch_bounds__(64)
+rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
+                    const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
+                    float4* __restrict__ out, uint32_t* __restrict__ samples,
+                    unsigned long long* __restrict__ total, const int* __restrict__ order,
+                    uint32_t* __restrict__ tile_cost, int boost) {
   extern __shared__ float4 tfp[];
   load_tf_lds(tfp, tf_g, A.tf_n);
-  const int b = blockIdx.x;
-  int L;
-  if (order) L = order[b];
-  else if ((nunits & 7) == 0) L = (b & 7) * (nunits >> 3) + (b >> 3);
-  else L = b;
-  const int lane = threadIdx.x & 63, wave = WPB == 1 ? 0 : (threadIdx.x >> 6);
+  const int b = blockIdx.x, nt = A.ntiles;
   int t;
-  bool tile_ok = true;
-  if (WPB == 1) {
-    t = L;
-  } else if (!A.packed) {   // block L = (bx, by) in 16x16 units -> wave tile (2bx + w&1, 2by + w>>1)
-    const int by = L / nbx, bx = L - by * nbx;
-    const int ntile_x = (A.W + 7) >> 3, ntile_y = (A.H + 7) >> 3;
-    const int ty = (by << 1) + (wave >> 1), tx = (bx << 1) + (wave & 1);
-    tile_ok = tx < ntile_x && ty < ntile_y;
-    t = ty * ntile_x + tx;
-  } else {                  // packed: block = 2x2 sub-tiles of one rank tile; nbx = blocks per tile row
-    const int s = A.tile >> 3, bpt = nbx * nbx;
-    const int k = L / bpt, j = L - k * bpt;
-    const int sy = ((j / nbx) << 1) + (wave >> 1), sx = ((j % nbx) << 1) + (wave & 1);
-    t = k * s * s + sy * s + sx;
+  if (order) {
+    t = order[b];
+    if (t < 0) return;   // padding slot of a shorter band
+    if ((b >> 3) < boost) __builtin_amdgcn_s_setprio(2);
+  } else if ((nt & 7) == 0) {
+    t = (b & 7) * (nt >> 3) + (b >> 3);
+  } else {
+    t = b;
   }
-  if (!tile_ok) return;     // wave-uniform: a wave tile past the image edge
+  const int lane = threadIdx.x;
   int px, py;
   long long oidx;
   tile_pixel(A, t, lane, px, py, oidx);
   const bool inside = px < A.W && py < A.H;
   float4 dst = make_float4(0.f, 0.f, 0.f, 0.f);
   uint32_t cnt = 0;
-  if (inside) march_ray<K, PHONG>(A, cells, grad, tfp, px, py, dst, cnt);
+  if (inside) march_ray<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
   finish_tile(A, t, lane, inside, oidx, dst, cnt, out, samples, total, tile_cost);
 }
 
 // LPT order from the previous frame's per-tile costs: workgroup `seg` sorts the
-// units of XCD band seg (bitonic sort in LDS, descending cost, ties by index)
+// tiles of XCD band seg (bitonic sort in LDS, descending cost, ties by index)
 // and deals them to physical blocks seg, seg+8, seg+16, ... (the blocks XCD
 // seg receives), so every XCD keeps its screen band and starts with its
-// longest units.  A unit is one wave tile, or (blocks_mode) a 16x16 block whose
-// cost sums its 4 wave tiles.
+// longest tiles.
 __global__ void __launch_bounds__(1024)
-tile_order_kernel(const uint32_t* __restrict__ tile_cost, int nunits, int blocks_mode, int nbx,
-                  int ntile_x, int ntile_y, int* __restrict__ order) {
+tile_order_kernel(const uint32_t* __restrict__ tile_cost, int nunits, int* __restrict__ order) {
   extern __shared__ unsigned long long keys[];
   const int b0 = (blockIdx.x * nunits) >> 3, b1 = ((blockIdx.x + 1) * nunits) >> 3;
   const int seg = b1 - b0;
@@ -316,17 +322,8 @@ tile_order_kernel(const uint32_t* __restrict__ tile_cost, int nunits, int blocks
   for (int i = threadIdx.x; i < P; i += blockDim.x) {
     unsigned long long k = 0;
     if (i < seg) {
-      uint32_t u = (uint32_t)(b0 + i), c = 0;
-      if (blocks_mode) {
-        int by = (int)u / nbx, bx = (int)u - by * nbx;
-        for (int w = 0; w < 4; w++) {
-          int ty = (by << 1) + (w >> 1), tx = (bx << 1) + (w & 1);
-          if (tx < ntile_x && ty < ntile_y) c += tile_cost[ty * ntile_x + tx];
-        }
-      } else {
-        c = tile_cost[u];
-      }
-      k = ((unsigned long long)c << 32) | (0xffffffffu - u);
+      uint32_t u = (uint32_t)(b0 + i);
+      k = ((unsigned long long)tile_cost[u] << 32) | (0xffffffffu - u);
     }
     keys[i] = k;
   }
@@ -344,6 +341,9 @@ tile_order_kernel(const uint32_t* __restrict__ tile_cost, int nunits, int blocks
       __syncthreads();
     }
   }
+  // band sizes differ by at most one: bands with the extra tile come last
+  // ((b*n)>>3 rounding), so physical block seg + 8*i exists for every i < seg
+  // as long as the grid is launched with 8*ceil(n/8) blocks, see launcher
   for (int i = threadIdx.x; i < seg; i += blockDim.x) {
     int u = (int)(0xffffffffu - (uint32_t)keys[i]);
     order[blockIdx.x + 8 * i] = u;
@@ -354,20 +354,29 @@ tile_order_kernel(const uint32_t* __restrict__ tile_cost, int nunits, int blocks
 // Launchers
 // ---------------------------------------------------------------------------
 
+template <int K, bool PHONG, int LAYOUT>
+static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
+                             unsigned long long* total, const int* order, uint32_t* tile_cost,
+                             const RenderPlan& plan, hipStream_t s) {
+  size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
+  const uint4* cells = (const uint4*)c.d_cells;
+  if (LAYOUT == kLayoutLinear) cells += c.cells.linear_origin;   // cell (1,1,1) <-> texel (0,0,0)
+  // with an order the grid is 8*ceil(n/8) blocks; the padding blocks (unused
+  // order slots) are marked -1 and exit at once
+  int grid = order ? plan.order_slots : plan.ntiles;
+  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, LAYOUT>), dim3(grid), dim3(64), lds, s, a,
+                     cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, total,
+                     order, tile_cost, order ? plan.boost : 0);
+  return hipGetLastError();
+}
+
 template <int K, bool PHONG>
 static hipError_t launch_kp(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                             unsigned long long* total, const int* order, uint32_t* tile_cost,
                             const RenderPlan& plan, hipStream_t s) {
-  size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
-  if (plan.wave_blocks)
-    hipLaunchKernelGGL((rc1pass_blocks_kernel<K, PHONG, 1>), dim3(plan.ntiles), dim3(64), lds, s,
-                       a, (const uint4*)c.d_cells, (const uint2*)c.d_grad, (const float4*)c.d_tf,
-                       out, samples, total, order, tile_cost, plan.ntiles, 0);
-  else
-    hipLaunchKernelGGL((rc1pass_blocks_kernel<K, PHONG, 4>), dim3(plan.nblocks), dim3(256), lds, s,
-                       a, (const uint4*)c.d_cells, (const uint2*)c.d_grad, (const float4*)c.d_tf,
-                       out, samples, total, order, tile_cost, plan.nblocks, plan.nbx);
-  return hipGetLastError();
+  return c.cells.layout == kLayoutLinear
+             ? launch_kpl<K, PHONG, kLayoutLinear>(c, a, out, samples, total, order, tile_cost, plan, s)
+             : launch_kpl<K, PHONG, kLayoutBrick>(c, a, out, samples, total, order, tile_cost, plan, s);
 }
 
 template <int K>
@@ -381,25 +390,32 @@ static hipError_t launch_k(const Ctx& c, const Rc1passArgs& a, bool phong, float
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
                           uint32_t* samples, unsigned long long* total, const int* order,
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
-  if (plan.nblocks <= 0 || a.ntiles <= 0) return hipSuccess;
+  if (a.ntiles <= 0) return hipSuccess;
   if (a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
   switch (c.batch) {
-    case 1: return launch_k<1>(c, a, phong, out, samples, total, order, tile_cost, plan, s);
     case 2: return launch_k<2>(c, a, phong, out, samples, total, order, tile_cost, plan, s);
     case 8: return launch_k<8>(c, a, phong, out, samples, total, order, tile_cost, plan, s);
     default: return launch_k<4>(c, a, phong, out, samples, total, order, tile_cost, plan, s);
   }
 }
 
+__global__ void fill_int_kernel(int* p, int n, int v) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
 hipError_t launch_tile_order(const uint32_t* tile_cost, const RenderPlan& plan, int* order,
                              hipStream_t s) {
-  const int nunits = plan.wave_blocks ? plan.ntiles : plan.nblocks;
+  const int nunits = plan.ntiles;
   const int seg = (nunits + 7) >> 3;
   int P = 1;
   while (P < seg) P <<= 1;
   if (P > 16384) return hipErrorInvalidValue;
+  if (plan.order_slots != nunits)   // padding slots of short bands
+    hipLaunchKernelGGL(fill_int_kernel, dim3((plan.order_slots + 255) / 256), dim3(256), 0, s,
+                       order, plan.order_slots, -1);
   hipLaunchKernelGGL(tile_order_kernel, dim3(8), dim3(1024), (size_t)P * 8, s, tile_cost, nunits,
-                     plan.wave_blocks ? 0 : 1, plan.nbx, plan.ntile_x, plan.ntile_y, order);
+                     order);
   return hipGetLastError();
 }
 

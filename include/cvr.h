@@ -125,11 +125,14 @@ const char* cvr_last_error(const cvr_ctx* ctx);
  * A new context starts on a private non-blocking stream of its own. */
 cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
 /* Tuning options (results are identical for every setting):
- *   "batch"      samples addressed + fetched per batch of the march (1, 2, 4, 8; default 4)
- *   "schedule"   1: one 8x8 wave tile per workgroup (default); 0: 2x2 wave tiles
+ *   "batch"      samples addressed + fetched per batch of the march (2, 4, 8; default 4)
  *   "tile_order" 1: each XCD takes the tiles of its screen band longest-first (LPT),
  *                using the previous frame's per-tile critical paths (default);
- *                0: screen order */
+ *                0: screen order
+ *   "boost"      percent of each band's longest tiles launched at raised wave
+ *                priority (with tile_order 1; default 5)
+ *   "layout"     cell layout of the next cvr_set_volume: 0 bricked 4^3 (default),
+ *                1 linear x-fastest */
 cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
 int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);
