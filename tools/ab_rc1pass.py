@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""A/B timing of rc1pass kernel variants (batch size, tile order) in ONE process,
-interleaved rounds (methodology rule 24).  Every variant's image is checked bit-equal
-to the first variant's.  Usage: python tools/ab_rc1pass.py [--size 512] [--res 1024]"""
+"""A/B timing of rc1pass kernel variants in ONE process, interleaved rounds
+(methodology rule 24).  Every variant's image is checked bit-equal to the first
+variant's.  Variant syntax: L<layout>b<batch>o<tile_order>p<boost%>, e.g. L0b4o1p5.
+Usage: python tools/ab_rc1pass.py [--size 512] [--res 1024] [--variants ...]"""
 import argparse
 import ctypes
 import json
 import os
+import re
 import sys
 
 import numpy as np
@@ -17,6 +19,13 @@ from cpp_volume_rendering_amd import datasets as D  # noqa: E402
 from cpp_volume_rendering_amd.renderer import Camera, Device, build_tf_rgbt, make_frame  # noqa: E402
 
 
+def parse_variant(v):
+    m = re.fullmatch(r"L(\d)b(\d)o(\d)p(\d+)", v)
+    if not m:
+        raise ValueError(f"bad variant {v}")
+    return tuple(int(x) for x in m.groups())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=512)
@@ -24,18 +33,24 @@ def main():
     ap.add_argument("--field", default="ml")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=20)
-    ap.add_argument("--variants", default="s0b4o1,s1b4o1q2,s1b4o1q4,s1b4o1q5,s1b4o1q8,s1b4o1q16,s1b4o0q5")
+    ap.add_argument("--variants", default="L0b4o1p0,L0b4o1p5,L0b4o1p15,L1b4o1p5,L0b8o1p5,L1b8o1p5")
     ap.add_argument("--phong", action="store_true")
     a = ap.parse_args()
     n, W = a.size, a.res
     vol = D.marschner_lobb_u8(n) if a.field == "ml" else D.blobs_u8(n)
-    dev = Device(0)
-    dev.set_volume(vol, D.voxel_scale(n))
-    dev.set_transfer_function(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
-    if a.phong:
-        dev.set_gradient(1)
+    variants = a.variants.split(",")
+    parsed = {v: parse_variant(v) for v in variants}
+    devs = {}
     s = torch.cuda.Stream()
-    dev.set_stream(s.cuda_stream)
+    for layout in sorted({p[0] for p in parsed.values()}):
+        dev = Device(0)
+        N.check(N.lib().cvr_set_option(dev.handle, b"layout", layout), "layout")
+        dev.set_volume(vol, D.voxel_scale(n))
+        dev.set_transfer_function(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
+        if a.phong:
+            dev.set_gradient(1)
+        dev.set_stream(s.cuda_stream)
+        devs[layout] = dev
     frame = make_frame(Camera(**D.INITIAL_STATE_CAMERA), W, W)
     p = N.Rc1passParams()
     p.apply_gradient_shading = int(a.phong)
@@ -47,51 +62,43 @@ def main():
     out = N.Output(img.data_ptr(), None, tot.data_ptr(), 1)
     L = N.lib()
 
-    def run(frames):
+    def run(dev, frames):
         for _ in range(frames):
             N.check(L.cvr_render_rc1pass(dev.handle, ctypes.byref(frame), ctypes.byref(p),
                                          ctypes.byref(out)), "render", dev.handle)
 
-    variants = a.variants.split(",")
     res = {v: [] for v in variants}
     ref_img = None
     S = None
-    for rnd in range(a.rounds):
+    for _ in range(a.rounds):
         for v in variants:
-            qb = 0
-            if "q" in v:
-                qb = int(v[v.index("q") + 1:])
-                v_ = v[:v.index("q")]
-            else:
-                v_ = v
-            sch = int(v_[1:v_.index("b")])
-            b, o = int(v_[v_.index("b") + 1:v_.index("o")]), int(v_[v_.index("o") + 1:])
-            N.check(L.cvr_set_option(dev.handle, b"schedule", sch), "opt")
+            layout, b, o, boost = parsed[v]
+            dev = devs[layout]
             N.check(L.cvr_set_option(dev.handle, b"batch", b), "opt")
             N.check(L.cvr_set_option(dev.handle, b"tile_order", o), "opt")
+            N.check(L.cvr_set_option(dev.handle, b"boost", boost), "opt")
             with torch.cuda.stream(s):
-                run(3)   # warm up + learn the order
+                run(dev, 3)   # warm up + learn the order
                 tot.zero_()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
-                run(a.frames)
+                run(dev, a.frames)
                 e1.record(s)
             s.synchronize()
-            ms = e0.elapsed_time(e1) / a.frames
-            res[v].append(ms)
+            res[v].append(e0.elapsed_time(e1) / a.frames)
             cur = img.cpu().numpy()
             if ref_img is None:
                 ref_img = cur
                 S = int(tot.item()) // a.frames
             else:
                 assert np.array_equal(cur.view(np.uint32), ref_img.view(np.uint32)), f"{v} differs"
-    out_rows = []
+    rows = []
     for v in variants:
         med = float(np.median(res[v]))
-        out_rows.append({"variant": v, "median_ms": round(med, 4), "min_ms": round(min(res[v]), 4),
-                         "gsamples_s": round(S / med / 1e6, 1)})
+        rows.append({"variant": v, "median_ms": round(med, 4), "min_ms": round(min(res[v]), 4),
+                     "gsamples_s": round(S / med / 1e6, 1)})
     print(json.dumps({"size": n, "res": W, "field": a.field, "phong": a.phong,
-                      "samples_per_frame": S, "rows": out_rows}, indent=1))
+                      "samples_per_frame": S, "rows": rows}, indent=1))
 
 
 if __name__ == "__main__":
