@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
-VAR=${1:-s0b4o1}
+VAR=${1:-L0b4o1p5}
 EXTRA=${2:-}
 mkdir -p gpurun_out/pmc
 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
