@@ -198,6 +198,7 @@ void cvr_destroy(cvr_ctx* ctx) {
   free_dev(c->d_scratch);
   p = c->d_order; free_dev(p); c->d_order = nullptr;
   p = c->d_tile_cost; free_dev(p); c->d_tile_cost = nullptr;
+  p = c->d_tile_stats; free_dev(p); c->d_tile_stats = nullptr;
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -235,6 +236,10 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->layout = value;   // takes effect at the next cvr_set_volume
     return CVR_OK;
   }
+  if (!std::strcmp(key, "tile_stats")) {
+    c->tile_stats = value != 0;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "boost")) {
     if (value < 0 || value > 100) return fail(c, CVR_ERR_ARG, "boost must be a percentage");
     c->boost_pct = value;
@@ -250,6 +255,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "tile_order")) return c->use_order;
   if (!std::strcmp(key, "layout")) return c->layout;
   if (!std::strcmp(key, "boost")) return c->boost_pct;
+  if (!std::strcmp(key, "tile_stats")) return c->tile_stats;
   return -1;
 }
 
@@ -437,6 +443,15 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     npix = (size_t)A.my_tiles * f->tile_size * f->tile_size;
   }
   A.ntiles = plan.ntiles;
+  A.tile_stats = nullptr;
+  if (c->tile_stats) {
+    if (c->tile_stats_n < plan.ntiles) {
+      void* p = c->d_tile_stats; free_dev(p); c->d_tile_stats = nullptr; c->tile_stats_n = 0;
+      HIP_TRY(c, hipMalloc((void**)&c->d_tile_stats, (size_t)plan.ntiles * 32));
+      c->tile_stats_n = plan.ntiles;
+    }
+    A.tile_stats = c->d_tile_stats;
+  }
   plan.order_slots = 8 * ((plan.ntiles + 7) / 8);
   plan.boost = (int)(((long long)(plan.ntiles / 8) * c->boost_pct) / 100);
 
@@ -495,6 +510,19 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     if (o->total) HIP_TRY(c, hipMemcpyAsync(o->total, d_total, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
   }
+  return CVR_OK;
+}
+
+cvr_status cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int* out_tiles) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c || !out_tiles) return CVR_ERR_ARG;
+  *out_tiles = c->tile_stats_n;
+  if (!out) return CVR_OK;
+  if (!c->d_tile_stats) return fail(c, CVR_ERR_STATE, "tile_stats option was not enabled");
+  int n = max_tiles < c->tile_stats_n ? max_tiles : c->tile_stats_n;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpy(out, c->d_tile_stats, (size_t)n * 32, hipMemcpyDeviceToHost));
   return CVR_OK;
 }
 

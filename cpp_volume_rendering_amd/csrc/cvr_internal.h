@@ -51,6 +51,7 @@ struct Rc1passArgs {
   int tile, rank, nranks, ntx, my_tiles;
   int packed;
   int ntiles;                        // 8x8 wave tiles of this launch
+  unsigned long long* tile_stats;    // diagnostics (tile_stats option) or null
 };
 
 // How one frame is cut into work: one 8x8 wave tile per workgroup.
@@ -85,6 +86,9 @@ struct Ctx {
   int batch = 4;
   int layout = kLayoutBrick;       // cell layout used by the next cvr_set_volume
   int boost_pct = 5;               // % of every band's longest tiles run at raised priority
+  int tile_stats = 0;              // record per-tile timing (diagnostics)
+  unsigned long long* d_tile_stats = nullptr;
+  int tile_stats_n = 0;
   int use_order = 1;               // 1: longest-first (LPT) from the previous frame's costs
   int* d_order = nullptr;          // unit permutation for the next frame
   uint32_t* d_tile_cost = nullptr; // per-wave-tile critical path of the last frame

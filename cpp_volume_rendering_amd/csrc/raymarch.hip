@@ -297,6 +297,8 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     t = b;
   }
   const int lane = threadIdx.x;
+  unsigned long long t_start = 0;
+  if (A.tile_stats) t_start = __builtin_amdgcn_s_memrealtime();
   int px, py;
   long long oidx;
   tile_pixel(A, t, lane, px, py, oidx);
@@ -305,6 +307,20 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   uint32_t cnt = 0;
   if (inside) march_ray<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
   finish_tile(A, t, lane, inside, oidx, dst, cnt, out, samples, total, tile_cost);
+  if (A.tile_stats) {   // diagnostics: 100 MHz start/end stamps, longest ray, placement
+    uint32_t m = cnt;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+    unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if (lane == 0) {
+      A.tile_stats[t * 4 + 0] = t_start;
+      A.tile_stats[t * 4 + 1] = t_end;
+      A.tile_stats[t * 4 + 2] = m;
+      A.tile_stats[t * 4 + 3] = ((unsigned long long)b << 32) | hw;
+    }
+  }
 }
 
 // LPT order from the previous frame's per-tile costs: workgroup `seg` sorts the

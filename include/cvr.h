@@ -132,7 +132,8 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *   "boost"      percent of each band's longest tiles launched at raised wave
  *                priority (with tile_order 1; default 5)
  *   "layout"     cell layout of the next cvr_set_volume: 0 bricked 4^3 (default),
- *                1 linear x-fastest */
+ *                1 linear x-fastest
+ *   "tile_stats" 1: record per-tile timing of every frame (diagnostics) */
 cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
 int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);
@@ -178,6 +179,11 @@ cvr_status  cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* frame,
 cvr_status  cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* frame,
                                     const void* d_packed, int tiles_per_rank_max,
                                     void* d_rgba);
+
+/* Diagnostics (tile_stats option): for each 8x8 tile of the last frame, four
+ * uint64: start and end stamp (s_memrealtime, 100 MHz), its longest ray's
+ * iteration count, (workgroup << 32 | HW_ID).  out = NULL queries *out_tiles. */
+cvr_status  cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int* out_tiles);
 
 /* ----------------------------------------------------------------------------
  * Host-side helpers (native replacements for the reference's MSVC-only
