@@ -236,6 +236,12 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->layout = value;   // takes effect at the next cvr_set_volume
     return CVR_OK;
   }
+  if (!std::strcmp(key, "quad")) {
+    if (value < 0 || value > 100) return fail(c, CVR_ERR_ARG, "quad must be a percentage");
+    c->quad_pct = value;
+    c->order_valid = 0;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "tile_stats")) {
     c->tile_stats = value != 0;
     return CVR_OK;
@@ -256,6 +262,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "layout")) return c->layout;
   if (!std::strcmp(key, "boost")) return c->boost_pct;
   if (!std::strcmp(key, "tile_stats")) return c->tile_stats;
+  if (!std::strcmp(key, "quad")) return c->quad_pct;
   return -1;
 }
 
@@ -452,8 +459,15 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     }
     A.tile_stats = c->d_tile_stats;
   }
-  plan.order_slots = 8 * ((plan.ntiles + 7) / 8);
-  plan.boost = (int)(((long long)(plan.ntiles / 8) * c->boost_pct) / 100);
+  plan.quad_pct = c->quad_pct;
+  {
+    // entries per band: its tiles + 3 extra for each quad-split tile; bands
+    // differ by at most one tile, the largest one sets the slot count
+    const int seg_max = (plan.ntiles + 7) / 8;
+    const int per_band = seg_max + 3 * (int)(((long long)seg_max * plan.quad_pct) / 100);
+    plan.order_slots = 8 * per_band;
+    plan.boost = (int)(((long long)per_band * c->boost_pct) / 100);
+  }
 
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
@@ -481,7 +495,8 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   // every XCD band by it (and re-arms the queue heads) for the next frame.
   const int units = plan.order_slots;
   const bool can_order = c->use_order && (units + 7) / 8 <= 16384;
-  const int key = (plan.ntiles << 2) ^ (packed ? (f->rank << 8) ^ (f->nranks << 12) ^ 1 : 0);
+  const int key = (plan.ntiles << 2) ^ (plan.quad_pct << 24) ^
+                  (packed ? (f->rank << 8) ^ (f->nranks << 12) ^ 1 : 0);
   const int* order = nullptr;
   uint32_t* tile_cost = nullptr;
   if (can_order) {
@@ -491,6 +506,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
       c->order_units = 0;
       HIP_TRY(c, hipMalloc((void**)&c->d_order, (size_t)units * sizeof(int)));
       HIP_TRY(c, hipMalloc((void**)&c->d_tile_cost, (size_t)plan.ntiles * sizeof(uint32_t) + 64));
+      HIP_TRY(c, hipMemsetAsync(c->d_tile_cost, 0, (size_t)plan.ntiles * sizeof(uint32_t) + 64, s));
       c->order_units = units;
       c->order_valid = 0;
     }

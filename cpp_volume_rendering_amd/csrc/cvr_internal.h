@@ -23,6 +23,7 @@ struct CellGrid {
   int layout;
   int cx, cy, cz;        // cells per axis = N + 1
   int bx, by, bz;        // bricks per axis = ceil(cells / 4)        (brick layout)
+  int bxby;              // bx * by
   int pitch_y, pitch_z;  // cx, cx*cy                                (linear layout)
   long long linear_origin;  // index of cell (1,1,1) = texel (0,0,0) (linear layout)
 };
@@ -57,8 +58,9 @@ struct Rc1passArgs {
 // How one frame is cut into work: one 8x8 wave tile per workgroup.
 struct RenderPlan {
   int ntiles;                        // 8x8 wave tiles (one workgroup each)
-  int order_slots;                   // 8 * ceil(ntiles / 8): grid size under an LPT order
-  int boost;                         // per band, the first `boost` tiles run at priority 2
+  int order_slots;                   // grid size under an LPT order (8 x entries per band)
+  int boost;                         // per band, the first `boost` entries run at priority 2
+  int quad_pct;                      // per band, this % of the longest tiles march 4 lanes/ray
 };
 
 struct Ctx {
@@ -85,7 +87,8 @@ struct Ctx {
   // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
   int batch = 4;
   int layout = kLayoutBrick;       // cell layout used by the next cvr_set_volume
-  int boost_pct = 5;               // % of every band's longest tiles run at raised priority
+  int boost_pct = 5;               // % of every band's longest entries run at raised priority
+  int quad_pct = 10;               // % of every band's longest tiles marched 4 lanes per ray
   int tile_stats = 0;              // record per-tile timing (diagnostics)
   unsigned long long* d_tile_stats = nullptr;
   int tile_stats_n = 0;
@@ -109,7 +112,7 @@ hipError_t launch_gradient(const Ctx& c, int mode, hipStream_t s);
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
                           uint32_t* samples, unsigned long long* total, const int* order,
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s);
-hipError_t launch_tile_order(const uint32_t* tile_cost, const RenderPlan& plan, int* order,
+hipError_t launch_tile_order(uint32_t* tile_cost, const RenderPlan& plan, int* order,
                              hipStream_t s);
 hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
                                int nranks, int tiles_per_rank_max, hipStream_t s);
@@ -121,6 +124,7 @@ inline CellGrid make_cell_grid(const int N[3], int layout) {
   g.bx = (g.cx + kBrick - 1) / kBrick;
   g.by = (g.cy + kBrick - 1) / kBrick;
   g.bz = (g.cz + kBrick - 1) / kBrick;
+  g.bxby = g.bx * g.by;
   g.pitch_y = g.cx;
   g.pitch_z = g.cx * g.cy;
   g.linear_origin = 1 + (long long)g.pitch_y + (long long)g.pitch_z;

@@ -1,24 +1,27 @@
 // raymarch.hip — gfx950 kernels of the structured single-pass ray-caster.
 //
 // Re-designs cppvolrend's ray_marching_1p.comp (rc1pass) for CDNA4:
-//   * one wave64 = one 8x8 pixel tile (the reference's 8x8 local size,
-//     rc1prenderer.cpp:77-86);
 //   * no HIP texture objects on gfx950, so trilinear filtering is done in
 //     software from a padded "cell8" layout: every sample is ONE 16-byte load of
 //     the 8 fp16 corners GL_LINEAR + CLAMP_TO_EDGE would read from the R16F
-//     volume (libs/volvis_utils/utils.cpp:20-56), bricked 4x4x4 for locality;
+//     volume (libs/volvis_utils/utils.cpp:20-56); the x-lerps run as
+//     mixed-precision FMAs straight on the packed halves;
 //   * the 1D transfer function (RGBA16F, GenerateTexture_1D_RGBt) lives in LDS;
-//   * per-ray state in registers; K samples addressed and fetched per batch
-//     (K x 16 B in flight per lane), classified, then composited in order with
-//     the per-lane early ray termination (dst.a > 0.99);
-//   * scheduling: one wave tile per workgroup; each XCD owns one horizontal
-//     band of the screen (L2 locality) and receives its tiles longest-first
-//     when the previous frame's per-tile costs are known (LPT), the longest
-//     ones at raised wave priority.
+//   * two ways to march a ray, chosen per 8x8 screen tile:
+//       - ray-parallel: one lane per ray, K samples addressed and fetched per
+//         batch (K x 16 B in flight per lane), composited in order;
+//       - sample-parallel ("quad"): four lanes per ray, each fetching and
+//         classifying one of the next four samples, then an in-order composite
+//         over the quad with DPP broadcasts.  Used for the longest tiles: it
+//         cuts a long ray's dependency chain 4x, which is what bounds a frame;
+//   * scheduling: one wave per workgroup; each XCD owns one horizontal band of
+//     the screen (L2 locality) and, from the previous frame's per-tile critical
+//     paths, receives its band longest-first (LPT) with the longest tiles split
+//     into four quad-marched quarters.
 //
 // Arithmetic follows CVR-SPEC: explicit fmaf, IEEE div/sqrt, the
-// polynomial cvr_expf / cvr_powf.  The file is compiled with -ffp-contract=off
-// so results are bit-identical to oracle/cvr_oracle.cpp.
+// polynomial cvr_expf.  Compiled with -ffp-contract=off; both march variants
+// produce bit-identical results, equal to oracle/cvr_oracle.cpp.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -27,17 +30,17 @@
 namespace cvr {
 
 constexpr int kMaxTfLds = 4096;
+constexpr int kQuadFlag = 1 << 28;   // order entry = tile | (quarter + 1) << 28 for quad tiles
 
 // ---------------------------------------------------------------------------
 // Work decomposition
 // ---------------------------------------------------------------------------
 
-// Wave tile `t` (8x8 pixels) -> pixel of `lane` and its output index.
+// Tile `t` (8x8 pixels), local pixel (lx, ly) -> pixel and output index.
 // Unpacked: tiles are row-major over the (W/8)x(H/8) grid.  Packed (screen
 // split): tile t = k*(T/8)^2 + j is sub-tile j of this rank's k-th TxT tile.
-__device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lane, int& px, int& py,
-                                           long long& out_idx) {
-  const int lx = lane & 7, ly = lane >> 3;
+__device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lx, int ly, int& px,
+                                           int& py, long long& out_idx) {
   if (!A.packed) {
     const int ntx8 = (A.W + 7) >> 3;
     const int ty = t / ntx8, tx = t - ty * ntx8;
@@ -57,15 +60,15 @@ __device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lane
 }
 
 // ---------------------------------------------------------------------------
-// The ray
+// Sampling
 // ---------------------------------------------------------------------------
 
-// One sample's cell address + weights (stage 1 of the batched march).
-struct SamplePos { int idx; float ax, ay, az; int ix, iy, iz; };   // idx may be < 0 (linear: origin-relative)
+// One sample's cell address + weights.  idx may be < 0 in the linear layout
+// (it is relative to the cell of texel (0,0,0)).
+struct SamplePos { int idx; float ax, ay, az; int ix, iy, iz; };
 
 template <int LAYOUT>
-__device__ __forceinline__ SamplePos sample_pos(float x, float y, float z, const Rc1passArgs& A,
-                                                uint32_t bxby) {
+__device__ __forceinline__ SamplePos sample_pos(float x, float y, float z, const Rc1passArgs& A) {
   // GL_LINEAR texel-centre convention.  Clamping to [-1, N-1] (one v_med3) is
   // value-neutral under CLAMP_TO_EDGE and keeps the padded cell index
   // floor(x)+1 inside [0, N].
@@ -81,7 +84,8 @@ __device__ __forceinline__ SamplePos sample_pos(float x, float y, float z, const
     p.idx = __mul24(p.iz, A.cells.pitch_z) + __mul24(p.iy, A.cells.pitch_y) + p.ix;
   } else {
     uint32_t cx = (uint32_t)(p.ix + 1), cy = (uint32_t)(p.iy + 1), cz = (uint32_t)(p.iz + 1);
-    uint32_t brick = __umul24(cz >> 2, bxby) + __umul24(cy >> 2, (uint32_t)A.cells.bx) + (cx >> 2);
+    uint32_t brick = __umul24(cz >> 2, (uint32_t)A.cells.bxby) +
+                     __umul24(cy >> 2, (uint32_t)A.cells.bx) + (cx >> 2);
     p.idx = (int)((brick << 6) | ((cz & 3u) << 4) | ((cy & 3u) << 2) | (cx & 3u));
   }
   return p;
@@ -112,6 +116,19 @@ __device__ __forceinline__ float trilerp_cell(uint4 raw, float ax, float ay, flo
   return lerpf(c0, c1, az);
 }
 
+// texture(TexTransferFunc, density) from the padded LDS table: x = d*n - 0.5
+// reads the adjacent entries tfp[floor(x)+1], tfp[floor(x)+2]; d in [0,1]
+// (a lerp of [0,1] values) keeps floor(x)+1 in [0, n].
+__device__ __forceinline__ float4 classify(const float4* __restrict__ tfp, float fn, float dens) {
+  float x = fmaf(dens, fn, -0.5f);
+  float fl = floorf(x);
+  float a = x - fl;
+  int i = (int)fl + 1;
+  float4 t0 = tfp[i], t1 = tfp[i + 1];
+  return make_float4(lerpf(t0.x, t1.x, a), lerpf(t0.y, t1.y, a), lerpf(t0.z, t1.z, a),
+                     lerpf(t0.w, t1.w, a));
+}
+
 // Blinn-Phong (ray_marching_1p.comp:48-81), CVR-SPEC arithmetic.
 __device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint2* __restrict__ grad,
                                             const SamplePos& sp, f3 dir, float t, f3 tpos, f3 hg,
@@ -136,25 +153,25 @@ __device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint2* _
   }
 }
 
-// One ray of ray_marching_1p.comp:87-176.  The arithmetic per sample is
-// exactly the reference's sequential loop (s accumulates h one step at a time);
-// the batching only changes when the loads are issued.
-template <int K, bool PHONG, int LAYOUT>
-__device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
-                                          const uint2* __restrict__ grad,
-                                          const float4* __restrict__ tfp, int px, int py,
-                                          float4& dst, uint32_t& cnt) {
-  dst = make_float4(0.f, 0.f, 0.f, 0.f);
-  cnt = 0;
-  // ray generation, ray_marching_1p.comp:93-99
+// ---------------------------------------------------------------------------
+// The ray
+// ---------------------------------------------------------------------------
+
+struct Ray {
+  f3 dir, tpos, o, dt;   // direction, entry point (texture space), texel-space origin/step
+  float D;               // distance to evaluate, |tfar - tnear|
+};
+
+// Ray generation + slab test, ray_marching_1p.comp:93-121 and
+// ray_bbox_intersection.comp:18-52.  Returns false for a miss.
+__device__ __forceinline__ bool ray_setup(const Rc1passArgs& A, int px, int py, Ray& r) {
   float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
   float vx = fmaf(fx / (float)A.W, 2.0f, -1.0f);
   float vy = fmaf(fy / (float)A.H, 2.0f, -1.0f);
   f3 c{(vx * A.tan_half_fovy) * A.aspect, vy * A.tan_half_fovy, -1.0f};
   f3 d{dot3(c, f3{A.col0[0], A.col0[1], A.col0[2]}), dot3(c, f3{A.col1[0], A.col1[1], A.col1[2]}),
        dot3(c, f3{A.col2[0], A.col2[1], A.col2[2]})};
-  f3 dir = normalize3(normalize3(d));
-  // slab test, ray_bbox_intersection.comp:18-30
+  f3 dir = normalize3(normalize3(d));      // RayAABBIntersection normalises again (:219)
   f3 inv{1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z};
   const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
   const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
@@ -164,17 +181,31 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
   float tfar = fminf(fminf(fmaxf(ta.x, tb.x), fmaxf(ta.y, tb.y)), fmaxf(ta.z, tb.z));
   bool hit = tfar > tnear;
   tnear = fmaxf(tnear, 0.0f);
-  if (!hit) return;   // misses keep the cleared (0,0,0,0), renderoutputframe.cpp:187-190
-  const float D = fabsf(tfar - tnear);
-  const f3 tpos{fmaf(dir.x, tnear, eye.x) + hg.x, fmaf(dir.y, tnear, eye.y) + hg.y,
-                fmaf(dir.z, tnear, eye.z) + hg.z};
-  const f3 o{fmaf(tpos.x, A.n_over_g[0], -0.5f), fmaf(tpos.y, A.n_over_g[1], -0.5f),
-             fmaf(tpos.z, A.n_over_g[2], -0.5f)};
-  const f3 dt{dir.x * A.n_over_g[0], dir.y * A.n_over_g[1], dir.z * A.n_over_g[2]};
-  const float step = A.step;
-  const uint32_t bxby = (uint32_t)A.cells.bx * (uint32_t)A.cells.by;
-  const int n = A.tf_n;
-  const float fn = (float)n;
+  r.dir = dir;
+  r.D = fabsf(tfar - tnear);
+  r.tpos = f3{fmaf(dir.x, tnear, eye.x) + hg.x, fmaf(dir.y, tnear, eye.y) + hg.y,
+              fmaf(dir.z, tnear, eye.z) + hg.z};
+  r.o = f3{fmaf(r.tpos.x, A.n_over_g[0], -0.5f), fmaf(r.tpos.y, A.n_over_g[1], -0.5f),
+           fmaf(r.tpos.z, A.n_over_g[2], -0.5f)};
+  r.dt = f3{dir.x * A.n_over_g[0], dir.y * A.n_over_g[1], dir.z * A.n_over_g[2]};
+  return hit;
+}
+
+// Ray-parallel march (one lane per ray) of ray_marching_1p.comp:124-172.  The
+// arithmetic per sample is exactly the reference's sequential loop (s
+// accumulates h one step at a time); batching only changes when loads issue.
+template <int K, bool PHONG, int LAYOUT>
+__device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
+                                          const uint2* __restrict__ grad,
+                                          const float4* __restrict__ tfp, int px, int py,
+                                          float4& dst, uint32_t& cnt) {
+  dst = make_float4(0.f, 0.f, 0.f, 0.f);
+  cnt = 0;
+  Ray r;
+  if (!ray_setup(A, px, py, r)) return;   // misses keep (0,0,0,0), renderoutputframe.cpp:187-190
+  const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
+  const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
+  const float step = A.step, D = r.D, fn = (float)A.tf_n;
   float s = 0.0f;
   bool done = !(s < D);
   while (!done) {
@@ -190,24 +221,15 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       hj[j] = fminf(step, D - ss);
       tj[j] = fmaf(hj[j], 0.5f, ss);
       ss = ss + hj[j];
-      sp[j] = sample_pos<LAYOUT>(fmaf(dt.x, tj[j], o.x), fmaf(dt.y, tj[j], o.y),
-                                 fmaf(dt.z, tj[j], o.z), A, bxby);
+      sp[j] = sample_pos<LAYOUT>(fmaf(r.dt.x, tj[j], r.o.x), fmaf(r.dt.y, tj[j], r.o.y),
+                                 fmaf(r.dt.z, tj[j], r.o.z), A);
       raw[j] = cells[sp[j].idx];
     }
-    // stage 2: density and transfer-function classification (padded LDS table:
-    // x = d*n - 0.5 reads the adjacent entries tfp[floor(x)+1], tfp[floor(x)+2])
+    // stage 2: density and transfer-function classification
     float4 src[K];
 #pragma unroll
-    for (int j = 0; j < K; j++) {
-      float dens = trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az);
-      float x = fmaf(dens, fn, -0.5f);
-      float fl = floorf(x);
-      float a = x - fl;
-      int i = (int)fl + 1;   // dens in [0,1] (a lerp of [0,1] values) -> i in [0, n]
-      float4 t0 = tfp[i], t1 = tfp[i + 1];
-      src[j] = make_float4(lerpf(t0.x, t1.x, a), lerpf(t0.y, t1.y, a), lerpf(t0.z, t1.z, a),
-                           lerpf(t0.w, t1.w, a));
-    }
+    for (int j = 0; j < K; j++)
+      src[j] = classify(tfp, fn, trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az));
     // stage 3: front-to-back composite + ERT, in sample order
 #pragma unroll
     for (int j = 0; j < K; j++) {
@@ -218,7 +240,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
           cnt++;
           float4 sc = src[j];
           if (sc.w > 0.0f) {
-            if (PHONG) shade_phong(A, grad, sp[j], dir, tj[j], tpos, hg, eye, sc);
+            if (PHONG) shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
             float a = 1.0f - cvr_expf_nb(-(sc.w * hj[j]));
             float om = 1.0f - dst.w;
             dst.x = fmaf(om, sc.x * a, dst.x);
@@ -235,47 +257,114 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
   }
 }
 
+template <int K>
+__device__ __forceinline__ float quad_bcast(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), K | (K << 2) | (K << 4) | (K << 6),
+                                                 0xf, 0xf, false));
+}
+
+// Sample-parallel march: the 4 lanes of a quad share one ray; per iteration
+// lane j takes the j-th of the ray's next 4 samples (positions from the same
+// sequential s += h recurrence), fetches and classifies it, then every lane of
+// the quad composites the 4 samples in order (DPP quad broadcasts) and applies
+// the ERT exit, so all four hold the ray's identical state.  A transparent or
+// out-of-range sample enters the composite as exact zeros, which leaves dst
+// bit-unchanged — the same result as the reference skipping it (:142).
+// Must be called by all 64 lanes (DPP reads neighbours); `active` = lane's ray is live.
+template <bool PHONG, int LAYOUT>
+__device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
+                                               const uint4* __restrict__ cells,
+                                               const uint2* __restrict__ grad,
+                                               const float4* __restrict__ tfp, int px, int py,
+                                               bool active, float4& dst, uint32_t& cnt) {
+  const int j = threadIdx.x & 3;
+  dst = make_float4(0.f, 0.f, 0.f, 0.f);
+  cnt = 0;
+  Ray r;
+  bool hit = ray_setup(A, px, py, r);
+  const float D = (active && hit) ? r.D : 0.0f;
+  const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
+  const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
+  const float step = A.step, fn = (float)A.tf_n;
+  float s = 0.0f;
+  bool done = !(s < D);
+  while (!__all(done)) {
+    // this lane's sample: the j-th step of the sequential recurrence from s
+    float ss = s, sj = 0.0f, hj = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      float h = fminf(step, D - ss);
+      if (k == j) { sj = ss; hj = h; }
+      ss = ss + h;
+    }
+    const bool vj = !done && sj < D;
+    const float tj = fmaf(hj, 0.5f, sj);
+    SamplePos sp = sample_pos<LAYOUT>(fmaf(r.dt.x, tj, r.o.x), fmaf(r.dt.y, tj, r.o.y),
+                                      fmaf(r.dt.z, tj, r.o.z), A);
+    float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
+    float a = 0.0f, pr = 0.0f, pg = 0.0f, pb = 0.0f;
+    if (vj && sc.w > 0.0f) {
+      if (PHONG) shade_phong(A, grad, sp, r.dir, tj, r.tpos, hg, eye, sc);
+      a = 1.0f - cvr_expf_nb(-(sc.w * hj));
+      pr = sc.x * a; pg = sc.y * a; pb = sc.z * a;
+    }
+    // in-order composite of the quad's 4 samples (every lane of the quad)
+    const unsigned long long vm = __ballot(vj);
+    const unsigned qv = (unsigned)(vm >> (threadIdx.x & ~3u)) & 0xfu;
+#define CVR_QUAD_STEP(K)                                                        \
+    {                                                                           \
+      float ak = quad_bcast<K>(a), rk = quad_bcast<K>(pr);                      \
+      float gk = quad_bcast<K>(pg), bk = quad_bcast<K>(pb);                     \
+      if (!done) {                                                              \
+        if (qv & (1u << K)) {                                                   \
+          cnt++;                                                                \
+          float om = 1.0f - dst.w;                                              \
+          dst.x = fmaf(om, rk, dst.x);                                          \
+          dst.y = fmaf(om, gk, dst.y);                                          \
+          dst.z = fmaf(om, bk, dst.z);                                          \
+          dst.w = fmaf(om, ak, dst.w);                                          \
+          if (dst.w > 0.99f) done = true;                                       \
+        } else {                                                                \
+          done = true;                                                          \
+        }                                                                       \
+      }                                                                         \
+    }
+    CVR_QUAD_STEP(0)
+    CVR_QUAD_STEP(1)
+    CVR_QUAD_STEP(2)
+    CVR_QUAD_STEP(3)
+#undef CVR_QUAD_STEP
+    s = ss;
+  }
+}
+
 __device__ __forceinline__ void load_tf_lds(float4* tfp, const float4* __restrict__ tf_g, int n) {
   // Padded TF: tfp[k] = T[clamp(k-1, 0, n-1)], k in [0, n+1] (CLAMP_TO_EDGE folded in).
   for (int i = threadIdx.x; i < n + 2; i += blockDim.x) tfp[i] = tf_g[min(max(i - 1, 0), n - 1)];
   __syncthreads();
 }
 
-// Writes one wave tile's results; lanes outside the image store zeros only in
-// the packed layout (edge-tile padding).
-__device__ __forceinline__ void finish_tile(const Rc1passArgs& A, int t, int lane, bool inside,
-                                            long long oidx, float4 dst, uint32_t cnt,
-                                            float4* __restrict__ out, uint32_t* __restrict__ samples,
-                                            unsigned long long* __restrict__ total,
-                                            uint32_t* __restrict__ tile_cost) {
-  if (inside || A.packed) {
-    out[oidx] = dst;
-    if (samples) samples[oidx] = cnt;
-  }
-  if (total) {
-    unsigned long long v = cnt;
+__device__ __forceinline__ uint32_t wave_max(uint32_t m) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (lane == 0 && v) atomicAdd(total, v);
-  }
-  if (tile_cost) {   // the tile's critical path (its longest ray), for the next frame's order
-    uint32_t m = cnt;
+  for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+  return m;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
-    if (lane == 0) tile_cost[t] = m;
-  }
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
 }
 
 // ---------------------------------------------------------------------------
-// Kernels
+// Kernel
 // ---------------------------------------------------------------------------
 
-// One workgroup = one wave = one 8x8 tile, so a long ray only ever holds its
-// own wave slot.  Tile t comes from the LPT order when given (each XCD gets its
-// screen band longest-first), else from the XCD-banded remap (blocks b and b+8
-// share an XCD, so XCD b%8 gets one contiguous band of the screen).  The first
-// `boost` tiles of every band (its longest, by the previous frame) raise their
-// wave priority so their long dependency chains issue ahead of short tiles.
+// One workgroup = one wave.  Entry e of the launch order is a whole 8x8 tile
+// (one lane per ray) or, for the longest tiles, one 4x4 quarter of a tile
+// (four lanes per ray).  Without an order, block b -> tile in XCD bands
+// (blocks b and b+8 share an XCD, so XCD b%8 gets one contiguous band).
+// Waves of the `boost` longest tiles of each band raise their priority.
 template <int K, bool PHONG, int LAYOUT>
 __global__ void __launch_bounds__(64)
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
@@ -286,10 +375,12 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   extern __shared__ float4 tfp[];
   load_tf_lds(tfp, tf_g, A.tf_n);
   const int b = blockIdx.x, nt = A.ntiles;
-  int t;
+  int t, quarter = -1;
   if (order) {
-    t = order[b];
-    if (t < 0) return;   // padding slot of a shorter band
+    const int e = order[b];
+    if (e < 0) return;                      // padding slot of a shorter band
+    t = e & (kQuadFlag - 1);
+    quarter = (e >> 28) - 1;
     if ((b >> 3) < boost) __builtin_amdgcn_s_setprio(2);
   } else if ((nt & 7) == 0) {
     t = (b & 7) * (nt >> 3) + (b >> 3);
@@ -301,20 +392,44 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   if (A.tile_stats) t_start = __builtin_amdgcn_s_memrealtime();
   int px, py;
   long long oidx;
-  tile_pixel(A, t, lane, px, py, oidx);
-  const bool inside = px < A.W && py < A.H;
-  float4 dst = make_float4(0.f, 0.f, 0.f, 0.f);
-  uint32_t cnt = 0;
-  if (inside) march_ray<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
-  finish_tile(A, t, lane, inside, oidx, dst, cnt, out, samples, total, tile_cost);
+  float4 dst;
+  uint32_t cnt;
+  bool writer;
+  if (quarter < 0) {          // whole tile, one lane per ray
+    tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
+    const bool inside = px < A.W && py < A.H;
+    dst = make_float4(0.f, 0.f, 0.f, 0.f);
+    cnt = 0;
+    if (inside) march_ray<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
+    writer = inside || A.packed;
+  } else {                    // quarter of a tile, four lanes per ray
+    const int ray = lane >> 2;
+    tile_pixel(A, t, ((quarter & 1) << 2) | (ray & 3), ((quarter >> 1) << 2) | (ray >> 2), px, py,
+               oidx);
+    const bool inside = px < A.W && py < A.H;
+    march_ray_quad<PHONG, LAYOUT>(A, cells, grad, tfp, px, py, inside, dst, cnt);
+    writer = (lane & 3) == 0 && (inside || A.packed);
+    if ((lane & 3) != 0) cnt = 0;           // one count per ray
+  }
+  if (writer) {
+    out[oidx] = dst;
+    if (samples) samples[oidx] = cnt;
+  }
+  if (total) {
+    unsigned long long v = wave_sum(cnt);
+    if (lane == 0 && v) atomicAdd(total, v);
+  }
+  uint32_t m = 0;
+  if (tile_cost || A.tile_stats) m = wave_max(cnt);
+  if (tile_cost && lane == 0) {   // the tile's critical path (its longest ray), next frame's order
+    if (quarter < 0) tile_cost[t] = m;
+    else atomicMax(&tile_cost[t], m);
+  }
   if (A.tile_stats) {   // diagnostics: 100 MHz start/end stamps, longest ray, placement
-    uint32_t m = cnt;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
     unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     unsigned hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    if (lane == 0) {
+    if (lane == 0 && quarter <= 0) {
       A.tile_stats[t * 4 + 0] = t_start;
       A.tile_stats[t * 4 + 1] = t_end;
       A.tile_stats[t * 4 + 2] = m;
@@ -323,47 +438,62 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   }
 }
 
-// LPT order from the previous frame's per-tile costs: workgroup `seg` sorts the
-// tiles of XCD band seg (bitonic sort in LDS, descending cost, ties by index)
-// and deals them to physical blocks seg, seg+8, seg+16, ... (the blocks XCD
-// seg receives), so every XCD keeps its screen band and starts with its
-// longest tiles.
+// ---------------------------------------------------------------------------
+// Launch order (LPT) from the previous frame
+// ---------------------------------------------------------------------------
+
+// Workgroup `band` orders the tiles of XCD band `band` by descending critical
+// path (bucketed into 256 cost levels: O(n), ties in any order — the order
+// never changes a pixel), expands the longest `nquad` tiles into four quad
+// quarters, and deals the entries to physical blocks band, band+8, ... (the
+// blocks XCD `band` receives).  Slots past the band's entries are -1.  Resets
+// tile_cost for the next frame's atomicMax.
 __global__ void __launch_bounds__(1024)
-tile_order_kernel(const uint32_t* __restrict__ tile_cost, int nunits, int* __restrict__ order) {
-  extern __shared__ unsigned long long keys[];
-  const int b0 = (blockIdx.x * nunits) >> 3, b1 = ((blockIdx.x + 1) * nunits) >> 3;
+tile_order_kernel(uint32_t* __restrict__ tile_cost, int ntiles, int quad_pct, int slots_per_band,
+                  int* __restrict__ order) {
+  __shared__ unsigned hist[256];
+  __shared__ unsigned start[256];
+  __shared__ unsigned maxc;
+  extern __shared__ int sorted[];   // ceil(ntiles / 8) entries
+  const int band = blockIdx.x;
+  const int b0 = (band * ntiles) >> 3, b1 = ((band + 1) * ntiles) >> 3;
   const int seg = b1 - b0;
-  int P = 1;
-  while (P < seg) P <<= 1;
-  for (int i = threadIdx.x; i < P; i += blockDim.x) {
-    unsigned long long k = 0;
-    if (i < seg) {
-      uint32_t u = (uint32_t)(b0 + i);
-      k = ((unsigned long long)tile_cost[u] << 32) | (0xffffffffu - u);
-    }
-    keys[i] = k;
+  if (threadIdx.x < 256) hist[threadIdx.x] = 0;
+  if (threadIdx.x == 0) maxc = 0;
+  __syncthreads();
+  unsigned lmax = 0;
+  for (int i = threadIdx.x; i < seg; i += blockDim.x) lmax = max(lmax, tile_cost[b0 + i]);
+  atomicMax(&maxc, lmax);
+  __syncthreads();
+  const unsigned mc = maxc + 1;
+  for (int i = threadIdx.x; i < seg; i += blockDim.x) {
+    unsigned c = tile_cost[b0 + i];
+    unsigned bucket = 255u - (unsigned)(((unsigned long long)c * 256u) / mc);
+    atomicAdd(&hist[bucket], 1u);
   }
   __syncthreads();
-  for (int size = 2; size <= P; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < P; i += blockDim.x) {
-        int j = i ^ stride;
-        if (j > i) {
-          bool desc = (i & size) == 0;
-          unsigned long long a = keys[i], b = keys[j];
-          if ((a < b) == desc) { keys[i] = b; keys[j] = a; }
-        }
-      }
-      __syncthreads();
-    }
+  if (threadIdx.x == 0) {
+    unsigned acc = 0;
+    for (int k = 0; k < 256; k++) { start[k] = acc; acc += hist[k]; }
   }
-  // band sizes differ by at most one: bands with the extra tile come last
-  // ((b*n)>>3 rounding), so physical block seg + 8*i exists for every i < seg
-  // as long as the grid is launched with 8*ceil(n/8) blocks, see launcher
+  __syncthreads();
   for (int i = threadIdx.x; i < seg; i += blockDim.x) {
-    int u = (int)(0xffffffffu - (uint32_t)keys[i]);
-    order[blockIdx.x + 8 * i] = u;
+    unsigned c = tile_cost[b0 + i];
+    unsigned bucket = 255u - (unsigned)(((unsigned long long)c * 256u) / mc);
+    unsigned pos = atomicAdd(&start[bucket], 1u);
+    sorted[pos] = b0 + i;
   }
+  __syncthreads();
+  const int nquad = (int)(((long long)seg * quad_pct) / 100);
+  const int nent = seg + 3 * nquad;
+  for (int e = threadIdx.x; e < slots_per_band; e += blockDim.x) {
+    int v = -1;
+    if (e < 4 * nquad) v = sorted[e >> 2] | (((e & 3) + 1) << 28);
+    else if (e < nent) v = sorted[e - 3 * nquad];
+    order[band + 8 * e] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < seg; i += blockDim.x) tile_cost[b0 + i] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -377,8 +507,6 @@ static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, ui
   size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
   const uint4* cells = (const uint4*)c.d_cells;
   if (LAYOUT == kLayoutLinear) cells += c.cells.linear_origin;   // cell (1,1,1) <-> texel (0,0,0)
-  // with an order the grid is 8*ceil(n/8) blocks; the padding blocks (unused
-  // order slots) are marked -1 and exit at once
   int grid = order ? plan.order_slots : plan.ntiles;
   hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, LAYOUT>), dim3(grid), dim3(64), lds, s, a,
                      cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, total,
@@ -415,23 +543,12 @@ hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4
   }
 }
 
-__global__ void fill_int_kernel(int* p, int n, int v) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = v;
-}
-
-hipError_t launch_tile_order(const uint32_t* tile_cost, const RenderPlan& plan, int* order,
+hipError_t launch_tile_order(uint32_t* tile_cost, const RenderPlan& plan, int* order,
                              hipStream_t s) {
-  const int nunits = plan.ntiles;
-  const int seg = (nunits + 7) >> 3;
-  int P = 1;
-  while (P < seg) P <<= 1;
-  if (P > 16384) return hipErrorInvalidValue;
-  if (plan.order_slots != nunits)   // padding slots of short bands
-    hipLaunchKernelGGL(fill_int_kernel, dim3((plan.order_slots + 255) / 256), dim3(256), 0, s,
-                       order, plan.order_slots, -1);
-  hipLaunchKernelGGL(tile_order_kernel, dim3(8), dim3(1024), (size_t)P * 8, s, tile_cost, nunits,
-                     order);
+  const int seg_max = (plan.ntiles + 7) >> 3;
+  if (seg_max > 32768) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tile_order_kernel, dim3(8), dim3(1024), (size_t)seg_max * sizeof(int), s,
+                     tile_cost, plan.ntiles, plan.quad_pct, plan.order_slots / 8, order);
   return hipGetLastError();
 }
 

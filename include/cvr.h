@@ -129,8 +129,10 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *   "tile_order" 1: each XCD takes the tiles of its screen band longest-first (LPT),
  *                using the previous frame's per-tile critical paths (default);
  *                0: screen order
- *   "boost"      percent of each band's longest tiles launched at raised wave
+ *   "boost"      percent of each band's longest entries launched at raised wave
  *                priority (with tile_order 1; default 5)
+ *   "quad"       percent of each band's longest tiles marched sample-parallel, four
+ *                lanes per ray (with tile_order 1; default 10)
  *   "layout"     cell layout of the next cvr_set_volume: 0 bricked 4^3 (default),
  *                1 linear x-fastest
  *   "tile_stats" 1: record per-tile timing of every frame (diagnostics) */

@@ -206,3 +206,64 @@ def test_headline_512_properties(dev, oracle, bonsai_tf):
     assert_bitexact(r.rgba.cpu().numpy(), g1, "renderer device output")
     assert int(r.total.item()) == t1
     r.Clean()
+
+
+SCHEDULES = [
+    dict(tile_order=0, batch=4, layout=0),
+    dict(tile_order=1, quad=10, boost=5, batch=4, layout=0),
+    dict(tile_order=1, quad=100, boost=0, batch=2, layout=1),
+    dict(tile_order=1, quad=0, boost=50, batch=8, layout=1),
+    dict(tile_order=1, quad=35, boost=5, batch=4, layout=1),
+]
+
+
+@pytest.mark.parametrize("sched", range(len(SCHEDULES)))
+@pytest.mark.parametrize("name", ["ml64_ragged", "ml_aniso", "phong_fd", "camera_inside"])
+def test_schedules_bitexact(oracle, bonsai_tf, name, sched):
+    """Every scheduling / march variant (LPT order, quad = 4-lanes-per-ray march for the
+    longest tiles, batch size, cell layout) reproduces the oracle bit for bit, on the
+    first frame (screen order) and on later frames (learned LPT order + quad tiles)."""
+    c = CASES[name]
+    opts = SCHEDULES[sched]
+    vol = c["vol"]()
+    cam = c.get("cam", INITIAL)
+    kw = dict(step=c.get("step", 0.0), phong=c.get("phong", False), gmode=c.get("gmode", 0),
+              light=c.get("light", (0, 0, 0)), shading=c.get("shading", (0.5, 0.5, 0.8, 30.0)))
+    o_rgba, o_cnt, o_total = oracle_render(oracle, vol, c["scale"], bonsai_tf, cam, c["W"],
+                                           c["H"], **kw)
+    d = Device(0)
+    try:
+        for k in ("layout",):
+            N.check(N.lib().cvr_set_option(d.handle, k.encode(), opts[k]), k)
+        for k in ("tile_order", "quad", "boost", "batch"):
+            if k in opts:
+                N.check(N.lib().cvr_set_option(d.handle, k.encode(), opts[k]), k)
+        for frame in range(3):
+            g_rgba, g_cnt, g_total = gpu_render(d, vol, c["scale"], bonsai_tf, cam, c["W"], c["H"],
+                                                set_data=(frame == 0), **kw)
+            assert_bitexact(g_cnt, o_cnt, f"{name} frame {frame} counts")
+            assert_bitexact(g_rgba, o_rgba, f"{name} frame {frame} rgba")
+            assert g_total == o_total
+    finally:
+        d.close()
+
+
+@pytest.mark.parametrize("nranks,tile", [(3, 16), (8, 32)])
+def test_screen_tiles_with_quad_schedule(bonsai_tf, nranks, tile):
+    """Packed (multi-GPU) tiles under the LPT + quad schedule equal the full frame."""
+    vol = _ml(64)
+    W, H = 200, 136
+    d = Device(0)
+    try:
+        N.check(N.lib().cvr_set_option(d.handle, b"quad", 50), "quad")
+        full, full_cnt, _ = gpu_render(d, vol, D.voxel_scale(64), bonsai_tf, INITIAL, W, H)
+        tpr = T.max_tiles_per_rank(W, H, tile, nranks)
+        packed_all = np.zeros((nranks, tpr, tile, tile, 4), np.float32)
+        for r in range(nranks):
+            for rep in range(2):   # second pass runs with the learned order
+                rgba, cnt, _ = gpu_render(d, vol, D.voxel_scale(64), bonsai_tf, INITIAL, W, H,
+                                          tile=tile, rank=r, nranks=nranks, set_data=False)
+            packed_all[r, :rgba.shape[0]] = rgba
+        assert_bitexact(T.unpack(packed_all, W, H, tile, nranks), full, "unpacked")
+    finally:
+        d.close()
