@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of rc1pass kernel variants in ONE process, interleaved rounds
 (methodology rule 24).  Every variant's image is checked bit-equal to the first
-variant's.  Variant syntax: L<layout>b<batch>o<tile_order>p<boost%>, e.g. L0b4o1p5.
+variant's.  Variant syntax: L<layout>b<batch>o<tile_order>p<boost%>q<quad%>, e.g. L0b4o1p5q10.
 Usage: python tools/ab_rc1pass.py [--size 512] [--res 1024] [--variants ...]"""
 import argparse
 import ctypes
@@ -20,7 +20,7 @@ from cpp_volume_rendering_amd.renderer import Camera, Device, build_tf_rgbt, mak
 
 
 def parse_variant(v):
-    m = re.fullmatch(r"L(\d)b(\d)o(\d)p(\d+)", v)
+    m = re.fullmatch(r"L(\d)b(\d)o(\d)p(\d+)q(\d+)", v)
     if not m:
         raise ValueError(f"bad variant {v}")
     return tuple(int(x) for x in m.groups())
@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--field", default="ml")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=20)
-    ap.add_argument("--variants", default="L0b4o1p0,L0b4o1p5,L0b4o1p15,L1b4o1p5,L0b8o1p5,L1b8o1p5")
+    ap.add_argument("--variants", default="L1b4o1p5q0,L1b4o1p5q5,L1b4o1p5q10,L1b4o1p5q20,L1b4o1p5q40,L1b4o1p0q10,L0b4o1p5q10,L1b4o0p0q0")
     ap.add_argument("--phong", action="store_true")
     a = ap.parse_args()
     n, W = a.size, a.res
@@ -72,11 +72,12 @@ def main():
     S = None
     for _ in range(a.rounds):
         for v in variants:
-            layout, b, o, boost = parsed[v]
+            layout, b, o, boost, quad = parsed[v]
             dev = devs[layout]
             N.check(L.cvr_set_option(dev.handle, b"batch", b), "opt")
             N.check(L.cvr_set_option(dev.handle, b"tile_order", o), "opt")
             N.check(L.cvr_set_option(dev.handle, b"boost", boost), "opt")
+            N.check(L.cvr_set_option(dev.handle, b"quad", quad), "opt")
             with torch.cuda.stream(s):
                 run(dev, 3)   # warm up + learn the order
                 tot.zero_()
