@@ -236,6 +236,10 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->layout = value;   // takes effect at the next cvr_set_volume
     return CVR_OK;
   }
+  if (!std::strcmp(key, "pipeline")) {
+    c->pipeline = value != 0;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "quad")) {
     if (value < 0 || value > 100) return fail(c, CVR_ERR_ARG, "quad must be a percentage");
     c->quad_pct = value;
@@ -263,6 +267,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "boost")) return c->boost_pct;
   if (!std::strcmp(key, "tile_stats")) return c->tile_stats;
   if (!std::strcmp(key, "quad")) return c->quad_pct;
+  if (!std::strcmp(key, "pipeline")) return c->pipeline;
   return -1;
 }
 

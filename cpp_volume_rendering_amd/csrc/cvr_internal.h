@@ -86,6 +86,7 @@ struct Ctx {
   int grad_mode = 0;
   // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
   int batch = 4;
+  int pipeline = 0;                // 1: two batches in flight (software-pipelined march)
   int layout = kLayoutBrick;       // cell layout used by the next cvr_set_volume
   int boost_pct = 5;               // % of every band's longest entries run at raised priority
   int quad_pct = 10;               // % of every band's longest tiles marched 4 lanes per ray

@@ -257,6 +257,98 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
   }
 }
 
+// Software-pipelined ray-parallel march: the K loads of batch i+1 are issued
+// before batch i is classified and composited, so a wave's memory latency
+// overlaps its own VALU work instead of adding to it (two batches in flight,
+// ping-ponged without register copies).  Speculative loads past the ERT exit
+// or past D read in-bounds cells (clamped) and are discarded.
+template <int K>
+struct Batch {
+  float h[K], t[K];
+  bool v[K];
+  SamplePos sp[K];
+  uint4 raw[K];
+};
+
+template <int K, int LAYOUT>
+__device__ __forceinline__ void issue_batch(const Rc1passArgs& A, const Ray& r, float step,
+                                            const uint4* __restrict__ cells, float& ss,
+                                            Batch<K>& B) {
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    B.v[j] = ss < r.D;
+    B.h[j] = fminf(step, r.D - ss);
+    B.t[j] = fmaf(B.h[j], 0.5f, ss);
+    ss = ss + B.h[j];
+    B.sp[j] = sample_pos<LAYOUT>(fmaf(r.dt.x, B.t[j], r.o.x), fmaf(r.dt.y, B.t[j], r.o.y),
+                                 fmaf(r.dt.z, B.t[j], r.o.z), A);
+    B.raw[j] = cells[B.sp[j].idx];
+  }
+}
+
+// Classifies and composites one batch in sample order; returns true once the
+// ray has terminated (ERT or end of the ray).
+template <int K, bool PHONG>
+__device__ __forceinline__ bool process_batch(const Rc1passArgs& A, const Ray& r,
+                                              const uint2* __restrict__ grad,
+                                              const float4* __restrict__ tfp, float fn,
+                                              const Batch<K>& B, float4& dst, uint32_t& cnt) {
+  float4 src[K];
+#pragma unroll
+  for (int j = 0; j < K; j++)
+    src[j] = classify(tfp, fn, trilerp_cell(B.raw[j], B.sp[j].ax, B.sp[j].ay, B.sp[j].az));
+  bool done = false;
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    if (!done) {
+      if (!B.v[j]) {
+        done = true;
+      } else {
+        cnt++;
+        float4 sc = src[j];
+        if (sc.w > 0.0f) {
+          if (PHONG) {
+            const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
+            const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
+            shade_phong(A, grad, B.sp[j], r.dir, B.t[j], r.tpos, hg, eye, sc);
+          }
+          float a = 1.0f - cvr_expf_nb(-(sc.w * B.h[j]));
+          float om = 1.0f - dst.w;
+          dst.x = fmaf(om, sc.x * a, dst.x);
+          dst.y = fmaf(om, sc.y * a, dst.y);
+          dst.z = fmaf(om, sc.z * a, dst.z);
+          dst.w = fmaf(om, a, dst.w);
+          if (dst.w > 0.99f) done = true;
+        }
+      }
+    }
+  }
+  return done;
+}
+
+template <int K, bool PHONG, int LAYOUT>
+__device__ __forceinline__ void march_ray_pipe(const Rc1passArgs& A,
+                                               const uint4* __restrict__ cells,
+                                               const uint2* __restrict__ grad,
+                                               const float4* __restrict__ tfp, int px, int py,
+                                               float4& dst, uint32_t& cnt) {
+  dst = make_float4(0.f, 0.f, 0.f, 0.f);
+  cnt = 0;
+  Ray r;
+  if (!ray_setup(A, px, py, r)) return;   // misses keep (0,0,0,0), renderoutputframe.cpp:187-190
+  if (!(0.0f < r.D)) return;
+  const float step = A.step, fn = (float)A.tf_n;
+  float ss = 0.0f;
+  Batch<K> b0, b1;
+  issue_batch<K, LAYOUT>(A, r, step, cells, ss, b0);
+  while (true) {
+    issue_batch<K, LAYOUT>(A, r, step, cells, ss, b1);
+    if (process_batch<K, PHONG>(A, r, grad, tfp, fn, b0, dst, cnt)) break;
+    issue_batch<K, LAYOUT>(A, r, step, cells, ss, b0);
+    if (process_batch<K, PHONG>(A, r, grad, tfp, fn, b1, dst, cnt)) break;
+  }
+}
+
 template <int K>
 __device__ __forceinline__ float quad_bcast(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), K | (K << 2) | (K << 4) | (K << 6),
@@ -365,7 +457,7 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // (four lanes per ray).  Without an order, block b -> tile in XCD bands
 // (blocks b and b+8 share an XCD, so XCD b%8 gets one contiguous band).
 // Waves of the `boost` longest tiles of each band raise their priority.
-template <int K, bool PHONG, int LAYOUT>
+template <int K, bool PHONG, int LAYOUT, bool PIPE>
 __global__ void __launch_bounds__(64)
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
@@ -400,7 +492,10 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     const bool inside = px < A.W && py < A.H;
     dst = make_float4(0.f, 0.f, 0.f, 0.f);
     cnt = 0;
-    if (inside) march_ray<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
+    if (inside) {
+      if (PIPE) march_ray_pipe<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
+      else march_ray<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
+    }
     writer = inside || A.packed;
   } else {                    // quarter of a tile, four lanes per ray
     const int ray = lane >> 2;
@@ -500,7 +595,7 @@ tile_order_kernel(uint32_t* __restrict__ tile_cost, int ntiles, int quad_pct, in
 // Launchers
 // ---------------------------------------------------------------------------
 
-template <int K, bool PHONG, int LAYOUT>
+template <int K, bool PHONG, int LAYOUT, bool PIPE>
 static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                              unsigned long long* total, const int* order, uint32_t* tile_cost,
                              const RenderPlan& plan, hipStream_t s) {
@@ -508,7 +603,7 @@ static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, ui
   const uint4* cells = (const uint4*)c.d_cells;
   if (LAYOUT == kLayoutLinear) cells += c.cells.linear_origin;   // cell (1,1,1) <-> texel (0,0,0)
   int grid = order ? plan.order_slots : plan.ntiles;
-  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, LAYOUT>), dim3(grid), dim3(64), lds, s, a,
+  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, LAYOUT, PIPE>), dim3(grid), dim3(64), lds, s, a,
                      cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, total,
                      order, tile_cost, order ? plan.boost : 0);
   return hipGetLastError();
@@ -518,9 +613,13 @@ template <int K, bool PHONG>
 static hipError_t launch_kp(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                             unsigned long long* total, const int* order, uint32_t* tile_cost,
                             const RenderPlan& plan, hipStream_t s) {
+  if (c.pipeline)
+    return c.cells.layout == kLayoutLinear
+               ? launch_kpl<K, PHONG, kLayoutLinear, true>(c, a, out, samples, total, order, tile_cost, plan, s)
+               : launch_kpl<K, PHONG, kLayoutBrick, true>(c, a, out, samples, total, order, tile_cost, plan, s);
   return c.cells.layout == kLayoutLinear
-             ? launch_kpl<K, PHONG, kLayoutLinear>(c, a, out, samples, total, order, tile_cost, plan, s)
-             : launch_kpl<K, PHONG, kLayoutBrick>(c, a, out, samples, total, order, tile_cost, plan, s);
+             ? launch_kpl<K, PHONG, kLayoutLinear, false>(c, a, out, samples, total, order, tile_cost, plan, s)
+             : launch_kpl<K, PHONG, kLayoutBrick, false>(c, a, out, samples, total, order, tile_cost, plan, s);
 }
 
 template <int K>

@@ -131,6 +131,7 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                0: screen order
  *   "boost"      percent of each band's longest entries launched at raised wave
  *                priority (with tile_order 1; default 5)
+ *   "pipeline"   1: software-pipelined march, two batches of loads in flight per lane
  *   "quad"       percent of each band's longest tiles marched sample-parallel, four
  *                lanes per ray (with tile_order 1; default 10)
  *   "layout"     cell layout of the next cvr_set_volume: 0 bricked 4^3 (default),
