@@ -174,23 +174,30 @@ def main():
     torch.cuda.synchronize(dev)
 
     total.zero_()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(a.steps)]
+    # HIP events around the ray-march kernel alone, recorded by the library on
+    # the stream it launches on (torch events would also cover the LPT-order kernel)
+    N.check(L.cvr_set_option(r.device.handle, b"kernel_timing", a.steps), "kernel_timing",
+            r.device.handle)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
-        ev[i][0].record(stream)
         step_once()
-        ev[i][1].record(stream)
         gather_once()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kt = (ctypes.c_float * a.steps)()
+    nkt = ctypes.c_int()
+    N.check(L.cvr_read_kernel_times(r.device.handle, kt, a.steps, ctypes.byref(nkt)),
+            "cvr_read_kernel_times", r.device.handle)
+    assert nkt.value == a.steps
+    kern_ms = float(np.mean(kt[:nkt.value]))
+    batch = L.cvr_get_option(r.device.handle, b"batch")
+    layout = L.cvr_get_option(r.device.handle, b"layout")
     assert int(total.item()) == S_rank * a.steps, "sample count changed between frames"
 
     if world > 1:
@@ -215,7 +222,8 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic(a.pmc, wkey),
-                "kernel": "rc1pass_kernel", "kernel_ms": round(kern_ms, 4),
+                "kernel": f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, {layout}, false>",
+                "kernel_ms": round(kern_ms, 4),
                 "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank}
         res = {
             "metric": "Msamples/s (rays x steps), rc1pass ray-march, 512^3 volume at 1024^2",
@@ -238,7 +246,8 @@ def main():
                        "volume": n, "viewport": [W, H], "samples_per_frame": S_all,
                        "parallelism": f"screen tiles {tile}x{tile} over {world} GPU(s)"
                                       if world > 1 else "1 GPU",
-                       "storage": "cell8 fp16 (16 B/cell, bricked 4^3)"},
+                       "storage": "cell8 fp16 (16 B/cell, "
+                                  + ("x-fastest linear)" if layout == 1 else "bricked 4^3)")},
             "roofline": roof,
         }
         if world == 1 and not a.no_cpu_baseline:

@@ -199,6 +199,8 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_order; free_dev(p); c->d_order = nullptr;
   p = c->d_tile_cost; free_dev(p); c->d_tile_cost = nullptr;
   p = c->d_tile_stats; free_dev(p); c->d_tile_stats = nullptr;
+  for (hipEvent_t e : c->ev_start) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_stop) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -236,10 +238,6 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->layout = value;   // takes effect at the next cvr_set_volume
     return CVR_OK;
   }
-  if (!std::strcmp(key, "pipeline")) {
-    c->pipeline = value != 0;
-    return CVR_OK;
-  }
   if (!std::strcmp(key, "quad")) {
     if (value < 0 || value > 100) return fail(c, CVR_ERR_ARG, "quad must be a percentage");
     c->quad_pct = value;
@@ -248,6 +246,24 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
   }
   if (!std::strcmp(key, "tile_stats")) {
     c->tile_stats = value != 0;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "kernel_timing")) {
+    if (value < 0 || value > 4096) return fail(c, CVR_ERR_ARG, "kernel_timing must be 0..4096 frames");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (hipEvent_t e : c->ev_start) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_stop) (void)hipEventDestroy(e);
+    c->ev_start.clear();
+    c->ev_stop.clear();
+    c->timed_frames = 0;
+    for (int i = 0; i < value; i++) {
+      hipEvent_t a, b;
+      HIP_TRY(c, hipEventCreate(&a));
+      c->ev_start.push_back(a);
+      HIP_TRY(c, hipEventCreate(&b));
+      c->ev_stop.push_back(b);
+    }
     return CVR_OK;
   }
   if (!std::strcmp(key, "boost")) {
@@ -267,7 +283,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "boost")) return c->boost_pct;
   if (!std::strcmp(key, "tile_stats")) return c->tile_stats;
   if (!std::strcmp(key, "quad")) return c->quad_pct;
-  if (!std::strcmp(key, "pipeline")) return c->pipeline;
+  if (!std::strcmp(key, "kernel_timing")) return (int)c->ev_start.size();
   return -1;
 }
 
@@ -349,7 +365,11 @@ cvr_status cvr_set_transfer_function(cvr_ctx* ctx, const float* rgbt, int n) {
   if (!rgbt || n < 2 || n > 4096)
     return fail(c, CVR_ERR_ARG, "cvr_set_transfer_function: need 2 <= n <= 4096 entries");
   std::vector<float> q((size_t)n * 4);
-  for (size_t i = 0; i < q.size(); i++) q[i] = half_round(rgbt[i]);   // GL_RGBA16F
+  float amax = 0.0f;
+  for (size_t i = 0; i < q.size(); i++) {
+    q[i] = half_round(rgbt[i]);   // GL_RGBA16F
+    if (i % 4 == 3) amax = std::isfinite(q[i]) ? std::max(amax, q[i]) : NAN;
+  }
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (n != c->tf_n) {
@@ -358,6 +378,7 @@ cvr_status cvr_set_transfer_function(cvr_ctx* ctx, const float* rgbt, int n) {
     c->tf_n = n;
   }
   HIP_TRY(c, hipMemcpy(c->d_tf, q.data(), (size_t)n * 16, hipMemcpyHostToDevice));
+  c->tf_max_alpha = amax;
   return CVR_OK;
 }
 
@@ -437,6 +458,9 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   A.cells = c->cells;
   A.step = p->step > 0 ? p->step : cvr_default_step(c->scale);
   A.tf_n = c->tf_n;
+  // Sample opacity: a TF lerp lies within [0, max alpha] up to an ulp, and h <= step.
+  const double ext = (double)c->tf_max_alpha * (double)A.step * (1.0 + 1.0 / 1024.0);
+  A.exp_fast = (ext >= 0.0 && ext <= 86.0) ? 1 : 0;
   A.ka = p->ka; A.kd = p->kd; A.ks = p->ks; A.shininess = p->shininess;
   for (int i = 0; i < 3; i++) { A.ispec[i] = p->ispecular[i]; A.light[i] = p->light_pos[i]; }
   cvr::RenderPlan plan{};
@@ -519,7 +543,14 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     order = c->order_valid ? c->d_order : nullptr;
     tile_cost = c->d_tile_cost;
   }
+  const size_t nev = c->ev_start.size();
+  const size_t slot = nev ? (size_t)(c->timed_frames % (long long)nev) : 0;
+  if (nev) HIP_TRY(c, hipEventRecord(c->ev_start[slot], s));
   HIP_TRY(c, cvr::launch_rc1pass(*c, A, phong, d_out, d_samples, d_total, order, tile_cost, plan, s));
+  if (nev) {
+    HIP_TRY(c, hipEventRecord(c->ev_stop[slot], s));
+    c->timed_frames++;
+  }
   if (tile_cost) {
     HIP_TRY(c, cvr::launch_tile_order(tile_cost, plan, c->d_order, s));
     c->order_valid = 1;
@@ -544,6 +575,25 @@ cvr_status cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int* 
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   HIP_TRY(c, hipMemcpy(out, c->d_tile_stats, (size_t)n * 32, hipMemcpyDeviceToHost));
+  return CVR_OK;
+}
+
+cvr_status cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* out_frames) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c || !out_frames || max_frames < 0 || (max_frames > 0 && !ms)) return CVR_ERR_ARG;
+  const long long nev = (long long)c->ev_start.size();
+  if (!nev) return fail(c, CVR_ERR_STATE, "kernel_timing option was not enabled");
+  const long long have = c->timed_frames < nev ? c->timed_frames : nev;
+  const int n = (int)(have < max_frames ? have : max_frames);
+  HIP_TRY(c, hipSetDevice(c->device));
+  // the most recent n frames, oldest first
+  for (int i = 0; i < n; i++) {
+    const size_t slot = (size_t)((c->timed_frames - n + i) % nev);
+    HIP_TRY(c, hipEventSynchronize(c->ev_stop[slot]));
+    HIP_TRY(c, hipEventElapsedTime(&ms[i], c->ev_start[slot], c->ev_stop[slot]));
+  }
+  *out_frames = n;
+  c->timed_frames = 0;
   return CVR_OK;
 }
 

@@ -145,5 +145,21 @@ __device__ __forceinline__ float cvr_expf_nb(float x) {
   return x != x ? x : y;
 }
 
+// cvr_expf for x in [-86, 0]: the same value without the range selects (the
+// host enables it only when every sample's -(alpha*h) is known to lie there).
+__device__ __forceinline__ float cvr_expf_neg(float x) {
+  float n = rintf(x * 1.44269504088896341f);
+  float r = fmaf(n, -0.693359375f, x);
+  r = fmaf(n, 2.12194440e-4f, r);
+  float p = 1.9875691500e-4f;
+  p = fmaf(p, r, 1.3981999507e-3f);
+  p = fmaf(p, r, 8.3334519073e-3f);
+  p = fmaf(p, r, 4.1665795894e-2f);
+  p = fmaf(p, r, 1.6666665459e-1f);
+  p = fmaf(p, r, 5.0000001201e-1f);
+  float r2 = r * r;
+  return ldexpf(fmaf(p, r2, r) + 1.0f, (int)n);
+}
+
 
 }  // namespace cvr

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../../include/cvr.h"
 
@@ -44,6 +45,7 @@ struct Rc1passArgs {
   CellGrid cells;
   float step;
   int tf_n;
+  int exp_fast;                      // 1: every -(alpha*h) lies in [-86, 0] (no exp range checks)
   // Blinn-Phong (ray_marching_1p.comp:48-81)
   float ka, kd, ks, shininess;
   float ispec[3];
@@ -80,19 +82,22 @@ struct Ctx {
   // transfer function (RGBA16F values as float)
   float* d_tf = nullptr;
   int tf_n = 0;
+  float tf_max_alpha = 0.0f;         // largest (fp16-rounded) TF opacity; NaN if any is not finite
   // gradient (4 x fp16 per voxel, x-fastest)
   void* d_grad = nullptr;
   size_t grad_bytes = 0;
   int grad_mode = 0;
   // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
   int batch = 4;
-  int pipeline = 0;                // 1: two batches in flight (software-pipelined march)
-  int layout = kLayoutBrick;       // cell layout used by the next cvr_set_volume
+  int layout = kLayoutLinear;      // cell layout used by the next cvr_set_volume
   int boost_pct = 5;               // % of every band's longest entries run at raised priority
-  int quad_pct = 10;               // % of every band's longest tiles marched 4 lanes per ray
+  int quad_pct = 0;                // % of every band's longest tiles marched 4 lanes per ray
   int tile_stats = 0;              // record per-tile timing (diagnostics)
   unsigned long long* d_tile_stats = nullptr;
   int tile_stats_n = 0;
+  // kernel_timing option: HIP events around every frame's ray-march launch (ring)
+  std::vector<hipEvent_t> ev_start, ev_stop;
+  long long timed_frames = 0;
   int use_order = 1;               // 1: longest-first (LPT) from the previous frame's costs
   int* d_order = nullptr;          // unit permutation for the next frame
   uint32_t* d_tile_cost = nullptr; // per-wave-tile critical path of the last frame

@@ -12,12 +12,12 @@
 //         batch (K x 16 B in flight per lane), composited in order;
 //       - sample-parallel ("quad"): four lanes per ray, each fetching and
 //         classifying one of the next four samples, then an in-order composite
-//         over the quad with DPP broadcasts.  Used for the longest tiles: it
-//         cuts a long ray's dependency chain 4x, which is what bounds a frame;
+//         over the quad with DPP broadcasts.  Optional (option "quad", off by
+//         default: measured slower than ray-parallel even for the longest
+//         tiles) and compiled into a separate kernel;
 //   * scheduling: one wave per workgroup; each XCD owns one horizontal band of
 //     the screen (L2 locality) and, from the previous frame's per-tile critical
-//     paths, receives its band longest-first (LPT) with the longest tiles split
-//     into four quad-marched quarters.
+//     paths, receives its band longest-first (LPT).
 //
 // Arithmetic follows CVR-SPEC: explicit fmaf, IEEE div/sqrt, the
 // polynomial cvr_expf.  Compiled with -ffp-contract=off; both march variants
@@ -63,30 +63,30 @@ __device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lx, 
 // Sampling
 // ---------------------------------------------------------------------------
 
-// One sample's cell address + weights.  idx may be < 0 in the linear layout
-// (it is relative to the cell of texel (0,0,0)).
-struct SamplePos { int idx; float ax, ay, az; int ix, iy, iz; };
+// One sample's cell address + weights.  Texel coordinates are clamped to
+// [0, N-1]: under CLAMP_TO_EDGE a coordinate in [-1, 0) blends texel 0 with
+// itself and the clamped one weights texel 0 by exactly 1 — both give v0
+// bit-exactly (fmaf(a, 0, v0) = fmaf(0, d, v0) = v0 for v0 >= 0) — and with
+// x >= 0 the floor is the truncating convert and the weight one v_fract.
+struct SamplePos { uint32_t idx; float ax, ay, az; int ix, iy, iz; };
 
 template <int LAYOUT>
 __device__ __forceinline__ SamplePos sample_pos(float x, float y, float z, const Rc1passArgs& A) {
-  // GL_LINEAR texel-centre convention.  Clamping to [-1, N-1] (one v_med3) is
-  // value-neutral under CLAMP_TO_EDGE and keeps the padded cell index
-  // floor(x)+1 inside [0, N].
-  x = __builtin_amdgcn_fmed3f(x, -1.0f, A.nm1[0]);
-  y = __builtin_amdgcn_fmed3f(y, -1.0f, A.nm1[1]);
-  z = __builtin_amdgcn_fmed3f(z, -1.0f, A.nm1[2]);
-  float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+  x = __builtin_amdgcn_fmed3f(x, 0.0f, A.nm1[0]);
+  y = __builtin_amdgcn_fmed3f(y, 0.0f, A.nm1[1]);
+  z = __builtin_amdgcn_fmed3f(z, 0.0f, A.nm1[2]);
   SamplePos p;
-  p.ax = x - fx; p.ay = y - fy; p.az = z - fz;
-  p.ix = (int)fx; p.iy = (int)fy; p.iz = (int)fz;
+  p.ax = __builtin_amdgcn_fractf(x); p.ay = __builtin_amdgcn_fractf(y); p.az = __builtin_amdgcn_fractf(z);
+  p.ix = (int)x; p.iy = (int)y; p.iz = (int)z;
   if (LAYOUT == kLayoutLinear) {
     // cell (ix+1, iy+1, iz+1) of the (N+1)^3 grid; the +1 offsets live in the base pointer
-    p.idx = __mul24(p.iz, A.cells.pitch_z) + __mul24(p.iy, A.cells.pitch_y) + p.ix;
+    p.idx = __umul24((uint32_t)p.iz, (uint32_t)A.cells.pitch_z) +
+            __umul24((uint32_t)p.iy, (uint32_t)A.cells.pitch_y) + (uint32_t)p.ix;
   } else {
     uint32_t cx = (uint32_t)(p.ix + 1), cy = (uint32_t)(p.iy + 1), cz = (uint32_t)(p.iz + 1);
     uint32_t brick = __umul24(cz >> 2, (uint32_t)A.cells.bxby) +
                      __umul24(cy >> 2, (uint32_t)A.cells.bx) + (cx >> 2);
-    p.idx = (int)((brick << 6) | ((cz & 3u) << 4) | ((cy & 3u) << 2) | (cx & 3u));
+    p.idx = (brick << 6) | ((cz & 3u) << 4) | ((cy & 3u) << 2) | (cx & 3u);
   }
   return p;
 }
@@ -100,10 +100,12 @@ __device__ __forceinline__ float pair_diff(uint32_t w) {
   return d;
 }
 
-// lerp(lo, hi, t) of a packed fp16 pair = fmaf(t, hi - lo, lo): two v_fma_mix_f32.
+// lerp(lo, hi, t) of a packed fp16 pair = fmaf(t, hi - lo, lo): two
+// v_fma_mix_f32, the second taking lo straight from the low half.
 __device__ __forceinline__ float pair_lerp(uint32_t w, float t) {
-  half2_t p = __builtin_bit_cast(half2_t, w);
-  return fmaf(t, pair_diff(w), (float)p.x);
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(t), "v"(pair_diff(w)), "v"(w));
+  return r;
 }
 
 __device__ __forceinline__ float trilerp_cell(uint4 raw, float ax, float ay, float az) {
@@ -241,7 +243,8 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
           float4 sc = src[j];
           if (sc.w > 0.0f) {
             if (PHONG) shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
-            float a = 1.0f - cvr_expf_nb(-(sc.w * hj[j]));
+            const float x = -(sc.w * hj[j]);
+            float a = 1.0f - (A.exp_fast ? cvr_expf_neg(x) : cvr_expf_nb(x));
             float om = 1.0f - dst.w;
             dst.x = fmaf(om, sc.x * a, dst.x);
             dst.y = fmaf(om, sc.y * a, dst.y);
@@ -254,98 +257,6 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
     }
     s = ss;
     if (!(s < D)) done = true;
-  }
-}
-
-// Software-pipelined ray-parallel march: the K loads of batch i+1 are issued
-// before batch i is classified and composited, so a wave's memory latency
-// overlaps its own VALU work instead of adding to it (two batches in flight,
-// ping-ponged without register copies).  Speculative loads past the ERT exit
-// or past D read in-bounds cells (clamped) and are discarded.
-template <int K>
-struct Batch {
-  float h[K], t[K];
-  bool v[K];
-  SamplePos sp[K];
-  uint4 raw[K];
-};
-
-template <int K, int LAYOUT>
-__device__ __forceinline__ void issue_batch(const Rc1passArgs& A, const Ray& r, float step,
-                                            const uint4* __restrict__ cells, float& ss,
-                                            Batch<K>& B) {
-#pragma unroll
-  for (int j = 0; j < K; j++) {
-    B.v[j] = ss < r.D;
-    B.h[j] = fminf(step, r.D - ss);
-    B.t[j] = fmaf(B.h[j], 0.5f, ss);
-    ss = ss + B.h[j];
-    B.sp[j] = sample_pos<LAYOUT>(fmaf(r.dt.x, B.t[j], r.o.x), fmaf(r.dt.y, B.t[j], r.o.y),
-                                 fmaf(r.dt.z, B.t[j], r.o.z), A);
-    B.raw[j] = cells[B.sp[j].idx];
-  }
-}
-
-// Classifies and composites one batch in sample order; returns true once the
-// ray has terminated (ERT or end of the ray).
-template <int K, bool PHONG>
-__device__ __forceinline__ bool process_batch(const Rc1passArgs& A, const Ray& r,
-                                              const uint2* __restrict__ grad,
-                                              const float4* __restrict__ tfp, float fn,
-                                              const Batch<K>& B, float4& dst, uint32_t& cnt) {
-  float4 src[K];
-#pragma unroll
-  for (int j = 0; j < K; j++)
-    src[j] = classify(tfp, fn, trilerp_cell(B.raw[j], B.sp[j].ax, B.sp[j].ay, B.sp[j].az));
-  bool done = false;
-#pragma unroll
-  for (int j = 0; j < K; j++) {
-    if (!done) {
-      if (!B.v[j]) {
-        done = true;
-      } else {
-        cnt++;
-        float4 sc = src[j];
-        if (sc.w > 0.0f) {
-          if (PHONG) {
-            const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
-            const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
-            shade_phong(A, grad, B.sp[j], r.dir, B.t[j], r.tpos, hg, eye, sc);
-          }
-          float a = 1.0f - cvr_expf_nb(-(sc.w * B.h[j]));
-          float om = 1.0f - dst.w;
-          dst.x = fmaf(om, sc.x * a, dst.x);
-          dst.y = fmaf(om, sc.y * a, dst.y);
-          dst.z = fmaf(om, sc.z * a, dst.z);
-          dst.w = fmaf(om, a, dst.w);
-          if (dst.w > 0.99f) done = true;
-        }
-      }
-    }
-  }
-  return done;
-}
-
-template <int K, bool PHONG, int LAYOUT>
-__device__ __forceinline__ void march_ray_pipe(const Rc1passArgs& A,
-                                               const uint4* __restrict__ cells,
-                                               const uint2* __restrict__ grad,
-                                               const float4* __restrict__ tfp, int px, int py,
-                                               float4& dst, uint32_t& cnt) {
-  dst = make_float4(0.f, 0.f, 0.f, 0.f);
-  cnt = 0;
-  Ray r;
-  if (!ray_setup(A, px, py, r)) return;   // misses keep (0,0,0,0), renderoutputframe.cpp:187-190
-  if (!(0.0f < r.D)) return;
-  const float step = A.step, fn = (float)A.tf_n;
-  float ss = 0.0f;
-  Batch<K> b0, b1;
-  issue_batch<K, LAYOUT>(A, r, step, cells, ss, b0);
-  while (true) {
-    issue_batch<K, LAYOUT>(A, r, step, cells, ss, b1);
-    if (process_batch<K, PHONG>(A, r, grad, tfp, fn, b0, dst, cnt)) break;
-    issue_batch<K, LAYOUT>(A, r, step, cells, ss, b0);
-    if (process_batch<K, PHONG>(A, r, grad, tfp, fn, b1, dst, cnt)) break;
   }
 }
 
@@ -397,7 +308,8 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
     float a = 0.0f, pr = 0.0f, pg = 0.0f, pb = 0.0f;
     if (vj && sc.w > 0.0f) {
       if (PHONG) shade_phong(A, grad, sp, r.dir, tj, r.tpos, hg, eye, sc);
-      a = 1.0f - cvr_expf_nb(-(sc.w * hj));
+      const float x = -(sc.w * hj);
+      a = 1.0f - (A.exp_fast ? cvr_expf_neg(x) : cvr_expf_nb(x));
       pr = sc.x * a; pg = sc.y * a; pb = sc.z * a;
     }
     // in-order composite of the quad's 4 samples (every lane of the quad)
@@ -457,7 +369,7 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // (four lanes per ray).  Without an order, block b -> tile in XCD bands
 // (blocks b and b+8 share an XCD, so XCD b%8 gets one contiguous band).
 // Waves of the `boost` longest tiles of each band raise their priority.
-template <int K, bool PHONG, int LAYOUT, bool PIPE>
+template <int K, bool PHONG, int LAYOUT, bool QUAD>
 __global__ void __launch_bounds__(64)
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
@@ -472,7 +384,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     const int e = order[b];
     if (e < 0) return;                      // padding slot of a shorter band
     t = e & (kQuadFlag - 1);
-    quarter = (e >> 28) - 1;
+    if (QUAD) quarter = (e >> 28) - 1;
     if ((b >> 3) < boost) __builtin_amdgcn_s_setprio(2);
   } else if ((nt & 7) == 0) {
     t = (b & 7) * (nt >> 3) + (b >> 3);
@@ -487,15 +399,12 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   float4 dst;
   uint32_t cnt;
   bool writer;
-  if (quarter < 0) {          // whole tile, one lane per ray
+  if (!QUAD || quarter < 0) {   // whole tile, one lane per ray
     tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
     const bool inside = px < A.W && py < A.H;
     dst = make_float4(0.f, 0.f, 0.f, 0.f);
     cnt = 0;
-    if (inside) {
-      if (PIPE) march_ray_pipe<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
-      else march_ray<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
-    }
+    if (inside) march_ray<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
     writer = inside || A.packed;
   } else {                    // quarter of a tile, four lanes per ray
     const int ray = lane >> 2;
@@ -595,7 +504,7 @@ tile_order_kernel(uint32_t* __restrict__ tile_cost, int ntiles, int quad_pct, in
 // Launchers
 // ---------------------------------------------------------------------------
 
-template <int K, bool PHONG, int LAYOUT, bool PIPE>
+template <int K, bool PHONG, int LAYOUT, bool QUAD>
 static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                              unsigned long long* total, const int* order, uint32_t* tile_cost,
                              const RenderPlan& plan, hipStream_t s) {
@@ -603,7 +512,7 @@ static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, ui
   const uint4* cells = (const uint4*)c.d_cells;
   if (LAYOUT == kLayoutLinear) cells += c.cells.linear_origin;   // cell (1,1,1) <-> texel (0,0,0)
   int grid = order ? plan.order_slots : plan.ntiles;
-  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, LAYOUT, PIPE>), dim3(grid), dim3(64), lds, s, a,
+  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, LAYOUT, QUAD>), dim3(grid), dim3(64), lds, s, a,
                      cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, total,
                      order, tile_cost, order ? plan.boost : 0);
   return hipGetLastError();
@@ -613,7 +522,9 @@ template <int K, bool PHONG>
 static hipError_t launch_kp(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                             unsigned long long* total, const int* order, uint32_t* tile_cost,
                             const RenderPlan& plan, hipStream_t s) {
-  if (c.pipeline)
+  // the quad march is compiled into its own kernel: it costs the ray-parallel
+  // path registers (occupancy) even when no entry uses it
+  if (order && plan.quad_pct > 0)
     return c.cells.layout == kLayoutLinear
                ? launch_kpl<K, PHONG, kLayoutLinear, true>(c, a, out, samples, total, order, tile_cost, plan, s)
                : launch_kpl<K, PHONG, kLayoutBrick, true>(c, a, out, samples, total, order, tile_cost, plan, s);

@@ -131,12 +131,13 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                0: screen order
  *   "boost"      percent of each band's longest entries launched at raised wave
  *                priority (with tile_order 1; default 5)
- *   "pipeline"   1: software-pipelined march, two batches of loads in flight per lane
  *   "quad"       percent of each band's longest tiles marched sample-parallel, four
- *                lanes per ray (with tile_order 1; default 10)
- *   "layout"     cell layout of the next cvr_set_volume: 0 bricked 4^3 (default),
- *                1 linear x-fastest
- *   "tile_stats" 1: record per-tile timing of every frame (diagnostics) */
+ *                lanes per ray (with tile_order 1; default 0)
+ *   "layout"     cell layout of the next cvr_set_volume: 0 bricked 4^3,
+ *                1 linear x-fastest (default)
+ *   "tile_stats" 1: record per-tile timing of every frame (diagnostics)
+ *   "kernel_timing" N > 0: time the ray-march kernel of the last N frames
+ *                (cvr_read_kernel_times); 0 off (default) */
 cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
 int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);
@@ -187,6 +188,12 @@ cvr_status  cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* frame,
  * uint64: start and end stamp (s_memrealtime, 100 MHz), its longest ray's
  * iteration count, (workgroup << 32 | HW_ID).  out = NULL queries *out_tiles. */
 cvr_status  cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int* out_tiles);
+
+/* Measurement (kernel_timing option = ring of N frames): milliseconds of the
+ * ray-march kernel alone (HIP events recorded on the context stream around its
+ * launch) for the most recent min(N, frames since the last read, max_frames)
+ * frames, oldest first.  Waits for those frames; resets the frame count. */
+cvr_status  cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* out_frames);
 
 /* ----------------------------------------------------------------------------
  * Host-side helpers (native replacements for the reference's MSVC-only

@@ -154,7 +154,8 @@ def render_rc1pass(vol16: np.ndarray, scale, tf: np.ndarray, camera: dict, W: in
                    light=(0.0, 0.0, 0.0), threads: int = 0, rows=None):
     """Full frame (or rows=(y0,y1)) of ray_marching_1p.comp. Returns (rgba HxWx4, counts HxW, S)."""
     vol16 = np.ascontiguousarray(vol16, np.float32)
-    tf = np.ascontiguousarray(tf, np.float32)
+    # the TF texture is GL_RGBA16F (GenerateTexture_1D_RGBt): entries round to half (RNE)
+    tf = np.ascontiguousarray(np.asarray(tf, np.float32).astype(np.float16), np.float32)
     if grad is not None:
         grad = np.ascontiguousarray(grad, np.float32)
     P = _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shininess, ispec,

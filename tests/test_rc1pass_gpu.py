@@ -110,6 +110,10 @@ CASES = {
     # Blinn-Phong with finite-difference and Sobel gradients (config 3 path)
     "phong_fd": dict(vol=lambda: _ml(64), scale=D.voxel_scale(64), W=160, H=160, phong=True,
                      gmode=1, light=D.LIGHT_LIST0_POSITION),
+    # opacities so large that -(alpha*h) leaves exp's fast range (range-checked exp path,
+    # exp underflows to 0 past -86)
+    "dense_tf": dict(vol=lambda: _ml(48), scale=D.voxel_scale(48), W=128, H=112, step=1.7,
+                     tf_alpha_scale=400.0),
     "phong_sobel": dict(vol=lambda: _ml(48), scale=D.voxel_scale(48), W=128, H=128, phong=True,
                         gmode=2, light=D.LIGHT_LIST0_POSITION, shading=(0.3, 0.6, 0.5, 12.5)),
 }
@@ -119,6 +123,9 @@ CASES = {
 def test_rc1pass_bitexact_vs_oracle(dev, oracle, bonsai_tf, name):
     c = CASES[name]
     vol = c["vol"]()
+    if "tf_alpha_scale" in c:
+        bonsai_tf = bonsai_tf.copy()
+        bonsai_tf[:, 3] *= c["tf_alpha_scale"]
     cam = c.get("cam", INITIAL)
     kw = dict(step=c.get("step", 0.0), phong=c.get("phong", False), gmode=c.get("gmode", 0),
               light=c.get("light", (0, 0, 0)), shading=c.get("shading", (0.5, 0.5, 0.8, 30.0)))
@@ -267,3 +274,22 @@ def test_screen_tiles_with_quad_schedule(bonsai_tf, nranks, tile):
         assert_bitexact(T.unpack(packed_all, W, H, tile, nranks), full, "unpacked")
     finally:
         d.close()
+
+
+def test_kernel_timing_ring(dev, bonsai_tf):
+    """kernel_timing: the library's HIP events around the ray-march launch."""
+    vol = _ml(32)
+    L = N.lib()
+    N.check(L.cvr_set_option(dev.handle, b"kernel_timing", 3), "kernel_timing")
+    try:
+        for i in range(5):
+            gpu_render(dev, vol, D.voxel_scale(32), bonsai_tf, INITIAL, 64, 64, set_data=(i == 0))
+        ms = (ctypes.c_float * 8)()
+        n = ctypes.c_int()
+        N.check(L.cvr_read_kernel_times(dev.handle, ms, 8, ctypes.byref(n)), "read", dev.handle)
+        assert n.value == 3 and all(0.0 < ms[i] < 1000.0 for i in range(3))
+        N.check(L.cvr_read_kernel_times(dev.handle, ms, 8, ctypes.byref(n)), "read", dev.handle)
+        assert n.value == 0
+    finally:
+        N.check(L.cvr_set_option(dev.handle, b"kernel_timing", 0), "kernel_timing")
+    assert L.cvr_read_kernel_times(dev.handle, ms, 8, ctypes.byref(n)) == N.CVR_ERR_STATE
