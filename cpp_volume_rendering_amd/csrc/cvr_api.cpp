@@ -199,6 +199,7 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_order; free_dev(p); c->d_order = nullptr;
   p = c->d_tile_cost; free_dev(p); c->d_tile_cost = nullptr;
   p = c->d_tile_stats; free_dev(p); c->d_tile_stats = nullptr;
+  p = c->d_tile_samples; free_dev(p); c->d_tile_samples = nullptr;
   for (hipEvent_t e : c->ev_start) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_stop) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -543,18 +544,34 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     order = c->order_valid ? c->d_order : nullptr;
     tile_cost = c->d_tile_cost;
   }
+  // Sample total: every wave tile stores its count, the epilogue sums them
+  // (one atomic per band; a per-wave atomic on one word serialises the frame).
+  unsigned long long* tile_samples = nullptr;
+  if (d_total) {
+    if (c->tile_samples_n < plan.ntiles) {
+      void* p = c->d_tile_samples; free_dev(p); c->d_tile_samples = nullptr; c->tile_samples_n = 0;
+      HIP_TRY(c, hipMalloc((void**)&c->d_tile_samples, (size_t)plan.ntiles * 8));
+      HIP_TRY(c, hipMemsetAsync(c->d_tile_samples, 0, (size_t)plan.ntiles * 8, s));
+      c->tile_samples_n = plan.ntiles;
+    }
+    tile_samples = c->d_tile_samples;
+  }
   const size_t nev = c->ev_start.size();
   const size_t slot = nev ? (size_t)(c->timed_frames % (long long)nev) : 0;
   if (nev) HIP_TRY(c, hipEventRecord(c->ev_start[slot], s));
-  HIP_TRY(c, cvr::launch_rc1pass(*c, A, phong, d_out, d_samples, d_total, order, tile_cost, plan, s));
+  HIP_TRY(c, cvr::launch_rc1pass(*c, A, phong, d_out, d_samples, tile_samples, order, tile_cost,
+                                 plan, s));
   if (nev) {
     HIP_TRY(c, hipEventRecord(c->ev_stop[slot], s));
     c->timed_frames++;
   }
-  if (tile_cost) {
-    HIP_TRY(c, cvr::launch_tile_order(tile_cost, plan, c->d_order, s));
-    c->order_valid = 1;
-    c->order_key = key;
+  if (tile_cost || tile_samples) {
+    HIP_TRY(c, cvr::launch_tile_epilogue(tile_cost, tile_samples, d_total, plan,
+                                         tile_cost ? c->d_order : nullptr, s));
+    if (tile_cost) {
+      c->order_valid = 1;
+      c->order_key = key;
+    }
   }
   if (!o->on_device) {
     HIP_TRY(c, hipMemcpyAsync(o->rgba, d_out, rgba_bytes, hipMemcpyDeviceToHost, s));

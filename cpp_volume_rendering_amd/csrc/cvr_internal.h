@@ -105,6 +105,8 @@ struct Ctx {
   int order_key = -1;              // plan signature the order was learned for
   int order_valid = 0;
   int num_cus = 0;
+  unsigned long long* d_tile_samples = nullptr;   // per-wave-tile sample counts (zeroed)
+  int tile_samples_n = 0;
   // scratch
   unsigned long long* d_total = nullptr;
   void* d_scratch = nullptr;      // host-output staging
@@ -116,10 +118,12 @@ hipError_t launch_build_cells_impl(const void* vox, int bpv, const uint16_t* lut
                                    const CellGrid& g, void* cells, hipStream_t s);
 hipError_t launch_gradient(const Ctx& c, int mode, hipStream_t s);
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
-                          uint32_t* samples, unsigned long long* total, const int* order,
+                          uint32_t* samples, unsigned long long* tile_samples, const int* order,
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s);
-hipError_t launch_tile_order(uint32_t* tile_cost, const RenderPlan& plan, int* order,
-                             hipStream_t s);
+// after a frame: sums tile_samples into *total and/or builds the next LPT order
+hipError_t launch_tile_epilogue(uint32_t* tile_cost, unsigned long long* tile_samples,
+                                unsigned long long* total, const RenderPlan& plan, int* order,
+                                hipStream_t s);
 hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
                                int nranks, int tiles_per_rank_max, hipStream_t s);
 

@@ -260,21 +260,48 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
   }
 }
 
-template <int K>
+// Value of `v` in lane L of this lane's quad (DPP quad_perm broadcast).
+template <int L>
 __device__ __forceinline__ float quad_bcast(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), K | (K << 2) | (K << 4) | (K << 6),
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), L | (L << 2) | (L << 4) | (L << 6),
                                                  0xf, 0xf, false));
 }
 
-// Sample-parallel march: the 4 lanes of a quad share one ray; per iteration
-// lane j takes the j-th of the ray's next 4 samples (positions from the same
-// sequential s += h recurrence), fetches and classifies it, then every lane of
-// the quad composites the 4 samples in order (DPP quad broadcasts) and applies
-// the ERT exit, so all four hold the ray's identical state.  A transparent or
-// out-of-range sample enters the composite as exact zeros, which leaves dst
-// bit-unchanged — the same result as the reference skipping it (:142).
+// One premultiplied sample of the quad march: (alpha, r*alpha, g*alpha, b*alpha).
+struct QSample { float a, r, g, b; };
+
+// Composite sample k (owned by quad lane L) into dst, in sample order.
+template <int L>
+__device__ __forceinline__ void quad_composite(const QSample& q, bool valid, bool& done,
+                                               float4& dst, uint32_t& cnt) {
+  const float ak = quad_bcast<L>(q.a), rk = quad_bcast<L>(q.r);
+  const float gk = quad_bcast<L>(q.g), bk = quad_bcast<L>(q.b);
+  if (!done) {
+    if (valid) {
+      cnt++;
+      const float om = 1.0f - dst.w;
+      dst.x = fmaf(om, rk, dst.x);
+      dst.y = fmaf(om, gk, dst.y);
+      dst.z = fmaf(om, bk, dst.z);
+      dst.w = fmaf(om, ak, dst.w);
+      if (dst.w > 0.99f) done = true;
+    } else {
+      done = true;
+    }
+  }
+}
+
+// Sample-parallel march: the 4 lanes of a quad share one ray.  Each iteration
+// covers the ray's next 4K samples (positions from the same sequential s += h
+// recurrence); sample 4k+j belongs to quad lane j, which fetches and classifies
+// its K samples with all K loads in flight.  Every lane then composites the 4K
+// samples in order (DPP quad broadcasts) and applies the ERT exit, so all four
+// hold the ray's identical state.  A transparent sample enters the composite as
+// exact zeros, which leaves dst bit-unchanged — the same result as the
+// reference skipping it (:142).  One memory round trip advances a ray 4K
+// samples instead of K: the longest tiles' critical path shrinks ~4x.
 // Must be called by all 64 lanes (DPP reads neighbours); `active` = lane's ray is live.
-template <bool PHONG, int LAYOUT>
+template <int K, bool PHONG, int LAYOUT>
 __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
                                                const uint4* __restrict__ cells,
                                                const uint2* __restrict__ grad,
@@ -289,55 +316,55 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
   const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
   const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
   const float step = A.step, fn = (float)A.tf_n;
+  const unsigned qshift = threadIdx.x & ~3u;
   float s = 0.0f;
   bool done = !(s < D);
   while (!__all(done)) {
-    // this lane's sample: the j-th step of the sequential recurrence from s
-    float ss = s, sj = 0.0f, hj = 0.0f;
+    // this lane's samples: steps 4k+j of the sequential recurrence from s
+    float sj[K], hj[K];
+    float ss = s;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      float h = fminf(step, D - ss);
-      if (k == j) { sj = ss; hj = h; }
-      ss = ss + h;
+    for (int k = 0; k < K; k++) {
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const float h = fminf(step, D - ss);
+        if (l == j) { sj[k] = ss; hj[k] = h; }
+        ss = ss + h;
+      }
     }
-    const bool vj = !done && sj < D;
-    const float tj = fmaf(hj, 0.5f, sj);
-    SamplePos sp = sample_pos<LAYOUT>(fmaf(r.dt.x, tj, r.o.x), fmaf(r.dt.y, tj, r.o.y),
-                                      fmaf(r.dt.z, tj, r.o.z), A);
-    float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
-    float a = 0.0f, pr = 0.0f, pg = 0.0f, pb = 0.0f;
-    if (vj && sc.w > 0.0f) {
-      if (PHONG) shade_phong(A, grad, sp, r.dir, tj, r.tpos, hg, eye, sc);
-      const float x = -(sc.w * hj);
-      a = 1.0f - (A.exp_fast ? cvr_expf_neg(x) : cvr_expf_nb(x));
-      pr = sc.x * a; pg = sc.y * a; pb = sc.z * a;
+    SamplePos sp[K];
+    uint4 raw[K];
+    float tj[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      tj[k] = fmaf(hj[k], 0.5f, sj[k]);
+      sp[k] = sample_pos<LAYOUT>(fmaf(r.dt.x, tj[k], r.o.x), fmaf(r.dt.y, tj[k], r.o.y),
+                                 fmaf(r.dt.z, tj[k], r.o.z), A);
+      raw[k] = cells[sp[k].idx];
     }
-    // in-order composite of the quad's 4 samples (every lane of the quad)
-    const unsigned long long vm = __ballot(vj);
-    const unsigned qv = (unsigned)(vm >> (threadIdx.x & ~3u)) & 0xfu;
-#define CVR_QUAD_STEP(K)                                                        \
-    {                                                                           \
-      float ak = quad_bcast<K>(a), rk = quad_bcast<K>(pr);                      \
-      float gk = quad_bcast<K>(pg), bk = quad_bcast<K>(pb);                     \
-      if (!done) {                                                              \
-        if (qv & (1u << K)) {                                                   \
-          cnt++;                                                                \
-          float om = 1.0f - dst.w;                                              \
-          dst.x = fmaf(om, rk, dst.x);                                          \
-          dst.y = fmaf(om, gk, dst.y);                                          \
-          dst.z = fmaf(om, bk, dst.z);                                          \
-          dst.w = fmaf(om, ak, dst.w);                                          \
-          if (dst.w > 0.99f) done = true;                                       \
-        } else {                                                                \
-          done = true;                                                          \
-        }                                                                       \
-      }                                                                         \
+    QSample q[K];
+    unsigned qv[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      float4 sc = classify(tfp, fn, trilerp_cell(raw[k], sp[k].ax, sp[k].ay, sp[k].az));
+      const bool vj = !done && sj[k] < D;
+      q[k] = QSample{0.0f, 0.0f, 0.0f, 0.0f};
+      if (vj && sc.w > 0.0f) {
+        if (PHONG) shade_phong(A, grad, sp[k], r.dir, tj[k], r.tpos, hg, eye, sc);
+        const float x = -(sc.w * hj[k]);
+        const float a = 1.0f - (A.exp_fast ? cvr_expf_neg(x) : cvr_expf_nb(x));
+        q[k] = QSample{a, sc.x * a, sc.y * a, sc.z * a};
+      }
+      qv[k] = (unsigned)(__ballot(vj) >> qshift) & 0xfu;
     }
-    CVR_QUAD_STEP(0)
-    CVR_QUAD_STEP(1)
-    CVR_QUAD_STEP(2)
-    CVR_QUAD_STEP(3)
-#undef CVR_QUAD_STEP
+    // in-order composite of the 4K samples (every lane of the quad)
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      quad_composite<0>(q[k], qv[k] & 1u, done, dst, cnt);
+      quad_composite<1>(q[k], qv[k] & 2u, done, dst, cnt);
+      quad_composite<2>(q[k], qv[k] & 4u, done, dst, cnt);
+      quad_composite<3>(q[k], qv[k] & 8u, done, dst, cnt);
+    }
     s = ss;
   }
 }
@@ -374,7 +401,7 @@ __global__ void __launch_bounds__(64)
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
                     float4* __restrict__ out, uint32_t* __restrict__ samples,
-                    unsigned long long* __restrict__ total, const int* __restrict__ order,
+                    unsigned long long* __restrict__ tile_samples, const int* __restrict__ order,
                     uint32_t* __restrict__ tile_cost, int boost) {
   extern __shared__ float4 tfp[];
   load_tf_lds(tfp, tf_g, A.tf_n);
@@ -411,7 +438,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     tile_pixel(A, t, ((quarter & 1) << 2) | (ray & 3), ((quarter >> 1) << 2) | (ray >> 2), px, py,
                oidx);
     const bool inside = px < A.W && py < A.H;
-    march_ray_quad<PHONG, LAYOUT>(A, cells, grad, tfp, px, py, inside, dst, cnt);
+    march_ray_quad<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, inside, dst, cnt);
     writer = (lane & 3) == 0 && (inside || A.packed);
     if ((lane & 3) != 0) cnt = 0;           // one count per ray
   }
@@ -419,9 +446,15 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     out[oidx] = dst;
     if (samples) samples[oidx] = cnt;
   }
-  if (total) {
+  if (tile_samples) {   // per-tile sample count; summed by tile_order_kernel (no hot atomic)
     unsigned long long v = wave_sum(cnt);
-    if (lane == 0 && v) atomicAdd(total, v);
+    if (lane == 0) {
+      if (QUAD && quarter >= 0) {
+        if (v) atomicAdd(&tile_samples[t], v);
+      } else {
+        tile_samples[t] = v;
+      }
+    }
   }
   uint32_t m = 0;
   if (tile_cost || A.tile_stats) m = wave_max(cnt);
@@ -446,58 +479,106 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
 // Launch order (LPT) from the previous frame
 // ---------------------------------------------------------------------------
 
-// Workgroup `band` orders the tiles of XCD band `band` by descending critical
-// path (bucketed into 256 cost levels: O(n), ties in any order — the order
-// never changes a pixel), expands the longest `nquad` tiles into four quad
-// quarters, and deals the entries to physical blocks band, band+8, ... (the
-// blocks XCD `band` receives).  Slots past the band's entries are -1.  Resets
-// tile_cost for the next frame's atomicMax.
-__global__ void __launch_bounds__(1024)
-tile_order_kernel(uint32_t* __restrict__ tile_cost, int ntiles, int quad_pct, int slots_per_band,
-                  int* __restrict__ order) {
+// Per-frame epilogue, one workgroup per XCD band:
+//  * `tile_samples` (optional): sums the band's per-tile sample counts into
+//    *total (one atomic per band instead of one per wave on a single word) and
+//    resets them;
+//  * `tile_cost` (optional): orders the band's tiles by descending critical
+//    path (bucketed into 256 cost levels: O(n), ties in any order — the order
+//    never changes a pixel), expands the longest `nquad` tiles into four quad
+//    quarters, and deals the entries to physical blocks band, band+8, ... (the
+//    blocks XCD `band` receives); slots past the band's entries are -1.  Resets
+//    tile_cost for the next frame's atomicMax.
+constexpr int kOrderThreads = 1024;
+constexpr int kOrderPerThread = 4;   // tiles a thread keeps in registers (larger bands loop)
+
+__global__ void __launch_bounds__(kOrderThreads)
+tile_epilogue_kernel(uint32_t* __restrict__ tile_cost, unsigned long long* __restrict__ tile_samples,
+                     unsigned long long* __restrict__ total, int ntiles, int quad_pct,
+                     int slots_per_band, int* __restrict__ order) {
   __shared__ unsigned hist[256];
   __shared__ unsigned start[256];
   __shared__ unsigned maxc;
+  __shared__ unsigned long long wsum[kOrderThreads / 64];
   extern __shared__ int sorted[];   // ceil(ntiles / 8) entries
-  const int band = blockIdx.x;
+  const int band = blockIdx.x, tid = threadIdx.x;
   const int b0 = (band * ntiles) >> 3, b1 = ((band + 1) * ntiles) >> 3;
   const int seg = b1 - b0;
-  if (threadIdx.x < 256) hist[threadIdx.x] = 0;
-  if (threadIdx.x == 0) maxc = 0;
+  if (tile_samples) {
+    unsigned long long acc = 0;
+    for (int i = tid; i < seg; i += kOrderThreads) {
+      acc += tile_samples[b0 + i];
+      tile_samples[b0 + i] = 0ull;
+    }
+    acc = wave_sum(acc);
+    if ((tid & 63) == 0) wsum[tid >> 6] = acc;
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long t = 0;
+      for (int w = 0; w < kOrderThreads / 64; w++) t += wsum[w];
+      if (total && t) atomicAdd(total, t);
+    }
+  }
+  if (!tile_cost) return;
+  if (tid < 256) hist[tid] = 0;
+  if (tid == 0) maxc = 0;
   __syncthreads();
+  // the band's costs, read once (a thread's tiles are tid, tid + 1024, ...)
+  uint32_t cst[kOrderPerThread];
   unsigned lmax = 0;
-  for (int i = threadIdx.x; i < seg; i += blockDim.x) lmax = max(lmax, tile_cost[b0 + i]);
-  atomicMax(&maxc, lmax);
+#pragma unroll
+  for (int k = 0; k < kOrderPerThread; k++) {
+    const int i = tid + k * kOrderThreads;
+    cst[k] = i < seg ? tile_cost[b0 + i] : 0u;
+    lmax = max(lmax, cst[k]);
+  }
+  for (int i = tid + kOrderPerThread * kOrderThreads; i < seg; i += kOrderThreads)
+    lmax = max(lmax, tile_cost[b0 + i]);
+  lmax = wave_max(lmax);
+  if ((tid & 63) == 0) atomicMax(&maxc, lmax);
   __syncthreads();
-  const unsigned mc = maxc + 1;
-  for (int i = threadIdx.x; i < seg; i += blockDim.x) {
-    unsigned c = tile_cost[b0 + i];
-    unsigned bucket = 255u - (unsigned)(((unsigned long long)c * 256u) / mc);
-    atomicAdd(&hist[bucket], 1u);
+  const unsigned long long mc = (unsigned long long)maxc + 1;
+  auto bucket_of = [mc](uint32_t c) { return 255u - (unsigned)(((unsigned long long)c * 256u) / mc); };
+#pragma unroll
+  for (int k = 0; k < kOrderPerThread; k++)
+    if (tid + k * kOrderThreads < seg) atomicAdd(&hist[bucket_of(cst[k])], 1u);
+  for (int i = tid + kOrderPerThread * kOrderThreads; i < seg; i += kOrderThreads)
+    atomicAdd(&hist[bucket_of(tile_cost[b0 + i])], 1u);
+  __syncthreads();
+  if (tid < 64) {   // exclusive scan of the 256 counts by one wave (4 per lane)
+    const unsigned h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2],
+                   h3 = hist[4 * tid + 3];
+    const unsigned part = h0 + h1 + h2 + h3;
+    unsigned incl = part;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned o = (unsigned)__shfl_up((int)incl, off, 64);
+      if (tid >= off) incl += o;
+    }
+    unsigned ex = incl - part;
+    start[4 * tid] = ex; ex += h0;
+    start[4 * tid + 1] = ex; ex += h1;
+    start[4 * tid + 2] = ex; ex += h2;
+    start[4 * tid + 3] = ex;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned acc = 0;
-    for (int k = 0; k < 256; k++) { start[k] = acc; acc += hist[k]; }
+#pragma unroll
+  for (int k = 0; k < kOrderPerThread; k++) {
+    const int i = tid + k * kOrderThreads;
+    if (i < seg) sorted[atomicAdd(&start[bucket_of(cst[k])], 1u)] = b0 + i;
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < seg; i += blockDim.x) {
-    unsigned c = tile_cost[b0 + i];
-    unsigned bucket = 255u - (unsigned)(((unsigned long long)c * 256u) / mc);
-    unsigned pos = atomicAdd(&start[bucket], 1u);
-    sorted[pos] = b0 + i;
-  }
+  for (int i = tid + kOrderPerThread * kOrderThreads; i < seg; i += kOrderThreads)
+    sorted[atomicAdd(&start[bucket_of(tile_cost[b0 + i])], 1u)] = b0 + i;
   __syncthreads();
   const int nquad = (int)(((long long)seg * quad_pct) / 100);
   const int nent = seg + 3 * nquad;
-  for (int e = threadIdx.x; e < slots_per_band; e += blockDim.x) {
+  for (int e = tid; e < slots_per_band; e += kOrderThreads) {
     int v = -1;
     if (e < 4 * nquad) v = sorted[e >> 2] | (((e & 3) + 1) << 28);
     else if (e < nent) v = sorted[e - 3 * nquad];
     order[band + 8 * e] = v;
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < seg; i += blockDim.x) tile_cost[b0 + i] = 0u;
+  for (int i = tid; i < seg; i += kOrderThreads) tile_cost[b0 + i] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -506,59 +587,61 @@ tile_order_kernel(uint32_t* __restrict__ tile_cost, int ntiles, int quad_pct, in
 
 template <int K, bool PHONG, int LAYOUT, bool QUAD>
 static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
-                             unsigned long long* total, const int* order, uint32_t* tile_cost,
+                             unsigned long long* tile_samples, const int* order, uint32_t* tile_cost,
                              const RenderPlan& plan, hipStream_t s) {
   size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
   const uint4* cells = (const uint4*)c.d_cells;
   if (LAYOUT == kLayoutLinear) cells += c.cells.linear_origin;   // cell (1,1,1) <-> texel (0,0,0)
   int grid = order ? plan.order_slots : plan.ntiles;
   hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, LAYOUT, QUAD>), dim3(grid), dim3(64), lds, s, a,
-                     cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, total,
+                     cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, tile_samples,
                      order, tile_cost, order ? plan.boost : 0);
   return hipGetLastError();
 }
 
 template <int K, bool PHONG>
 static hipError_t launch_kp(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
-                            unsigned long long* total, const int* order, uint32_t* tile_cost,
+                            unsigned long long* tile_samples, const int* order, uint32_t* tile_cost,
                             const RenderPlan& plan, hipStream_t s) {
   // the quad march is compiled into its own kernel: it costs the ray-parallel
   // path registers (occupancy) even when no entry uses it
   if (order && plan.quad_pct > 0)
     return c.cells.layout == kLayoutLinear
-               ? launch_kpl<K, PHONG, kLayoutLinear, true>(c, a, out, samples, total, order, tile_cost, plan, s)
-               : launch_kpl<K, PHONG, kLayoutBrick, true>(c, a, out, samples, total, order, tile_cost, plan, s);
+               ? launch_kpl<K, PHONG, kLayoutLinear, true>(c, a, out, samples, tile_samples, order, tile_cost, plan, s)
+               : launch_kpl<K, PHONG, kLayoutBrick, true>(c, a, out, samples, tile_samples, order, tile_cost, plan, s);
   return c.cells.layout == kLayoutLinear
-             ? launch_kpl<K, PHONG, kLayoutLinear, false>(c, a, out, samples, total, order, tile_cost, plan, s)
-             : launch_kpl<K, PHONG, kLayoutBrick, false>(c, a, out, samples, total, order, tile_cost, plan, s);
+             ? launch_kpl<K, PHONG, kLayoutLinear, false>(c, a, out, samples, tile_samples, order, tile_cost, plan, s)
+             : launch_kpl<K, PHONG, kLayoutBrick, false>(c, a, out, samples, tile_samples, order, tile_cost, plan, s);
 }
 
 template <int K>
 static hipError_t launch_k(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
-                           uint32_t* samples, unsigned long long* total, const int* order,
+                           uint32_t* samples, unsigned long long* tile_samples, const int* order,
                            uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
-  return phong ? launch_kp<K, true>(c, a, out, samples, total, order, tile_cost, plan, s)
-               : launch_kp<K, false>(c, a, out, samples, total, order, tile_cost, plan, s);
+  return phong ? launch_kp<K, true>(c, a, out, samples, tile_samples, order, tile_cost, plan, s)
+               : launch_kp<K, false>(c, a, out, samples, tile_samples, order, tile_cost, plan, s);
 }
 
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
-                          uint32_t* samples, unsigned long long* total, const int* order,
+                          uint32_t* samples, unsigned long long* tile_samples, const int* order,
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
   if (a.ntiles <= 0) return hipSuccess;
   if (a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
   switch (c.batch) {
-    case 2: return launch_k<2>(c, a, phong, out, samples, total, order, tile_cost, plan, s);
-    case 8: return launch_k<8>(c, a, phong, out, samples, total, order, tile_cost, plan, s);
-    default: return launch_k<4>(c, a, phong, out, samples, total, order, tile_cost, plan, s);
+    case 2: return launch_k<2>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
+    case 8: return launch_k<8>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
+    default: return launch_k<4>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
   }
 }
 
-hipError_t launch_tile_order(uint32_t* tile_cost, const RenderPlan& plan, int* order,
-                             hipStream_t s) {
+hipError_t launch_tile_epilogue(uint32_t* tile_cost, unsigned long long* tile_samples,
+                                unsigned long long* total, const RenderPlan& plan, int* order,
+                                hipStream_t s) {
   const int seg_max = (plan.ntiles + 7) >> 3;
-  if (seg_max > 32768) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tile_order_kernel, dim3(8), dim3(1024), (size_t)seg_max * sizeof(int), s,
-                     tile_cost, plan.ntiles, plan.quad_pct, plan.order_slots / 8, order);
+  if (tile_cost && seg_max > 16384) return hipErrorInvalidValue;   // sorted[] in LDS
+  hipLaunchKernelGGL(tile_epilogue_kernel, dim3(8), dim3(kOrderThreads),
+                     tile_cost ? (size_t)seg_max * sizeof(int) : 0, s, tile_cost, tile_samples,
+                     total, plan.ntiles, plan.quad_pct, plan.order_slots / 8, order);
   return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--variants", default="L1b4o1p5q0,L1b2o1p5q0,L0b4o1p5q0,L1b4o1p0q0,L1b4o0p0q0,L1b4o1p5q10")
     ap.add_argument("--phong", action="store_true")
+    ap.add_argument("--no-total", action="store_true", help="time frames without the sample counter")
     a = ap.parse_args()
     n, W = a.size, a.res
     vol = D.marschner_lobb_u8(n) if a.field == "ml" else D.blobs_u8(n)
@@ -60,12 +61,13 @@ def main():
     img = torch.zeros((W, W, 4), dtype=torch.float32, device="cuda")
     tot = torch.zeros(1, dtype=torch.int64, device="cuda")
     out = N.Output(img.data_ptr(), None, tot.data_ptr(), 1)
+    out_nt = N.Output(img.data_ptr(), None, None, 1)
     L = N.lib()
 
-    def run(dev, frames):
+    def run(dev, frames, o=out):
         for _ in range(frames):
             N.check(L.cvr_render_rc1pass(dev.handle, ctypes.byref(frame), ctypes.byref(p),
-                                         ctypes.byref(out)), "render", dev.handle)
+                                         ctypes.byref(o)), "render", dev.handle)
 
     res = {v: [] for v in variants}
     ref_img = None
@@ -83,14 +85,20 @@ def main():
                 tot.zero_()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
-                run(dev, a.frames)
+                run(dev, a.frames, out_nt if a.no_total else out)
                 e1.record(s)
             s.synchronize()
             res[v].append(e0.elapsed_time(e1) / a.frames)
             cur = img.cpu().numpy()
             if ref_img is None:
                 ref_img = cur
-                S = int(tot.item()) // a.frames
+                if a.no_total:
+                    tot.zero_()
+                    run(dev, 1)
+                    torch.cuda.synchronize()
+                    S = int(tot.item())
+                else:
+                    S = int(tot.item()) // a.frames
             else:
                 assert np.array_equal(cur.view(np.uint32), ref_img.view(np.uint32)), f"{v} differs"
     rows = []

@@ -25,13 +25,14 @@ def main():
     ap.add_argument("--order", type=int, default=1)
     ap.add_argument("--boost", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--quad", type=int, default=0)
     ap.add_argument("--tag", default="run")
     a = ap.parse_args()
     n, W = a.size, a.res
     dev = Device(0)
     L = N.lib()
     for k, v in (("layout", a.layout), ("tile_order", a.order), ("boost", a.boost),
-                 ("batch", a.batch), ("tile_stats", 1)):
+                 ("batch", a.batch), ("quad", a.quad), ("tile_stats", 1)):
         N.check(L.cvr_set_option(dev.handle, k.encode(), v), k)
     dev.set_volume(D.marschner_lobb_u8(n), D.voxel_scale(n))
     dev.set_transfer_function(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
