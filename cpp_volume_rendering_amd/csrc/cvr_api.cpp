@@ -267,6 +267,11 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     }
     return CVR_OK;
   }
+  if (!std::strcmp(key, "debug_keep")) {   // diagnostics only: the image is incomplete
+    if (value < 0) return fail(c, CVR_ERR_ARG, "debug_keep must be >= 0");
+    c->debug_keep = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "boost")) {
     if (value < 0 || value > 100) return fail(c, CVR_ERR_ARG, "boost must be a percentage");
     c->boost_pct = value;
@@ -491,12 +496,16 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   }
   plan.quad_pct = c->quad_pct;
   {
-    // entries per band: its tiles + 3 extra for each quad-split tile; bands
-    // differ by at most one tile, the largest one sets the slot count
-    const int seg_max = (plan.ntiles + 7) / 8;
-    const int per_band = seg_max + 3 * (int)(((long long)seg_max * plan.quad_pct) / 100);
+    // Bands are cut by predicted work, so one may hold more than 1/8 of the
+    // tiles: up to 2x the even share (the epilogue falls back to even bands
+    // past that); every band gets that many slots (+3 per quad-split tile).
+    const int seg_avg = (plan.ntiles + 7) / 8;
+    plan.max_seg = std::min(std::min(plan.ntiles, 2 * seg_avg), cvr::kMaxBandTiles);
+    if (plan.max_seg < seg_avg) plan.max_seg = seg_avg;   // (too large to order; see can_order)
+    const int per_band = plan.max_seg + 3 * (int)(((long long)plan.max_seg * plan.quad_pct) / 100);
     plan.order_slots = 8 * per_band;
-    plan.boost = (int)(((long long)per_band * c->boost_pct) / 100);
+    plan.boost = (int)(((long long)seg_avg * c->boost_pct) / 100);
+    plan.keep = c->debug_keep;
   }
 
   HIP_TRY(c, hipSetDevice(c->device));
@@ -524,7 +533,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   // the kernel records each wave tile's critical path, tile_order_kernel sorts
   // every XCD band by it (and re-arms the queue heads) for the next frame.
   const int units = plan.order_slots;
-  const bool can_order = c->use_order && (units + 7) / 8 <= 16384;
+  const bool can_order = c->use_order && (plan.ntiles + 7) / 8 <= cvr::kMaxBandTiles;
   const int key = (plan.ntiles << 2) ^ (plan.quad_pct << 24) ^
                   (packed ? (f->rank << 8) ^ (f->nranks << 12) ^ 1 : 0);
   const int* order = nullptr;

@@ -63,7 +63,11 @@ struct RenderPlan {
   int order_slots;                   // grid size under an LPT order (8 x entries per band)
   int boost;                         // per band, the first `boost` entries run at priority 2
   int quad_pct;                      // per band, this % of the longest tiles march 4 lanes/ray
+  int keep;                          // diagnostics: >0 keeps only the first `keep` entries per band
+  int max_seg;                       // most tiles one (work-balanced) band may take
 };
+
+constexpr int kMaxBandTiles = 16384;   // the epilogue sorts a band in LDS (64 KiB)
 
 struct Ctx {
   int device = 0;
@@ -90,6 +94,7 @@ struct Ctx {
   // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
   int batch = 4;
   int layout = kLayoutLinear;      // cell layout used by the next cvr_set_volume
+  int debug_keep = 0;              // diagnostics (option "debug_keep"): render only the longest entries
   int boost_pct = 5;               // % of every band's longest entries run at raised priority
   int quad_pct = 0;                // % of every band's longest tiles marched 4 lanes per ray
   int tile_stats = 0;              // record per-tile timing (diagnostics)

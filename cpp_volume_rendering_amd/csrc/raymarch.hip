@@ -404,12 +404,11 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     unsigned long long* __restrict__ tile_samples, const int* __restrict__ order,
                     uint32_t* __restrict__ tile_cost, int boost) {
   extern __shared__ float4 tfp[];
-  load_tf_lds(tfp, tf_g, A.tf_n);
   const int b = blockIdx.x, nt = A.ntiles;
   int t, quarter = -1;
   if (order) {
     const int e = order[b];
-    if (e < 0) return;                      // padding slot of a shorter band
+    if (e < 0) return;                      // padding slot of a shorter band (whole workgroup)
     t = e & (kQuadFlag - 1);
     if (QUAD) quarter = (e >> 28) - 1;
     if ((b >> 3) < boost) __builtin_amdgcn_s_setprio(2);
@@ -418,6 +417,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   } else {
     t = b;
   }
+  load_tf_lds(tfp, tf_g, A.tf_n);
   const int lane = threadIdx.x;
   unsigned long long t_start = 0;
   if (A.tile_stats) t_start = __builtin_amdgcn_s_memrealtime();
@@ -483,32 +483,37 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
 //  * `tile_samples` (optional): sums the band's per-tile sample counts into
 //    *total (one atomic per band instead of one per wave on a single word) and
 //    resets them;
-//  * `tile_cost` (optional): orders the band's tiles by descending critical
-//    path (bucketed into 256 cost levels: O(n), ties in any order — the order
-//    never changes a pixel), expands the longest `nquad` tiles into four quad
-//    quarters, and deals the entries to physical blocks band, band+8, ... (the
-//    blocks XCD `band` receives); slots past the band's entries are -1.  Resets
-//    tile_cost for the next frame's atomicMax.
+//  * `tile_cost` (optional): builds the next frame's launch order.  The screen
+//    (row-major wave tiles) is cut into 8 contiguous bands of equal predicted
+//    work — weight = the tile's critical path + kTileWeightBias, prefix-summed
+//    over the whole frame — so every XCD finishes together while keeping a
+//    compact screen region (L2 locality).  If a band would exceed `max_seg`
+//    tiles the split falls back to equal tile counts.  Each band is ordered by
+//    descending critical path (bucketed into 256 cost levels: O(n), ties in any
+//    order — the order never changes a pixel), its longest `nquad` tiles are
+//    expanded into four quad quarters, and the entries are dealt to physical
+//    blocks band, band+8, ... (the blocks XCD `band` receives); slots past the
+//    band's entries are -1.  Resets tile_cost for the next frame's atomicMax.
 constexpr int kOrderThreads = 1024;
-constexpr int kOrderPerThread = 4;   // tiles a thread keeps in registers (larger bands loop)
+constexpr unsigned kTileWeightBias = 8;   // per-tile fixed cost in units of march iterations
 
 __global__ void __launch_bounds__(kOrderThreads)
 tile_epilogue_kernel(uint32_t* __restrict__ tile_cost, unsigned long long* __restrict__ tile_samples,
                      unsigned long long* __restrict__ total, int ntiles, int quad_pct,
-                     int slots_per_band, int* __restrict__ order) {
+                     int slots_per_band, int max_seg, int keep, int* __restrict__ order) {
   __shared__ unsigned hist[256];
   __shared__ unsigned start[256];
   __shared__ unsigned maxc;
   __shared__ unsigned long long wsum[kOrderThreads / 64];
-  extern __shared__ int sorted[];   // ceil(ntiles / 8) entries
+  __shared__ int bounds[9];
+  extern __shared__ int sorted[];   // max_seg entries
   const int band = blockIdx.x, tid = threadIdx.x;
-  const int b0 = (band * ntiles) >> 3, b1 = ((band + 1) * ntiles) >> 3;
-  const int seg = b1 - b0;
   if (tile_samples) {
+    const int s0 = (band * ntiles) >> 3, s1 = ((band + 1) * ntiles) >> 3;
     unsigned long long acc = 0;
-    for (int i = tid; i < seg; i += kOrderThreads) {
-      acc += tile_samples[b0 + i];
-      tile_samples[b0 + i] = 0ull;
+    for (int i = s0 + tid; i < s1; i += kOrderThreads) {
+      acc += tile_samples[i];
+      tile_samples[i] = 0ull;
     }
     acc = wave_sum(acc);
     if ((tid & 63) == 0) wsum[tid >> 6] = acc;
@@ -520,65 +525,99 @@ tile_epilogue_kernel(uint32_t* __restrict__ tile_cost, unsigned long long* __res
     }
   }
   if (!tile_cost) return;
-  if (tid < 256) hist[tid] = 0;
-  if (tid == 0) maxc = 0;
+
+  // 1) work-balanced band boundaries (every block computes all 8, identically)
+  const int chunk = (ntiles + kOrderThreads - 1) / kOrderThreads;
+  const int c0 = min(tid * chunk, ntiles), c1 = min(c0 + chunk, ntiles);
+  unsigned long long mine = 0;
+  for (int i = c0; i < c1; i++) mine += tile_cost[i] + kTileWeightBias;
   __syncthreads();
-  // the band's costs, read once (a thread's tiles are tid, tid + 1024, ...)
-  uint32_t cst[kOrderPerThread];
-  unsigned lmax = 0;
+  // block-wide exclusive scan of the per-thread sums
+  unsigned long long incl = mine;
 #pragma unroll
-  for (int k = 0; k < kOrderPerThread; k++) {
-    const int i = tid + k * kOrderThreads;
-    cst[k] = i < seg ? tile_cost[b0 + i] : 0u;
-    lmax = max(lmax, cst[k]);
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long o = __shfl_up(incl, off, 64);
+    if ((tid & 63) >= off) incl += o;
   }
-  for (int i = tid + kOrderPerThread * kOrderThreads; i < seg; i += kOrderThreads)
-    lmax = max(lmax, tile_cost[b0 + i]);
+  if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+  if (tid < 9) bounds[tid] = tid == 8 ? ntiles : (tid == 0 ? 0 : -1);
+  if (tid == 0) maxc = 0;
+  if (tid < 256) hist[tid] = 0;
+  __syncthreads();
+  unsigned long long wbase = 0, wtot = 0;
+  for (int w = 0; w < kOrderThreads / 64; w++) {
+    if (w < (tid >> 6)) wbase += wsum[w];
+    wtot += wsum[w];
+  }
+  unsigned long long p = wbase + incl - mine;   // weight before tile c0
+  for (int i = c0; i < c1; i++) {
+    // tile i starts band k when its prefix first reaches k/8 of the total
+    const unsigned long long w = tile_cost[i] + kTileWeightBias;
+    for (int k = 1; k < 8; k++) {
+      const unsigned long long target = (wtot * (unsigned long long)k) >> 3;
+      if (p < target && p + w >= target) bounds[k] = i + 1;
+    }
+    p += w;
+  }
+  __syncthreads();
+  bool balanced = true;
+  for (int k = 1; k < 8; k++) {
+    if (bounds[k] < 0) balanced = false;
+  }
+  if (balanced) {
+    for (int k = 0; k < 8; k++)
+      if (bounds[k + 1] < bounds[k] || bounds[k + 1] - bounds[k] > max_seg) balanced = false;
+  }
+  const int b0 = balanced ? bounds[band] : (band * ntiles) >> 3;
+  const int b1 = balanced ? bounds[band + 1] : ((band + 1) * ntiles) >> 3;
+  const int seg = b1 - b0;
+
+  // 2) LPT order of the band: bucket sort by critical path
+  unsigned lmax = 0;
+  for (int i = tid; i < seg; i += kOrderThreads) lmax = max(lmax, tile_cost[b0 + i]);
   lmax = wave_max(lmax);
   if ((tid & 63) == 0) atomicMax(&maxc, lmax);
   __syncthreads();
   const unsigned long long mc = (unsigned long long)maxc + 1;
   auto bucket_of = [mc](uint32_t c) { return 255u - (unsigned)(((unsigned long long)c * 256u) / mc); };
-#pragma unroll
-  for (int k = 0; k < kOrderPerThread; k++)
-    if (tid + k * kOrderThreads < seg) atomicAdd(&hist[bucket_of(cst[k])], 1u);
-  for (int i = tid + kOrderPerThread * kOrderThreads; i < seg; i += kOrderThreads)
-    atomicAdd(&hist[bucket_of(tile_cost[b0 + i])], 1u);
+  for (int i = tid; i < seg; i += kOrderThreads) atomicAdd(&hist[bucket_of(tile_cost[b0 + i])], 1u);
   __syncthreads();
   if (tid < 64) {   // exclusive scan of the 256 counts by one wave (4 per lane)
     const unsigned h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2],
                    h3 = hist[4 * tid + 3];
     const unsigned part = h0 + h1 + h2 + h3;
-    unsigned incl = part;
+    unsigned inc = part;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      const unsigned o = (unsigned)__shfl_up((int)incl, off, 64);
-      if (tid >= off) incl += o;
+      const unsigned o = (unsigned)__shfl_up((int)inc, off, 64);
+      if (tid >= off) inc += o;
     }
-    unsigned ex = incl - part;
+    unsigned ex = inc - part;
     start[4 * tid] = ex; ex += h0;
     start[4 * tid + 1] = ex; ex += h1;
     start[4 * tid + 2] = ex; ex += h2;
     start[4 * tid + 3] = ex;
   }
   __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kOrderPerThread; k++) {
-    const int i = tid + k * kOrderThreads;
-    if (i < seg) sorted[atomicAdd(&start[bucket_of(cst[k])], 1u)] = b0 + i;
-  }
-  for (int i = tid + kOrderPerThread * kOrderThreads; i < seg; i += kOrderThreads)
+  for (int i = tid; i < seg; i += kOrderThreads)
     sorted[atomicAdd(&start[bucket_of(tile_cost[b0 + i])], 1u)] = b0 + i;
   __syncthreads();
   const int nquad = (int)(((long long)seg * quad_pct) / 100);
-  const int nent = seg + 3 * nquad;
+  const int nent = keep > 0 ? min(seg + 3 * nquad, keep) : seg + 3 * nquad;
   for (int e = tid; e < slots_per_band; e += kOrderThreads) {
     int v = -1;
     if (e < 4 * nquad) v = sorted[e >> 2] | (((e & 3) + 1) << 28);
     else if (e < nent) v = sorted[e - 3 * nquad];
     order[band + 8 * e] = v;
   }
-  for (int i = tid; i < seg; i += kOrderThreads) tile_cost[b0 + i] = 0u;
+  // tile_cost is not cleared here: every block reads all of it for the
+  // boundaries (see launch_tile_epilogue)
+}
+
+// Clears tile_cost for the next frame's atomicMax (after every band has read it).
+__global__ void clear_u32_kernel(uint32_t* __restrict__ p, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -637,12 +676,22 @@ hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4
 hipError_t launch_tile_epilogue(uint32_t* tile_cost, unsigned long long* tile_samples,
                                 unsigned long long* total, const RenderPlan& plan, int* order,
                                 hipStream_t s) {
-  const int seg_max = (plan.ntiles + 7) >> 3;
-  if (tile_cost && seg_max > 16384) return hipErrorInvalidValue;   // sorted[] in LDS
+  const int max_seg = plan.max_seg;
+  if (tile_cost && (max_seg > kMaxBandTiles || max_seg < (plan.ntiles + 7) / 8))
+    return hipErrorInvalidValue;
   hipLaunchKernelGGL(tile_epilogue_kernel, dim3(8), dim3(kOrderThreads),
-                     tile_cost ? (size_t)seg_max * sizeof(int) : 0, s, tile_cost, tile_samples,
-                     total, plan.ntiles, plan.quad_pct, plan.order_slots / 8, order);
-  return hipGetLastError();
+                     tile_cost ? (size_t)max_seg * sizeof(int) : 0, s, tile_cost, tile_samples,
+                     total, plan.ntiles, plan.quad_pct, plan.order_slots / 8, max_seg, plan.keep,
+                     order);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !tile_cost) return e;
+  // quad quarters atomicMax into tile_cost: it must start the next frame at zero
+  if (plan.quad_pct > 0) {
+    hipLaunchKernelGGL(clear_u32_kernel, dim3((plan.ntiles + 255) / 256), dim3(256), 0, s,
+                       tile_cost, plan.ntiles);
+    e = hipGetLastError();
+  }
+  return e;
 }
 
 }  // namespace cvr
