@@ -267,6 +267,16 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     }
     return CVR_OK;
   }
+  if (!std::strcmp(key, "tile_cost")) {
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "tile_cost must be 0 (longest ray) or 1 (time)");
+    c->cost_time = value;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "max_waves_cu")) {
+    if (value < 0 || value > 32) return fail(c, CVR_ERR_ARG, "max_waves_cu must be 0..32");
+    c->max_waves_cu = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "debug_keep")) {   // diagnostics only: the image is incomplete
     if (value < 0) return fail(c, CVR_ERR_ARG, "debug_keep must be >= 0");
     c->debug_keep = value;
@@ -287,6 +297,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "tile_order")) return c->use_order;
   if (!std::strcmp(key, "layout")) return c->layout;
   if (!std::strcmp(key, "boost")) return c->boost_pct;
+  if (!std::strcmp(key, "tile_cost")) return c->cost_time;
   if (!std::strcmp(key, "tile_stats")) return c->tile_stats;
   if (!std::strcmp(key, "quad")) return c->quad_pct;
   if (!std::strcmp(key, "kernel_timing")) return (int)c->ev_start.size();
@@ -486,6 +497,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   }
   A.ntiles = plan.ntiles;
   A.tile_stats = nullptr;
+  A.cost_time = c->cost_time;
   if (c->tile_stats) {
     if (c->tile_stats_n < plan.ntiles) {
       void* p = c->d_tile_stats; free_dev(p); c->d_tile_stats = nullptr; c->tile_stats_n = 0;

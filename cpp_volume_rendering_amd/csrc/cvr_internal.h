@@ -55,6 +55,7 @@ struct Rc1passArgs {
   int packed;
   int ntiles;                        // 8x8 wave tiles of this launch
   unsigned long long* tile_stats;    // diagnostics (tile_stats option) or null
+  int cost_time;                     // LPT cost = measured tile time (1) or longest ray (0)
 };
 
 // How one frame is cut into work: one 8x8 wave tile per workgroup.
@@ -94,6 +95,8 @@ struct Ctx {
   // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
   int batch = 4;
   int layout = kLayoutLinear;      // cell layout used by the next cvr_set_volume
+  int cost_time = 0;               // option "tile_cost": 0 longest ray, 1 measured time (worse)
+  int max_waves_cu = 0;            // experiment (option "max_waves_cu"): cap residency via LDS
   int debug_keep = 0;              // diagnostics (option "debug_keep"): render only the longest entries
   int boost_pct = 5;               // % of every band's longest entries run at raised priority
   int quad_pct = 0;                // % of every band's longest tiles marched 4 lanes per ray

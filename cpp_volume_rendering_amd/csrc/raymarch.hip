@@ -23,6 +23,7 @@
 // polynomial cvr_expf.  Compiled with -ffp-contract=off; both march variants
 // produce bit-identical results, equal to oracle/cvr_oracle.cpp.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 
 #include "cvr_device.h"
@@ -420,7 +421,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   load_tf_lds(tfp, tf_g, A.tf_n);
   const int lane = threadIdx.x;
   unsigned long long t_start = 0;
-  if (A.tile_stats) t_start = __builtin_amdgcn_s_memrealtime();
+  if (A.tile_stats || A.cost_time) t_start = __builtin_amdgcn_s_memrealtime();
   int px, py;
   long long oidx;
   float4 dst;
@@ -458,9 +459,14 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   }
   uint32_t m = 0;
   if (tile_cost || A.tile_stats) m = wave_max(cnt);
-  if (tile_cost && lane == 0) {   // the tile's critical path (its longest ray), next frame's order
-    if (quarter < 0) tile_cost[t] = m;
-    else atomicMax(&tile_cost[t], m);
+  if (tile_cost && lane == 0) {   // next frame's order: the tile's measured time or its longest ray
+    uint32_t c = m;
+    if (A.cost_time) {
+      const unsigned long long d = __builtin_amdgcn_s_memrealtime() - t_start;   // 100 MHz ticks
+      c = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+    }
+    if (quarter < 0) tile_cost[t] = c;
+    else atomicMax(&tile_cost[t], c);
   }
   if (A.tile_stats) {   // diagnostics: 100 MHz start/end stamps, longest ray, placement
     unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
@@ -495,7 +501,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
 //    blocks band, band+8, ... (the blocks XCD `band` receives); slots past the
 //    band's entries are -1.  Resets tile_cost for the next frame's atomicMax.
 constexpr int kOrderThreads = 1024;
-constexpr unsigned kTileWeightBias = 8;   // per-tile fixed cost in units of march iterations
+constexpr unsigned kTileWeightBias = 8;   // per-tile floor of the cost (iterations or 10 ns ticks)
 
 __global__ void __launch_bounds__(kOrderThreads)
 tile_epilogue_kernel(uint32_t* __restrict__ tile_cost, unsigned long long* __restrict__ tile_samples,
@@ -629,6 +635,7 @@ static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, ui
                              unsigned long long* tile_samples, const int* order, uint32_t* tile_cost,
                              const RenderPlan& plan, hipStream_t s) {
   size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
+  if (c.max_waves_cu > 0) lds = std::max(lds, (size_t)(160 * 1024 / c.max_waves_cu) & ~(size_t)255);
   const uint4* cells = (const uint4*)c.d_cells;
   if (LAYOUT == kLayoutLinear) cells += c.cells.linear_origin;   // cell (1,1,1) <-> texel (0,0,0)
   int grid = order ? plan.order_slots : plan.ntiles;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of rc1pass kernel variants in ONE process, interleaved rounds
 (methodology rule 24).  Every variant's image is checked bit-equal to the first
-variant's.  Variant syntax: L<layout>b<batch>o<tile_order>p<boost%>q<quad%>, e.g. L0b4o1p5q10.
+variant's.  Variant syntax: L<layout>b<batch>o<tile_order>p<boost%>q<quad%>[c<tile_cost>][w<max waves/CU>], e.g. L1b4o1p5q0c0w20.
 Usage: python tools/ab_rc1pass.py [--size 512] [--res 1024] [--variants ...]"""
 import argparse
 import ctypes
@@ -20,10 +20,12 @@ from cpp_volume_rendering_amd.renderer import Camera, Device, build_tf_rgbt, mak
 
 
 def parse_variant(v):
-    m = re.fullmatch(r"L(\d)b(\d)o(\d)p(\d+)q(\d+)", v)
+    m = re.fullmatch(r"L(\d)b(\d)o(\d)p(\d+)q(\d+)(?:c(\d))?(?:w(\d+))?", v)
     if not m:
         raise ValueError(f"bad variant {v}")
-    return tuple(int(x) for x in m.groups())
+    g = m.groups()
+    return tuple(int(x) for x in g[:5]) + (int(g[5]) if g[5] is not None else 0,
+                                            int(g[6]) if g[6] is not None else 0)
 
 
 def main():
@@ -74,12 +76,14 @@ def main():
     S = None
     for _ in range(a.rounds):
         for v in variants:
-            layout, b, o, boost, quad = parsed[v]
+            layout, b, o, boost, quad, cost, mw = parsed[v]
             dev = devs[layout]
             N.check(L.cvr_set_option(dev.handle, b"batch", b), "opt")
             N.check(L.cvr_set_option(dev.handle, b"tile_order", o), "opt")
             N.check(L.cvr_set_option(dev.handle, b"boost", boost), "opt")
             N.check(L.cvr_set_option(dev.handle, b"quad", quad), "opt")
+            N.check(L.cvr_set_option(dev.handle, b"tile_cost", cost), "opt")
+            N.check(L.cvr_set_option(dev.handle, b"max_waves_cu", mw), "opt")
             with torch.cuda.stream(s):
                 run(dev, 3)   # warm up + learn the order
                 tot.zero_()
