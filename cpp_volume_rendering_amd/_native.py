@@ -16,6 +16,8 @@ import os
 import torch  # noqa: F401  (must precede the dlopen below, see module docstring)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libcvr.so")
+# tools/ab_builds.sh: A/B timing of two builds of the library in one GPU session
+LIB_PATH = os.environ.get("CVR_LIB_OVERRIDE", LIB_PATH)
 
 CVR_OK, CVR_ERR_ARG, CVR_ERR_HIP, CVR_ERR_OOM, CVR_ERR_STATE, CVR_ERR_IO = range(6)
 GRADIENT_NONE, GRADIENT_FINITE_DIFFERENCES, GRADIENT_SOBEL_FELDMAN = 0, 1, 2

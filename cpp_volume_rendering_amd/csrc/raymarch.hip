@@ -197,7 +197,7 @@ __device__ __forceinline__ bool ray_setup(const Rc1passArgs& A, int px, int py, 
 // Ray-parallel march (one lane per ray) of ray_marching_1p.comp:124-172.  The
 // arithmetic per sample is exactly the reference's sequential loop (s
 // accumulates h one step at a time); batching only changes when loads issue.
-template <int K, bool PHONG, int LAYOUT>
+template <int K, bool PHONG, int LAYOUT, bool XF>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
                                           const uint2* __restrict__ grad,
                                           const float4* __restrict__ tfp, int px, int py,
@@ -233,7 +233,10 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
 #pragma unroll
     for (int j = 0; j < K; j++)
       src[j] = classify(tfp, fn, trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az));
-    // stage 3: front-to-back composite + ERT, in sample order
+    // stage 3: front-to-back composite + ERT, in sample order.  The branches
+    // matter: a wave whose samples are all transparent (empty space) skips
+    // the exp and the composite together (a branch-free select form measured
+    // 1.4x slower on the headline frame).
 #pragma unroll
     for (int j = 0; j < K; j++) {
       if (!done) {
@@ -245,8 +248,8 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
           if (sc.w > 0.0f) {
             if (PHONG) shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
             const float x = -(sc.w * hj[j]);
-            float a = 1.0f - (A.exp_fast ? cvr_expf_neg(x) : cvr_expf_nb(x));
-            float om = 1.0f - dst.w;
+            const float a = 1.0f - (XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
+            const float om = 1.0f - dst.w;
             dst.x = fmaf(om, sc.x * a, dst.x);
             dst.y = fmaf(om, sc.y * a, dst.y);
             dst.z = fmaf(om, sc.z * a, dst.z);
@@ -302,7 +305,7 @@ __device__ __forceinline__ void quad_composite(const QSample& q, bool valid, boo
 // reference skipping it (:142).  One memory round trip advances a ray 4K
 // samples instead of K: the longest tiles' critical path shrinks ~4x.
 // Must be called by all 64 lanes (DPP reads neighbours); `active` = lane's ray is live.
-template <int K, bool PHONG, int LAYOUT>
+template <int K, bool PHONG, int LAYOUT, bool XF>
 __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
                                                const uint4* __restrict__ cells,
                                                const uint2* __restrict__ grad,
@@ -353,7 +356,7 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
       if (vj && sc.w > 0.0f) {
         if (PHONG) shade_phong(A, grad, sp[k], r.dir, tj[k], r.tpos, hg, eye, sc);
         const float x = -(sc.w * hj[k]);
-        const float a = 1.0f - (A.exp_fast ? cvr_expf_neg(x) : cvr_expf_nb(x));
+        const float a = 1.0f - (XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
         q[k] = QSample{a, sc.x * a, sc.y * a, sc.z * a};
       }
       qv[k] = (unsigned)(__ballot(vj) >> qshift) & 0xfu;
@@ -397,7 +400,7 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // (four lanes per ray).  Without an order, block b -> tile in XCD bands
 // (blocks b and b+8 share an XCD, so XCD b%8 gets one contiguous band).
 // Waves of the `boost` longest tiles of each band raise their priority.
-template <int K, bool PHONG, int LAYOUT, bool QUAD>
+template <int K, bool PHONG, int LAYOUT, bool QUAD, bool XF>
 __global__ void __launch_bounds__(64)
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
@@ -432,14 +435,14 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     const bool inside = px < A.W && py < A.H;
     dst = make_float4(0.f, 0.f, 0.f, 0.f);
     cnt = 0;
-    if (inside) march_ray<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, dst, cnt);
+    if (inside) march_ray<K, PHONG, LAYOUT, XF>(A, cells, grad, tfp, px, py, dst, cnt);
     writer = inside || A.packed;
   } else {                    // quarter of a tile, four lanes per ray
     const int ray = lane >> 2;
     tile_pixel(A, t, ((quarter & 1) << 2) | (ray & 3), ((quarter >> 1) << 2) | (ray >> 2), px, py,
                oidx);
     const bool inside = px < A.W && py < A.H;
-    march_ray_quad<K, PHONG, LAYOUT>(A, cells, grad, tfp, px, py, inside, dst, cnt);
+    march_ray_quad<K, PHONG, LAYOUT, XF>(A, cells, grad, tfp, px, py, inside, dst, cnt);
     writer = (lane & 3) == 0 && (inside || A.packed);
     if ((lane & 3) != 0) cnt = 0;           // one count per ray
   }
@@ -630,42 +633,50 @@ __global__ void clear_u32_kernel(uint32_t* __restrict__ p, int n) {
 // Launchers
 // ---------------------------------------------------------------------------
 
-template <int K, bool PHONG, int LAYOUT, bool QUAD>
-static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
-                             unsigned long long* tile_samples, const int* order, uint32_t* tile_cost,
-                             const RenderPlan& plan, hipStream_t s) {
+// Kernel variant: K (batch), PHONG, LAYOUT, QUAD (quad path compiled in: it
+// costs the ray-parallel path registers even when unused), XF (range-free exp).
+template <int K, bool PHONG, int LAYOUT, bool QUAD, bool XF>
+static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
+                                 unsigned long long* tile_samples, const int* order,
+                                 uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
   size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
   if (c.max_waves_cu > 0) lds = std::max(lds, (size_t)(160 * 1024 / c.max_waves_cu) & ~(size_t)255);
   const uint4* cells = (const uint4*)c.d_cells;
   if (LAYOUT == kLayoutLinear) cells += c.cells.linear_origin;   // cell (1,1,1) <-> texel (0,0,0)
   int grid = order ? plan.order_slots : plan.ntiles;
-  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, LAYOUT, QUAD>), dim3(grid), dim3(64), lds, s, a,
-                     cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples, tile_samples,
-                     order, tile_cost, order ? plan.boost : 0);
+  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, LAYOUT, QUAD, XF>), dim3(grid), dim3(64), lds, s,
+                     a, cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples,
+                     tile_samples, order, tile_cost, order ? plan.boost : 0);
   return hipGetLastError();
+}
+
+template <int K, bool PHONG, int LAYOUT>
+static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
+                             unsigned long long* ts, const int* order, uint32_t* tile_cost,
+                             const RenderPlan& plan, hipStream_t s) {
+  const bool quad = order && plan.quad_pct > 0;
+  if (quad)
+    return a.exp_fast ? launch_variant<K, PHONG, LAYOUT, true, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                      : launch_variant<K, PHONG, LAYOUT, true, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
+  return a.exp_fast ? launch_variant<K, PHONG, LAYOUT, false, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                    : launch_variant<K, PHONG, LAYOUT, false, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
 }
 
 template <int K, bool PHONG>
 static hipError_t launch_kp(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
-                            unsigned long long* tile_samples, const int* order, uint32_t* tile_cost,
+                            unsigned long long* ts, const int* order, uint32_t* tile_cost,
                             const RenderPlan& plan, hipStream_t s) {
-  // the quad march is compiled into its own kernel: it costs the ray-parallel
-  // path registers (occupancy) even when no entry uses it
-  if (order && plan.quad_pct > 0)
-    return c.cells.layout == kLayoutLinear
-               ? launch_kpl<K, PHONG, kLayoutLinear, true>(c, a, out, samples, tile_samples, order, tile_cost, plan, s)
-               : launch_kpl<K, PHONG, kLayoutBrick, true>(c, a, out, samples, tile_samples, order, tile_cost, plan, s);
   return c.cells.layout == kLayoutLinear
-             ? launch_kpl<K, PHONG, kLayoutLinear, false>(c, a, out, samples, tile_samples, order, tile_cost, plan, s)
-             : launch_kpl<K, PHONG, kLayoutBrick, false>(c, a, out, samples, tile_samples, order, tile_cost, plan, s);
+             ? launch_kpl<K, PHONG, kLayoutLinear>(c, a, out, samples, ts, order, tile_cost, plan, s)
+             : launch_kpl<K, PHONG, kLayoutBrick>(c, a, out, samples, ts, order, tile_cost, plan, s);
 }
 
 template <int K>
 static hipError_t launch_k(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
-                           uint32_t* samples, unsigned long long* tile_samples, const int* order,
+                           uint32_t* samples, unsigned long long* ts, const int* order,
                            uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
-  return phong ? launch_kp<K, true>(c, a, out, samples, tile_samples, order, tile_cost, plan, s)
-               : launch_kp<K, false>(c, a, out, samples, tile_samples, order, tile_cost, plan, s);
+  return phong ? launch_kp<K, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
+               : launch_kp<K, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
 }
 
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
@@ -673,11 +684,8 @@ hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
   if (a.ntiles <= 0) return hipSuccess;
   if (a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
-  switch (c.batch) {
-    case 2: return launch_k<2>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
-    case 8: return launch_k<8>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
-    default: return launch_k<4>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
-  }
+  if (c.batch == 2) return launch_k<2>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
+  return launch_k<4>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
 }
 
 hipError_t launch_tile_epilogue(uint32_t* tile_cost, unsigned long long* tile_samples,

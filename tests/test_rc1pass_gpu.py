@@ -219,7 +219,7 @@ SCHEDULES = [
     dict(tile_order=0, batch=4, layout=0),
     dict(tile_order=1, quad=10, boost=5, batch=4, layout=0),
     dict(tile_order=1, quad=100, boost=0, batch=2, layout=1),
-    dict(tile_order=1, quad=0, boost=50, batch=8, layout=1),
+    dict(tile_order=1, quad=0, boost=50, batch=2, layout=1),
     dict(tile_order=1, quad=35, boost=5, batch=4, layout=1),
 ]
 
