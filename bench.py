@@ -197,7 +197,7 @@ def main():
     assert nkt.value == a.steps
     kern_ms = float(np.mean(kt[:nkt.value]))
     batch = L.cvr_get_option(r.device.handle, b"batch")
-    layout = L.cvr_get_option(r.device.handle, b"layout")
+    macro = L.cvr_get_option(r.device.handle, b"macro")
     assert int(total.item()) == S_rank * a.steps, "sample count changed between frames"
 
     if world > 1:
@@ -222,7 +222,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic(a.pmc, wkey),
-                "kernel": f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, {layout}, false>",
+                "kernel": f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, *, false, true>",
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank}
         res = {
@@ -246,8 +246,9 @@ def main():
                        "volume": n, "viewport": [W, H], "samples_per_frame": S_all,
                        "parallelism": f"screen tiles {tile}x{tile} over {world} GPU(s)"
                                       if world > 1 else "1 GPU",
-                       "storage": "cell8 fp16 (16 B/cell, "
-                                  + ("x-fastest linear)" if layout == 1 else "bricked 4^3)")},
+                       "storage": "cell8 fp16 (16 B/cell, x-fastest)",
+                       "empty_space_skip": f"macro cells 2^{macro}, auto (on at >= 15 % empty)"
+                                           if macro > 0 else "off"},
             "roofline": roof,
         }
         if world == 1 and not a.no_cpu_baseline:

@@ -194,6 +194,10 @@ void cvr_destroy(cvr_ctx* ctx) {
   free_dev(c->d_cells);
   void* p = c->d_tf; free_dev(p); c->d_tf = nullptr;
   free_dev(c->d_grad);
+  p = c->d_lut; free_dev(p); c->d_lut = nullptr;
+  p = c->d_macro_minmax; free_dev(p); c->d_macro_minmax = nullptr;
+  p = c->d_occ; free_dev(p); c->d_occ = nullptr;
+  p = c->d_tf_prefix; free_dev(p); c->d_tf_prefix = nullptr;
   p = c->d_total; free_dev(p); c->d_total = nullptr;
   free_dev(c->d_scratch);
   p = c->d_order; free_dev(p); c->d_order = nullptr;
@@ -233,12 +237,6 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->order_valid = 0;
     return CVR_OK;
   }
-  if (!std::strcmp(key, "layout")) {
-    if (value != cvr::kLayoutBrick && value != cvr::kLayoutLinear)
-      return fail(c, CVR_ERR_ARG, "layout must be 0 (bricked) or 1 (linear)");
-    c->layout = value;   // takes effect at the next cvr_set_volume
-    return CVR_OK;
-  }
   if (!std::strcmp(key, "quad")) {
     if (value < 0 || value > 100) return fail(c, CVR_ERR_ARG, "quad must be a percentage");
     c->quad_pct = value;
@@ -265,6 +263,18 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
       HIP_TRY(c, hipEventCreate(&b));
       c->ev_stop.push_back(b);
     }
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "macro")) {
+    if (value != 0 && (value < 2 || value > 6))
+      return fail(c, CVR_ERR_ARG, "macro must be 0 (no empty-space skipping) or 2..6");
+    c->macro_shift = value;
+    c->occ_valid = 0;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "skip_min_pct")) {
+    if (value < 0 || value > 101) return fail(c, CVR_ERR_ARG, "skip_min_pct must be 0..101");
+    c->skip_min_pct = value;
     return CVR_OK;
   }
   if (!std::strcmp(key, "tile_cost")) {
@@ -295,9 +305,12 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!c || !key) return -1;
   if (!std::strcmp(key, "batch")) return c->batch;
   if (!std::strcmp(key, "tile_order")) return c->use_order;
-  if (!std::strcmp(key, "layout")) return c->layout;
   if (!std::strcmp(key, "boost")) return c->boost_pct;
   if (!std::strcmp(key, "tile_cost")) return c->cost_time;
+  if (!std::strcmp(key, "macro")) return c->macro_shift;
+  if (!std::strcmp(key, "skip_min_pct")) return c->skip_min_pct;
+  if (!std::strcmp(key, "occ_empty_permille"))   // read-only: empty macro cells (after a render)
+    return c->occ_valid ? (int)(c->occ_empty * 1000.0f + 0.5f) : -1;
   if (!std::strcmp(key, "tile_stats")) return c->tile_stats;
   if (!std::strcmp(key, "quad")) return c->quad_pct;
   if (!std::strcmp(key, "kernel_timing")) return (int)c->ev_start.size();
@@ -343,17 +356,21 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
   std::vector<uint16_t> lut(nv);
   for (int v = 0; v < nv; v++)
     lut[v] = to_half_bits((float)((double)v / (bpv == 1 ? (256.0 - 1.0) : (65536.0 - 1.0))));
-  uint16_t* d_lut = nullptr;
-  HIP_TRY(c, hipMalloc(&d_lut, nv * sizeof(uint16_t)));
+  { void* p = c->d_lut; free_dev(p); c->d_lut = nullptr; }
+  { void* p = c->d_macro_minmax; free_dev(p); c->d_macro_minmax = nullptr; }
+  { void* p = c->d_occ; free_dev(p); c->d_occ = nullptr; }
+  c->mm_shift = -1;
+  c->occ_valid = 0;
+  HIP_TRY(c, hipMalloc((void**)&c->d_lut, nv * sizeof(uint16_t)));
+  uint16_t* d_lut = c->d_lut;
   hipError_t e = hipMemcpyAsync(d_lut, lut.data(), nv * sizeof(uint16_t), hipMemcpyHostToDevice,
                                 c->stream);
-  c->cells = cvr::make_cell_grid(c->N, c->layout);
+  c->cells = cvr::make_cell_grid(c->N);
   c->cells_bytes = cvr::cell_count(c->cells) * 16;
   if (e == hipSuccess) e = hipMalloc(&c->d_cells, c->cells_bytes);
   if (e == hipSuccess)
     e = cvr::launch_build_cells_impl(c->d_vox, bpv, d_lut, c->N, c->cells, c->d_cells, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  (void)hipFree(d_lut);
   if (e != hipSuccess) {
     free_dev(c->d_cells); c->cells_bytes = 0;
     return fail(c, e == hipErrorOutOfMemory ? CVR_ERR_OOM : CVR_ERR_HIP,
@@ -396,6 +413,18 @@ cvr_status cvr_set_transfer_function(cvr_ctx* ctx, const float* rgbt, int n) {
   }
   HIP_TRY(c, hipMemcpy(c->d_tf, q.data(), (size_t)n * 16, hipMemcpyHostToDevice));
   c->tf_max_alpha = amax;
+  // occupancy support: prefix[k] = #{padded entries j < k with alpha > 0}, where
+  // padded entry j is T[clamp(j - 1, 0, n - 1)] (j = 0 .. n + 1)
+  std::vector<int> prefix((size_t)n + 3, 0);
+  for (int j = 0; j < n + 2; j++) {
+    const float a = q[(size_t)std::min(std::max(j - 1, 0), n - 1) * 4 + 3];
+    prefix[(size_t)j + 1] = prefix[(size_t)j] + (a > 0.0f || a != a ? 1 : 0);
+  }
+  { void* p = c->d_tf_prefix; free_dev(p); c->d_tf_prefix = nullptr; }
+  HIP_TRY(c, hipMalloc((void**)&c->d_tf_prefix, prefix.size() * sizeof(int)));
+  HIP_TRY(c, hipMemcpy(c->d_tf_prefix, prefix.data(), prefix.size() * sizeof(int),
+                       hipMemcpyHostToDevice));
+  c->occ_valid = 0;
   return CVR_OK;
 }
 
@@ -432,6 +461,37 @@ static cvr_status ensure_scratch(Ctx* c, size_t bytes) {
   c->scratch_bytes = 0;
   HIP_TRY(c, hipMalloc(&c->d_scratch, bytes));
   c->scratch_bytes = bytes;
+  return CVR_OK;
+}
+
+// Occupancy of the macro cells for the current volume, TF and macro size
+// (rebuilt lazily after any of them changes; on the context stream).
+static cvr_status ensure_occupancy(Ctx* c) {
+  if (c->occ_valid) return CVR_OK;
+  if (!c->d_lut || !c->d_tf_prefix) return fail(c, CVR_ERR_STATE, "occupancy: no volume or TF");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int sh = c->macro_shift;
+  if (c->mm_shift != sh) {
+    for (int i = 0; i < 3; i++) c->mdim[i] = ((c->N[i] - 1) >> sh) + 1;
+    const size_t nm = (size_t)c->mdim[0] * c->mdim[1] * c->mdim[2];
+    { void* p = c->d_macro_minmax; free_dev(p); c->d_macro_minmax = nullptr; }
+    { void* p = c->d_occ; free_dev(p); c->d_occ = nullptr; }
+    HIP_TRY(c, hipMalloc((void**)&c->d_macro_minmax, nm * sizeof(uint32_t)));
+    HIP_TRY(c, hipMalloc((void**)&c->d_occ, nm));
+    HIP_TRY(c, cvr::launch_macro_minmax(*c, sh, c->mdim, c->d_macro_minmax, c->stream));
+    c->mm_shift = sh;
+  }
+  const int nm = c->mdim[0] * c->mdim[1] * c->mdim[2];
+  if (!c->d_total) HIP_TRY(c, hipMalloc((void**)&c->d_total, sizeof(unsigned long long)));
+  unsigned int* d_n = reinterpret_cast<unsigned int*>(c->d_total);
+  HIP_TRY(c, hipMemsetAsync(d_n, 0, sizeof(unsigned int), c->stream));
+  HIP_TRY(c, cvr::launch_occupancy(c->d_macro_minmax, nm, c->d_lut, c->d_tf_prefix, c->tf_n,
+                                   c->d_occ, d_n, c->stream));
+  unsigned int n_empty = 0;
+  HIP_TRY(c, hipMemcpyAsync(&n_empty, d_n, sizeof(n_empty), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->occ_empty = (float)n_empty / (float)nm;
+  c->occ_valid = 1;
   return CVR_OK;
 }
 
@@ -498,6 +558,18 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   A.ntiles = plan.ntiles;
   A.tile_stats = nullptr;
   A.cost_time = c->cost_time;
+  A.occ = nullptr;
+  if (c->macro_shift > 0) {
+    cvr_status st = ensure_occupancy(c);
+    if (st != CVR_OK) return st;
+    // the skip path costs the march registers and a probe: worth it only
+    // with enough empty space (the Marschner-Lobb headline field has ~4 %)
+    if (c->occ_empty * 100.0f >= (float)c->skip_min_pct) {
+      A.occ = c->d_occ;
+      for (int i = 0; i < 3; i++) A.mdim[i] = c->mdim[i];
+      A.mshift = c->macro_shift;
+    }
+  }
   if (c->tile_stats) {
     if (c->tile_stats_n < plan.ntiles) {
       void* p = c->d_tile_stats; free_dev(p); c->d_tile_stats = nullptr; c->tile_stats_n = 0;

@@ -14,19 +14,12 @@ namespace cvr {
 // Padded-cell volume layout ("cell8"): cell (a,b,c), a in [0, N], holds the 8
 // corner values that GL trilinear filtering reads for texel coordinate
 // x in [a-1, a): corners clamp(a-1) and clamp(a) per axis (CLAMP_TO_EDGE).
-// One sample = one 16-byte (fp16 corners) load.  Cells are grouped in 4x4x4
-// bricks (1 KiB) so that a wave's 8x8 ray tile hits few cache lines.
-constexpr int kBrick = 4;
-constexpr int kLayoutBrick = 0;   // 4x4x4-cell bricks (1 KiB), bricks x-fastest
-constexpr int kLayoutLinear = 1;  // (N+1)^3 cells, x-fastest
-
+// One sample = one 16-byte (fp16 corners) load.  Cells are x-fastest (a 4x4x4
+// bricked order measured 6-18 % slower on the headline frame and was dropped).
 struct CellGrid {
-  int layout;
-  int cx, cy, cz;        // cells per axis = N + 1
-  int bx, by, bz;        // bricks per axis = ceil(cells / 4)        (brick layout)
-  int bxby;              // bx * by
-  int pitch_y, pitch_z;  // cx, cx*cy                                (linear layout)
-  long long linear_origin;  // index of cell (1,1,1) = texel (0,0,0) (linear layout)
+  int cx, cy, cz;           // cells per axis = N + 1
+  int pitch_y, pitch_z;     // cx, cx*cy
+  long long linear_origin;  // index of cell (1,1,1) = texel (0,0,0)
 };
 
 // Per-frame constants of the rc1pass kernel (passed by value).
@@ -56,6 +49,10 @@ struct Rc1passArgs {
   int ntiles;                        // 8x8 wave tiles of this launch
   unsigned long long* tile_stats;    // diagnostics (tile_stats option) or null
   int cost_time;                     // LPT cost = measured tile time (1) or longest ray (0)
+  // empty-space skipping: occupancy byte per macro cell (null = off)
+  const uint8_t* occ;
+  int mdim[3];                       // macro cells per axis
+  int mshift;                        // macro cell = 2^mshift texels a side
 };
 
 // How one frame is cut into work: one 8x8 wave tile per workgroup.
@@ -84,6 +81,17 @@ struct Ctx {
   void* d_cells = nullptr;        // cell8 fp16 layout
   size_t cells_bytes = 0;
   CellGrid cells{};
+  uint16_t* d_lut = nullptr;      // raw value -> R16F bits (GetNormalizedSample)
+  // empty-space skipping (option "macro": log2 of the macro cell, 0 = off)
+  int macro_shift = 3;
+  int mm_shift = -1;              // shift the macro min/max below was built for
+  int mdim[3] = {0, 0, 0};
+  uint32_t* d_macro_minmax = nullptr;
+  uint8_t* d_occ = nullptr;
+  int occ_valid = 0;              // occupancy matches the current volume, TF and shift
+  float occ_empty = 0.0f;         // fraction of empty macro cells
+  int skip_min_pct = 15;          // skipping is compiled in when >= this % of cells are empty
+  int* d_tf_prefix = nullptr;     // count of padded TF entries with alpha > 0 before k
   // transfer function (RGBA16F values as float)
   float* d_tf = nullptr;
   int tf_n = 0;
@@ -94,7 +102,6 @@ struct Ctx {
   int grad_mode = 0;
   // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
   int batch = 4;
-  int layout = kLayoutLinear;      // cell layout used by the next cvr_set_volume
   int cost_time = 0;               // option "tile_cost": 0 longest ray, 1 measured time (worse)
   int max_waves_cu = 0;            // experiment (option "max_waves_cu"): cap residency via LDS
   int debug_keep = 0;              // diagnostics (option "debug_keep"): render only the longest entries
@@ -132,26 +139,23 @@ hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4
 hipError_t launch_tile_epilogue(uint32_t* tile_cost, unsigned long long* tile_samples,
                                 unsigned long long* total, const RenderPlan& plan, int* order,
                                 hipStream_t s);
+hipError_t launch_macro_minmax(const Ctx& c, int shift, const int mdim[3], uint32_t* out,
+                               hipStream_t s);
+hipError_t launch_occupancy(const uint32_t* minmax, int n_macro, const uint16_t* lut,
+                            const int* prefix, int tf_n, uint8_t* occ, unsigned int* n_empty,
+                            hipStream_t s);
 hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
                                int nranks, int tiles_per_rank_max, hipStream_t s);
 
-inline CellGrid make_cell_grid(const int N[3], int layout) {
+inline CellGrid make_cell_grid(const int N[3]) {
   CellGrid g;
-  g.layout = layout;
   g.cx = N[0] + 1; g.cy = N[1] + 1; g.cz = N[2] + 1;
-  g.bx = (g.cx + kBrick - 1) / kBrick;
-  g.by = (g.cy + kBrick - 1) / kBrick;
-  g.bz = (g.cz + kBrick - 1) / kBrick;
-  g.bxby = g.bx * g.by;
   g.pitch_y = g.cx;
   g.pitch_z = g.cx * g.cy;
   g.linear_origin = 1 + (long long)g.pitch_y + (long long)g.pitch_z;
   return g;
 }
 
-inline size_t cell_count(const CellGrid& g) {
-  if (g.layout == kLayoutLinear) return (size_t)g.cx * g.cy * g.cz;
-  return (size_t)g.bx * g.by * g.bz * (kBrick * kBrick * kBrick);
-}
+inline size_t cell_count(const CellGrid& g) { return (size_t)g.cx * g.cy * g.cz; }
 
 }  // namespace cvr

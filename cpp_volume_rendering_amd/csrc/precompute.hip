@@ -1,15 +1,16 @@
 // precompute.hip — one-time device precompute of the ray-caster's inputs:
-// the padded/bricked cell8 volume layout (GL_R16F semantics), the gradient
+// the padded cell8 volume layout (GL_R16F semantics), the gradient
 // volume (finite differences / Sobel-Feldman, RGB16F), and the rank-0 tile
 // unpack of the screen-tile split.
 #include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
 #include <cstdint>
 
 #include "cvr_internal.h"
 
 namespace cvr {
 
-// Build the padded, bricked cell8 layout from raw voxels using the host-made
+// Build the padded cell8 layout (x-fastest (N+1)^3 cells) from raw voxels using the host-made
 // value table lut[v] = half(float(v / 255.0)) (GL_R16F upload of
 // GetNormalizedSample, utils.cpp:20-56).
 template <typename VT>
@@ -19,20 +20,10 @@ __global__ void build_cells_kernel(const VT* __restrict__ vox, const uint16_t* _
   size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= ncells) return;
   uint32_t i = (uint32_t)idx;
-  int a, b, c;
-  if (g.layout == kLayoutLinear) {
-    a = (int)(i % (uint32_t)g.cx);
-    uint32_t r = i / (uint32_t)g.cx;
-    b = (int)(r % (uint32_t)g.cy);
-    c = (int)(r / (uint32_t)g.cy);
-  } else {
-    uint32_t inner = i & 63u, brick = i >> 6;
-    a = (int)(inner & 3u); b = (int)((inner >> 2) & 3u); c = (int)(inner >> 4);
-    int bxi = (int)(brick % (uint32_t)g.bx);
-    uint32_t rest = brick / (uint32_t)g.bx;
-    int byi = (int)(rest % (uint32_t)g.by), bzi = (int)(rest / (uint32_t)g.by);
-    a += bxi * 4; b += byi * 4; c += bzi * 4;
-  }
+  const int a = (int)(i % (uint32_t)g.cx);
+  const uint32_t rest = i / (uint32_t)g.cx;
+  const int b = (int)(rest % (uint32_t)g.cy);
+  const int c = (int)(rest / (uint32_t)g.cy);
   uint4 r = make_uint4(0, 0, 0, 0);
   if (a < g.cx && b < g.cy && c < g.cz) {
     int x0 = max(a - 1, 0), x1 = min(a, nx - 1);
@@ -155,6 +146,85 @@ hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, 
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(unpack_tiles_kernel, dim3((unsigned)nb), dim3(bs), 0, s, packed, out, W, H,
                      tile, nranks, tpr_max, ntx, n);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Empty-space skipping: macro-cell value ranges and TF occupancy
+// ---------------------------------------------------------------------------
+
+// Raw-value range (max << 16 | min) of texels [m*w, m*w + w] (clamped) on every
+// axis: the texels a trilinear sample whose floor lies in macro cell m reads.
+template <typename VT>
+__global__ void macro_minmax_kernel(const VT* __restrict__ vox, int nx, int ny, int nz, int shift,
+                                    int mx, int my, int mz, uint32_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= mx * my * mz) return;
+  const int cx = i % mx, cy = (i / mx) % my, cz = i / (mx * my);
+  const int w = 1 << shift;
+  const int x0 = cx * w, x1 = min(x0 + w, nx - 1);
+  const int y0 = cy * w, y1 = min(y0 + w, ny - 1);
+  const int z0 = cz * w, z1 = min(z0 + w, nz - 1);
+  uint32_t lo = 0xffffu, hi = 0u;
+  for (int z = z0; z <= z1; z++)
+    for (int y = y0; y <= y1; y++) {
+      const VT* row = vox + ((size_t)z * ny + y) * nx;
+      for (int x = x0; x <= x1; x++) {
+        const uint32_t v = row[x];
+        lo = min(lo, v);
+        hi = max(hi, v);
+      }
+    }
+  out[i] = (hi << 16) | lo;
+}
+
+hipError_t launch_macro_minmax(const Ctx& c, int shift, const int mdim[3], uint32_t* out,
+                               hipStream_t s) {
+  const int n = mdim[0] * mdim[1] * mdim[2];
+  const int bs = 128;
+  if (c.bpv == 1)
+    hipLaunchKernelGGL(macro_minmax_kernel<uint8_t>, dim3((n + bs - 1) / bs), dim3(bs), 0, s,
+                       (const uint8_t*)c.d_vox, c.N[0], c.N[1], c.N[2], shift, mdim[0], mdim[1],
+                       mdim[2], out);
+  else
+    hipLaunchKernelGGL(macro_minmax_kernel<uint16_t>, dim3((n + bs - 1) / bs), dim3(bs), 0, s,
+                       (const uint16_t*)c.d_vox, c.N[0], c.N[1], c.N[2], shift, mdim[0], mdim[1],
+                       mdim[2], out);
+  return hipGetLastError();
+}
+
+// Occupancy byte of a macro cell for the current TF.  A density d reads the
+// padded TF entries k = floor(fmaf(d, n, -0.5)) + 1 and k + 1 (classify in
+// raymarch.hip); the alpha there is a lerp of those two, so it is <= 0 when
+// both are.  The densities of the cell lie in [lut[min], lut[max]] (widened by
+// 2^-10 against the rounding of the trilinear lerps); the cell is empty when
+// no padded entry in the range has alpha > 0 (`prefix` counts them).
+__global__ void occupancy_kernel(const uint32_t* __restrict__ minmax, int n_macro,
+                                 const uint16_t* __restrict__ lut, const int* __restrict__ prefix,
+                                 int tf_n, uint8_t* __restrict__ occ,
+                                 unsigned int* __restrict__ n_empty) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_macro) return;
+  const uint32_t mm = minmax[i];
+  const float lo = __half2float(__ushort_as_half(lut[mm & 0xffffu])) - 1.0f / 1024.0f;
+  const float hi = __half2float(__ushort_as_half(lut[mm >> 16])) + 1.0f / 1024.0f;
+  const float fn = (float)tf_n;
+  int kl = (int)floorf(fmaf(lo, fn, -0.5f)) + 1;
+  int kh = (int)floorf(fmaf(hi, fn, -0.5f)) + 2;
+  kl = max(kl, 0);
+  kh = min(kh, tf_n + 1);
+  const bool o = kl <= kh && prefix[kh + 1] - prefix[kl] > 0;
+  occ[i] = o ? 1 : 0;
+  const unsigned long long e = __ballot(!o);   // one atomic per wave
+  if ((threadIdx.x & 63) == 0 && e) atomicAdd(n_empty, (unsigned)__popcll(e));
+}
+
+hipError_t launch_occupancy(const uint32_t* minmax, int n_macro, const uint16_t* lut,
+                            const int* prefix, int tf_n, uint8_t* occ, unsigned int* n_empty,
+                            hipStream_t s) {
+  const int bs = 256;
+  hipLaunchKernelGGL(occupancy_kernel, dim3((n_macro + bs - 1) / bs), dim3(bs), 0, s, minmax,
+                     n_macro, lut, prefix, tf_n, occ, n_empty);
   return hipGetLastError();
 }
 

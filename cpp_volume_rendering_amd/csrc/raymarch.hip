@@ -71,7 +71,6 @@ __device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lx, 
 // x >= 0 the floor is the truncating convert and the weight one v_fract.
 struct SamplePos { uint32_t idx; float ax, ay, az; int ix, iy, iz; };
 
-template <int LAYOUT>
 __device__ __forceinline__ SamplePos sample_pos(float x, float y, float z, const Rc1passArgs& A) {
   x = __builtin_amdgcn_fmed3f(x, 0.0f, A.nm1[0]);
   y = __builtin_amdgcn_fmed3f(y, 0.0f, A.nm1[1]);
@@ -79,16 +78,10 @@ __device__ __forceinline__ SamplePos sample_pos(float x, float y, float z, const
   SamplePos p;
   p.ax = __builtin_amdgcn_fractf(x); p.ay = __builtin_amdgcn_fractf(y); p.az = __builtin_amdgcn_fractf(z);
   p.ix = (int)x; p.iy = (int)y; p.iz = (int)z;
-  if (LAYOUT == kLayoutLinear) {
-    // cell (ix+1, iy+1, iz+1) of the (N+1)^3 grid; the +1 offsets live in the base pointer
-    p.idx = __umul24((uint32_t)p.iz, (uint32_t)A.cells.pitch_z) +
-            __umul24((uint32_t)p.iy, (uint32_t)A.cells.pitch_y) + (uint32_t)p.ix;
-  } else {
-    uint32_t cx = (uint32_t)(p.ix + 1), cy = (uint32_t)(p.iy + 1), cz = (uint32_t)(p.iz + 1);
-    uint32_t brick = __umul24(cz >> 2, (uint32_t)A.cells.bxby) +
-                     __umul24(cy >> 2, (uint32_t)A.cells.bx) + (cx >> 2);
-    p.idx = (brick << 6) | ((cz & 3u) << 4) | ((cy & 3u) << 2) | (cx & 3u);
-  }
+  // cell (ix+1, iy+1, iz+1) of the (N+1)^3 x-fastest grid; the +1 offsets live
+  // in the base pointer
+  p.idx = __umul24((uint32_t)p.iz, (uint32_t)A.cells.pitch_z) +
+          __umul24((uint32_t)p.iy, (uint32_t)A.cells.pitch_y) + (uint32_t)p.ix;
   return p;
 }
 
@@ -162,6 +155,7 @@ __device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint2* _
 
 struct Ray {
   f3 dir, tpos, o, dt;   // direction, entry point (texture space), texel-space origin/step
+  f3 inv_dt;             // 1 / dt (macro-cell exits)
   float D;               // distance to evaluate, |tfar - tnear|
 };
 
@@ -191,13 +185,52 @@ __device__ __forceinline__ bool ray_setup(const Rc1passArgs& A, int px, int py, 
   r.o = f3{fmaf(r.tpos.x, A.n_over_g[0], -0.5f), fmaf(r.tpos.y, A.n_over_g[1], -0.5f),
            fmaf(r.tpos.z, A.n_over_g[2], -0.5f)};
   r.dt = f3{dir.x * A.n_over_g[0], dir.y * A.n_over_g[1], dir.z * A.n_over_g[2]};
+  if (A.occ) r.inv_dt = f3{1.0f / r.dt.x, 1.0f / r.dt.y, 1.0f / r.dt.z};
   return hit;
+}
+
+// Macro-cell skip.  The macro cell m (2^mshift texels a side) of a sample is
+// taken from its clamped texel coordinate exactly as sample_pos computes it; its
+// occupancy byte says whether any trilinear density over texels
+// [m*2^s, (m+1)*2^s] can have alpha > 0.  Samples are stepped over while their
+// centre t stays below the ray's exit from the macro box shrunk by
+// kMacroMargin texels (which absorbs the rounding of t_exit and of the sample
+// positions, ~1e-4 texels), so every skipped sample lies in the cell.
+// Returns true if at least one sample was skipped.
+constexpr float kMacroMargin = 1.0f / 64.0f;
+
+__device__ __forceinline__ bool skip_empty(const Rc1passArgs& A, const Ray& r, float step, float D,
+                                           float& s, uint32_t& cnt) {
+  const float h0 = fminf(step, D - s);
+  const float t0 = fmaf(h0, 0.5f, s);
+  const float x = __builtin_amdgcn_fmed3f(fmaf(r.dt.x, t0, r.o.x), 0.0f, A.nm1[0]);
+  const float y = __builtin_amdgcn_fmed3f(fmaf(r.dt.y, t0, r.o.y), 0.0f, A.nm1[1]);
+  const float z = __builtin_amdgcn_fmed3f(fmaf(r.dt.z, t0, r.o.z), 0.0f, A.nm1[2]);
+  const int sh = A.mshift;
+  const int mx = (int)x >> sh, my = (int)y >> sh, mz = (int)z >> sh;
+  if (A.occ[(mz * A.mdim[1] + my) * A.mdim[0] + mx]) return false;
+  const float w = (float)(1 << sh);
+  // exit parameter of the shrunk box on each axis (1/dt = +-inf on a parallel
+  // axis gives +-inf or NaN, both ignored by fminf against the other axes)
+  const float bx = r.dt.x > 0.0f ? (float)(mx + 1) * w - kMacroMargin : (float)mx * w + kMacroMargin;
+  const float by = r.dt.y > 0.0f ? (float)(my + 1) * w - kMacroMargin : (float)my * w + kMacroMargin;
+  const float bz = r.dt.z > 0.0f ? (float)(mz + 1) * w - kMacroMargin : (float)mz * w + kMacroMargin;
+  const float t_exit = fminf(fminf((bx - r.o.x) * r.inv_dt.x, (by - r.o.y) * r.inv_dt.y),
+                             (bz - r.o.z) * r.inv_dt.z);
+  const float s_in = s;
+  while (s < D) {
+    const float h = fminf(step, D - s);
+    if (!(fmaf(h, 0.5f, s) < t_exit)) break;
+    s = s + h;
+    cnt++;
+  }
+  return s != s_in;
 }
 
 // Ray-parallel march (one lane per ray) of ray_marching_1p.comp:124-172.  The
 // arithmetic per sample is exactly the reference's sequential loop (s
 // accumulates h one step at a time); batching only changes when loads issue.
-template <int K, bool PHONG, int LAYOUT, bool XF>
+template <int K, bool PHONG, bool SKIP, bool XF>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
                                           const uint2* __restrict__ grad,
                                           const float4* __restrict__ tfp, int px, int py,
@@ -211,7 +244,23 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
   const float step = A.step, D = r.D, fn = (float)A.tf_n;
   float s = 0.0f;
   bool done = !(s < D);
+  bool probe = true;
   while (!done) {
+    // Empty-space skipping (bit-exact): if the macro cell holding the next
+    // sample is transparent for the current TF (every density its texels can
+    // interpolate to classifies to alpha <= 0), the samples whose positions stay
+    // inside it are counted and stepped over with the same s += h recurrence,
+    // without loads: the reference composites nothing for them (:142).
+    // Probed only after a batch that composited nothing: inside visible
+    // material the lookup would add a dependent memory round trip per batch.
+    if (SKIP && probe) {
+      probe = false;
+      if (skip_empty(A, r, step, D, s, cnt)) {
+        probe = true;
+        if (!(s < D)) done = true;
+        continue;
+      }
+    }
     // stage 1: the next K sample positions (sequential s += h) and their loads
     float hj[K], tj[K];
     bool vj[K];
@@ -224,7 +273,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       hj[j] = fminf(step, D - ss);
       tj[j] = fmaf(hj[j], 0.5f, ss);
       ss = ss + hj[j];
-      sp[j] = sample_pos<LAYOUT>(fmaf(r.dt.x, tj[j], r.o.x), fmaf(r.dt.y, tj[j], r.o.y),
+      sp[j] = sample_pos(fmaf(r.dt.x, tj[j], r.o.x), fmaf(r.dt.y, tj[j], r.o.y),
                                  fmaf(r.dt.z, tj[j], r.o.z), A);
       raw[j] = cells[sp[j].idx];
     }
@@ -233,6 +282,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
 #pragma unroll
     for (int j = 0; j < K; j++)
       src[j] = classify(tfp, fn, trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az));
+    bool visible = false;
     // stage 3: front-to-back composite + ERT, in sample order.  The branches
     // matter: a wave whose samples are all transparent (empty space) skips
     // the exp and the composite together (a branch-free select form measured
@@ -246,6 +296,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
           cnt++;
           float4 sc = src[j];
           if (sc.w > 0.0f) {
+            visible = true;
             if (PHONG) shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
             const float x = -(sc.w * hj[j]);
             const float a = 1.0f - (XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
@@ -261,6 +312,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
     }
     s = ss;
     if (!(s < D)) done = true;
+    probe = !visible;
   }
 }
 
@@ -305,7 +357,7 @@ __device__ __forceinline__ void quad_composite(const QSample& q, bool valid, boo
 // reference skipping it (:142).  One memory round trip advances a ray 4K
 // samples instead of K: the longest tiles' critical path shrinks ~4x.
 // Must be called by all 64 lanes (DPP reads neighbours); `active` = lane's ray is live.
-template <int K, bool PHONG, int LAYOUT, bool XF>
+template <int K, bool PHONG, bool XF>
 __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
                                                const uint4* __restrict__ cells,
                                                const uint2* __restrict__ grad,
@@ -342,7 +394,7 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
 #pragma unroll
     for (int k = 0; k < K; k++) {
       tj[k] = fmaf(hj[k], 0.5f, sj[k]);
-      sp[k] = sample_pos<LAYOUT>(fmaf(r.dt.x, tj[k], r.o.x), fmaf(r.dt.y, tj[k], r.o.y),
+      sp[k] = sample_pos(fmaf(r.dt.x, tj[k], r.o.x), fmaf(r.dt.y, tj[k], r.o.y),
                                  fmaf(r.dt.z, tj[k], r.o.z), A);
       raw[k] = cells[sp[k].idx];
     }
@@ -400,7 +452,7 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // (four lanes per ray).  Without an order, block b -> tile in XCD bands
 // (blocks b and b+8 share an XCD, so XCD b%8 gets one contiguous band).
 // Waves of the `boost` longest tiles of each band raise their priority.
-template <int K, bool PHONG, int LAYOUT, bool QUAD, bool XF>
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF>
 __global__ void __launch_bounds__(64)
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
@@ -435,14 +487,14 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     const bool inside = px < A.W && py < A.H;
     dst = make_float4(0.f, 0.f, 0.f, 0.f);
     cnt = 0;
-    if (inside) march_ray<K, PHONG, LAYOUT, XF>(A, cells, grad, tfp, px, py, dst, cnt);
+    if (inside) march_ray<K, PHONG, SKIP, XF>(A, cells, grad, tfp, px, py, dst, cnt);
     writer = inside || A.packed;
   } else {                    // quarter of a tile, four lanes per ray
     const int ray = lane >> 2;
     tile_pixel(A, t, ((quarter & 1) << 2) | (ray & 3), ((quarter >> 1) << 2) | (ray >> 2), px, py,
                oidx);
     const bool inside = px < A.W && py < A.H;
-    march_ray_quad<K, PHONG, LAYOUT, XF>(A, cells, grad, tfp, px, py, inside, dst, cnt);
+    march_ray_quad<K, PHONG, XF>(A, cells, grad, tfp, px, py, inside, dst, cnt);
     writer = (lane & 3) == 0 && (inside || A.packed);
     if ((lane & 3) != 0) cnt = 0;           // one count per ray
   }
@@ -633,42 +685,42 @@ __global__ void clear_u32_kernel(uint32_t* __restrict__ p, int n) {
 // Launchers
 // ---------------------------------------------------------------------------
 
-// Kernel variant: K (batch), PHONG, LAYOUT, QUAD (quad path compiled in: it
-// costs the ray-parallel path registers even when unused), XF (range-free exp).
-template <int K, bool PHONG, int LAYOUT, bool QUAD, bool XF>
+// Kernel variant: K (batch), PHONG, SKIP (empty-space skipping compiled in),
+// QUAD (quad path compiled in), XF (range-free exp).  Paths a frame does not
+// use are compiled out: they would cost the hot loop registers (occupancy).
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF>
 static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                                  unsigned long long* tile_samples, const int* order,
                                  uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
   size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
   if (c.max_waves_cu > 0) lds = std::max(lds, (size_t)(160 * 1024 / c.max_waves_cu) & ~(size_t)255);
-  const uint4* cells = (const uint4*)c.d_cells;
-  if (LAYOUT == kLayoutLinear) cells += c.cells.linear_origin;   // cell (1,1,1) <-> texel (0,0,0)
+  // cell (1,1,1) <-> texel (0,0,0)
+  const uint4* cells = (const uint4*)c.d_cells + c.cells.linear_origin;
   int grid = order ? plan.order_slots : plan.ntiles;
-  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, LAYOUT, QUAD, XF>), dim3(grid), dim3(64), lds, s,
+  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF>), dim3(grid), dim3(64), lds, s,
                      a, cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples,
                      tile_samples, order, tile_cost, order ? plan.boost : 0);
   return hipGetLastError();
 }
 
-template <int K, bool PHONG, int LAYOUT>
-static hipError_t launch_kpl(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
+template <int K, bool PHONG, bool SKIP>
+static hipError_t launch_kps(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                              unsigned long long* ts, const int* order, uint32_t* tile_cost,
                              const RenderPlan& plan, hipStream_t s) {
   const bool quad = order && plan.quad_pct > 0;
   if (quad)
-    return a.exp_fast ? launch_variant<K, PHONG, LAYOUT, true, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
-                      : launch_variant<K, PHONG, LAYOUT, true, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
-  return a.exp_fast ? launch_variant<K, PHONG, LAYOUT, false, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
-                    : launch_variant<K, PHONG, LAYOUT, false, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
+    return a.exp_fast ? launch_variant<K, PHONG, SKIP, true, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                      : launch_variant<K, PHONG, SKIP, true, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
+  return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                    : launch_variant<K, PHONG, SKIP, false, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
 }
 
 template <int K, bool PHONG>
 static hipError_t launch_kp(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                             unsigned long long* ts, const int* order, uint32_t* tile_cost,
                             const RenderPlan& plan, hipStream_t s) {
-  return c.cells.layout == kLayoutLinear
-             ? launch_kpl<K, PHONG, kLayoutLinear>(c, a, out, samples, ts, order, tile_cost, plan, s)
-             : launch_kpl<K, PHONG, kLayoutBrick>(c, a, out, samples, ts, order, tile_cost, plan, s);
+  return a.occ ? launch_kps<K, PHONG, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
+               : launch_kps<K, PHONG, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
 }
 
 template <int K>

@@ -133,8 +133,6 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                priority (with tile_order 1; default 5)
  *   "quad"       percent of each band's longest tiles marched sample-parallel, four
  *                lanes per ray (with tile_order 1; default 0)
- *   "layout"     cell layout of the next cvr_set_volume: 0 bricked 4^3,
- *                1 linear x-fastest (default)
  *   "tile_stats" 1: record per-tile timing of every frame (diagnostics)
  *   "kernel_timing" N > 0: time the ray-march kernel of the last N frames
  *                (cvr_read_kernel_times); 0 off (default) */

@@ -119,13 +119,18 @@ CASES = {
 }
 
 
+def case_tf(c, tf):
+    if "tf_alpha_scale" in c:
+        tf = tf.copy()
+        tf[:, 3] *= c["tf_alpha_scale"]
+    return tf
+
+
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_rc1pass_bitexact_vs_oracle(dev, oracle, bonsai_tf, name):
     c = CASES[name]
     vol = c["vol"]()
-    if "tf_alpha_scale" in c:
-        bonsai_tf = bonsai_tf.copy()
-        bonsai_tf[:, 3] *= c["tf_alpha_scale"]
+    bonsai_tf = case_tf(c, bonsai_tf)
     cam = c.get("cam", INITIAL)
     kw = dict(step=c.get("step", 0.0), phong=c.get("phong", False), gmode=c.get("gmode", 0),
               light=c.get("light", (0, 0, 0)), shading=c.get("shading", (0.5, 0.5, 0.8, 30.0)))
@@ -216,23 +221,29 @@ def test_headline_512_properties(dev, oracle, bonsai_tf):
 
 
 SCHEDULES = [
-    dict(tile_order=0, batch=4, layout=0),
-    dict(tile_order=1, quad=10, boost=5, batch=4, layout=0),
-    dict(tile_order=1, quad=100, boost=0, batch=2, layout=1),
-    dict(tile_order=1, quad=0, boost=50, batch=2, layout=1),
-    dict(tile_order=1, quad=35, boost=5, batch=4, layout=1),
+    dict(tile_order=0, batch=4),
+    dict(tile_order=1, quad=10, boost=5, batch=4),
+    dict(tile_order=1, quad=100, boost=0, batch=2),
+    dict(tile_order=1, quad=0, boost=50, batch=2),
+    dict(tile_order=1, quad=35, boost=5, batch=4),
+    # empty-space skipping forced on (any fraction of empty macro cells)
+    dict(tile_order=1, batch=4, macro=3, skip_min_pct=0),
+    dict(tile_order=0, batch=2, macro=2, skip_min_pct=0),
+    dict(tile_order=1, batch=4, macro=5, skip_min_pct=0, quad=10),
 ]
 
 
 @pytest.mark.parametrize("sched", range(len(SCHEDULES)))
-@pytest.mark.parametrize("name", ["ml64_ragged", "ml_aniso", "phong_fd", "camera_inside"])
+@pytest.mark.parametrize("name", ["ml64_ragged", "ml_aniso", "phong_fd", "camera_inside",
+                                  "blobs_sparse", "dense_tf"])
 def test_schedules_bitexact(oracle, bonsai_tf, name, sched):
     """Every scheduling / march variant (LPT order, quad = 4-lanes-per-ray march for the
-    longest tiles, batch size, cell layout) reproduces the oracle bit for bit, on the
+    longest tiles, batch size, empty-space skipping) reproduces the oracle bit for bit, on the
     first frame (screen order) and on later frames (learned LPT order + quad tiles)."""
     c = CASES[name]
     opts = SCHEDULES[sched]
     vol = c["vol"]()
+    bonsai_tf = case_tf(c, bonsai_tf)
     cam = c.get("cam", INITIAL)
     kw = dict(step=c.get("step", 0.0), phong=c.get("phong", False), gmode=c.get("gmode", 0),
               light=c.get("light", (0, 0, 0)), shading=c.get("shading", (0.5, 0.5, 0.8, 30.0)))
@@ -240,9 +251,7 @@ def test_schedules_bitexact(oracle, bonsai_tf, name, sched):
                                            c["H"], **kw)
     d = Device(0)
     try:
-        for k in ("layout",):
-            N.check(N.lib().cvr_set_option(d.handle, k.encode(), opts[k]), k)
-        for k in ("tile_order", "quad", "boost", "batch"):
+        for k in ("tile_order", "quad", "boost", "batch", "macro", "skip_min_pct"):
             if k in opts:
                 N.check(N.lib().cvr_set_option(d.handle, k.encode(), opts[k]), k)
         for frame in range(3):

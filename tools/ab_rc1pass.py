@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of rc1pass kernel variants in ONE process, interleaved rounds
 (methodology rule 24).  Every variant's image is checked bit-equal to the first
-variant's.  Variant syntax: L<layout>b<batch>o<tile_order>p<boost%>q<quad%>[c<tile_cost>][w<max waves/CU>], e.g. L1b4o1p5q0c0w20.
+variant's.  Variant syntax: b<batch>o<tile_order>p<boost%>q<quad%>[c<tile_cost>][w<max waves/CU>][m<macro shift, 0 off>][s<skip_min_pct>], e.g. b4o1p5q0m3s0.
 Usage: python tools/ab_rc1pass.py [--size 512] [--res 1024] [--variants ...]"""
 import argparse
 import ctypes
@@ -20,12 +20,13 @@ from cpp_volume_rendering_amd.renderer import Camera, Device, build_tf_rgbt, mak
 
 
 def parse_variant(v):
-    m = re.fullmatch(r"L(\d)b(\d)o(\d)p(\d+)q(\d+)(?:c(\d))?(?:w(\d+))?", v)
+    m = re.fullmatch(r"(?:L1)?b(\d)o(\d)p(\d+)q(\d+)(?:c(\d))?(?:w(\d+))?(?:m(\d))?(?:s(\d+))?", v)
     if not m:
         raise ValueError(f"bad variant {v}")
     g = m.groups()
-    return tuple(int(x) for x in g[:5]) + (int(g[5]) if g[5] is not None else 0,
-                                            int(g[6]) if g[6] is not None else 0)
+    d = (-1, -1, -1, -1)   # tile_cost, max_waves_cu, macro, skip_min_pct (-1: library default)
+    return tuple(int(x) for x in g[:4]) + tuple(int(x) if x is not None else dflt
+                                                for x, dflt in zip(g[4:], d))
 
 
 def main():
@@ -35,7 +36,7 @@ def main():
     ap.add_argument("--field", default="ml")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=20)
-    ap.add_argument("--variants", default="L1b4o1p5q0,L1b2o1p5q0,L0b4o1p5q0,L1b4o1p0q0,L1b4o0p0q0,L1b4o1p5q10")
+    ap.add_argument("--variants", default="b4o1p5q0,b2o1p5q0,b4o1p0q0,b4o0p0q0,b4o1p5q10")
     ap.add_argument("--phong", action="store_true")
     ap.add_argument("--no-total", action="store_true", help="time frames without the sample counter")
     a = ap.parse_args()
@@ -43,17 +44,17 @@ def main():
     vol = D.marschner_lobb_u8(n) if a.field == "ml" else D.blobs_u8(n)
     variants = a.variants.split(",")
     parsed = {v: parse_variant(v) for v in variants}
-    devs = {}
     s = torch.cuda.Stream()
-    for layout in sorted({p[0] for p in parsed.values()}):
-        dev = Device(0)
-        N.check(N.lib().cvr_set_option(dev.handle, b"layout", layout), "layout")
-        dev.set_volume(vol, D.voxel_scale(n))
-        dev.set_transfer_function(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
-        if a.phong:
-            dev.set_gradient(1)
-        dev.set_stream(s.cuda_stream)
-        devs[layout] = dev
+    L0 = N.lib()
+    dev = Device(0)
+    dev.set_volume(vol, D.voxel_scale(n))
+    dev.set_transfer_function(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
+    if a.phong:
+        dev.set_gradient(1)
+    dev.set_stream(s.cuda_stream)
+    # library defaults, restored for the options a variant leaves unspecified
+    defaults = {k: L0.cvr_get_option(dev.handle, k.encode())
+                for k in ("tile_cost", "max_waves_cu", "macro", "skip_min_pct")}
     frame = make_frame(Camera(**D.INITIAL_STATE_CAMERA), W, W)
     p = N.Rc1passParams()
     p.apply_gradient_shading = int(a.phong)
@@ -76,14 +77,15 @@ def main():
     S = None
     for _ in range(a.rounds):
         for v in variants:
-            layout, b, o, boost, quad, cost, mw = parsed[v]
-            dev = devs[layout]
+            b, o, boost, quad, cost, mw, macro, skip = parsed[v]
             N.check(L.cvr_set_option(dev.handle, b"batch", b), "opt")
             N.check(L.cvr_set_option(dev.handle, b"tile_order", o), "opt")
             N.check(L.cvr_set_option(dev.handle, b"boost", boost), "opt")
             N.check(L.cvr_set_option(dev.handle, b"quad", quad), "opt")
-            N.check(L.cvr_set_option(dev.handle, b"tile_cost", cost), "opt")
-            N.check(L.cvr_set_option(dev.handle, b"max_waves_cu", mw), "opt")
+            for key, val in (("tile_cost", cost), ("max_waves_cu", mw), ("macro", macro),
+                             ("skip_min_pct", skip)):
+                N.check(L.cvr_set_option(dev.handle, key.encode(),
+                                         val if val >= 0 else defaults[key]), key)
             with torch.cuda.stream(s):
                 run(dev, 3)   # warm up + learn the order
                 tot.zero_()

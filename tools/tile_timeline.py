@@ -21,7 +21,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--res", type=int, default=1024)
-    ap.add_argument("--layout", type=int, default=1)
     ap.add_argument("--order", type=int, default=1)
     ap.add_argument("--boost", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4)
@@ -32,7 +31,7 @@ def main():
     n, W = a.size, a.res
     dev = Device(0)
     L = N.lib()
-    for k, v in (("layout", a.layout), ("tile_order", a.order), ("boost", a.boost),
+    for k, v in (("tile_order", a.order), ("boost", a.boost),
                  ("batch", a.batch), ("quad", a.quad), ("debug_keep", a.keep), ("tile_stats", 1)):
         N.check(L.cvr_set_option(dev.handle, k.encode(), v), k)
     dev.set_volume(D.marschner_lobb_u8(n), D.voxel_scale(n))
