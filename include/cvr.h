@@ -24,10 +24,9 @@
  *   cvr_render_rc1pass           <- RayCasting1Pass::Update + Redraw
  *                                   cppvolrend/structured/rc1pass/rc1prenderer.cpp:72-151
  *                                   (the dispatch of ray_marching_1p.comp:85-179)
- *   cvr_render_dosct             <- RC1PConeTracingDirOcclusionShading::Update + Redraw
- *                                   cppvolrend/structured/rc1pdosct/dosrcrenderer.cpp:134-260
- *   cvr_render_extbsd            <- RC1PExtinctionBasedShading::Update + Redraw
- *                                   cppvolrend/structured/rc1pextbsd/ebsrenderer.cpp:125-260
+ *   (planned, not yet exported: cvr_render_dosct <- RC1PConeTracingDirOcclusionShading,
+ *    dosrcrenderer.cpp:134-260; cvr_render_extbsd <- RC1PExtinctionBasedShading,
+ *    ebsrenderer.cpp:125-260)
  *   cvr_status (never exit())    <- gl::ExitOnGLError  libs/gl_utils/utils.cpp:11-30
  *
  * Threading: one context per device, externally synchronised (the reference
