@@ -200,8 +200,14 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_tf_prefix; free_dev(p); c->d_tf_prefix = nullptr;
   p = c->d_total; free_dev(p); c->d_total = nullptr;
   free_dev(c->d_scratch);
-  p = c->d_order; free_dev(p); c->d_order = nullptr;
-  p = c->d_tile_cost; free_dev(p); c->d_tile_cost = nullptr;
+  if (c->side) (void)hipStreamSynchronize(c->side);
+  for (auto& o : c->oslot) {
+    p = o.d_order; free_dev(p); o.d_order = nullptr;
+    p = o.d_cost; free_dev(p); o.d_cost = nullptr;
+    if (o.done) (void)hipEventDestroy(o.done);
+  }
+  if (c->ev_frame) (void)hipEventDestroy(c->ev_frame);
+  if (c->side) (void)hipStreamDestroy(c->side);
   p = c->d_tile_stats; free_dev(p); c->d_tile_stats = nullptr;
   p = c->d_tile_samples; free_dev(p); c->d_tile_samples = nullptr;
   for (hipEvent_t e : c->ev_start) (void)hipEventDestroy(e);
@@ -234,13 +240,13 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
   if (!std::strcmp(key, "tile_order")) {
     if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "tile_order must be 0 or 1");
     c->use_order = value;
-    c->order_valid = 0;
+    for (auto& o : c->oslot) o.valid = 0;
     return CVR_OK;
   }
   if (!std::strcmp(key, "quad")) {
     if (value < 0 || value > 100) return fail(c, CVR_ERR_ARG, "quad must be a percentage");
     c->quad_pct = value;
-    c->order_valid = 0;
+    for (auto& o : c->oslot) o.valid = 0;
     return CVR_OK;
   }
   if (!std::strcmp(key, "tile_stats")) {
@@ -287,6 +293,22 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->max_waves_cu = value;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "async_order")) {
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "async_order must be 0 or 1");
+    if (c->side) HIP_TRY(c, hipStreamSynchronize(c->side));
+    c->async_order = value;
+    for (auto& o : c->oslot) { o.valid = 0; o.pending = false; }
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "order_interval")) {
+    if (value < 1 || value > 1000000) return fail(c, CVR_ERR_ARG, "order_interval must be >= 1");
+    c->order_interval = value;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "debug_epi_stop")) {   // diagnostics: truncated order builds
+    c->epi_stop = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "debug_keep")) {   // diagnostics only: the image is incomplete
     if (value < 0) return fail(c, CVR_ERR_ARG, "debug_keep must be >= 0");
     c->debug_keep = value;
@@ -308,6 +330,11 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "boost")) return c->boost_pct;
   if (!std::strcmp(key, "tile_cost")) return c->cost_time;
   if (!std::strcmp(key, "macro")) return c->macro_shift;
+  if (!std::strcmp(key, "max_waves_cu")) return c->max_waves_cu;
+  if (!std::strcmp(key, "debug_keep")) return c->debug_keep;
+  if (!std::strcmp(key, "debug_epi_stop")) return c->epi_stop;
+  if (!std::strcmp(key, "async_order")) return c->async_order;
+  if (!std::strcmp(key, "order_interval")) return c->order_interval;
   if (!std::strcmp(key, "skip_min_pct")) return c->skip_min_pct;
   if (!std::strcmp(key, "occ_empty_permille"))   // read-only: empty macro cells (after a render)
     return c->occ_valid ? (int)(c->occ_empty * 1000.0f + 0.5f) : -1;
@@ -322,6 +349,7 @@ cvr_status cvr_synchronize(cvr_ctx* ctx) {
   if (!c) return CVR_ERR_ARG;
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (c->side) HIP_TRY(c, hipStreamSynchronize(c->side));
   return CVR_OK;
 }
 
@@ -590,6 +618,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     plan.order_slots = 8 * per_band;
     plan.boost = (int)(((long long)seg_avg * c->boost_pct) / 100);
     plan.keep = c->debug_keep;
+    plan.epi_stop = c->epi_stop;
   }
 
   HIP_TRY(c, hipSetDevice(c->device));
@@ -613,31 +642,43 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   // outputs: the context's own counter is reset here.
   if (d_total && !o->on_device) HIP_TRY(c, hipMemsetAsync(d_total, 0, sizeof(unsigned long long), s));
 
-  // Longest-first (LPT) order learned from the previous frame of the same plan:
-  // the kernel records each wave tile's critical path, tile_order_kernel sorts
-  // every XCD band by it (and re-arms the queue heads) for the next frame.
-  const int units = plan.order_slots;
+  // Longest-first (LPT) order learned three frames back (same plan): the kernel
+  // records each wave tile's critical path into this frame's slot, and the
+  // slot's order is rebuilt from it on the side stream while the next frame
+  // renders (tile_epilogue_kernel: work-balanced XCD bands + bucket LPT).
   const bool can_order = c->use_order && (plan.ntiles + 7) / 8 <= cvr::kMaxBandTiles;
   const int key = (plan.ntiles << 2) ^ (plan.quad_pct << 24) ^
                   (packed ? (f->rank << 8) ^ (f->nranks << 12) ^ 1 : 0);
   const int* order = nullptr;
   uint32_t* tile_cost = nullptr;
+  Ctx::OrderSlot& os = c->oslot[c->async_order ? c->frame_no % Ctx::kOrderSlots : 0];
   if (can_order) {
-    if (c->order_units < units || !c->d_tile_cost) {
-      void* p = c->d_order; free_dev(p); c->d_order = nullptr;
-      p = c->d_tile_cost; free_dev(p); c->d_tile_cost = nullptr;
-      c->order_units = 0;
-      HIP_TRY(c, hipMalloc((void**)&c->d_order, (size_t)units * sizeof(int)));
-      HIP_TRY(c, hipMalloc((void**)&c->d_tile_cost, (size_t)plan.ntiles * sizeof(uint32_t) + 64));
-      HIP_TRY(c, hipMemsetAsync(c->d_tile_cost, 0, (size_t)plan.ntiles * sizeof(uint32_t) + 64, s));
-      c->order_units = units;
-      c->order_valid = 0;
+    if (!c->side) {
+      int lo = 0, hi = 0;
+      HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_TRY(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi));
+      HIP_TRY(c, hipEventCreateWithFlags(&c->ev_frame, hipEventDisableTiming));
+      for (auto& o : c->oslot) HIP_TRY(c, hipEventCreateWithFlags(&o.done, hipEventDisableTiming));
     }
-    if (c->order_key != key) c->order_valid = 0;
-    order = c->order_valid ? c->d_order : nullptr;
-    tile_cost = c->d_tile_cost;
+    // the slot's previous sort must be done before this frame reads its order
+    // and overwrites its costs (it ran alongside the previous frame)
+    if (os.pending) HIP_TRY(c, hipStreamWaitEvent(s, os.done, 0));
+    if (os.units < plan.order_slots || os.ntiles < plan.ntiles) {
+      HIP_TRY(c, hipStreamSynchronize(c->side));
+      void* p = os.d_order; free_dev(p); os.d_order = nullptr;
+      p = os.d_cost; free_dev(p); os.d_cost = nullptr;
+      os.units = os.ntiles = 0;
+      os.valid = 0;
+      HIP_TRY(c, hipMalloc((void**)&os.d_order, (size_t)plan.order_slots * sizeof(int)));
+      HIP_TRY(c, hipMalloc((void**)&os.d_cost, (size_t)plan.ntiles * sizeof(uint32_t) + 64));
+      HIP_TRY(c, hipMemsetAsync(os.d_cost, 0, (size_t)plan.ntiles * sizeof(uint32_t) + 64, s));
+      os.units = plan.order_slots;
+      os.ntiles = plan.ntiles;
+    }
+    order = (os.valid && os.key == key) ? os.d_order : nullptr;
+    tile_cost = os.d_cost;
   }
-  // Sample total: every wave tile stores its count, the epilogue sums them
+  // Sample total: every wave tile stores its count, a sum epilogue adds them up
   // (one atomic per band; a per-wave atomic on one word serialises the frame).
   unsigned long long* tile_samples = nullptr;
   if (d_total) {
@@ -658,14 +699,30 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     HIP_TRY(c, hipEventRecord(c->ev_stop[slot], s));
     c->timed_frames++;
   }
-  if (tile_cost || tile_samples) {
-    HIP_TRY(c, cvr::launch_tile_epilogue(tile_cost, tile_samples, d_total, plan,
-                                         tile_cost ? c->d_order : nullptr, s));
-    if (tile_cost) {
-      c->order_valid = 1;
-      c->order_key = key;
-    }
+  // The order is rebuilt every order_interval-th frame (and whenever it is
+  // missing or stale for this plan): costs shift slowly between frames, and
+  // the rebuild (~15 us on the frame's stream) would otherwise cost ~10 %.
+  const bool rebuild = tile_cost && !c->async_order &&
+                       (!order || c->frame_no % std::max(1, c->order_interval) == 0);
+  if (rebuild) {
+    // one epilogue on the frame's stream: sum + order for the next frame
+    HIP_TRY(c, cvr::launch_tile_epilogue(tile_cost, tile_samples, d_total, plan, os.d_order, s));
+    os.pending = false;
+    os.valid = 1;
+    os.key = key;
+  } else if (tile_samples) {
+    HIP_TRY(c, cvr::launch_tile_epilogue(nullptr, tile_samples, d_total, plan, nullptr, s));
   }
+  if (tile_cost && c->async_order) {
+    HIP_TRY(c, hipEventRecord(c->ev_frame, s));
+    HIP_TRY(c, hipStreamWaitEvent(c->side, c->ev_frame, 0));
+    HIP_TRY(c, cvr::launch_tile_epilogue(tile_cost, nullptr, nullptr, plan, os.d_order, c->side));
+    HIP_TRY(c, hipEventRecord(os.done, c->side));
+    os.pending = true;
+    os.valid = 1;
+    os.key = key;
+  }
+  c->frame_no++;
   if (!o->on_device) {
     HIP_TRY(c, hipMemcpyAsync(o->rgba, d_out, rgba_bytes, hipMemcpyDeviceToHost, s));
     if (o->samples) HIP_TRY(c, hipMemcpyAsync(o->samples, d_samples, smp_bytes, hipMemcpyDeviceToHost, s));

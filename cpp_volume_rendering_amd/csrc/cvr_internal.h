@@ -63,9 +63,10 @@ struct RenderPlan {
   int quad_pct;                      // per band, this % of the longest tiles march 4 lanes/ray
   int keep;                          // diagnostics: >0 keeps only the first `keep` entries per band
   int max_seg;                       // most tiles one (work-balanced) band may take
+  int epi_stop;                      // diagnostics: the epilogue stops after phase k (0 = full)
 };
 
-constexpr int kMaxBandTiles = 16384;   // the epilogue sorts a band in LDS (64 KiB)
+constexpr int kMaxBandTiles = 8192;    // the epilogue sorts a band in LDS (32 KiB + group prefixes)
 
 struct Ctx {
   int device = 0;
@@ -104,6 +105,7 @@ struct Ctx {
   int batch = 4;
   int cost_time = 0;               // option "tile_cost": 0 longest ray, 1 measured time (worse)
   int max_waves_cu = 0;            // experiment (option "max_waves_cu"): cap residency via LDS
+  int epi_stop = 0;                // diagnostics (option "debug_epi_stop")
   int debug_keep = 0;              // diagnostics (option "debug_keep"): render only the longest entries
   int boost_pct = 5;               // % of every band's longest entries run at raised priority
   int quad_pct = 0;                // % of every band's longest tiles marched 4 lanes per ray
@@ -113,12 +115,29 @@ struct Ctx {
   // kernel_timing option: HIP events around every frame's ray-march launch (ring)
   std::vector<hipEvent_t> ev_start, ev_stop;
   long long timed_frames = 0;
-  int use_order = 1;               // 1: longest-first (LPT) from the previous frame's costs
-  int* d_order = nullptr;          // unit permutation for the next frame
-  uint32_t* d_tile_cost = nullptr; // per-wave-tile critical path of the last frame
-  int order_units = 0;             // units the order buffer is sized for
-  int order_key = -1;              // plan signature the order was learned for
-  int order_valid = 0;
+  int use_order = 1;               // 1: longest-first (LPT) from an earlier frame's costs
+  // The LPT order is built off the critical path: frame i's costs are sorted
+  // on a side stream while frames i+1, i+2 render, and frame i+3 uses the
+  // result (kOrderSlots slots in rotation; frame i uses and refills slot
+  // i % kOrderSlots).  With two slots the sort, which only gets CUs in the
+  // next frame's tail, still held up the frame after (~11 us per frame).
+  struct OrderSlot {
+    int* d_order = nullptr;        // launch order (8 x slots per band)
+    uint32_t* d_cost = nullptr;    // per-wave-tile critical path, written by the frame
+    int units = 0;                 // order entries allocated
+    int ntiles = 0;                // cost entries allocated
+    int key = -1;                  // plan signature of the order in d_order
+    int valid = 0;
+    hipEvent_t done = nullptr;     // the side-stream sort of this slot has finished
+    bool pending = false;
+  };
+  static constexpr int kOrderSlots = 3;
+  int async_order = 0;             // option "async_order": 1 = sort on a side stream (lag 3)
+  int order_interval = 8;          // option "order_interval": rebuild the order every n-th frame
+  OrderSlot oslot[kOrderSlots];
+  long long frame_no = 0;
+  hipStream_t side = nullptr;      // high-priority stream for the order builds
+  hipEvent_t ev_frame = nullptr;   // end of a frame's ray-march (the side stream waits on it)
   int num_cus = 0;
   unsigned long long* d_tile_samples = nullptr;   // per-wave-tile sample counts (zeroed)
   int tile_samples_n = 0;

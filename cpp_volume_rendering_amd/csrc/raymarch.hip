@@ -556,18 +556,24 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
 //    blocks band, band+8, ... (the blocks XCD `band` receives); slots past the
 //    band's entries are -1.  Resets tile_cost for the next frame's atomicMax.
 constexpr int kOrderThreads = 1024;
-constexpr unsigned kTileWeightBias = 8;   // per-tile floor of the cost (iterations or 10 ns ticks)
+constexpr unsigned kTileWeightBias = 8;
+constexpr int kGroupChunk = 256;    // 64-tile groups scanned per pass of the boundary search
 
 __global__ void __launch_bounds__(kOrderThreads)
 tile_epilogue_kernel(uint32_t* __restrict__ tile_cost, unsigned long long* __restrict__ tile_samples,
                      unsigned long long* __restrict__ total, int ntiles, int quad_pct,
-                     int slots_per_band, int max_seg, int keep, int* __restrict__ order) {
+                     int slots_per_band, int max_seg, int keep, int stop_after,
+                     int* __restrict__ order) {
   __shared__ unsigned hist[256];
   __shared__ unsigned start[256];
   __shared__ unsigned maxc;
   __shared__ unsigned long long wsum[kOrderThreads / 64];
   __shared__ int bounds[9];
-  extern __shared__ int sorted[];   // max_seg entries
+  __shared__ unsigned long long gsum[kGroupChunk];
+  __shared__ unsigned long long gcarry;
+  extern __shared__ int dyn_lds[];   // gpref[ngroups] (u64), then sorted[max_seg]
+  unsigned long long* gpref = reinterpret_cast<unsigned long long*>(dyn_lds);
+  int* sorted = dyn_lds + 2 * ((ntiles + 63) >> 6);
   const int band = blockIdx.x, tid = threadIdx.x;
   if (tile_samples) {
     const int s0 = (band * ntiles) >> 3, s1 = ((band + 1) * ntiles) >> 3;
@@ -585,40 +591,66 @@ tile_epilogue_kernel(uint32_t* __restrict__ tile_cost, unsigned long long* __res
       if (total && t) atomicAdd(total, t);
     }
   }
-  if (!tile_cost) return;
+  if (!tile_cost || stop_after == 9) return;
 
-  // 1) work-balanced band boundaries (every block computes all 8, identically)
-  const int chunk = (ntiles + kOrderThreads - 1) / kOrderThreads;
-  const int c0 = min(tid * chunk, ntiles), c1 = min(c0 + chunk, ntiles);
-  unsigned long long mine = 0;
-  for (int i = c0; i < c1; i++) mine += tile_cost[i] + kTileWeightBias;
-  __syncthreads();
-  // block-wide exclusive scan of the per-thread sums
-  unsigned long long incl = mine;
+  // 1) work-balanced band boundaries (every block computes all 8, identically),
+  //    at the granularity of 64-tile groups: a wave reads a group with one
+  //    coalesced load and reduces it; one wave scans the group sums; band k
+  //    starts after the group whose prefix reaches k/8 of the total weight.
+  //    (Per-thread contiguous chunks made every load instruction touch 64
+  //    cache lines: ~20 us for this phase alone.)
+  const int ngroups = (ntiles + 63) >> 6;
+  const int lane = tid & 63, wid = tid >> 6;
+  __syncthreads();   // gsum aliases wsum's neighbours in LDS below
+  constexpr int kGroupsPerWave = kGroupChunk / (kOrderThreads / 64);
+  for (int g0 = 0; g0 < ngroups; g0 += kGroupChunk) {
+    const int gend = min(g0 + kGroupChunk, ngroups);
+    uint32_t w[kGroupsPerWave];   // all loads in flight before any reduction
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const unsigned long long o = __shfl_up(incl, off, 64);
-    if ((tid & 63) >= off) incl += o;
+    for (int j = 0; j < kGroupsPerWave; j++) {
+      const int g = g0 + wid + j * (kOrderThreads / 64), i = (g << 6) + lane;
+      w[j] = (g < gend && i < ntiles) ? tile_cost[i] + kTileWeightBias : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kGroupsPerWave; j++) {
+      const int g = g0 + wid + j * (kOrderThreads / 64);
+      const unsigned long long v = wave_sum((unsigned long long)w[j]);
+      if (lane == 0 && g < gend) gsum[g - g0] = v;
+    }
+    __syncthreads();
+    if (wid == 0) {   // inclusive scan of this chunk of group sums, carried across chunks
+      const int n = min(kGroupChunk, ngroups - g0);
+      unsigned long long carry = g0 == 0 ? 0ull : gcarry;
+      for (int base = 0; base < n; base += 64) {
+        unsigned long long v = base + lane < n ? gsum[base + lane] : 0ull;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const unsigned long long o = __shfl_up(v, off, 64);
+          if (lane >= off) v += o;
+        }
+        v += carry;
+        if (base + lane < n) gsum[base + lane] = v;
+        carry = __shfl(v, 63, 64);
+      }
+      if (lane == 0) gcarry = carry;
+    }
+    __syncthreads();
+    // record the chunk's inclusive prefixes for the boundary search
+    for (int g = g0 + tid; g < min(g0 + kGroupChunk, ngroups); g += kOrderThreads)
+      gpref[g] = gsum[g - g0];
+    __syncthreads();
   }
-  if ((tid & 63) == 63) wsum[tid >> 6] = incl;
   if (tid < 9) bounds[tid] = tid == 8 ? ntiles : (tid == 0 ? 0 : -1);
   if (tid == 0) maxc = 0;
   if (tid < 256) hist[tid] = 0;
   __syncthreads();
-  unsigned long long wbase = 0, wtot = 0;
-  for (int w = 0; w < kOrderThreads / 64; w++) {
-    if (w < (tid >> 6)) wbase += wsum[w];
-    wtot += wsum[w];
-  }
-  unsigned long long p = wbase + incl - mine;   // weight before tile c0
-  for (int i = c0; i < c1; i++) {
-    // tile i starts band k when its prefix first reaches k/8 of the total
-    const unsigned long long w = tile_cost[i] + kTileWeightBias;
+  const unsigned long long wtot = gpref[ngroups - 1];
+  for (int g = tid; g < ngroups; g += kOrderThreads) {
+    const unsigned long long end = gpref[g], beg = g == 0 ? 0ull : gpref[g - 1];
     for (int k = 1; k < 8; k++) {
       const unsigned long long target = (wtot * (unsigned long long)k) >> 3;
-      if (p < target && p + w >= target) bounds[k] = i + 1;
+      if (beg < target && target <= end) bounds[k] = min((g + 1) << 6, ntiles);
     }
-    p += w;
   }
   __syncthreads();
   bool balanced = true;
@@ -632,17 +664,35 @@ tile_epilogue_kernel(uint32_t* __restrict__ tile_cost, unsigned long long* __res
   const int b0 = balanced ? bounds[band] : (band * ntiles) >> 3;
   const int b1 = balanced ? bounds[band + 1] : ((band + 1) * ntiles) >> 3;
   const int seg = b1 - b0;
+  if (stop_after == 1) return;
 
-  // 2) LPT order of the band: bucket sort by critical path
+  // 2) LPT order of the band: bucket sort by critical path.  The band's costs
+  //    are read once into registers (kBandRegs per thread; longer bands loop).
+  constexpr int kBandRegs = 4;
+  uint32_t cst[kBandRegs];
+#pragma unroll
+  for (int k = 0; k < kBandRegs; k++) {
+    const int i = tid + k * kOrderThreads;
+    cst[k] = i < seg ? tile_cost[b0 + i] : 0u;
+  }
   unsigned lmax = 0;
-  for (int i = tid; i < seg; i += kOrderThreads) lmax = max(lmax, tile_cost[b0 + i]);
+#pragma unroll
+  for (int k = 0; k < kBandRegs; k++) lmax = max(lmax, cst[k]);
+  for (int i = tid + kBandRegs * kOrderThreads; i < seg; i += kOrderThreads)
+    lmax = max(lmax, tile_cost[b0 + i]);
   lmax = wave_max(lmax);
   if ((tid & 63) == 0) atomicMax(&maxc, lmax);
   __syncthreads();
+  if (stop_after == 2) return;
   const unsigned long long mc = (unsigned long long)maxc + 1;
   auto bucket_of = [mc](uint32_t c) { return 255u - (unsigned)(((unsigned long long)c * 256u) / mc); };
-  for (int i = tid; i < seg; i += kOrderThreads) atomicAdd(&hist[bucket_of(tile_cost[b0 + i])], 1u);
+#pragma unroll
+  for (int k = 0; k < kBandRegs; k++)
+    if (tid + k * kOrderThreads < seg) atomicAdd(&hist[bucket_of(cst[k])], 1u);
+  for (int i = tid + kBandRegs * kOrderThreads; i < seg; i += kOrderThreads)
+    atomicAdd(&hist[bucket_of(tile_cost[b0 + i])], 1u);
   __syncthreads();
+  if (stop_after == 3) return;
   if (tid < 64) {   // exclusive scan of the 256 counts by one wave (4 per lane)
     const unsigned h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2],
                    h3 = hist[4 * tid + 3];
@@ -660,9 +710,15 @@ tile_epilogue_kernel(uint32_t* __restrict__ tile_cost, unsigned long long* __res
     start[4 * tid + 3] = ex;
   }
   __syncthreads();
-  for (int i = tid; i < seg; i += kOrderThreads)
+#pragma unroll
+  for (int k = 0; k < kBandRegs; k++) {
+    const int i = tid + k * kOrderThreads;
+    if (i < seg) sorted[atomicAdd(&start[bucket_of(cst[k])], 1u)] = b0 + i;
+  }
+  for (int i = tid + kBandRegs * kOrderThreads; i < seg; i += kOrderThreads)
     sorted[atomicAdd(&start[bucket_of(tile_cost[b0 + i])], 1u)] = b0 + i;
   __syncthreads();
+  if (stop_after == 4) return;
   const int nquad = (int)(((long long)seg * quad_pct) / 100);
   const int nent = keep > 0 ? min(seg + 3 * nquad, keep) : seg + 3 * nquad;
   for (int e = tid; e < slots_per_band; e += kOrderThreads) {
@@ -746,10 +802,11 @@ hipError_t launch_tile_epilogue(uint32_t* tile_cost, unsigned long long* tile_sa
   const int max_seg = plan.max_seg;
   if (tile_cost && (max_seg > kMaxBandTiles || max_seg < (plan.ntiles + 7) / 8))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tile_epilogue_kernel, dim3(8), dim3(kOrderThreads),
-                     tile_cost ? (size_t)max_seg * sizeof(int) : 0, s, tile_cost, tile_samples,
+  const size_t lds = tile_cost ? (size_t)((plan.ntiles + 63) >> 6) * 8 + (size_t)max_seg * sizeof(int)
+                              : 0;
+  hipLaunchKernelGGL(tile_epilogue_kernel, dim3(8), dim3(kOrderThreads), lds, s, tile_cost, tile_samples,
                      total, plan.ntiles, plan.quad_pct, plan.order_slots / 8, max_seg, plan.keep,
-                     order);
+                     plan.epi_stop, order);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !tile_cost) return e;
   // quad quarters atomicMax into tile_cost: it must start the next frame at zero

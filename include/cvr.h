@@ -132,6 +132,13 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                priority (with tile_order 1; default 5)
  *   "quad"       percent of each band's longest tiles marched sample-parallel, four
  *                lanes per ray (with tile_order 1; default 0)
+ *   "order_interval" rebuild the LPT order every n-th frame (default 8; costs
+ *                drift slowly, a rebuild costs ~15 us on the frame's stream)
+ *   "async_order" 1: rebuild it on a side stream instead, used 3 frames later
+ *                (default 0: cross-stream events cost more than they save)
+ *   "macro"      empty-space skipping: log2 of the macro cell (2..6, default 3;
+ *                0 off); compiled in only when >= "skip_min_pct" % (default 15)
+ *                of the macro cells are empty for the current volume and TF
  *   "tile_stats" 1: record per-tile timing of every frame (diagnostics)
  *   "kernel_timing" N > 0: time the ray-march kernel of the last N frames
  *                (cvr_read_kernel_times); 0 off (default) */

@@ -230,6 +230,9 @@ SCHEDULES = [
     dict(tile_order=1, batch=4, macro=3, skip_min_pct=0),
     dict(tile_order=0, batch=2, macro=2, skip_min_pct=0),
     dict(tile_order=1, batch=4, macro=5, skip_min_pct=0, quad=10),
+    # order built on a side stream (lag 3) / rebuilt every frame
+    dict(tile_order=1, batch=4, async_order=1, quad=10),
+    dict(tile_order=1, batch=2, order_interval=1, boost=0),
 ]
 
 
@@ -251,10 +254,11 @@ def test_schedules_bitexact(oracle, bonsai_tf, name, sched):
                                            c["H"], **kw)
     d = Device(0)
     try:
-        for k in ("tile_order", "quad", "boost", "batch", "macro", "skip_min_pct"):
+        for k in ("tile_order", "quad", "boost", "batch", "macro", "skip_min_pct", "async_order",
+                  "order_interval"):
             if k in opts:
                 N.check(N.lib().cvr_set_option(d.handle, k.encode(), opts[k]), k)
-        for frame in range(3):
+        for frame in range(5):
             g_rgba, g_cnt, g_total = gpu_render(d, vol, c["scale"], bonsai_tf, cam, c["W"], c["H"],
                                                 set_data=(frame == 0), **kw)
             assert_bitexact(g_cnt, o_cnt, f"{name} frame {frame} counts")
@@ -276,7 +280,7 @@ def test_screen_tiles_with_quad_schedule(bonsai_tf, nranks, tile):
         tpr = T.max_tiles_per_rank(W, H, tile, nranks)
         packed_all = np.zeros((nranks, tpr, tile, tile, 4), np.float32)
         for r in range(nranks):
-            for rep in range(2):   # second pass runs with the learned order
+            for rep in range(4):   # the fourth pass runs with the learned order (lag 3)
                 rgba, cnt, _ = gpu_render(d, vol, D.voxel_scale(64), bonsai_tf, INITIAL, W, H,
                                           tile=tile, rank=r, nranks=nranks, set_data=False)
             packed_all[r, :rgba.shape[0]] = rgba

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of rc1pass kernel variants in ONE process, interleaved rounds
 (methodology rule 24).  Every variant's image is checked bit-equal to the first
-variant's.  Variant syntax: b<batch>o<tile_order>p<boost%>q<quad%>[c<tile_cost>][w<max waves/CU>][m<macro shift, 0 off>][s<skip_min_pct>], e.g. b4o1p5q0m3s0.
+variant's.  Variant syntax: b<batch>o<tile_order>p<boost%>q<quad%>[c<tile_cost>][w<max waves/CU>][m<macro shift, 0 off>][s<skip_min_pct>][a<async_order>][i<order_interval>], e.g. b4o1p5q0a0i4.
 Usage: python tools/ab_rc1pass.py [--size 512] [--res 1024] [--variants ...]"""
 import argparse
 import ctypes
@@ -20,11 +20,12 @@ from cpp_volume_rendering_amd.renderer import Camera, Device, build_tf_rgbt, mak
 
 
 def parse_variant(v):
-    m = re.fullmatch(r"(?:L1)?b(\d)o(\d)p(\d+)q(\d+)(?:c(\d))?(?:w(\d+))?(?:m(\d))?(?:s(\d+))?", v)
+    m = re.fullmatch(r"(?:L1)?b(\d)o(\d)p(\d+)q(\d+)(?:c(\d))?(?:w(\d+))?(?:m(\d))?(?:s(\d+))?(?:a(\d))?(?:i(\d+))?", v)
     if not m:
         raise ValueError(f"bad variant {v}")
     g = m.groups()
-    d = (-1, -1, -1, -1)   # tile_cost, max_waves_cu, macro, skip_min_pct (-1: library default)
+    d = (-1, -1, -1, -1, -1, -1)   # tile_cost, max_waves_cu, macro, skip_min_pct, async_order,
+                                   # order_interval (-1: library default)
     return tuple(int(x) for x in g[:4]) + tuple(int(x) if x is not None else dflt
                                                 for x, dflt in zip(g[4:], d))
 
@@ -54,7 +55,8 @@ def main():
     dev.set_stream(s.cuda_stream)
     # library defaults, restored for the options a variant leaves unspecified
     defaults = {k: L0.cvr_get_option(dev.handle, k.encode())
-                for k in ("tile_cost", "max_waves_cu", "macro", "skip_min_pct")}
+                for k in ("tile_cost", "max_waves_cu", "macro", "skip_min_pct", "async_order",
+                          "order_interval")}
     frame = make_frame(Camera(**D.INITIAL_STATE_CAMERA), W, W)
     p = N.Rc1passParams()
     p.apply_gradient_shading = int(a.phong)
@@ -77,13 +79,14 @@ def main():
     S = None
     for _ in range(a.rounds):
         for v in variants:
-            b, o, boost, quad, cost, mw, macro, skip = parsed[v]
+            b, o, boost, quad, cost, mw, macro, skip, asy, oint = parsed[v]
             N.check(L.cvr_set_option(dev.handle, b"batch", b), "opt")
             N.check(L.cvr_set_option(dev.handle, b"tile_order", o), "opt")
             N.check(L.cvr_set_option(dev.handle, b"boost", boost), "opt")
             N.check(L.cvr_set_option(dev.handle, b"quad", quad), "opt")
             for key, val in (("tile_cost", cost), ("max_waves_cu", mw), ("macro", macro),
-                             ("skip_min_pct", skip)):
+                             ("skip_min_pct", skip), ("async_order", asy),
+                             ("order_interval", oint)):
                 N.check(L.cvr_set_option(dev.handle, key.encode(),
                                          val if val >= 0 else defaults[key]), key)
             with torch.cuda.stream(s):
