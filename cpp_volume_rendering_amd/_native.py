@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "cvr_set_transfer_function", "cvr_set_gradient", "cvr_device_bytes", "cvr_tiles_for_rank",
     "cvr_render_rc1pass", "cvr_unpack_tiles_device", "cvr_copy_tile_stats", "cvr_read_kernel_times", "cvr_camera_lookat", "cvr_default_step",
     "cvr_tf1d_build_rgbt", "cvr_read_tf1d", "cvr_read_raw", "cvr_read_syn",
-    "cvr_read_camera_state", "cvr_read_light_position",
+    "cvr_read_camera_state", "cvr_read_light_position", "cvr_build_cone_tables",
 )
 
 
@@ -60,6 +60,22 @@ class Rc1passParams(ctypes.Structure):
                 ("ka", ctypes.c_float), ("kd", ctypes.c_float), ("ks", ctypes.c_float),
                 ("shininess", ctypes.c_float), ("ispecular", ctypes.c_float * 3),
                 ("light_pos", ctypes.c_float * 3)]
+
+
+MAX_CONE_SECTIONS = 1024
+
+
+class ConeParams(ctypes.Structure):
+    _fields_ = [("half_angle_deg", ctypes.c_float), ("max_packing", ctypes.c_int),
+                ("covered_distance", ctypes.c_float), ("ui_weight", ctypes.c_float),
+                ("initial_step", ctypes.c_float)]
+
+
+class ConeTables(ctypes.Structure):
+    _fields_ = [("n_sections", ctypes.c_int), ("counts", ctypes.c_int * 3),
+                ("initial_step", ctypes.c_float), ("ray7_adj_weight", ctypes.c_float),
+                ("ui_weight", ctypes.c_float), ("axes", (ctypes.c_float * 3) * 10),
+                ("sections", (ctypes.c_float * 4) * MAX_CONE_SECTIONS)]
 
 
 _lib = None
@@ -114,6 +130,7 @@ def lib() -> ctypes.CDLL:
         "cvr_read_camera_state": ([ctypes.c_char_p, I, ctypes.POINTER(Camera), ctypes.c_char_p,
                                    I, IP], I),
         "cvr_read_light_position": ([ctypes.c_char_p, I, I, FP, IP], I),
+        "cvr_build_cone_tables": ([ctypes.POINTER(ConeParams), F, ctypes.POINTER(ConeTables)], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

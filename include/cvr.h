@@ -112,6 +112,33 @@ typedef struct cvr_rc1pass_params {
   float light_pos[3];          /* RenderingParameters::GetBlinnPhongLightingPosition */
 } cvr_rc1pass_params;
 
+/* Directional-occlusion cones (RC1PConeTracingDirOcclusionShading,
+ * cppvolrend/structured/rc1pdosct): the parameters of one ConeGaussianSampler
+ * (conegaussiansampler.h) and the tables the renderer uploads from it. */
+#define CVR_MAX_CONE_SECTIONS 1024
+typedef struct cvr_cone_params {
+  float half_angle_deg;    /* SetConeHalfAngle (clamped to [0.5, 89.5]); occlusion 20, shadow 0.5 */
+  int   max_packing;       /* SetMaxGaussianPacking: 0 = 1 ray, 1 = 3 rays, 2 = 7 rays
+                              (occlusion 1, shadow 0; dosrcrenderer.cpp:47-58)            */
+  float covered_distance;  /* SetCoveredDistance (>= 10); <= 0 at render: diagonal * 0.50
+                              (occlusion) / 0.75 (shadow), dosrcrenderer.cpp:112-113      */
+  float ui_weight;         /* SetUIWeightPercentage; occlusion 0.35, shadow 1.0           */
+  float initial_step;      /* <= 0: 3.0 (the sampler's default)                           */
+} cvr_cone_params;
+
+typedef struct cvr_cone_tables {
+  int   n_sections;        /* sections below                                            */
+  int   counts[3];         /* gaussian_samples_1 / _3 / _7                               */
+  float initial_step;      /* Occ/SdwInitialStep                                         */
+  float ray7_adj_weight;   /* (float)GetRay7AdjacentWeight                               */
+  float ui_weight;         /* Occ/SdwUIWeight                                            */
+  float axes[10][3];       /* Get3ConeRayID(0..2), Get7ConeRayID(0..6)                   */
+  float sections[CVR_MAX_CONE_SECTIONS][4];
+                           /* per section (interval distance, mip level, d_integral,
+                              amplitude) as floats, before the RGBA16F upload
+                              (GetConeSectionsInfoTex, conegaussiansampler.cpp:179-205) */
+} cvr_cone_tables;
+
 /* ----------------------------------------------------------------------------
  * Context
  * -------------------------------------------------------------------------- */
@@ -203,6 +230,12 @@ cvr_status  cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* 
  * Host-side helpers (native replacements for the reference's MSVC-only
  * readers and its CPU table builders).  They touch no device.
  * -------------------------------------------------------------------------- */
+/* ConeGaussianSampler::ComputeConeIntegrationSteps + ComputeAdditionalInfo
+ * (conegaussiansampler.cpp:212-414) for one cone; sigma0 = the extinction
+ * volume's base Gaussian sigma (ExtinctionCoefficientVolume default 1). */
+cvr_status  cvr_build_cone_tables(const cvr_cone_params* params, float sigma0,
+                                  cvr_cone_tables* out);
+
 /* Derived render constants, exposed for testing: the view matrix the ray
  * generator uses (glm::lookAt, column-major 4x4) and tan(fovy/2). */
 cvr_status  cvr_camera_lookat(const cvr_camera* cam, float out_view[16], float* out_tan_half_fovy);

@@ -16,7 +16,11 @@ out = subprocess.run([os.path.join(ROOT, "oracle", "_ref", "ref_golden"),
                       os.path.join(REF, "data", "#list_camera_states")],
                      check=True, capture_output=True, text=True).stdout
 data = json.loads(out[out.index("{"):])
-data["_generator"] = "oracle/ref/ref_golden.cpp linked with the reference's own sources"
+cones = subprocess.run([os.path.join(ROOT, "oracle", "_ref", "ref_cones")],
+                       check=True, capture_output=True, text=True).stdout
+data["cones"] = json.loads(cones[cones.index("{"):])
+data["_generator"] = ("oracle/ref/ref_golden.cpp and ref_cones.cpp linked with the "
+                      "reference's own sources")
 with open(os.path.join(ROOT, "tests", "golden", "ref_vectors.json"), "w") as f:
     json.dump(data, f)
 print("wrote tests/golden/ref_vectors.json:", sorted(data))
