@@ -29,7 +29,8 @@ EXPORTED_SYMBOLS = (
     "cvr_set_transfer_function", "cvr_set_gradient", "cvr_device_bytes", "cvr_tiles_for_rank",
     "cvr_render_rc1pass", "cvr_unpack_tiles_device", "cvr_copy_tile_stats", "cvr_read_kernel_times", "cvr_camera_lookat", "cvr_default_step",
     "cvr_tf1d_build_rgbt", "cvr_read_tf1d", "cvr_read_raw", "cvr_read_syn",
-    "cvr_read_camera_state", "cvr_read_light_position", "cvr_build_cone_tables",
+    "cvr_read_camera_state", "cvr_read_light_position", "cvr_read_light", "cvr_build_cone_tables",
+    "cvr_set_extinction_volume", "cvr_copy_extinction_level", "cvr_render_dosct",
 )
 
 
@@ -76,6 +77,21 @@ class ConeTables(ctypes.Structure):
                 ("initial_step", ctypes.c_float), ("ray7_adj_weight", ctypes.c_float),
                 ("ui_weight", ctypes.c_float), ("axes", (ctypes.c_float * 3) * 10),
                 ("sections", (ctypes.c_float * 4) * MAX_CONE_SECTIONS)]
+
+
+class Light(ctypes.Structure):
+    _fields_ = [("position", ctypes.c_float * 3), ("forward", ctypes.c_float * 3),
+                ("up", ctypes.c_float * 3), ("right", ctypes.c_float * 3),
+                ("spot_angle_deg", ctypes.c_float)]
+
+
+class DosParams(ctypes.Structure):
+    _fields_ = [("step", ctypes.c_float), ("apply_gradient_shading", ctypes.c_int),
+                ("ka", ctypes.c_float), ("kd", ctypes.c_float), ("ks", ctypes.c_float),
+                ("shininess", ctypes.c_float), ("ispecular", ctypes.c_float * 3),
+                ("light", Light), ("apply_occlusion", ctypes.c_int),
+                ("apply_shadow", ctypes.c_int), ("shadow_type", ctypes.c_int),
+                ("occlusion", ConeParams), ("shadow", ConeParams)]
 
 
 _lib = None
@@ -130,7 +146,12 @@ def lib() -> ctypes.CDLL:
         "cvr_read_camera_state": ([ctypes.c_char_p, I, ctypes.POINTER(Camera), ctypes.c_char_p,
                                    I, IP], I),
         "cvr_read_light_position": ([ctypes.c_char_p, I, I, FP, IP], I),
+        "cvr_read_light": ([ctypes.c_char_p, I, I, ctypes.POINTER(Light), IP], I),
         "cvr_build_cone_tables": ([ctypes.POINTER(ConeParams), F, ctypes.POINTER(ConeTables)], I),
+        "cvr_set_extinction_volume": ([P, FP, I, IP, F], I),
+        "cvr_copy_extinction_level": ([P, I, FP, IP, IP], I),
+        "cvr_render_dosct": ([P, ctypes.POINTER(Frame), ctypes.POINTER(DosParams),
+                              ctypes.POINTER(Output)], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -56,6 +56,11 @@ float half_round(float f) {
   _Float16 h = (_Float16)f;
   return (float)h;
 }
+float half_to_float_host(uint16_t b) {
+  _Float16 h;
+  std::memcpy(&h, &b, 2);
+  return (float)h;
+}
 
 struct V3 { float x, y, z; };
 inline V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
@@ -198,6 +203,9 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_macro_minmax; free_dev(p); c->d_macro_minmax = nullptr;
   p = c->d_occ; free_dev(p); c->d_occ = nullptr;
   p = c->d_tf_prefix; free_dev(p); c->d_tf_prefix = nullptr;
+  p = c->d_ext; free_dev(p); c->d_ext = nullptr;
+  p = c->d_cones; free_dev(p); c->d_cones = nullptr;
+  delete[] c->cone_tab;
   p = c->d_total; free_dev(p); c->d_total = nullptr;
   free_dev(c->d_scratch);
   if (c->side) (void)hipStreamSynchronize(c->side);
@@ -389,6 +397,8 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
   { void* p = c->d_occ; free_dev(p); c->d_occ = nullptr; }
   c->mm_shift = -1;
   c->occ_valid = 0;
+  { void* p = c->d_ext; free_dev(p); c->d_ext = nullptr; c->ext_levels = 0; }
+  c->cone_valid = 0;
   HIP_TRY(c, hipMalloc((void**)&c->d_lut, nv * sizeof(uint16_t)));
   uint16_t* d_lut = c->d_lut;
   hipError_t e = hipMemcpyAsync(d_lut, lut.data(), nv * sizeof(uint16_t), hipMemcpyHostToDevice,
@@ -523,24 +533,11 @@ static cvr_status ensure_occupancy(Ctx* c) {
   return CVR_OK;
 }
 
-cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pass_params* p,
-                              const cvr_output* o) {
-  Ctx* c = reinterpret_cast<Ctx*>(ctx);
-  if (!c) return CVR_ERR_ARG;
-  if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: null argument");
-  if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
-    return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: bad viewport %dx%d", f->width, f->height);
-  if (!c->d_cells) return fail(c, CVR_ERR_STATE, "cvr_render_rc1pass: no volume set");
-  if (!c->d_tf) return fail(c, CVR_ERR_STATE, "cvr_render_rc1pass: no transfer function set");
-  const bool phong = p->apply_gradient_shading != 0;
-  if (phong && !c->d_grad)
-    return fail(c, CVR_ERR_STATE, "cvr_render_rc1pass: gradient shading needs cvr_set_gradient");
-  const bool packed = f->nranks > 1;
-  if (packed && (f->tile_size < 16 || f->tile_size % 16 != 0 || f->rank < 0 || f->rank >= f->nranks))
-    return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: bad tiling (tile %d, rank %d/%d)",
-                f->tile_size, f->rank, f->nranks);
-
-  cvr::Rc1passArgs A{};
+// Camera, volume and tiling constants of one frame (shared by every renderer):
+// ray generation (glm lookAt + tan(fovy/2)), VolumeGridSize, step, TF size, and
+// the 8x8 wave tiles of the whole image or of this rank's packed tiles.
+static void fill_frame_args(Ctx* c, const cvr_frame* f, float step, cvr::Rc1passArgs& A,
+                            int& ntiles, size_t& npix) {
   float V[16], tanh;
   cvr_camera_lookat(&f->camera, V, &tanh);
   for (int i = 0; i < 3; i++) {
@@ -561,18 +558,14 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     A.N[i] = c->N[i];
   }
   A.cells = c->cells;
-  A.step = p->step > 0 ? p->step : cvr_default_step(c->scale);
+  A.step = step > 0 ? step : cvr_default_step(c->scale);
   A.tf_n = c->tf_n;
   // Sample opacity: a TF lerp lies within [0, max alpha] up to an ulp, and h <= step.
   const double ext = (double)c->tf_max_alpha * (double)A.step * (1.0 + 1.0 / 1024.0);
   A.exp_fast = (ext >= 0.0 && ext <= 86.0) ? 1 : 0;
-  A.ka = p->ka; A.kd = p->kd; A.ks = p->ks; A.shininess = p->shininess;
-  for (int i = 0; i < 3; i++) { A.ispec[i] = p->ispecular[i]; A.light[i] = p->light_pos[i]; }
-  cvr::RenderPlan plan{};
-  size_t npix;
-  if (!packed) {
+  if (f->nranks <= 1) {
     A.packed = 0;
-    plan.ntiles = ((f->width + 7) / 8) * ((f->height + 7) / 8);
+    ntiles = ((f->width + 7) / 8) * ((f->height + 7) / 8);
     npix = (size_t)f->width * f->height;
   } else {
     A.packed = 1;
@@ -580,10 +573,35 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     A.ntx = (f->width + f->tile_size - 1) / f->tile_size;
     A.my_tiles = cvr_tiles_for_rank(f, f->rank);
     const int s8 = f->tile_size / 8;
-    plan.ntiles = A.my_tiles * s8 * s8;
+    ntiles = A.my_tiles * s8 * s8;
     npix = (size_t)A.my_tiles * f->tile_size * f->tile_size;
   }
-  A.ntiles = plan.ntiles;
+  A.ntiles = ntiles;
+}
+
+cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pass_params* p,
+                              const cvr_output* o) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: null argument");
+  if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
+    return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: bad viewport %dx%d", f->width, f->height);
+  if (!c->d_cells) return fail(c, CVR_ERR_STATE, "cvr_render_rc1pass: no volume set");
+  if (!c->d_tf) return fail(c, CVR_ERR_STATE, "cvr_render_rc1pass: no transfer function set");
+  const bool phong = p->apply_gradient_shading != 0;
+  if (phong && !c->d_grad)
+    return fail(c, CVR_ERR_STATE, "cvr_render_rc1pass: gradient shading needs cvr_set_gradient");
+  const bool packed = f->nranks > 1;
+  if (packed && (f->tile_size < 16 || f->tile_size % 16 != 0 || f->rank < 0 || f->rank >= f->nranks))
+    return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: bad tiling (tile %d, rank %d/%d)",
+                f->tile_size, f->rank, f->nranks);
+
+  cvr::Rc1passArgs A{};
+  cvr::RenderPlan plan{};
+  size_t npix;
+  fill_frame_args(c, f, p->step, A, plan.ntiles, npix);
+  A.ka = p->ka; A.kd = p->kd; A.ks = p->ks; A.shininess = p->shininess;
+  for (int i = 0; i < 3; i++) { A.ispec[i] = p->ispecular[i]; A.light[i] = p->light_pos[i]; }
   A.tile_stats = nullptr;
   A.cost_time = c->cost_time;
   A.occ = nullptr;
@@ -773,6 +791,219 @@ cvr_status cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* f, const void*
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, cvr::launch_unpack_tiles((const float4*)d_packed, (float4*)d_rgba, f->width, f->height,
                                       f->tile_size, f->nranks, tpr_max, c->stream));
+  return CVR_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// Directional-occlusion shading (rc1pdosct)
+// ---------------------------------------------------------------------------
+
+cvr_status cvr_set_extinction_volume(cvr_ctx* ctx, const float* tf_rgba, int n, const int res_in[3],
+                                     float sigma0) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!tf_rgba || n < 2 || n > cvr::kMaxTfLds)
+    return fail(c, CVR_ERR_ARG, "cvr_set_extinction_volume: need 2 <= n <= 4096 TF entries");
+  if (!c->d_cells) return fail(c, CVR_ERR_STATE, "cvr_set_extinction_volume: no volume set");
+  int res[3] = {128, 128, 128};   // ExtinctionCoefficientVolume defaults (:10-15)
+  if (res_in)
+    for (int i = 0; i < 3; i++) res[i] = res_in[i];
+  for (int i = 0; i < 3; i++)
+    if (res[i] < 1 || res[i] > 4096) return fail(c, CVR_ERR_ARG, "cvr_set_extinction_volume: bad resolution");
+  if (!(sigma0 > 0.0f)) sigma0 = 1.0f;
+  int nl = 1;
+  for (int m = std::max(res[0], std::max(res[1], res[2])); m > 1; m >>= 1) nl++;
+  if (nl > cvr::kMaxExtLevels) return fail(c, CVR_ERR_ARG, "cvr_set_extinction_volume: too many levels");
+  long long off[cvr::kMaxExtLevels + 1] = {0};
+  for (int L = 0; L < nl; L++) {
+    long long v = 1;
+    for (int i = 0; i < 3; i++) v *= std::max(1, res[i] >> L);
+    off[L + 1] = off[L] + v;
+  }
+  // the RGBA16F opacity TF (GenerateTexture_1D_RGBA, transferfunction1d.cpp:58-87)
+  std::vector<float> q((size_t)n * 4);
+  for (size_t i = 0; i < q.size(); i++) q[i] = half_round(tf_rgba[i]);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  { void* p = c->d_ext; free_dev(p); c->d_ext = nullptr; c->ext_levels = 0; }
+  float4* d_tf = nullptr;
+  HIP_TRY(c, hipMalloc((void**)&d_tf, (size_t)n * 16));
+  hipError_t e = hipMemcpy(d_tf, q.data(), (size_t)n * 16, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_ext, (size_t)off[nl] * sizeof(uint16_t));
+  if (e == hipSuccess) e = cvr::launch_ext_volume(*c, d_tf, n, res, sigma0, nl, off, c->d_ext, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_tf);
+  if (e != hipSuccess) {
+    void* p = c->d_ext; free_dev(p); c->d_ext = nullptr;
+    return fail(c, e == hipErrorOutOfMemory ? CVR_ERR_OOM : CVR_ERR_HIP,
+                "cvr_set_extinction_volume: %s", hipGetErrorString(e));
+  }
+  for (int i = 0; i < 3; i++) c->ext_res[i] = res[i];
+  c->ext_levels = nl;
+  for (int L = 0; L <= nl; L++) c->ext_off[L] = off[L];
+  c->ext_sigma0 = sigma0;
+  c->cone_valid = 0;
+  return CVR_OK;
+}
+
+cvr_status cvr_copy_extinction_level(cvr_ctx* ctx, int level, float* out, int dims[3],
+                                     int* n_levels) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (n_levels) *n_levels = c->ext_levels;
+  if (!c->d_ext) return fail(c, CVR_ERR_STATE, "cvr_copy_extinction_level: no extinction volume");
+  if (level < 0 || level >= c->ext_levels) return fail(c, CVR_ERR_ARG, "cvr_copy_extinction_level: bad level");
+  int d[3];
+  for (int i = 0; i < 3; i++) d[i] = std::max(1, c->ext_res[i] >> level);
+  if (dims) for (int i = 0; i < 3; i++) dims[i] = d[i];
+  if (!out) return CVR_OK;
+  const size_t nv = (size_t)d[0] * d[1] * d[2];
+  std::vector<uint16_t> h(nv);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpy(h.data(), c->d_ext + c->ext_off[level], nv * 2, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < nv; i++) out[i] = half_to_float_host(h[i]);
+  return CVR_OK;
+}
+
+static bool same_cone(const cvr_cone_params& a, const cvr_cone_params& b) {
+  return std::memcmp(&a, &b, sizeof(a)) == 0;
+}
+
+cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_params* p,
+                            const cvr_output* o) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_dosct: null argument");
+  if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
+    return fail(c, CVR_ERR_ARG, "cvr_render_dosct: bad viewport %dx%d", f->width, f->height);
+  if (!c->d_cells || !c->d_tf) return fail(c, CVR_ERR_STATE, "cvr_render_dosct: no volume or TF");
+  if (!c->d_ext) return fail(c, CVR_ERR_STATE, "cvr_render_dosct: needs cvr_set_extinction_volume");
+  const bool phong = p->apply_gradient_shading != 0;
+  if (phong && !c->d_grad) return fail(c, CVR_ERR_STATE, "cvr_render_dosct: Phong needs cvr_set_gradient");
+  if (p->shadow_type < 0 || p->shadow_type > 2) return fail(c, CVR_ERR_ARG, "cvr_render_dosct: bad shadow type");
+  if (f->nranks > 1 && (f->tile_size < 16 || f->tile_size % 16 != 0 || f->rank < 0 || f->rank >= f->nranks))
+    return fail(c, CVR_ERR_ARG, "cvr_render_dosct: bad tiling");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+
+  // cone tables: covered distance <= 0 -> the volume diagonal * 0.50 / 0.75
+  // (GetDiagonal in double, dosrcrenderer.cpp:112-113)
+  cvr_cone_params cp[2] = {p->occlusion, p->shadow};
+  {
+    double vw = c->N[0] * (double)c->scale[0], vh = c->N[1] * (double)c->scale[1],
+           vd = c->N[2] * (double)c->scale[2];
+    const double diag = std::sqrt(vw * vw + vh * vh + vd * vd);
+    if (!(cp[0].covered_distance > 0.0f)) cp[0].covered_distance = (float)(diag * 0.50f);
+    if (!(cp[1].covered_distance > 0.0f)) cp[1].covered_distance = (float)(diag * 0.75f);
+  }
+  if (!c->cone_valid || !same_cone(cp[0], c->cone_key[0]) || !same_cone(cp[1], c->cone_key[1])) {
+    if (!c->cone_tab) c->cone_tab = new cvr_cone_tables[2];
+    for (int k = 0; k < 2; k++) {
+      cvr_status st = cvr_build_cone_tables(&cp[k], c->ext_sigma0, &c->cone_tab[k]);
+      if (st != CVR_OK) return fail(c, st, "cvr_render_dosct: cone tables (%s)", k ? "shadow" : "occlusion");
+    }
+    std::vector<float> up(2 * CVR_MAX_CONE_SECTIONS * 4, 0.0f);
+    for (int k = 0; k < 2; k++)
+      for (int i = 0; i < c->cone_tab[k].n_sections; i++)
+        for (int j = 0; j < 4; j++)   // GetConeSectionsInfoTex uploads RGBA16F
+          up[((size_t)k * CVR_MAX_CONE_SECTIONS + i) * 4 + j] = half_round(c->cone_tab[k].sections[i][j]);
+    if (!c->d_cones) HIP_TRY(c, hipMalloc((void**)&c->d_cones, up.size() * sizeof(float)));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    HIP_TRY(c, hipMemcpy(c->d_cones, up.data(), up.size() * sizeof(float), hipMemcpyHostToDevice));
+    c->cone_key[0] = cp[0];
+    c->cone_key[1] = cp[1];
+    c->cone_valid = 1;
+  }
+
+  cvr::DosArgs Q{};
+  int ntiles = 0;
+  size_t npix = 0;
+  fill_frame_args(c, f, p->step, Q.a, ntiles, npix);
+  Q.a.ka = p->ka;   // Phong ambient/diffuse/specular weights of the surface term
+  Q.a.kd = p->kd;
+  Q.a.ks = p->ks;
+  Q.a.shininess = p->shininess;
+  for (int i = 0; i < 3; i++) { Q.a.ispec[i] = p->ispecular[i]; Q.a.light[i] = p->light.position[i]; }
+  for (int i = 0; i < 3; i++) Q.G[i] = (float)c->N[i] * c->scale[i];
+  Q.ext_levels = c->ext_levels;
+  for (int L = 0; L < c->ext_levels; L++) {
+    for (int i = 0; i < 3; i++) Q.ext_dim[L][i] = std::max(1, c->ext_res[i] >> L);
+    Q.ext_off[L] = c->ext_off[L];
+  }
+  Q.apply_occlusion = p->apply_occlusion != 0;
+  Q.apply_shadow = p->apply_shadow != 0;
+  Q.shadow_type = p->shadow_type;
+  Q.phong = phong;
+  // ShadeSample (:607-656): ka only with occlusion, kd/ks only with shadows
+  Q.ka = Q.apply_occlusion ? p->ka : 0.0f;
+  Q.kd = Q.apply_shadow ? p->kd : 0.0f;
+  Q.ks = Q.apply_shadow ? p->ks : 0.0f;
+  for (int i = 0; i < 3; i++) {
+    Q.lfwd[i] = p->light.forward[i];
+    Q.lup[i] = p->light.up[i];
+    Q.lright[i] = p->light.right[i];
+  }
+  // SpotLightMaxAngle: glm::cos(glm::pi<float>() * angle / 180.f) (dosrcrenderer.cpp:158)
+  Q.spot_cos = std::cos(3.14159265358979323846f * p->light.spot_angle_deg / 180.0f);
+  for (int k = 0; k < 2; k++) {
+    cvr::DosCone& C = k ? Q.sdw : Q.occ;
+    const cvr_cone_tables& T = c->cone_tab[k];
+    for (int i = 0; i < 3; i++) C.counts[i] = T.counts[i];
+    C.initial_step = T.initial_step;
+    C.ray7w = T.ray7_adj_weight;
+    C.ui_weight = T.ui_weight;
+    for (int i = 0; i < 10; i++)
+      for (int j = 0; j < 3; j++) C.axes[3 * i + j] = T.axes[i][j];
+    C.sections = c->d_cones + (size_t)k * CVR_MAX_CONE_SECTIONS;
+  }
+
+  float4* d_out;
+  uint32_t* d_samples;
+  unsigned long long* d_total;
+  const size_t rgba_bytes = npix * 16, smp_bytes = npix * 4;
+  if (o->on_device) {
+    d_out = (float4*)o->rgba;
+    d_samples = (uint32_t*)o->samples;
+    d_total = (unsigned long long*)o->total;
+  } else {
+    cvr_status st = ensure_scratch(c, rgba_bytes + (o->samples ? smp_bytes : 0));
+    if (st != CVR_OK) return st;
+    d_out = (float4*)c->d_scratch;
+    d_samples = o->samples ? (uint32_t*)((char*)c->d_scratch + rgba_bytes) : nullptr;
+    d_total = o->total ? c->d_total : nullptr;
+  }
+  if (d_total && !o->on_device) HIP_TRY(c, hipMemsetAsync(d_total, 0, sizeof(unsigned long long), s));
+  unsigned long long* tile_samples = nullptr;
+  if (d_total) {
+    if (c->tile_samples_n < ntiles) {
+      void* q = c->d_tile_samples; free_dev(q); c->d_tile_samples = nullptr; c->tile_samples_n = 0;
+      HIP_TRY(c, hipMalloc((void**)&c->d_tile_samples, (size_t)ntiles * 8));
+      HIP_TRY(c, hipMemsetAsync(c->d_tile_samples, 0, (size_t)ntiles * 8, s));
+      c->tile_samples_n = ntiles;
+    }
+    tile_samples = c->d_tile_samples;
+  }
+  const size_t nev = c->ev_start.size();
+  const size_t slot = nev ? (size_t)(c->timed_frames % (long long)nev) : 0;
+  if (nev) HIP_TRY(c, hipEventRecord(c->ev_start[slot], s));
+  HIP_TRY(c, cvr::launch_dos(*c, Q, d_out, d_samples, tile_samples, s));
+  if (nev) {
+    HIP_TRY(c, hipEventRecord(c->ev_stop[slot], s));
+    c->timed_frames++;
+  }
+  if (tile_samples) {
+    cvr::RenderPlan plan{};
+    plan.ntiles = ntiles;
+    HIP_TRY(c, cvr::launch_tile_epilogue(nullptr, tile_samples, d_total, plan, nullptr, s));
+  }
+  if (!o->on_device) {
+    HIP_TRY(c, hipMemcpyAsync(o->rgba, d_out, rgba_bytes, hipMemcpyDeviceToHost, s));
+    if (o->samples) HIP_TRY(c, hipMemcpyAsync(o->samples, d_samples, smp_bytes, hipMemcpyDeviceToHost, s));
+    if (o->total) HIP_TRY(c, hipMemcpyAsync(o->total, d_total, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
   return CVR_OK;
 }
 

@@ -39,15 +39,12 @@ __device__ __forceinline__ float cvr_expf(float x) {
   return ldexpf(y, (int)n);
 }
 
-// pow(x, y) for x >= 0, CVR-SPEC (identical to oracle cvr_powf)
-__device__ __forceinline__ float cvr_powf(float x, float y) {
-  if (x != x || y != y) return x + y;
-  if (!(x > 0.0f) || x < 1.17549435e-38f) {
-    if (y > 0.0f) return 0.0f;
-    if (y == 0.0f) return 1.0f;
-    return __builtin_inff();
-  }
-  if (x == __builtin_inff()) return y > 0.0f ? __builtin_inff() : (y == 0.0f ? 1.0f : 0.0f);
+// ln(x), CVR-SPEC (identical to oracle cvr_logf): Cephes logf polynomial.
+__device__ __forceinline__ float cvr_logf(float x) {
+  if (x != x) return x;
+  if (x < 0.0f) return __builtin_nanf("");
+  if (x < 1.17549435e-38f) return -__builtin_inff();
+  if (x == __builtin_inff()) return x;
   uint32_t bits = __float_as_uint(x);
   int e = (int)((bits >> 23) & 0xffu) - 126;
   float m = __uint_as_float((bits & 0x007fffffu) | 0x3f000000u);
@@ -68,8 +65,19 @@ __device__ __forceinline__ float cvr_powf(float x, float y) {
   r = fmaf(fe, -2.12194440e-4f, r);
   r = fmaf(-0.5f, z, r);
   float lnx = f + r;
-  lnx = fmaf(fe, 0.693359375f, lnx);
-  return cvr_expf(y * lnx);
+  return fmaf(fe, 0.693359375f, lnx);
+}
+
+// pow(x, y) for x >= 0, CVR-SPEC (identical to oracle cvr_powf)
+__device__ __forceinline__ float cvr_powf(float x, float y) {
+  if (x != x || y != y) return x + y;
+  if (!(x > 0.0f) || x < 1.17549435e-38f) {
+    if (y > 0.0f) return 0.0f;
+    if (y == 0.0f) return 1.0f;
+    return __builtin_inff();
+  }
+  if (x == __builtin_inff()) return y > 0.0f ? __builtin_inff() : (y == 0.0f ? 1.0f : 0.0f);
+  return cvr_expf(y * cvr_logf(x));
 }
 
 struct f3 { float x, y, z; };

@@ -55,6 +55,30 @@ struct Rc1passArgs {
   int mshift;                        // macro cell = 2^mshift texels a side
 };
 
+constexpr int kMaxTfLds = 4096;          // TF entries a kernel stages into LDS
+constexpr int kMaxExtLevels = 16;        // extinction mip levels (up to 32768^3)
+
+// Directional-occlusion shading (dos.hip): one cone's tables on the device.
+struct DosCone {
+  int counts[3];                     // sections of 1, 3, 7 rays
+  float initial_step, ray7w, ui_weight;
+  float axes[30];                    // 3-ray then 7-ray axes (x, y, z)
+  const float4* sections;            // (interval, mip, d_integral, amplitude), fp16-rounded
+};
+
+struct DosArgs {
+  Rc1passArgs a;                     // ray, volume, TF, Blinn-Phong constants, tiles
+  float G[3];                        // VolumeScaledSizes
+  int ext_levels;
+  int ext_dim[kMaxExtLevels][3];
+  long long ext_off[kMaxExtLevels];  // element offset of each level
+  int apply_occlusion, apply_shadow, shadow_type, phong;
+  float ka, kd, ks;                  // Kambient if occlusion, Kdiffuse/Kspecular if shadow, else 0
+  float lfwd[3], lup[3], lright[3];  // light camera vectors (RenderingParameters)
+  float spot_cos;                    // SpotLightMaxAngle uniform
+  DosCone occ, sdw;
+};
+
 // How one frame is cut into work: one 8x8 wave tile per workgroup.
 struct RenderPlan {
   int ntiles;                        // 8x8 wave tiles (one workgroup each)
@@ -139,6 +163,17 @@ struct Ctx {
   hipStream_t side = nullptr;      // high-priority stream for the order builds
   hipEvent_t ev_frame = nullptr;   // end of a frame's ray-march (the side stream waits on it)
   int num_cus = 0;
+  // extinction-coefficient mip volume (directional occlusion)
+  uint16_t* d_ext = nullptr;       // fp16 levels, concatenated
+  int ext_res[3] = {0, 0, 0};
+  int ext_levels = 0;
+  long long ext_off[kMaxExtLevels + 1] = {};
+  float ext_sigma0 = 1.0f;
+  // cone tables on the device (occlusion, shadow), rebuilt when their params change
+  float4* d_cones = nullptr;
+  cvr_cone_params cone_key[2] = {};
+  int cone_valid = 0;
+  cvr_cone_tables* cone_tab = nullptr;   // host copies [2]
   unsigned long long* d_tile_samples = nullptr;   // per-wave-tile sample counts (zeroed)
   int tile_samples_n = 0;
   // scratch
@@ -163,6 +198,11 @@ hipError_t launch_macro_minmax(const Ctx& c, int shift, const int mdim[3], uint3
 hipError_t launch_occupancy(const uint32_t* minmax, int n_macro, const uint16_t* lut,
                             const int* prefix, int tf_n, uint8_t* occ, unsigned int* n_empty,
                             hipStream_t s);
+hipError_t launch_ext_volume(const Ctx& c, const float4* d_tf_rgba, int tf_n, const int res[3],
+                             float sigma0, int nlevels, const long long* off, uint16_t* d_ext,
+                             hipStream_t s);
+hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,
+                      unsigned long long* tile_samples, hipStream_t s);
 hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
                                int nranks, int tiles_per_rank_max, hipStream_t s);
 

@@ -172,8 +172,8 @@ cvr_status cvr_read_camera_state(const char* path, int index, cvr_camera* out_ca
 }
 
 // LightSourceList::ReadLightSourceLists (lightsourcelist.cpp:81-148)
-cvr_status cvr_read_light_position(const char* path, int list, int light, float out_pos[3],
-                                   int* out_count) {
+cvr_status cvr_read_light(const char* path, int list, int light, cvr_light* out,
+                          int* out_count) {
   if (!path) return CVR_ERR_ARG;
   std::ifstream f(path);
   if (!f.is_open()) return CVR_ERR_IO;
@@ -196,11 +196,28 @@ cvr_status cvr_read_light_position(const char* path, int list, int light, float 
     lists.push_back(lights);
   }
   if (out_count) *out_count = (int)lists.size();
-  if (!out_pos) return CVR_OK;
+  if (!out) return CVR_OK;
   if (list < 0 || list >= (int)lists.size() || light < 0 || light >= (int)lists[list].size())
     return CVR_ERR_ARG;
-  for (int i = 0; i < 3; i++) out_pos[i] = lists[list][light][i];
+  const std::vector<float>& v = lists[list][light];
+  // position, forward (stored as z_axis = -forward and read back negated), up, right, angle
+  for (int i = 0; i < 3; i++) {
+    out->position[i] = v[i];
+    out->forward[i] = v[3 + i];
+    out->up[i] = v[6 + i];
+    out->right[i] = v[9 + i];
+  }
+  out->spot_angle_deg = v[12];
   return CVR_OK;
+}
+
+cvr_status cvr_read_light_position(const char* path, int list, int light, float out_pos[3],
+                                   int* out_count) {
+  cvr_light l;
+  cvr_status st = cvr_read_light(path, list, light, out_pos ? &l : nullptr, out_count);
+  if (st == CVR_OK && out_pos)
+    for (int i = 0; i < 3; i++) out_pos[i] = l.position[i];
+  return st;
 }
 
 #pragma GCC visibility pop

@@ -1,0 +1,190 @@
+// march_common.h — device pieces shared by the ray-march kernels (rc1pass in
+// raymarch.hip, directional occlusion in dos.hip): tile decomposition, the
+// cell8 trilinear sample, TF classification, Blinn-Phong, ray setup, and the
+// LDS TF staging / wave reductions.  CVR-SPEC arithmetic.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "cvr_device.h"
+
+namespace cvr {
+
+// ---------------------------------------------------------------------------
+// Work decomposition
+// ---------------------------------------------------------------------------
+
+// Tile `t` (8x8 pixels), local pixel (lx, ly) -> pixel and output index.
+// Unpacked: tiles are row-major over the (W/8)x(H/8) grid.  Packed (screen
+// split): tile t = k*(T/8)^2 + j is sub-tile j of this rank's k-th TxT tile.
+__device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lx, int ly, int& px,
+                                           int& py, long long& out_idx) {
+  if (!A.packed) {
+    const int ntx8 = (A.W + 7) >> 3;
+    const int ty = t / ntx8, tx = t - ty * ntx8;
+    px = (tx << 3) | lx;
+    py = (ty << 3) | ly;
+    out_idx = (long long)py * A.W + px;
+  } else {
+    const int s = A.tile >> 3;               // 8x8 sub-tiles per tile row
+    const int k = t / (s * s), j = t - k * s * s;
+    const int g = A.rank + k * A.nranks;     // global tile index
+    const int gy = g / A.ntx, gx = g - gy * A.ntx;
+    const int ox = ((j % s) << 3) | lx, oy = ((j / s) << 3) | ly;
+    px = gx * A.tile + ox;
+    py = gy * A.tile + oy;
+    out_idx = (long long)k * A.tile * A.tile + (long long)oy * A.tile + ox;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Sampling
+// ---------------------------------------------------------------------------
+
+// One sample's cell address + weights.  Texel coordinates are clamped to
+// [0, N-1]: under CLAMP_TO_EDGE a coordinate in [-1, 0) blends texel 0 with
+// itself and the clamped one weights texel 0 by exactly 1 — both give v0
+// bit-exactly (fmaf(a, 0, v0) = fmaf(0, d, v0) = v0 for v0 >= 0) — and with
+// x >= 0 the floor is the truncating convert and the weight one v_fract.
+struct SamplePos { uint32_t idx; float ax, ay, az; int ix, iy, iz; };
+
+__device__ __forceinline__ SamplePos sample_pos(float x, float y, float z, const Rc1passArgs& A) {
+  x = __builtin_amdgcn_fmed3f(x, 0.0f, A.nm1[0]);
+  y = __builtin_amdgcn_fmed3f(y, 0.0f, A.nm1[1]);
+  z = __builtin_amdgcn_fmed3f(z, 0.0f, A.nm1[2]);
+  SamplePos p;
+  p.ax = __builtin_amdgcn_fractf(x); p.ay = __builtin_amdgcn_fractf(y); p.az = __builtin_amdgcn_fractf(z);
+  p.ix = (int)x; p.iy = (int)y; p.iz = (int)z;
+  // cell (ix+1, iy+1, iz+1) of the (N+1)^3 x-fastest grid; the +1 offsets live
+  // in the base pointer
+  p.idx = __umul24((uint32_t)p.iz, (uint32_t)A.cells.pitch_z) +
+          __umul24((uint32_t)p.iy, (uint32_t)A.cells.pitch_y) + (uint32_t)p.ix;
+  return p;
+}
+
+// (float)hi - (float)lo of a packed fp16 pair, in ONE mixed-precision FMA
+// (hi * 1.0 + (-lo), computed exactly then rounded once = the fp32 subtraction
+// of the two exactly-converted halves).
+__device__ __forceinline__ float pair_diff(uint32_t w) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%1 op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(w));
+  return d;
+}
+
+// lerp(lo, hi, t) of a packed fp16 pair = fmaf(t, hi - lo, lo): two
+// v_fma_mix_f32, the second taking lo straight from the low half.
+__device__ __forceinline__ float pair_lerp(uint32_t w, float t) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(t), "v"(pair_diff(w)), "v"(w));
+  return r;
+}
+
+__device__ __forceinline__ float trilerp_cell(uint4 raw, float ax, float ay, float az) {
+  float c00 = pair_lerp(raw.x, ax);    // (v000, v100)
+  float c10 = pair_lerp(raw.y, ax);    // (v010, v110)
+  float c01 = pair_lerp(raw.z, ax);    // (v001, v101)
+  float c11 = pair_lerp(raw.w, ax);    // (v011, v111)
+  float c0 = lerpf(c00, c10, ay);
+  float c1 = lerpf(c01, c11, ay);
+  return lerpf(c0, c1, az);
+}
+
+// texture(TexTransferFunc, density) from the padded LDS table: x = d*n - 0.5
+// reads the adjacent entries tfp[floor(x)+1], tfp[floor(x)+2]; d in [0,1]
+// (a lerp of [0,1] values) keeps floor(x)+1 in [0, n].
+__device__ __forceinline__ float4 classify(const float4* __restrict__ tfp, float fn, float dens) {
+  float x = fmaf(dens, fn, -0.5f);
+  float fl = floorf(x);
+  float a = x - fl;
+  int i = (int)fl + 1;
+  float4 t0 = tfp[i], t1 = tfp[i + 1];
+  return make_float4(lerpf(t0.x, t1.x, a), lerpf(t0.y, t1.y, a), lerpf(t0.z, t1.z, a),
+                     lerpf(t0.w, t1.w, a));
+}
+
+// Blinn-Phong (ray_marching_1p.comp:48-81), CVR-SPEC arithmetic.
+__device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint2* __restrict__ grad,
+                                            const SamplePos& sp, f3 dir, float t, f3 tpos, f3 hg,
+                                            f3 eye, float4& src) {
+  Texel tx;
+  tx.ix = sp.ix; tx.iy = sp.iy; tx.iz = sp.iz;
+  tx.ax = sp.ax; tx.ay = sp.ay; tx.az = sp.az;
+  f3 g = sample_gradient(grad, A.N, tx);
+  if (g.x != 0.0f || g.y != 0.0f || g.z != 0.0f) {
+    f3 wp{fmaf(dir.x, t, tpos.x) - hg.x, fmaf(dir.y, t, tpos.y) - hg.y, fmaf(dir.z, t, tpos.z) - hg.z};
+    f3 n = normalize3(g);
+    f3 Ld = normalize3(f3{A.light[0] - wp.x, A.light[1] - wp.y, A.light[2] - wp.z});
+    f3 Ve = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
+    f3 Hv = normalize3(f3{Ve.x + Ld.x, Ve.y + Ld.y, Ve.z + Ld.z});
+    float dd = fmaxf(0.0f, dot3(n, Ld));
+    float ds = fmaxf(0.0f, dot3(Hv, n));
+    float pw = cvr_powf(ds, A.shininess);
+    float f = fmaf(A.kd, dd, A.ka);
+    src.x = fmaf(A.ispec[0] * A.ks, pw, src.x * f);
+    src.y = fmaf(A.ispec[1] * A.ks, pw, src.y * f);
+    src.z = fmaf(A.ispec[2] * A.ks, pw, src.z * f);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The ray
+// ---------------------------------------------------------------------------
+
+struct Ray {
+  f3 cam;                // camera_dir: normalize(d * mat3(View)) (normalised once)
+  f3 dir, tpos, o, dt;   // direction, entry point (texture space), texel-space origin/step
+  f3 inv_dt;             // 1 / dt (macro-cell exits)
+  float D;               // distance to evaluate, |tfar - tnear|
+};
+
+// Ray generation + slab test, ray_marching_1p.comp:93-121 and
+// ray_bbox_intersection.comp:18-52.  Returns false for a miss.
+__device__ __forceinline__ bool ray_setup(const Rc1passArgs& A, int px, int py, Ray& r) {
+  float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+  float vx = fmaf(fx / (float)A.W, 2.0f, -1.0f);
+  float vy = fmaf(fy / (float)A.H, 2.0f, -1.0f);
+  f3 c{(vx * A.tan_half_fovy) * A.aspect, vy * A.tan_half_fovy, -1.0f};
+  f3 d{dot3(c, f3{A.col0[0], A.col0[1], A.col0[2]}), dot3(c, f3{A.col1[0], A.col1[1], A.col1[2]}),
+       dot3(c, f3{A.col2[0], A.col2[1], A.col2[2]})};
+  const f3 cam = normalize3(d);
+  f3 dir = normalize3(cam);                // RayAABBIntersection normalises again (:219)
+  r.cam = cam;
+  f3 inv{1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z};
+  const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
+  const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
+  f3 ta{inv.x * (-hg.x - eye.x), inv.y * (-hg.y - eye.y), inv.z * (-hg.z - eye.z)};
+  f3 tb{inv.x * (hg.x - eye.x), inv.y * (hg.y - eye.y), inv.z * (hg.z - eye.z)};
+  float tnear = fmaxf(fmaxf(fminf(ta.x, tb.x), fminf(ta.y, tb.y)), fminf(ta.z, tb.z));
+  float tfar = fminf(fminf(fmaxf(ta.x, tb.x), fmaxf(ta.y, tb.y)), fmaxf(ta.z, tb.z));
+  bool hit = tfar > tnear;
+  tnear = fmaxf(tnear, 0.0f);
+  r.dir = dir;
+  r.D = fabsf(tfar - tnear);
+  r.tpos = f3{fmaf(dir.x, tnear, eye.x) + hg.x, fmaf(dir.y, tnear, eye.y) + hg.y,
+              fmaf(dir.z, tnear, eye.z) + hg.z};
+  r.o = f3{fmaf(r.tpos.x, A.n_over_g[0], -0.5f), fmaf(r.tpos.y, A.n_over_g[1], -0.5f),
+           fmaf(r.tpos.z, A.n_over_g[2], -0.5f)};
+  r.dt = f3{dir.x * A.n_over_g[0], dir.y * A.n_over_g[1], dir.z * A.n_over_g[2]};
+  if (A.occ) r.inv_dt = f3{1.0f / r.dt.x, 1.0f / r.dt.y, 1.0f / r.dt.z};
+  return hit;
+}
+
+__device__ __forceinline__ void load_tf_lds(float4* tfp, const float4* __restrict__ tf_g, int n) {
+  // Padded TF: tfp[k] = T[clamp(k-1, 0, n-1)], k in [0, n+1] (CLAMP_TO_EDGE folded in).
+  for (int i = threadIdx.x; i < n + 2; i += blockDim.x) tfp[i] = tf_g[min(max(i - 1, 0), n - 1)];
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t m) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+  return m;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+}  // namespace cvr

@@ -6,6 +6,9 @@ tests) read like the reference:
     RenderingManager::InitData  -> DataManager.read_* / RenderingParameters
     BaseVolumeRenderer          -> BaseVolumeRenderer   (cppvolrend/volrenderbase.h:25-96)
     RayCasting1Pass             -> RayCasting1Pass      (cppvolrend/structured/rc1pass/rc1prenderer.*)
+    RC1PConeTracingDirOcclusionShading
+                                -> RC1PConeTracingDirOcclusionShading
+                                                        (cppvolrend/structured/rc1pdosct/dosrcrenderer.*)
 
 Per frame: ``PrepareRender(camera)`` (calls ``Update`` when outdated) then
 ``Redraw()``, exactly as RenderingManager::Display does
@@ -60,6 +63,11 @@ class RenderingParameters:
     blinnphong_shininess: float = 30.0
     light_position: tuple = (-206.873, -51.0699, 557.011)   # data/#list_light_sources list 0
     light_specular: tuple = (1.0, 1.0, 1.0)                 # lightsourcelist.cpp:24
+    # the same light's camera frame and spot angle (LightSourceData, lightsourcelist.cpp:107-133)
+    light_forward: tuple = (-0.346883, -0.0856335, 0.933991)
+    light_up: tuple = (-0.0298143, 0.996327, 0.0802758)
+    light_right: tuple = (0.937434, -0.0, 0.348162)
+    spot_light_angle: float = 20.0
     camera: Camera = field(default_factory=Camera)
 
     def GetScreenWidth(self): return self.screen_width
@@ -67,6 +75,17 @@ class RenderingParameters:
     def GetCamera(self): return self.camera
     def GetBlinnPhongLightingPosition(self): return self.light_position
     def GetLightSourceSpecular(self): return self.light_specular
+    def GetBlinnPhongLightSourceCameraForward(self): return self.light_forward
+    def GetBlinnPhongLightSourceCameraUp(self): return self.light_up
+    def GetBlinnPhongLightSourceCameraRight(self): return self.light_right
+    def GetSpotLightMaxAngle(self): return self.spot_light_angle
+
+    def SetLight(self, light: "N.Light"):
+        self.light_position = tuple(light.position)
+        self.light_forward = tuple(light.forward)
+        self.light_up = tuple(light.up)
+        self.light_right = tuple(light.right)
+        self.spot_light_angle = float(light.spot_angle_deg)
 
 
 class DataManager:
@@ -76,6 +95,7 @@ class DataManager:
         self.volume: Optional[np.ndarray] = None    # (D, H, W) u8/u16, x fastest
         self.scale = (1.0, 1.0, 1.0)
         self.tf_rgbt: Optional[np.ndarray] = None  # (n, 4) float32: r, g, b, extinction
+        self.tf_rgba: Optional[np.ndarray] = None  # (n, 4) float32: r, g, b, opacity
         self.gradient_type = N.GRADIENT_NONE        # datamanager.cpp:27 (NONE by default)
         self.name = ""
 
@@ -87,11 +107,19 @@ class DataManager:
         self.scale = tuple(float(s) for s in scale)
         self.name = name
 
-    def SetTransferFunction(self, rgbt: np.ndarray):
+    def SetTransferFunction(self, rgbt: np.ndarray, rgba: Optional[np.ndarray] = None):
+        """rgbt: GenerateTexture_1D_RGBt (alpha as extinction, what the march samples);
+        rgba: GenerateTexture_1D_RGBA (alpha as opacity, what the extinction volume of
+        the occlusion renderer filters; transferfunction1d.cpp:58-87)."""
         rgbt = np.ascontiguousarray(rgbt, dtype=np.float32)
         if rgbt.ndim != 2 or rgbt.shape[1] != 4:
             raise ValueError("transfer function must be (n, 4) r, g, b, extinction")
         self.tf_rgbt = rgbt
+        if rgba is not None:
+            rgba = np.ascontiguousarray(rgba, dtype=np.float32)
+            if rgba.shape != rgbt.shape:
+                raise ValueError("RGBA transfer function must match the RGBt one")
+        self.tf_rgba = rgba
 
     def ReadVolume(self, path: str, scale=None):
         """.raw (name.<bytes>.<W>x<H>x<D>.raw) or .syn, like VolumeReader::ReadStructuredVolume."""
@@ -149,6 +177,14 @@ def read_camera_state(path: str, index: int = 0) -> Camera:
     N.check(N.lib().cvr_read_camera_state(path.encode(), index, c, name, 256, cnt),
             "cvr_read_camera_state")
     return Camera(tuple(c.eye), tuple(c.center), tuple(c.up), c.fovy_deg, 0.0)
+
+
+def read_light(path: str, list_index: int = 0, light: int = 0) -> N.Light:
+    out = N.Light()
+    cnt = ctypes.c_int()
+    N.check(N.lib().cvr_read_light(path.encode(), list_index, light, ctypes.byref(out), cnt),
+            "cvr_read_light")
+    return out
 
 
 def read_light_position(path: str, list_index: int = 0, light: int = 0):
@@ -213,6 +249,30 @@ class Device:
 
     def set_gradient(self, mode: int):
         N.check(N.lib().cvr_set_gradient(self.handle, int(mode)), "cvr_set_gradient", self.handle)
+
+    def set_extinction_volume(self, tf_rgba: np.ndarray, res=(128, 128, 128), sigma0: float = 1.0):
+        t = np.ascontiguousarray(tf_rgba, dtype=np.float32)
+        r = (ctypes.c_int * 3)(*[int(v) for v in res])
+        N.check(N.lib().cvr_set_extinction_volume(self.handle, N.fptr(t), t.shape[0], r,
+                                                  float(sigma0)),
+                "cvr_set_extinction_volume", self.handle)
+
+    def extinction_levels(self) -> list:
+        """Every level of the extinction pyramid as (d, h, w) float32 arrays."""
+        L = N.lib()
+        nl = ctypes.c_int()
+        dims = (ctypes.c_int * 3)()
+        N.check(L.cvr_copy_extinction_level(self.handle, 0, None, dims, nl),
+                "cvr_copy_extinction_level", self.handle)
+        out = []
+        for lv in range(nl.value):
+            N.check(L.cvr_copy_extinction_level(self.handle, lv, None, dims, None),
+                    "cvr_copy_extinction_level", self.handle)
+            a = np.zeros((dims[2], dims[1], dims[0]), np.float32)
+            N.check(L.cvr_copy_extinction_level(self.handle, lv, N.fptr(a), dims, None),
+                    "cvr_copy_extinction_level", self.handle)
+            out.append(a)
+        return out
 
     def device_bytes(self) -> int:
         return int(N.lib().cvr_device_bytes(self.handle))
@@ -366,6 +426,94 @@ class RayCasting1Pass(BaseVolumeRenderer):
             self._dev.close()
             self._dev = None
         super().Clean()
+
+
+def default_cone_params(occlusion: bool) -> N.ConeParams:
+    """sampler_occlusion / sampler_shadow defaults (dosrcrenderer.cpp:47-58); the covered
+    distance is left 0 so the library applies diagonal * 0.50 / 0.75 (:112-113)."""
+    c = N.ConeParams()
+    if occlusion:
+        c.half_angle_deg, c.max_packing, c.ui_weight = 20.0, 1, 0.35
+    else:
+        c.half_angle_deg, c.max_packing, c.ui_weight = 0.5, 0, 1.0
+    c.covered_distance = 0.0
+    c.initial_step = 3.0      # 3 * sigma0 (:366-367)
+    return c
+
+
+class RC1PConeTracingDirOcclusionShading(RayCasting1Pass):
+    """HIP implementation of RC1PConeTracingDirOcclusionShading
+    (cppvolrend/structured/rc1pdosct/dosrcrenderer.cpp): the single-pass march with
+    cone-traced directional ambient occlusion and cone shadows per sample."""
+
+    POINT_LIGHT, SPOT_LIGHT, DIRECTIONAL_LIGHT = 0, 1, 2   # type_of_shadow combo (:543)
+
+    def __init__(self, device: int = 0):
+        super().__init__(device)
+        self.glsl_apply_occlusion = True            # dosrcrenderer.cpp:44
+        self.glsl_apply_shadow = False              # :53
+        self.type_of_shadow = self.POINT_LIGHT      # :59
+        self.sampler_occlusion = default_cone_params(True)
+        self.sampler_shadow = default_cone_params(False)
+        self.ext_res = (128, 128, 128)              # extcoefvolumegenerator.cpp:10-15
+        self.base_level_sigma0 = 1.0
+        self._params = N.DosParams()
+
+    def GetName(self): return "1-Pass - Ray Casting - Dir. Occlusion Shading"
+    def GetAbbreviationName(self): return "s_1rc_dos"
+
+    def Init(self, swidth: int, sheight: int) -> bool:
+        dm = self.m_ext_data_manager
+        if dm is None or dm.tf_rgba is None:
+            return False
+        if not super().Init(swidth, sheight):
+            return False
+        self.GenerateExtCoefVolume()
+        return True
+
+    def GenerateExtCoefVolume(self):
+        """dosrcrenderer.cpp:745-764: the pyramid from the volume and the RGBA TF."""
+        self.device.set_extinction_volume(self.m_ext_data_manager.tf_rgba, self.ext_res,
+                                          self.base_level_sigma0)
+        self.SetOutdated()
+
+    def Update(self, camera: Camera) -> bool:
+        rp = self.m_ext_rendering_parameters or RenderingParameters()
+        self._frame = make_frame(camera, self.width, self.height)
+        p = self._params
+        p.step = float(self.m_u_step_size)
+        p.apply_gradient_shading = int(bool(self.m_apply_gradient_shading) and
+                                       self.m_ext_data_manager.gradient_type != N.GRADIENT_NONE)
+        p.ka, p.kd = rp.blinnphong_ka, rp.blinnphong_kd
+        p.ks, p.shininess = rp.blinnphong_ks, rp.blinnphong_shininess
+        p.ispecular[:] = [float(v) for v in rp.light_specular]
+        p.light.position[:] = [float(v) for v in rp.light_position]
+        p.light.forward[:] = [float(v) for v in rp.light_forward]
+        p.light.up[:] = [float(v) for v in rp.light_up]
+        p.light.right[:] = [float(v) for v in rp.light_right]
+        p.light.spot_angle_deg = float(rp.spot_light_angle)
+        p.apply_occlusion = int(bool(self.glsl_apply_occlusion))
+        p.apply_shadow = int(bool(self.glsl_apply_shadow))
+        p.shadow_type = int(self.type_of_shadow)
+        p.occlusion = self.sampler_occlusion
+        p.shadow = self.sampler_shadow
+        return True
+
+    def Redraw(self, stream: Optional[torch.cuda.Stream] = None, count_samples: bool = True):
+        if self._frame is None:
+            raise N.CvrError(N.CVR_ERR_STATE, "RC1PConeTracingDirOcclusionShading.Redraw",
+                             "Update() not called")
+        s = stream if stream is not None else torch.cuda.current_stream(self._device_index)
+        self.device.set_stream(s.cuda_stream)
+        if count_samples:
+            with torch.cuda.stream(s):
+                self.total.zero_()
+        out = N.Output(self.rgba.data_ptr(),
+                       self.samples.data_ptr() if count_samples else None,
+                       self.total.data_ptr() if count_samples else None, 1)
+        N.check(N.lib().cvr_render_dosct(self.device.handle, ctypes.byref(self._frame),
+                                         ctypes.byref(self._params), ctypes.byref(out)),
+                "cvr_render_dosct", self.device.handle)
 
 
 def composite_over_white(rgba: np.ndarray) -> np.ndarray:

@@ -24,8 +24,13 @@
  *   cvr_render_rc1pass           <- RayCasting1Pass::Update + Redraw
  *                                   cppvolrend/structured/rc1pass/rc1prenderer.cpp:72-151
  *                                   (the dispatch of ray_marching_1p.comp:85-179)
- *   (planned, not yet exported: cvr_render_dosct <- RC1PConeTracingDirOcclusionShading,
- *    dosrcrenderer.cpp:134-260; cvr_render_extbsd <- RC1PExtinctionBasedShading,
+ *   cvr_set_extinction_volume    <- ExtinctionCoefficientVolume::GenerateExtinctionCoefficientVolume
+ *                                   (Gaussian mip pyramid of TF opacity -> extinction)
+ *                                   cppvolrend/structured/rc1pdosct/extcoefvolume.cpp
+ *   cvr_render_dosct             <- RC1PConeTracingDirOcclusionShading::Update + Redraw
+ *                                   cppvolrend/structured/rc1pdosct/dosrcrenderer.cpp:134-260
+ *                                   (the dispatch of ray_marching_1p_dosct.comp)
+ *   (planned, not yet exported: cvr_render_extbsd <- RC1PExtinctionBasedShading,
  *    ebsrenderer.cpp:125-260)
  *   cvr_status (never exit())    <- gl::ExitOnGLError  libs/gl_utils/utils.cpp:11-30
  *
@@ -139,6 +144,32 @@ typedef struct cvr_cone_tables {
                               (GetConeSectionsInfoTex, conegaussiansampler.cpp:179-205) */
 } cvr_cone_tables;
 
+/* One light source of a #list_light_sources file (vis::LightSourceData,
+ * lightsourcelist.cpp:97-140) as RenderingParameters hands it to the shaders:
+ * WorldLightingPos, LightCamForward/Up/Right, SpotLightMaxAngle (degrees). */
+typedef struct cvr_light {
+  float position[3];
+  float forward[3];
+  float up[3];
+  float right[3];
+  float spot_angle_deg;
+} cvr_light;
+
+/* RC1PConeTracingDirOcclusionShading ("1-Pass - Dir. Occlusion Shading",
+ * s_1rcdosct): dosrcrenderer.cpp:24-60, 134-260. */
+typedef struct cvr_dos_params {
+  float step;                  /* <= 0: 0.5/sqrt(3)*|scale| (dosrcrenderer.cpp:124-125) */
+  int   apply_gradient_shading;/* ApplyPhongShading (needs cvr_set_gradient)           */
+  float ka, kd, ks, shininess; /* Blinn-Phong constants (renderingparameters.cpp:23-26) */
+  float ispecular[3];          /* Ispecular                                             */
+  cvr_light light;             /* the current light source                              */
+  int   apply_occlusion;       /* ApplyOcclusion (default 1)                            */
+  int   apply_shadow;          /* ApplyShadow (default 0)                               */
+  int   shadow_type;           /* TypeOfShadow: 0 point, 1 spot, 2 directional          */
+  cvr_cone_params occlusion;   /* sampler_occlusion: 20 deg, packing 1, weight 0.35     */
+  cvr_cone_params shadow;      /* sampler_shadow:    0.5 deg, packing 0, weight 1.0     */
+} cvr_dos_params;
+
 /* ----------------------------------------------------------------------------
  * Context
  * -------------------------------------------------------------------------- */
@@ -207,6 +238,24 @@ int         cvr_tiles_for_rank(const cvr_frame* frame, int rank);
 cvr_status  cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* frame,
                                const cvr_rc1pass_params* params, const cvr_output* out);
 
+/* Extinction-coefficient mip pyramid of the current volume for the DOS
+ * renderer (ExtinctionCoefficientVolume, extcoefvolume.cpp): level 0 at
+ * res (NULL: 128^3) is a 7^3 Gaussian (sigma0, default 1) of the opacity TF
+ * over the volume, level L the sigma 2^L Gaussian of level L-1 at res >> L,
+ * each stored R16F and converted to tau = -log(1 - opacity).  tf_rgba is the
+ * RGBA TF (GenerateTexture_1D_RGBA, alpha = opacity), n entries. */
+cvr_status  cvr_set_extinction_volume(cvr_ctx* ctx, const float* tf_rgba, int n,
+                                      const int res[3], float sigma0);
+/* Copy level `level` back as float (NULL out: dims / level count only). */
+cvr_status  cvr_copy_extinction_level(cvr_ctx* ctx, int level, float* out, int dims[3],
+                                      int* n_levels);
+
+/* One directional-occlusion frame: the ray-march of cvr_render_rc1pass with
+ * each sample shaded by cone-traced ambient occlusion and/or a cone shadow
+ * toward the light.  Needs cvr_set_extinction_volume. */
+cvr_status  cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* frame,
+                             const cvr_dos_params* params, const cvr_output* out);
+
 /* Rank-0 side of the screen-tile split: `d_packed` holds nranks consecutive
  * blocks of `tiles_per_rank_max` packed tiles (rank r's block at offset
  * r*tiles_per_rank_max*tile_size^2 pixels); scatter them into the W x H
@@ -272,6 +321,9 @@ cvr_status  cvr_read_camera_state(const char* path, int index, cvr_camera* out_c
  * position of light `light` of list `list`. */
 cvr_status  cvr_read_light_position(const char* path, int list, int light, float out_pos[3],
                                     int* out_count);
+/* The same light with its camera frame and spot angle (forward = -z_axis). */
+cvr_status  cvr_read_light(const char* path, int list, int light, cvr_light* out,
+                           int* out_count);
 
 #ifdef __cplusplus
 }

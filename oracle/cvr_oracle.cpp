@@ -130,15 +130,13 @@ float cvr_expf(float x) {
   return std::ldexp(y, (int)n);
 }
 
-// pow(x, y) for x >= 0: exp(y * ln x), ln by Cephes logf polynomial.
-float cvr_powf(float x, float y) {
-  if (x != x || y != y) return x + y;
-  if (!(x > 0.0f) || x < 1.17549435e-38f) {
-    if (y > 0.0f) return 0.0f;
-    if (y == 0.0f) return 1.0f;
-    return INFINITY;
-  }
-  if (x == INFINITY) return y > 0.0f ? INFINITY : (y == 0.0f ? 1.0f : 0.0f);
+// ln(x): Cephes logf polynomial (x in [sqrt(1/2), sqrt(2)) * 2^e).
+// 0 and subnormals -> -inf, negatives -> NaN.
+float cvr_logf(float x) {
+  if (x != x) return x;
+  if (x < 0.0f) return NAN;
+  if (x < 1.17549435e-38f) return -INFINITY;
+  if (x == INFINITY) return INFINITY;
   uint32_t bits = f2u(x);
   int e = (int)((bits >> 23) & 0xffu) - 126;
   float m = u2f((bits & 0x007fffffu) | 0x3f000000u);       // [0.5, 1)
@@ -159,8 +157,19 @@ float cvr_powf(float x, float y) {
   r = std::fmaf(fe, -2.12194440e-4f, r);
   r = std::fmaf(-0.5f, z, r);
   float lnx = f + r;
-  lnx = std::fmaf(fe, 0.693359375f, lnx);
-  return cvr_expf(y * lnx);
+  return std::fmaf(fe, 0.693359375f, lnx);
+}
+
+// pow(x, y) for x >= 0: exp(y * ln x).
+float cvr_powf(float x, float y) {
+  if (x != x || y != y) return x + y;
+  if (!(x > 0.0f) || x < 1.17549435e-38f) {
+    if (y > 0.0f) return 0.0f;
+    if (y == 0.0f) return 1.0f;
+    return INFINITY;
+  }
+  if (x == INFINITY) return y > 0.0f ? INFINITY : (y == 0.0f ? 1.0f : 0.0f);
+  return cvr_expf(y * cvr_logf(x));
 }
 
 // ---------------------------------------------------------------------------
@@ -187,6 +196,7 @@ ORACLE_API uint16_t oracle_float_to_half(float f) { return float_to_half(f); }
 ORACLE_API float oracle_half_to_float(uint16_t h) { return half_to_float(h); }
 ORACLE_API float oracle_expf(float x) { return cvr_expf(x); }
 ORACLE_API float oracle_powf(float x, float y) { return cvr_powf(x, y); }
+ORACLE_API float oracle_logf(float x) { return cvr_logf(x); }
 
 // glm::lookAt (column-major, out[col*4+row]) and tan(fovy/2).
 ORACLE_API void oracle_lookat(const float eye_[3], const float center_[3], const float up_[3],
@@ -526,4 +536,353 @@ ORACLE_API int oracle_num_threads(void) {
 #else
   return 1;
 #endif
+}
+
+// ===========================================================================
+// Directional-occlusion shading (rc1pdosct), SURVEY.md §8 rows A9-A13
+// ===========================================================================
+//
+// Extinction-coefficient mip volume, ExtinctionCoefficientVolume custom-resolution
+// path (extcoefvolumegenerator.cpp:230-408, glslextgen/gen_extcoefvol_anysize.comp,
+// gen_extcoefvol_anysize_mmlevel.comp, backtotau.comp), CVR-SPEC:
+//   level 0 voxel i: p = ((float)i + 0.5) * (G / R0); 7^3 taps f = k * S0 (k in -3..3,
+//     x outer, z inner); w = (S0*S0*S0) * exp(-((fx*fx + fy*fy) + fz*fz) / ((2*S0)*S0));
+//     c = 0 outside [0,1]^3 of (p+f)/G, else TF opacity (RGBA16F table, alpha) of the
+//     trilinear R16F density at texel fmaf(u, N, -0.5); sums in tap order; value
+//     q16(sum(w*c) / sum(w)).
+//   level L >= 1: R_L = max(1, R0 >> L); the same with Si = S0 * 2^L over level L-1
+//     (trilinear at fmaf(u, R_{L-1}, -0.5)), voxel size G / R_L.
+//   then every level: tau = q16(-1 * log(1 - opacity)).
+struct OracleExtVol {
+  const float* vol; int N[3]; float scale[3];   // R16F volume values, voxel scale
+  const float* tf_rgba; int tf_n;                // opacity TF (half-rounded RGBA)
+  int res[3]; float sigma0;
+};
+
+namespace {
+
+int ext_levels(const int res[3]) {
+  int m = std::max(res[0], std::max(res[1], res[2])), n = 1;
+  while (m > 1) { m >>= 1; n++; }
+  return n;
+}
+
+void ext_level_dims(const int res[3], int L, int out[3]) {
+  for (int i = 0; i < 3; i++) out[i] = std::max(1, res[i] >> L);
+}
+
+}  // namespace
+
+ORACLE_API int oracle_ext_levels(const int res[3]) { return ext_levels(res); }
+
+// out: all levels concatenated (level 0 first), x-fastest; returns the level count.
+ORACLE_API int oracle_ext_volume(const OracleExtVol* P, float* out, int nthreads) {
+  const int nl = ext_levels(P->res);
+  const v3 G = mk((float)P->N[0] * P->scale[0], (float)P->N[1] * P->scale[1],
+                  (float)P->N[2] * P->scale[2]);
+  Tex vol{P->vol, {P->N[0], P->N[1], P->N[2]}, 1};
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+  std::vector<int64_t> off(nl + 1, 0);
+  for (int L = 0; L < nl; L++) {
+    int d[3];
+    ext_level_dims(P->res, L, d);
+    off[L + 1] = off[L] + (int64_t)d[0] * d[1] * d[2];
+  }
+  for (int L = 0; L < nl; L++) {
+    int d[3], pd[3];
+    ext_level_dims(P->res, L, d);
+    if (L > 0) ext_level_dims(P->res, L - 1, pd);
+    const float S = L == 0 ? P->sigma0 : P->sigma0 * (float)(1 << L);
+    const v3 vs = mk(G.x / (float)d[0], G.y / (float)d[1], G.z / (float)d[2]);
+    const float S3 = (S * S) * S, den = (2.0f * S) * S;
+    Tex prev{out + (L > 0 ? off[L - 1] : 0), {pd[0], pd[1], pd[2]}, 1};
+    const int64_t nv = (int64_t)d[0] * d[1] * d[2];
+#pragma omp parallel for schedule(static)
+    for (int64_t v = 0; v < nv; v++) {
+      const int i = (int)(v % d[0]), j = (int)((v / d[0]) % d[1]), k = (int)(v / ((int64_t)d[0] * d[1]));
+      const v3 gp = mk(((float)i + 0.5f) * vs.x, ((float)j + 0.5f) * vs.y, ((float)k + 0.5f) * vs.z);
+      float swc = 0.0f, sw = 0.0f;
+      for (int tx = -3; tx <= 3; tx++)
+        for (int ty = -3; ty <= 3; ty++)
+          for (int tz = -3; tz <= 3; tz++) {
+            const float fx = (float)tx * S, fy = (float)ty * S, fz = (float)tz * S;
+            const float w = S3 * cvr_expf(-((fx * fx + fy * fy) + fz * fz) / den);
+            const v3 p = mk(gp.x + fx, gp.y + fy, gp.z + fz);
+            const v3 u = mk(p.x / G.x, p.y / G.y, p.z / G.z);
+            float c = 0.0f;
+            if (!(u.x < 0.0f || u.y < 0.0f || u.z < 0.0f || u.x > 1.0f || u.y > 1.0f || u.z > 1.0f)) {
+              if (L == 0) {
+                float dens, rgba[4];
+                vol.sample(std::fmaf(u.x, (float)P->N[0], -0.5f), std::fmaf(u.y, (float)P->N[1], -0.5f),
+                           std::fmaf(u.z, (float)P->N[2], -0.5f), &dens);
+                tf_lookup(P->tf_rgba, P->tf_n, dens, rgba);
+                c = rgba[3];
+              } else {
+                prev.sample(std::fmaf(u.x, (float)pd[0], -0.5f), std::fmaf(u.y, (float)pd[1], -0.5f),
+                            std::fmaf(u.z, (float)pd[2], -0.5f), &c);
+              }
+            }
+            swc = swc + w * c;
+            sw = sw + w;
+          }
+      out[off[L] + v] = q16(swc / sw);
+    }
+  }
+  for (int64_t v = 0; v < off[nl]; v++) out[v] = q16(-1.0f * cvr_logf(1.0f - out[v]));
+  return nl;
+}
+
+// Cone-traced directional occlusion + shadows (ray_bbox_marching.comp), CVR-SPEC:
+// the march, sampling and composite of rc1pass; for src.a > 0 ShadeSample
+// (:607-656) with the cones of :116-562.  Vector forms: pos + d * t = fmaf per
+// component; k*a.z + u*a.y + v*a.x = fmaf(v, a.x, fmaf(u, a.y, k * a.z));
+// cross = glm order without fma; dot/normalize as rc1pass.  Cone tables arrive
+// RGBA16F-rounded (GetConeSectionsInfoTex).
+struct OracleDosCone {
+  const float* sections; int counts[3];   // n x 4 (interval, mip, d_integral, amplitude)
+  float axes[30]; float initial_step, ray7w, ui_weight;
+};
+
+struct OracleDos {
+  OracleRc1pass base;                     // volume, TF (RGBt), camera, step, Blinn-Phong
+  const float* ext; int ext_res[3]; int ext_levels;
+  int apply_occlusion, apply_shadow, shadow_type;
+  float light_forward[3], light_up[3], light_right[3], spot_angle_deg;
+  OracleDosCone occ, sdw;
+};
+
+namespace {
+
+struct ExtVol {
+  const float* v; int res[3]; int nl; v3 G;
+  std::vector<int64_t> off;
+  // GetGaussianExtinction (:92-112): textureLod at an integer level, clamp-to-edge,
+  // plus the CONSIDER_BORDERS attenuation outside the box
+  float gge(v3 p, float mip) const {
+    int L = (int)mip;
+    L = std::min(std::max(L, 0), nl - 1);
+    int d[3];
+    ext_level_dims(res, L, d);
+    Tex t{v + off[L], {d[0], d[1], d[2]}, 1};
+    const v3 u = mk(p.x / G.x, p.y / G.y, p.z / G.z);
+    float rg;
+    t.sample(std::fmaf(u.x, (float)d[0], -0.5f), std::fmaf(u.y, (float)d[1], -0.5f),
+             std::fmaf(u.z, (float)d[2], -0.5f), &rg);
+    if (p.x < 0.0f || p.x > G.x || p.y < 0.0f || p.y > G.y || p.z < 0.0f || p.z > G.z) {
+      const float sg = std::ldexp(1.0f, (int)mip);   // pow(2.0, mip) of an integer level
+      const v3 c = mk(std::fmin(std::fmax(p.x, 0.0f), G.x) - p.x, std::fmin(std::fmax(p.y, 0.0f), G.y) - p.y,
+                      std::fmin(std::fmax(p.z, 0.0f), G.z) - p.z);
+      const float dist = (c.x * c.x + c.y * c.y) + c.z * c.z;
+      rg = rg * cvr_expf(-(dist) / ((2.0f * sg) * sg));
+    }
+    return rg;
+  }
+};
+
+inline v3 vmad(v3 d, float t, v3 p) {
+  return mk(std::fmaf(d.x, t, p.x), std::fmaf(d.y, t, p.y), std::fmaf(d.z, t, p.z));
+}
+inline v3 cone_axis(const float* a, v3 k, v3 u, v3 v) {
+  return mk(std::fmaf(v.x, a[0], std::fmaf(u.x, a[1], k.x * a[2])),
+            std::fmaf(v.y, a[0], std::fmaf(u.y, a[1], k.y * a[2])),
+            std::fmaf(v.z, a[0], std::fmaf(u.z, a[1], k.z * a[2])));
+}
+
+// Cone1/3/7 RayOcclusion == Cone1/3/7 RayShadow (the same accumulation); the
+// 1 -> 3 -> 7 ray splits of :124-140 / :210-217.  Returns the visibility.
+float cone_trace(const ExtVol& E, const OracleDosCone& C, v3 pos, v3 k, v3 u, v3 v) {
+  float rays[7], last[7];
+  float track = C.initial_step;
+  rays[0] = 0.0f;
+  last[0] = 0.0f;
+  int s = 0;
+  for (int i = 0; i < C.counts[0]; i++, s++) {
+    const float* sec = C.sections + 4 * s;
+    const float amptau = E.gge(vmad(k, track, pos), sec[1]) * sec[3];
+    rays[0] += ((last[0] + amptau) * sec[2]) * C.ui_weight;
+    last[0] = amptau;
+    track += sec[0];
+  }
+  if (C.counts[1] + C.counts[2] == 0) return cvr_expf(-rays[0]);
+  rays[2] = rays[0]; rays[1] = rays[0];
+  last[2] = last[0]; last[1] = last[0];
+  v3 vk[7];
+  for (int j = 0; j < 3; j++) vk[j] = cone_axis(C.axes + 3 * j, k, u, v);
+  for (int i = 0; i < C.counts[1]; i++, s++) {
+    const float* sec = C.sections + 4 * s;
+    for (int j = 0; j < 3; j++) {
+      const float amptau = E.gge(vmad(vk[j], track, pos), sec[1]) * sec[3];
+      rays[j] += ((last[j] + amptau) * sec[2]) * C.ui_weight;
+      last[j] = amptau;
+    }
+    track += sec[0];
+  }
+  if (C.counts[2] == 0)
+    return ((cvr_expf(-rays[0]) + cvr_expf(-rays[1])) + cvr_expf(-rays[2])) / 3.0f;
+  // transform 3 to 7
+  rays[6] = rays[5] = rays[2];
+  rays[4] = rays[3] = rays[1];
+  float avg = ((rays[2] + rays[1]) + rays[0]) / 3.0f;
+  rays[2] = rays[1] = rays[0];
+  rays[0] = avg;
+  last[6] = last[5] = last[2];
+  last[4] = last[3] = last[1];
+  float avgt = ((last[2] + last[1]) + last[0]) / 3.0f;
+  last[2] = last[1] = last[0];
+  last[0] = avgt;
+  for (int j = 0; j < 7; j++) vk[j] = cone_axis(C.axes + 3 * (3 + j), k, u, v);
+  for (int i = 0; i < C.counts[2]; i++, s++) {
+    const float* sec = C.sections + 4 * s;
+    for (int j = 0; j < 7; j++) {
+      const float amptau = E.gge(vmad(vk[j], track, pos), sec[1]) * sec[3];
+      rays[j] += ((last[j] + amptau) * sec[2]) * C.ui_weight;
+      last[j] = amptau;
+    }
+    track += sec[0];
+  }
+  float side = cvr_expf(-rays[1]);
+  for (int j = 2; j < 7; j++) side = side + cvr_expf(-rays[j]);
+  return (cvr_expf(-rays[0]) + side * C.ray7w) / (1.0f + C.ray7w * 6.0f);
+}
+
+}  // namespace
+
+ORACLE_API uint64_t oracle_render_dos(const OracleDos* Q, float* out_rgba, uint32_t* out_counts,
+                                      int nthreads) {
+  const OracleRc1pass& P = Q->base;
+  float V[16], tanf;
+  oracle_lookat(P.eye, P.center, P.up, P.fovy_deg, V, &tanf);
+  const float aspect = P.aspect > 0 ? P.aspect : (float)P.W / (float)P.H;
+  const v3 eye = mk(P.eye[0], P.eye[1], P.eye[2]);
+  const v3 G = mk((float)P.N[0] * P.scale[0], (float)P.N[1] * P.scale[1], (float)P.N[2] * P.scale[2]);
+  const v3 half = mk(G.x * 0.5f, G.y * 0.5f, G.z * 0.5f);
+  const v3 NoG = mk((float)P.N[0] / G.x, (float)P.N[1] / G.y, (float)P.N[2] / G.z);
+  const v3 light = mk(P.light[0], P.light[1], P.light[2]);
+  const v3 lfwd = mk(Q->light_forward[0], Q->light_forward[1], Q->light_forward[2]);
+  const v3 lup = mk(Q->light_up[0], Q->light_up[1], Q->light_up[2]);
+  const v3 lright = mk(Q->light_right[0], Q->light_right[1], Q->light_right[2]);
+  Tex vol{P.vol, {P.N[0], P.N[1], P.N[2]}, 1};
+  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3};
+  ExtVol E{Q->ext, {Q->ext_res[0], Q->ext_res[1], Q->ext_res[2]}, Q->ext_levels, G, {}};
+  E.off.assign(E.nl + 1, 0);
+  for (int L = 0; L < E.nl; L++) {
+    int d[3];
+    ext_level_dims(E.res, L, d);
+    E.off[L + 1] = E.off[L] + (int64_t)d[0] * d[1] * d[2];
+  }
+  // SpotLightMaxAngle uniform: glm::cos(glm::pi<float>() * angle / 180.f) (dosrcrenderer.cpp:158)
+  const float spot_cos = std::cos(3.14159265358979323846f * Q->spot_angle_deg / 180.0f);
+  const float ka = Q->apply_occlusion ? P.ka : 0.0f;
+  const float kd = Q->apply_shadow ? P.kd : 0.0f;
+  const float ks = Q->apply_shadow ? P.ks : 0.0f;
+  const int W = P.W, H = P.H;
+  std::vector<uint32_t> tmp;
+  uint32_t* counts = out_counts;
+  if (!counts) { tmp.resize((size_t)W * H); counts = tmp.data(); }
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int py = 0; py < H; py++) {
+    for (int px = 0; px < W; px++) {
+      const int64_t pix = (int64_t)py * W + px;
+      float dst[4] = {0, 0, 0, 0};
+      uint32_t cnt = 0;
+      float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+      float vx = std::fmaf(fx / (float)W, 2.0f, -1.0f);
+      float vy = std::fmaf(fy / (float)H, 2.0f, -1.0f);
+      v3 c = mk((vx * tanf) * aspect, vy * tanf, -1.0f);
+      v3 d = mk(dot3(c, mk(V[0], V[1], V[2])), dot3(c, mk(V[4], V[5], V[6])),
+                dot3(c, mk(V[8], V[9], V[10])));
+      const v3 cam_dir = normalize3(d);          // camera_dir (:668-669)
+      const v3 dir = normalize3(cam_dir);        // r.Dir, RayAABBIntersection (:590)
+      v3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+      v3 ta = mk(inv.x * (-half.x - eye.x), inv.y * (-half.y - eye.y), inv.z * (-half.z - eye.z));
+      v3 tb = mk(inv.x * (half.x - eye.x), inv.y * (half.y - eye.y), inv.z * (half.z - eye.z));
+      float tnear = std::fmax(std::fmax(std::fmin(ta.x, tb.x), std::fmin(ta.y, tb.y)), std::fmin(ta.z, tb.z));
+      float tfar = std::fmin(std::fmin(std::fmax(ta.x, tb.x), std::fmax(ta.y, tb.y)), std::fmax(ta.z, tb.z));
+      const bool hit = tfar > tnear;
+      tnear = std::fmax(tnear, 0.0f);
+      if (hit) {
+        // eye-space frame of the occlusion cones (:681-684)
+        const v3 v_right = normalize3(cross3(cam_dir, mk(0.0f, 1.0f, 0.0f)));
+        const v3 v_up = normalize3(cross3(mk(-cam_dir.x, -cam_dir.y, -cam_dir.z), v_right));
+        const float D = std::fabs(tfar - tnear);
+        const v3 tpos = mk(std::fmaf(dir.x, tnear, eye.x) + half.x, std::fmaf(dir.y, tnear, eye.y) + half.y,
+                           std::fmaf(dir.z, tnear, eye.z) + half.z);
+        const v3 o = mk(std::fmaf(tpos.x, NoG.x, -0.5f), std::fmaf(tpos.y, NoG.y, -0.5f), std::fmaf(tpos.z, NoG.z, -0.5f));
+        const v3 dt = mk(dir.x * NoG.x, dir.y * NoG.y, dir.z * NoG.z);
+        float s = 0.0f;
+        while (s < D) {
+          const float h = std::fmin(P.step, D - s);
+          const float t = std::fmaf(h, 0.5f, s);
+          const float x = std::fmaf(dt.x, t, o.x), y = std::fmaf(dt.y, t, o.y), z = std::fmaf(dt.z, t, o.z);
+          float dens;
+          vol.sample(x, y, z, &dens);
+          float src[4];
+          tf_lookup(P.tf, P.tf_n, dens, src);
+          cnt++;
+          if (src[3] > 0.0f) {
+            const v3 tx = vmad(dir, t, tpos);              // tx_pos, volume box at [0, G]
+            const v3 wp = mk(tx.x - half.x, tx.y - half.y, tx.z - half.z);
+            float iocc = 0.0f, isdw = 0.0f;
+            if (Q->apply_occlusion) {
+              const v3 k = normalize3(mk(eye.x - wp.x, eye.y - wp.y, eye.z - wp.z));
+              iocc = cone_trace(E, Q->occ, tx, k, v_up, v_right);
+            }
+            if (Q->apply_shadow) {
+              v3 k, u, v;
+              bool lit = true;
+              if (Q->shadow_type == 2) {
+                k = lfwd; v = lup; u = lright;
+              } else {
+                k = normalize3(mk(light.x - wp.x, light.y - wp.y, light.z - wp.z));
+                u = normalize3(cross3(k, lright));
+                v = normalize3(cross3(k, u));
+                if (Q->shadow_type == 1 && dot3(k, lfwd) < spot_cos) lit = false;
+              }
+              // Cone1RayShadow(pos, k, v, u) is called as (pos, k, u, v): swapped (:559-561)
+              isdw = lit ? cone_trace(E, Q->sdw, tx, k, v, u) : 0.0f;
+            }
+            const float inv_k = 1.0f / (ka + kd);
+            bool shaded_phong = false;
+            if (P.phong && P.grad) {
+              float g[3];
+              grd.sample(x, y, z, g);
+              if (g[0] != 0.0f || g[1] != 0.0f || g[2] != 0.0f) {
+                const v3 n = normalize3(mk(g[0], g[1], g[2]));
+                const v3 L = normalize3(mk(light.x - wp.x, light.y - wp.y, light.z - wp.z));
+                const v3 Ve = normalize3(mk(eye.x - wp.x, eye.y - wp.y, eye.z - wp.z));
+                const v3 Hv = normalize3(mk(Ve.x + L.x, Ve.y + L.y, Ve.z + L.z));
+                const float dd = std::fmax(0.0f, dot3(n, L));
+                const float ds = std::fmax(0.0f, dot3(Hv, n));
+                const float diff = inv_k * (iocc * ka + (isdw * kd) * dd);
+                const float spec = (isdw * ks) * cvr_powf(ds, P.shininess);
+                for (int q = 0; q < 3; q++) src[q] = std::fmaf(P.ispec[q], spec, src[q] * diff);
+                shaded_phong = true;
+              }
+            }
+            if (!shaded_phong && !(P.phong && P.grad)) {
+              for (int q = 0; q < 3; q++) src[q] = inv_k * ((src[q] * iocc) * ka + (src[q] * isdw) * kd);
+            }
+            const float a = 1.0f - cvr_expf(-(src[3] * h));
+            const float om = 1.0f - dst[3];
+            dst[0] = std::fmaf(om, src[0] * a, dst[0]);
+            dst[1] = std::fmaf(om, src[1] * a, dst[1]);
+            dst[2] = std::fmaf(om, src[2] * a, dst[2]);
+            dst[3] = std::fmaf(om, a, dst[3]);
+            if (dst[3] > 0.99f) break;
+          }
+          s = s + h;
+        }
+      }
+      if (out_rgba) for (int q = 0; q < 4; q++) out_rgba[pix * 4 + q] = dst[q];
+      counts[pix] = cnt;
+    }
+  }
+  uint64_t total = 0;
+  for (int64_t i = 0; i < (int64_t)W * H; i++) total += counts[i];
+  return total;
 }

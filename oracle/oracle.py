@@ -26,6 +26,27 @@ class OracleRc1pass(ctypes.Structure):
                 ("ispec", ctypes.c_float * 3), ("light", ctypes.c_float * 3)]
 
 
+class OracleExtVol(ctypes.Structure):
+    _fields_ = [("vol", ctypes.c_void_p), ("N", ctypes.c_int * 3), ("scale", ctypes.c_float * 3),
+                ("tf_rgba", ctypes.c_void_p), ("tf_n", ctypes.c_int), ("res", ctypes.c_int * 3),
+                ("sigma0", ctypes.c_float)]
+
+
+class OracleDosCone(ctypes.Structure):
+    _fields_ = [("sections", ctypes.c_void_p), ("counts", ctypes.c_int * 3),
+                ("axes", ctypes.c_float * 30), ("initial_step", ctypes.c_float),
+                ("ray7w", ctypes.c_float), ("ui_weight", ctypes.c_float)]
+
+
+class OracleDos(ctypes.Structure):
+    _fields_ = [("base", OracleRc1pass), ("ext", ctypes.c_void_p), ("ext_res", ctypes.c_int * 3),
+                ("ext_levels", ctypes.c_int), ("apply_occlusion", ctypes.c_int),
+                ("apply_shadow", ctypes.c_int), ("shadow_type", ctypes.c_int),
+                ("light_forward", ctypes.c_float * 3), ("light_up", ctypes.c_float * 3),
+                ("light_right", ctypes.c_float * 3), ("spot_angle_deg", ctypes.c_float),
+                ("occ", OracleDosCone), ("sdw", OracleDosCone)]
+
+
 def build() -> None:
     subprocess.run(["make", "-C", HERE, "-s"], check=True)
 
@@ -53,6 +74,12 @@ def lib():
         L.oracle_render_rc1pass_rows.argtypes = [ctypes.POINTER(OracleRc1pass), I, I, P, P, I]
         L.oracle_render_rc1pass_rows.restype = ctypes.c_uint64
         L.oracle_num_threads.restype = I
+        L.oracle_logf.argtypes, L.oracle_logf.restype = [F], F
+        L.oracle_ext_levels.argtypes, L.oracle_ext_levels.restype = [P], I
+        L.oracle_ext_volume.argtypes = [ctypes.POINTER(OracleExtVol), P, I]
+        L.oracle_ext_volume.restype = I
+        L.oracle_render_dos.argtypes = [ctypes.POINTER(OracleDos), P, P, I]
+        L.oracle_render_dos.restype = ctypes.c_uint64
         _lib = L
     return _lib
 
@@ -172,3 +199,91 @@ def render_rc1pass(vol16: np.ndarray, scale, tf: np.ndarray, camera: dict, W: in
 
 def num_threads() -> int:
     return int(lib().oracle_num_threads())
+
+
+def logf(x: float) -> float:
+    return lib().oracle_logf(x)
+
+
+def _q16_array(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, np.float32).astype(np.float16), np.float32)
+
+
+def ext_level_dims(res, L):
+    return [max(1, int(r) >> L) for r in res]
+
+
+def ext_volume(vol16: np.ndarray, scale, tf_rgba: np.ndarray, res=(128, 128, 128),
+               sigma0: float = 1.0, threads: int = 0):
+    """Extinction-coefficient mip volume (extcoefvolumegenerator.cpp:230-408).
+    Returns a list of levels, each (d, h, w) float32 of half-rounded extinctions."""
+    vol16 = np.ascontiguousarray(vol16, np.float32)
+    tf_rgba = _q16_array(tf_rgba)
+    P = OracleExtVol()
+    d, h, w = vol16.shape
+    P.vol = _p(vol16)
+    P.N[:] = [w, h, d]
+    P.scale[:] = [float(s) for s in scale]
+    P.tf_rgba = _p(tf_rgba)
+    P.tf_n = tf_rgba.shape[0]
+    P.res[:] = [int(r) for r in res]
+    P.sigma0 = float(sigma0)
+    nl = lib().oracle_ext_levels((ctypes.c_int * 3)(*P.res))
+    sizes = [int(np.prod(ext_level_dims(res, L))) for L in range(nl)]
+    flat = np.zeros(sum(sizes), np.float32)
+    lib().oracle_ext_volume(ctypes.byref(P), _p(flat), int(threads))
+    out, o = [], 0
+    for L in range(nl):
+        dx, dy, dz = ext_level_dims(res, L)
+        out.append(flat[o:o + sizes[L]].reshape(dz, dy, dx))
+        o += sizes[L]
+    return out
+
+
+def _cone(tables, keep):
+    """OracleDosCone from a cvr_cone_tables (sections RGBA16F-rounded as uploaded)."""
+    C = OracleDosCone()
+    n = tables.n_sections
+    sec = _q16_array([list(tables.sections[i]) for i in range(max(n, 1))])
+    keep.append(sec)
+    C.sections = _p(sec)
+    C.counts[:] = list(tables.counts)
+    C.axes[:] = [tables.axes[i][j] for i in range(10) for j in range(3)]
+    C.initial_step = tables.initial_step
+    C.ray7w = tables.ray7_adj_weight
+    C.ui_weight = tables.ui_weight
+    return C
+
+
+def render_dos(vol16, scale, tf_rgbt, ext_levels, camera, W, H, step, occ_tables, sdw_tables,
+               apply_occlusion=True, apply_shadow=False, shadow_type=0, light=None,
+               grad=None, phong=False, ka=0.5, kd=0.5, ks=0.8, shininess=30.0,
+               ispec=(1.0, 1.0, 1.0), threads: int = 0):
+    """Directional-occlusion shading frame (ray_bbox_marching.comp).  light = dict with
+    position/forward/up/right/spot_angle_deg.  Returns (rgba, counts, S)."""
+    vol16 = np.ascontiguousarray(vol16, np.float32)
+    tf = _q16_array(tf_rgbt)
+    if grad is not None:
+        grad = np.ascontiguousarray(grad, np.float32)
+    light = light or {}
+    pos = light.get("position", (0.0, 0.0, 0.0))
+    Q = OracleDos()
+    Q.base = _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shininess,
+                     ispec, pos)
+    res = list(ext_levels[0].shape[::-1])
+    flat = np.ascontiguousarray(np.concatenate([l.ravel() for l in ext_levels]), np.float32)
+    Q.ext = _p(flat)
+    Q.ext_res[:] = res
+    Q.ext_levels = len(ext_levels)
+    Q.apply_occlusion, Q.apply_shadow, Q.shadow_type = int(apply_occlusion), int(apply_shadow), int(shadow_type)
+    Q.light_forward[:] = [float(v) for v in light.get("forward", (0.0, 0.0, -1.0))]
+    Q.light_up[:] = [float(v) for v in light.get("up", (0.0, 1.0, 0.0))]
+    Q.light_right[:] = [float(v) for v in light.get("right", (1.0, 0.0, 0.0))]
+    Q.spot_angle_deg = float(light.get("spot_angle_deg", 4.0))
+    keep = []
+    Q.occ = _cone(occ_tables, keep)
+    Q.sdw = _cone(sdw_tables, keep)
+    rgba = np.zeros((H, W, 4), np.float32)
+    cnt = np.zeros((H, W), np.uint32)
+    S = lib().oracle_render_dos(ctypes.byref(Q), _p(rgba), _p(cnt), int(threads))
+    return rgba, cnt, int(S)

@@ -32,3 +32,12 @@ def bonsai_tf(oracle):
     from cpp_volume_rendering_amd import datasets as D
     table = oracle.tf_table_double(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA)
     return oracle.tf_rgbt(table)
+
+
+@pytest.fixture(scope="session")
+def bonsai_tf_rgba(oracle):
+    """GenerateTexture_1D_RGBA of the same TF (alpha = opacity, RGBA16F-rounded): the
+    table the extinction volume of the occlusion renderer filters."""
+    from cpp_volume_rendering_amd import datasets as D
+    table = oracle.tf_table_double(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA)
+    return oracle.tf_rgbt(table, extinction_input=True)
