@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Headline benchmark: rc1pass ray-march, Msamples/s at 1024^2 on a 512^3 volume.
 
+(--renderer dos: BASELINE.json config 4 instead, the directional-occlusion renderer
+with cone AO + cone shadows at 2048^2; a secondary line, not the headline.)
+
 Workload (BASELINE.json metric, SURVEY.md §8d "512^3 EA"): Marschner-Lobb field
 (alpha 0.25, f_M 6) quantised to u8, 512^3, voxel scale 1 (world box +-256),
 data/tf1dcp/bonsai_01.tf1d, camera "Initial State", 1024x1024, default step
@@ -36,6 +39,7 @@ from cpp_volume_rendering_amd import _native as N  # noqa: E402
 from cpp_volume_rendering_amd import datasets as D  # noqa: E402
 from cpp_volume_rendering_amd import screen_tiles as T  # noqa: E402
 from cpp_volume_rendering_amd.renderer import (Camera, DataManager, RayCasting1Pass,  # noqa: E402
+                                               RC1PConeTracingDirOcclusionShading,
                                                RenderingParameters, build_tf_rgbt, make_frame)
 
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md (spec)
@@ -44,10 +48,11 @@ HBM_PEAK_GBS = 8000.0    # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=0, help="default 50 (dos: 5)")
+    p.add_argument("--warmup", type=int, default=-1, help="default 5 (dos: 1)")
     p.add_argument("--size", type=int, default=512)
-    p.add_argument("--res", type=int, default=1024)
+    p.add_argument("--res", type=int, default=0, help="viewport (default 1024; dos 2048)")
+    p.add_argument("--renderer", choices=["rc1pass", "dos"], default="rc1pass")
     p.add_argument("--tile", type=int, default=32)
     p.add_argument("--field", choices=["ml", "blobs"], default="ml")
     p.add_argument("--phong", action="store_true")
@@ -57,7 +62,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(vol, scale, tf, cam, W, H, seconds):
+def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None):
     """The CPU oracle (C++/OpenMP restatement of ray_marching_1p.comp; the reference has
     no CPU ray-caster) on the host cores: whole frames of the same workload, repeated
     until `seconds` of wall time are spent (each frame starts from the centre band of
@@ -67,7 +72,17 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     v16 = O.volume_r16f(vol)
     step = O.default_step(scale)
-    rows_per_chunk = 16
+    rows_per_chunk = 16 if dos is None else 2
+    if dos is not None:
+        levels = O.ext_volume(v16, scale, dos["tf_rgba"], dos["res"], threads=threads)
+
+    def render_rows(y0, y1, nthreads):
+        if dos is None:
+            return O.render_rc1pass(v16, scale, tf, cam, W, H, step, rows=(y0, y1),
+                                    threads=nthreads)[2]
+        return O.render_dos(v16, scale, tf, levels, cam, W, H, step, dos["occ"], dos["sdw"],
+                            apply_shadow=True, light=dos["light"], rows=(y0, y1),
+                            threads=nthreads)[2]
     y = H // 2 - rows_per_chunk // 2
     order = []
     for k in range(H // rows_per_chunk + 2):
@@ -81,9 +96,7 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds):
         t0 = time.perf_counter()
         while True:
             for yy in order:
-                _, _, s = O.render_rc1pass(v16, scale, tf, cam, W, H, step,
-                                           rows=(yy, yy + rows_per_chunk), threads=nthreads)
-                S += s
+                S += render_rows(yy, yy + rows_per_chunk, nthreads)
                 rows += rows_per_chunk
                 if time.perf_counter() - t0 >= budget:
                     return S, rows, time.perf_counter() - t0
@@ -94,9 +107,30 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds):
             "kind": "port",
             "sample": f"{rows} image rows ({rows / H:.1f} frames, centre band outward) of the "
                       f"same {W}x{H} frame, {S} samples in {dt:.1f} s on {threads} threads; "
-                      f"C++/OpenMP oracle (no CPU ray-caster exists in the reference)",
+                      f"C++/OpenMP oracle (no CPU ray-caster exists in the reference)"
+                      + ("; extinction pyramid built outside the timed sample" if dos else ""),
             "single_thread_value": round(S1 / dt1 / 1e6, 3),
             "single_thread_sample": f"{rows1} rows, {S1} samples in {dt1:.1f} s"}
+
+
+def cone_tables_for(params, n, scale, frac):
+    """The cone tables cvr_render_dosct builds (covered distance <= 0: diagonal * frac)."""
+    p = N.ConeParams.from_buffer_copy(params)
+    if p.covered_distance <= 0:
+        diag = float(np.sqrt(sum((n * float(s)) ** 2 for s in scale)))
+        p.covered_distance = float(np.float32(diag * np.float32(frac)))
+    t = N.ConeTables()
+    N.check(N.lib().cvr_build_cone_tables(ctypes.byref(p), 1.0, ctypes.byref(t)), "cones")
+    return t
+
+
+def cone_fetches(r, n, scale):
+    """Trilinear extinction fetches per cone: n1 + 3 n3 + 7 n7 (occlusion, shadow)."""
+    out = []
+    for params, frac in ((r.sampler_occlusion, 0.50), (r.sampler_shadow, 0.75)):
+        t = cone_tables_for(params, n, scale, frac)
+        out.append(t.counts[0] + 3 * t.counts[1] + 7 * t.counts[2])
+    return out
 
 
 def load_traffic(path, workload_key):
@@ -121,20 +155,29 @@ def main():
     else:
         torch.cuda.set_device(0)
 
-    n, W = a.size, a.res
+    dos = a.renderer == "dos"
+    a.steps = a.steps or (5 if dos else 50)
+    a.warmup = a.warmup if a.warmup >= 0 else (1 if dos else 5)
+    n, W = a.size, a.res or (2048 if dos else 1024)
     H = W
     vol = D.marschner_lobb_u8(n) if a.field == "ml" else D.blobs_u8(n)
     scale = D.voxel_scale(n)
     tf = build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA)
+    # GenerateTexture_1D_RGBA of the same TF (alpha = opacity) for the extinction pyramid
+    tf_rgba = build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA, extinction_input=True)
     cam = Camera(**D.INITIAL_STATE_CAMERA)
 
     dm = DataManager()
     dm.SetVolume(vol, scale)
-    dm.SetTransferFunction(tf)
+    dm.SetTransferFunction(tf, tf_rgba)
     if a.phong:
         dm.SetGradientType(N.GRADIENT_FINITE_DIFFERENCES)
     rp = RenderingParameters(W, H, light_position=D.LIGHT_LIST0_POSITION)
-    r = RayCasting1Pass(local if world > 1 else 0)
+    if dos:
+        r = RC1PConeTracingDirOcclusionShading(local if world > 1 else 0)
+        r.glsl_apply_shadow = True        # config 4: cone AO + cone shadows (point light)
+    else:
+        r = RayCasting1Pass(local if world > 1 else 0)
     r.m_apply_gradient_shading = a.phong
     r.SetExternalResources(dm, rp)
     assert r.Init(W, H)
@@ -159,10 +202,11 @@ def main():
     L = N.lib()
     fptr, pptr = ctypes.byref(frame), ctypes.byref(r._params)
     out = N.Output(out_buf.data_ptr(), None, total.data_ptr(), 1)
+    render = L.cvr_render_dosct if dos else L.cvr_render_rc1pass
 
     def step_once():
-        N.check(L.cvr_render_rc1pass(r.device.handle, fptr, pptr, ctypes.byref(out)),
-                "cvr_render_rc1pass", r.device.handle)
+        N.check(render(r.device.handle, fptr, pptr, ctypes.byref(out)), "render",
+                r.device.handle)
 
     def gather_once():
         if world > 1:
@@ -171,10 +215,17 @@ def main():
                 N.check(L.cvr_unpack_tiles_device(r.device.handle, fptr, allp.data_ptr(), tpr,
                                                   image.data_ptr()), "unpack", r.device.handle)
 
-    # samples per frame (this rank), counted by the kernel
+    # samples per frame (this rank), counted by the kernel; for the shaded renderer
+    # also the shaded / shadow-lit samples (each traces a fixed number of cone fetches)
+    if dos:
+        N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 1), "opt", r.device.handle)
     step_once()
     torch.cuda.synchronize(dev)
     S_rank = int(total.item())
+    shade = (ctypes.c_uint64 * 2)()
+    if dos:
+        N.check(L.cvr_read_shade_counters(r.device.handle, shade), "shade", r.device.handle)
+        N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 0), "opt", r.device.handle)
 
     for _ in range(a.warmup):
         step_once()
@@ -188,8 +239,7 @@ def main():
     fptr_nt = ctypes.byref(out_nt)
 
     def step_timed():
-        N.check(L.cvr_render_rc1pass(r.device.handle, fptr, pptr, fptr_nt),
-                "cvr_render_rc1pass", r.device.handle)
+        N.check(render(r.device.handle, fptr, pptr, fptr_nt), "render", r.device.handle)
 
     if world > 1:
         dist.barrier()
@@ -239,16 +289,32 @@ def main():
         # per sample + float4 output per pixel (+ 48 B per sample for the Phong gradient,
         # counted on every sample as an upper bound of the shaded ones)
         b_alg = 8 * 1 * S_rank + 16 * pixels + (48 * S_rank if a.phong else 0)
+        if dos:
+            # + 8 fp16 corners (16 B) per trilinear extinction fetch of the cones
+            f_occ, f_sdw = cone_fetches(r, n, scale)
+            fetches = shade[0] * f_occ + shade[1] * f_sdw
+            b_alg += 16 * fetches
         achieved = b_alg / (kern_ms * 1e-3) / 1e9
-        wkey = f"rc1pass_{a.field}{n}_{W}x{H}{'_phong' if a.phong else ''}"
+        wkey = f"{a.renderer}_{a.field}{n}_{W}x{H}{'_phong' if a.phong else ''}"
+        kname = ("dos_tile_kernel" if dos else
+                 f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, *, false, true>")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic(a.pmc, wkey),
-                "kernel": f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, *, false, true>",
+                "traffic": load_traffic(a.pmc if not dos else a.pmc.replace("rc1pass", "dos"),
+                                        wkey),
+                "kernel": kname,
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank}
+        if dos:
+            roof.update({"shaded_samples": shade[0], "shadow_lit_samples": shade[1],
+                         "cone_fetches_per_shaded": [f_occ, f_sdw],
+                         "secondary_fetches": fetches})
+        metric = ("Msamples/s (rays x steps), rc1pass ray-march, 512^3 volume at 1024^2"
+                  if not dos else
+                  "Msamples/s (rays x steps), Dir. Occlusion Shading (cone AO + cone shadows), "
+                  "512^3 volume at 2048^2")
         res = {
-            "metric": "Msamples/s (rays x steps), rc1pass ray-march, 512^3 volume at 1024^2",
+            "metric": metric,
             "value": round(msps, 2),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -261,7 +327,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"rc1pass emission-absorption, Marschner-Lobb {n}^3 u8 "
+            "config": {"workload": (f"rc1pass emission-absorption, " if not dos else
+                                    f"rc1pdosct cone AO (20 deg, <=3 rays) + point-light cone "
+                                    f"shadows (0.5 deg), extinction pyramid 128^3, ")
+                                   + f"Marschner-Lobb {n}^3 u8 "
                                    f"({a.field}), {W}x{H}, bonsai_01.tf1d, camera "
                                    f"'Initial State', step 0.5, ERT 0.99"
                                    + (", Blinn-Phong FD gradient" if a.phong else ""),
@@ -274,8 +343,17 @@ def main():
             "roofline": roof,
         }
         if world == 1 and not a.no_cpu_baseline:
+            dos_cfg = None
+            if dos:
+                dos_cfg = {"tf_rgba": tf_rgba, "res": r.ext_res,
+                           "occ": cone_tables_for(r.sampler_occlusion, n, scale, 0.50),
+                           "sdw": cone_tables_for(r.sampler_shadow, n, scale, 0.75),
+                           "light": {"position": rp.light_position,
+                                     "forward": rp.light_forward, "up": rp.light_up,
+                                     "right": rp.light_right,
+                                     "spot_angle_deg": rp.spot_light_angle}}
             res["cpu_baseline"] = cpu_baseline(vol, scale, tf, D.INITIAL_STATE_CAMERA, W, H,
-                                               a.cpu_seconds)
+                                               a.cpu_seconds, dos_cfg)
         print(json.dumps(res))
     if world > 1:
         dist.barrier()

@@ -204,6 +204,9 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_occ; free_dev(p); c->d_occ = nullptr;
   p = c->d_tf_prefix; free_dev(p); c->d_tf_prefix = nullptr;
   p = c->d_ext; free_dev(p); c->d_ext = nullptr;
+  p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr;
+  p = c->d_ext_levels; free_dev(p); c->d_ext_levels = nullptr;
+  p = c->d_shade; free_dev(p); c->d_shade = nullptr;
   p = c->d_cones; free_dev(p); c->d_cones = nullptr;
   delete[] c->cone_tab;
   p = c->d_total; free_dev(p); c->d_total = nullptr;
@@ -255,6 +258,10 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     if (value < 0 || value > 100) return fail(c, CVR_ERR_ARG, "quad must be a percentage");
     c->quad_pct = value;
     for (auto& o : c->oslot) o.valid = 0;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "shade_counters")) {
+    c->shade_counters = value ? 1 : 0;
     return CVR_OK;
   }
   if (!std::strcmp(key, "tile_stats")) {
@@ -347,6 +354,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "occ_empty_permille"))   // read-only: empty macro cells (after a render)
     return c->occ_valid ? (int)(c->occ_empty * 1000.0f + 0.5f) : -1;
   if (!std::strcmp(key, "tile_stats")) return c->tile_stats;
+  if (!std::strcmp(key, "shade_counters")) return c->shade_counters;
   if (!std::strcmp(key, "quad")) return c->quad_pct;
   if (!std::strcmp(key, "kernel_timing")) return (int)c->ev_start.size();
   return -1;
@@ -398,6 +406,7 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
   c->mm_shift = -1;
   c->occ_valid = 0;
   { void* p = c->d_ext; free_dev(p); c->d_ext = nullptr; c->ext_levels = 0; }
+  { void* p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr; }
   c->cone_valid = 0;
   HIP_TRY(c, hipMalloc((void**)&c->d_lut, nv * sizeof(uint16_t)));
   uint16_t* d_lut = c->d_lut;
@@ -763,6 +772,16 @@ cvr_status cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int* 
   return CVR_OK;
 }
 
+cvr_status cvr_read_shade_counters(cvr_ctx* ctx, uint64_t out[2]) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c || !out) return CVR_ERR_ARG;
+  if (!c->d_shade) return fail(c, CVR_ERR_STATE, "shade_counters option was not enabled");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpy(out, c->d_shade, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return CVR_OK;
+}
+
 cvr_status cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* out_frames) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c || !out_frames || max_frames < 0 || (max_frames > 0 && !ms)) return CVR_ERR_ARG;
@@ -827,17 +846,42 @@ cvr_status cvr_set_extinction_volume(cvr_ctx* ctx, const float* tf_rgba, int n, 
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   { void* p = c->d_ext; free_dev(p); c->d_ext = nullptr; c->ext_levels = 0; }
+  { void* p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr; }
+  // cell8 texels are addressed with 32-bit byte offsets (16 B each)
+  if (off[nl] > (1LL << 28)) return fail(c, CVR_ERR_ARG, "cvr_set_extinction_volume: resolution too large");
   float4* d_tf = nullptr;
   HIP_TRY(c, hipMalloc((void**)&d_tf, (size_t)n * 16));
   hipError_t e = hipMemcpy(d_tf, q.data(), (size_t)n * 16, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_ext, (size_t)off[nl] * sizeof(uint16_t));
-  if (e == hipSuccess) e = cvr::launch_ext_volume(*c, d_tf, n, res, sigma0, nl, off, c->d_ext, c->stream);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_ext_cells, (size_t)off[nl] * sizeof(uint4));
+  if (e == hipSuccess)
+    e = cvr::launch_ext_volume(*c, d_tf, n, res, sigma0, nl, off, c->d_ext, c->d_ext_cells, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   (void)hipFree(d_tf);
   if (e != hipSuccess) {
     void* p = c->d_ext; free_dev(p); c->d_ext = nullptr;
+    p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr;
     return fail(c, e == hipErrorOutOfMemory ? CVR_ERR_OOM : CVR_ERR_HIP,
                 "cvr_set_extinction_volume: %s", hipGetErrorString(e));
+  }
+  {
+    cvr::ExtLevel lv[cvr::kMaxExtLevels] = {};
+    for (int L = 0; L < nl; L++) {
+      int d[3];
+      for (int i = 0; i < 3; i++) d[i] = std::max(1, res[i] >> L);
+      lv[L].off = (int)off[L];
+      lv[L].dx = d[0]; lv[L].dy = d[1]; lv[L].dz = d[2];
+      const float G[3] = {(float)c->N[0] * c->scale[0], (float)c->N[1] * c->scale[1],
+                          (float)c->N[2] * c->scale[2]};
+      lv[L].sx = (float)d[0] / G[0];   // d / G, rounded once
+      lv[L].sy = (float)d[1] / G[1];
+      lv[L].sz = (float)d[2] / G[2];
+      lv[L].mx = (float)(d[0] - 1);
+      lv[L].my = (float)(d[1] - 1);
+      lv[L].mz = (float)(d[2] - 1);
+    }
+    if (!c->d_ext_levels) HIP_TRY(c, hipMalloc((void**)&c->d_ext_levels, sizeof(lv)));
+    HIP_TRY(c, hipMemcpy(c->d_ext_levels, lv, sizeof(lv), hipMemcpyHostToDevice));
   }
   for (int i = 0; i < 3; i++) c->ext_res[i] = res[i];
   c->ext_levels = nl;
@@ -928,10 +972,7 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   for (int i = 0; i < 3; i++) { Q.a.ispec[i] = p->ispecular[i]; Q.a.light[i] = p->light.position[i]; }
   for (int i = 0; i < 3; i++) Q.G[i] = (float)c->N[i] * c->scale[i];
   Q.ext_levels = c->ext_levels;
-  for (int L = 0; L < c->ext_levels; L++) {
-    for (int i = 0; i < 3; i++) Q.ext_dim[L][i] = std::max(1, c->ext_res[i] >> L);
-    Q.ext_off[L] = c->ext_off[L];
-  }
+  Q.levels = c->d_ext_levels;
   Q.apply_occlusion = p->apply_occlusion != 0;
   Q.apply_shadow = p->apply_shadow != 0;
   Q.shadow_type = p->shadow_type;
@@ -988,7 +1029,13 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   const size_t nev = c->ev_start.size();
   const size_t slot = nev ? (size_t)(c->timed_frames % (long long)nev) : 0;
   if (nev) HIP_TRY(c, hipEventRecord(c->ev_start[slot], s));
-  HIP_TRY(c, cvr::launch_dos(*c, Q, d_out, d_samples, tile_samples, s));
+  unsigned long long* shade = nullptr;
+  if (c->shade_counters) {
+    if (!c->d_shade) HIP_TRY(c, hipMalloc((void**)&c->d_shade, 2 * sizeof(unsigned long long)));
+    HIP_TRY(c, hipMemsetAsync(c->d_shade, 0, 2 * sizeof(unsigned long long), s));
+    shade = c->d_shade;
+  }
+  HIP_TRY(c, cvr::launch_dos(*c, Q, d_out, d_samples, shade, tile_samples, s));
   if (nev) {
     HIP_TRY(c, hipEventRecord(c->ev_stop[slot], s));
     c->timed_frames++;

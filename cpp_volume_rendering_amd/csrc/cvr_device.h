@@ -39,6 +39,24 @@ __device__ __forceinline__ float cvr_expf(float x) {
   return ldexpf(y, (int)n);
 }
 
+// cvr_expf for x <= 0 (not NaN), without branches: the polynomial path on the
+// argument clamped into range, then 0 below -86 -- the same value as cvr_expf.
+__device__ __forceinline__ float cvr_expf_nonpos(float x) {
+  const float xc = fmaxf(x, -86.0f);
+  float n = rintf(xc * 1.44269504088896341f);
+  float r = fmaf(n, -0.693359375f, xc);
+  r = fmaf(n, 2.12194440e-4f, r);
+  float p = 1.9875691500e-4f;
+  p = fmaf(p, r, 1.3981999507e-3f);
+  p = fmaf(p, r, 8.3334519073e-3f);
+  p = fmaf(p, r, 4.1665795894e-2f);
+  p = fmaf(p, r, 1.6666665459e-1f);
+  p = fmaf(p, r, 5.0000001201e-1f);
+  float r2 = r * r;
+  float y = fmaf(p, r2, r) + 1.0f;
+  return x < -86.0f ? 0.0f : ldexpf(y, (int)n);
+}
+
 // ln(x), CVR-SPEC (identical to oracle cvr_logf): Cephes logf polynomial.
 __device__ __forceinline__ float cvr_logf(float x) {
   if (x != x) return x;

@@ -58,6 +58,15 @@ struct Rc1passArgs {
 constexpr int kMaxTfLds = 4096;          // TF entries a kernel stages into LDS
 constexpr int kMaxExtLevels = 16;        // extinction mip levels (up to 32768^3)
 
+// One level of the extinction pyramid as the cone fetches address it.
+struct ExtLevel {
+  int off;                           // first cell8 texel of the level
+  int dx, dy, dz;                    // dimensions
+  float sx, sy, sz;                  // d / G: texel coordinate = fma(p, d/G, -0.5)
+  float mx, my, mz;                  // d - 1 (clamp-to-edge bound)
+  int pad[2];
+};
+
 // Directional-occlusion shading (dos.hip): one cone's tables on the device.
 struct DosCone {
   int counts[3];                     // sections of 1, 3, 7 rays
@@ -70,8 +79,7 @@ struct DosArgs {
   Rc1passArgs a;                     // ray, volume, TF, Blinn-Phong constants, tiles
   float G[3];                        // VolumeScaledSizes
   int ext_levels;
-  int ext_dim[kMaxExtLevels][3];
-  long long ext_off[kMaxExtLevels];  // element offset of each level
+  const struct ExtLevel* levels;     // per level, device memory (read by scalar loads)
   int apply_occlusion, apply_shadow, shadow_type, phong;
   float ka, kd, ks;                  // Kambient if occlusion, Kdiffuse/Kspecular if shadow, else 0
   float lfwd[3], lup[3], lright[3];  // light camera vectors (RenderingParameters)
@@ -133,6 +141,8 @@ struct Ctx {
   int debug_keep = 0;              // diagnostics (option "debug_keep"): render only the longest entries
   int boost_pct = 5;               // % of every band's longest entries run at raised priority
   int quad_pct = 0;                // % of every band's longest tiles marched 4 lanes per ray
+  int shade_counters = 0;          // DOS/EBS: count shaded and shadow-lit samples
+  unsigned long long* d_shade = nullptr;   // [2]: shaded, lit (last frame)
   int tile_stats = 0;              // record per-tile timing (diagnostics)
   unsigned long long* d_tile_stats = nullptr;
   int tile_stats_n = 0;
@@ -164,7 +174,9 @@ struct Ctx {
   hipEvent_t ev_frame = nullptr;   // end of a frame's ray-march (the side stream waits on it)
   int num_cus = 0;
   // extinction-coefficient mip volume (directional occlusion)
-  uint16_t* d_ext = nullptr;       // fp16 levels, concatenated
+  uint16_t* d_ext = nullptr;       // fp16 levels, concatenated (x-fastest)
+  uint4* d_ext_cells = nullptr;    // the same levels as cell8 (8 fp16 corners per texel)
+  ExtLevel* d_ext_levels = nullptr;  // [kMaxExtLevels] addressing of the levels
   int ext_res[3] = {0, 0, 0};
   int ext_levels = 0;
   long long ext_off[kMaxExtLevels + 1] = {};
@@ -200,8 +212,10 @@ hipError_t launch_occupancy(const uint32_t* minmax, int n_macro, const uint16_t*
                             hipStream_t s);
 hipError_t launch_ext_volume(const Ctx& c, const float4* d_tf_rgba, int tf_n, const int res[3],
                              float sigma0, int nlevels, const long long* off, uint16_t* d_ext,
+                             uint4* d_ext_cells,
                              hipStream_t s);
 hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,
+                      unsigned long long* shade,
                       unsigned long long* tile_samples, hipStream_t s);
 hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
                                int nranks, int tiles_per_rank_max, hipStream_t s);

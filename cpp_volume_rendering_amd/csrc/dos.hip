@@ -136,9 +136,29 @@ __global__ void ext_to_tau_kernel(uint16_t* __restrict__ lv, long long n) {
   if (i < n) lv[i] = f2h_rne(-1.0f * cvr_logf(1.0f - h2f(lv[i])));
 }
 
+// The cone fetches read cell8 texels: texel (i, j, k) of a level holds its 8
+// trilinear corners (i|i+1, j|j+1, k|k+1, the +1 clamped to the edge) as fp16,
+// so one dwordx4 load feeds one fetch (the volume's own layout, see sample_pos).
+__global__ void ext_cells_kernel(const uint16_t* __restrict__ lv, uint4* __restrict__ cells, int dx,
+                                 int dy, int dz) {
+  const long long n = (long long)dx * dy * dz;
+  const long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  const int i = (int)(v % dx), j = (int)((v / dx) % dy), k = (int)(v / ((long long)dx * dy));
+  const int i1 = min(i + 1, dx - 1), j1 = min(j + 1, dy - 1), k1 = min(k + 1, dz - 1);
+  const long long sy = dx, sz = (long long)dx * dy;
+  auto at = [&](int x, int y, int z) -> uint32_t { return lv[z * sz + y * sy + x]; };
+  uint4 c;
+  c.x = at(i, j, k) | (at(i1, j, k) << 16);
+  c.y = at(i, j1, k) | (at(i1, j1, k) << 16);
+  c.z = at(i, j, k1) | (at(i1, j, k1) << 16);
+  c.w = at(i, j1, k1) | (at(i1, j1, k1) << 16);
+  cells[v] = c;
+}
+
 hipError_t launch_ext_volume(const Ctx& c, const float4* d_tf_rgba, int tf_n, const int res[3],
                              float sigma0, int nlevels, const long long* off, uint16_t* d_ext,
-                             hipStream_t s) {
+                             uint4* d_ext_cells, hipStream_t s) {
   if (tf_n > kMaxTfLds) return hipErrorInvalidValue;
   ExtBuildArgs E{};
   E.cells = c.cells;
@@ -165,7 +185,18 @@ hipError_t launch_ext_volume(const Ctx& c, const float4* d_tf_rgba, int tf_n, co
   }
   const long long n = off[nlevels];
   hipLaunchKernelGGL(ext_to_tau_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_ext, n);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  for (int L = 0; L < nlevels; L++) {
+    int d[3];
+    for (int i = 0; i < 3; i++) d[i] = res[i] >> L > 1 ? res[i] >> L : 1;
+    const long long nv = off[L + 1] - off[L];
+    hipLaunchKernelGGL(ext_cells_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s,
+                       d_ext + off[L], d_ext_cells + off[L], d[0], d[1], d[2]);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // ---------------------------------------------------------------------------
@@ -173,22 +204,52 @@ hipError_t launch_ext_volume(const Ctx& c, const float4* d_tf_rgba, int tf_n, co
 // ---------------------------------------------------------------------------
 
 // GetGaussianExtinction (:92-112): textureLod at an integer level (clamped to the
-// pyramid), plus the CONSIDER_BORDERS attenuation outside the volume box.
-__device__ __forceinline__ float gge(const DosArgs& Q, const uint16_t* __restrict__ ext, f3 p,
-                                     float mip) {
-  int L = (int)mip;
-  L = min(max(L, 0), Q.ext_levels - 1);
-  const int* d = Q.ext_dim[L];
-  const float ux = p.x / Q.G[0], uy = p.y / Q.G[1], uz = p.z / Q.G[2];
-  float rg = sample_level(ext + Q.ext_off[L], d, fmaf(ux, (float)d[0], -0.5f),
-                          fmaf(uy, (float)d[1], -0.5f), fmaf(uz, (float)d[2], -0.5f));
-  if (p.x < 0.0f || p.x > Q.G[0] || p.y < 0.0f || p.y > Q.G[1] || p.z < 0.0f || p.z > Q.G[2]) {
-    const float sg = ldexpf(1.0f, (int)mip);   // pow(2.0, mip) of an integer level
-    const float cx = fminf(fmaxf(p.x, 0.0f), Q.G[0]) - p.x;
-    const float cy = fminf(fmaxf(p.y, 0.0f), Q.G[1]) - p.y;
-    const float cz = fminf(fmaxf(p.z, 0.0f), Q.G[2]) - p.z;
+// pyramid; the level is wave-uniform, a section-table entry), plus the
+// CONSIDER_BORDERS attenuation outside the volume box.  Split in two so that a
+// batch of fetches issues all its loads before any of them is consumed.
+struct ExtTap {
+  uint32_t off;       // byte offset of the cell8 texel
+  float ax, ay, az;
+};
+
+// A level's addressing, by scalar loads (the index is wave-uniform).
+__device__ __forceinline__ ExtLevel load_level(const ExtLevel* lv, int L) {
+#if __HIP_DEVICE_COMPILE__
+  return ((const __attribute__((address_space(4))) ExtLevel*)lv)[L];
+#else
+  return lv[L];
+#endif
+}
+
+__device__ __forceinline__ ExtTap ext_tap(const ExtLevel& l, f3 p) {
+  const float x = __builtin_amdgcn_fmed3f(fmaf(p.x, l.sx, -0.5f), 0.0f, l.mx);
+  const float y = __builtin_amdgcn_fmed3f(fmaf(p.y, l.sy, -0.5f), 0.0f, l.my);
+  const float z = __builtin_amdgcn_fmed3f(fmaf(p.z, l.sz, -0.5f), 0.0f, l.mz);
+  ExtTap t;
+  // dims <= 2^12 and < 2^28 cells in all (checked on the host): 24-bit multiplies
+  const uint32_t row = __umul24((uint32_t)z, (uint32_t)l.dy) + (uint32_t)y;
+  t.off = (__umul24(row, (uint32_t)l.dx) + (uint32_t)x + (uint32_t)l.off) << 4;
+  t.ax = __builtin_amdgcn_fractf(x);
+  t.ay = __builtin_amdgcn_fractf(y);
+  t.az = __builtin_amdgcn_fractf(z);
+  return t;
+}
+
+__device__ __forceinline__ float ext_value(const DosArgs& Q, uint4 raw, const ExtTap& t, f3 p,
+                                           float mip) {
+  float rg = trilerp_cell(raw, t.ax, t.ay, t.az);
+  const bool outside = (p.x < 0.0f) | (p.x > Q.G[0]) | (p.y < 0.0f) | (p.y > Q.G[1]) |
+                       (p.z < 0.0f) | (p.z > Q.G[2]);
+  if (outside) {
+    // -(dist) / ((2 sg) sg) with sg = pow(2, mip): the divisor is 2^(2 mip + 1),
+    // so the quotient is exactly the product with 2^-(2 mip + 1)
+    const float inv = ldexpf(1.0f, -(2 * (int)mip + 1));
+    // clamp(p, 0, G) - p (positions are finite: med3 == min(max()))
+    const float cx = __builtin_amdgcn_fmed3f(p.x, 0.0f, Q.G[0]) - p.x;
+    const float cy = __builtin_amdgcn_fmed3f(p.y, 0.0f, Q.G[1]) - p.y;
+    const float cz = __builtin_amdgcn_fmed3f(p.z, 0.0f, Q.G[2]) - p.z;
     const float dist = (cx * cx + cy * cy) + cz * cz;
-    rg = rg * cvr_expf(-(dist) / ((2.0f * sg) * sg));
+    rg = rg * cvr_expf_nonpos(-(dist) * inv);
   }
   return rg;
 }
@@ -204,22 +265,103 @@ __device__ __forceinline__ f3 cross3(f3 x, f3 y) {   // glm / GLSL cross, no fma
   return f3{x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y};
 }
 
+// The level of a section (uniform: every lane walks the same table entry).
+__device__ __forceinline__ int level_of(const DosArgs& Q, float mip) {
+  return __builtin_amdgcn_readfirstlane(min(max((int)mip, 0), Q.ext_levels - 1));
+}
+
+// Sections of a J-ray stage, U at a time: the positions of U consecutive
+// sections depend only on the (uniform) table, so their U*J loads are issued
+// together, and the trapezoid sums then run in section order (the same
+// arithmetic as one section at a time).
+// The section table is read-only for the kernel's lifetime: read it through the
+// constant address space so that its (uniform) entries come in by scalar loads.
+__device__ __forceinline__ float4 load_section(const float4* sec, int i) {
+#if __HIP_DEVICE_COMPILE__
+  return ((const __attribute__((address_space(4))) float4*)sec)[i];
+#else
+  return sec[i];
+#endif
+}
+typedef const float4* ConstSections;
+
+template <int J, int U, int J0 = 0, int JN = J>
+__device__ __forceinline__ void cone_sections(const DosArgs& Q, const DosCone& C,
+                                              const uint4* __restrict__ ext, const float4 (&e)[U],
+                                              const float (&tr)[U], const f3 (&vk)[J], f3 pos,
+                                              float (&rays)[7], float (&last)[7]) {
+  f3 p[U][JN];
+  ExtTap tap[U][JN];
+  uint4 raw[U][JN];
+#pragma unroll
+  for (int q = 0; q < U; q++) {
+    const ExtLevel l = load_level(Q.levels, level_of(Q, e[q].y));
+#pragma unroll
+    for (int j = 0; j < JN; j++) {
+      p[q][j] = vmad(vk[J0 + j], tr[q], pos);
+      tap[q][j] = ext_tap(l, p[q][j]);
+      raw[q][j] = *(const uint4*)((const char*)ext + tap[q][j].off);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < U; q++)
+#pragma unroll
+    for (int j = 0; j < JN; j++) {
+      const float v = ext_value(Q, raw[q][j], tap[q][j], p[q][j], e[q].y) * e[q].w;
+      rays[J0 + j] += ((last[J0 + j] + v) * e[q].z) * C.ui_weight;
+      last[J0 + j] = v;
+    }
+}
+
+// U sections of a J-ray stage starting at table entry s (uniform).  The 7-ray
+// stage is split 4 + 3 rays to bound the fetches (registers) in flight.
+template <int J, int U>
+__device__ __forceinline__ void cone_step(const DosArgs& Q, const DosCone& C,
+                                          const uint4* __restrict__ ext, ConstSections sec, int s,
+                                          float& track, const f3 (&vk)[J], f3 pos,
+                                          float (&rays)[7], float (&last)[7]) {
+  float4 e[U];
+  float tr[U];
+#pragma unroll
+  for (int q = 0; q < U; q++) {
+    e[q] = load_section(sec, s + q);
+    tr[q] = track;
+    track += e[q].x;
+  }
+  if (J == 7) {
+    cone_sections<J, U, 0, 4>(Q, C, ext, e, tr, vk, pos, rays, last);
+    cone_sections<J, U, 4, 3>(Q, C, ext, e, tr, vk, pos, rays, last);
+  } else {
+    cone_sections<J, U>(Q, C, ext, e, tr, vk, pos, rays, last);
+  }
+}
+
+template <int J, int U>
+__device__ __forceinline__ void cone_stage(const DosArgs& Q, const DosCone& C,
+                                           const uint4* __restrict__ ext, ConstSections sec, int& s,
+                                           int n, float& track, const f3 (&vk)[J], f3 pos,
+                                           float (&rays)[7], float (&last)[7]) {
+  int i = 0;
+  for (; i + U <= n; i += U, s += U)
+    cone_step<J, U>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last);
+  for (; i < n; i++, s++)
+    cone_step<J, 1>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last);
+}
+
 // Cone1/3/7 RayOcclusion and Cone1/3/7 RayShadow (the same accumulation): the
 // visibility exp(-sum) of a cone from `pos` along k, split 1 -> 3 -> 7 rays.
-__device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint16_t* __restrict__ ext,
+// Every lane walks the same section table (wave-uniform loads and levels).
+__device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __restrict__ ext,
                             f3 pos, f3 k, f3 u, f3 v) {
   float rays[7], last[7];
   float track = C.initial_step;
   rays[0] = 0.0f;
   last[0] = 0.0f;
-  const float4* sec = C.sections;
+  const ConstSections sec = C.sections;
   int s = 0;
-  for (int i = 0; i < C.counts[0]; i++, s++) {
-    const float4 e = sec[s];
-    const float amptau = gge(Q, ext, vmad(k, track, pos), e.y) * e.w;
-    rays[0] += ((last[0] + amptau) * e.z) * C.ui_weight;
-    last[0] = amptau;
-    track += e.x;
+  {
+    const f3 vk[1] = {k};
+    cone_stage<1, 4>(Q, C, ext, sec, s, C.counts[0], track, vk, pos, rays, last);
   }
   if (C.counts[1] + C.counts[2] == 0) return cvr_expf(-rays[0]);
   rays[2] = rays[0]; rays[1] = rays[0];
@@ -228,16 +370,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint16_t* 
     f3 vk[3];
 #pragma unroll
     for (int j = 0; j < 3; j++) vk[j] = cone_axis(C.axes + 3 * j, k, u, v);
-    for (int i = 0; i < C.counts[1]; i++, s++) {
-      const float4 e = sec[s];
-#pragma unroll
-      for (int j = 0; j < 3; j++) {
-        const float amptau = gge(Q, ext, vmad(vk[j], track, pos), e.y) * e.w;
-        rays[j] += ((last[j] + amptau) * e.z) * C.ui_weight;
-        last[j] = amptau;
-      }
-      track += e.x;
-    }
+    cone_stage<3, 2>(Q, C, ext, sec, s, C.counts[1], track, vk, pos, rays, last);
   }
   if (C.counts[2] == 0)
     return ((cvr_expf(-rays[0]) + cvr_expf(-rays[1])) + cvr_expf(-rays[2])) / 3.0f;
@@ -252,18 +385,11 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint16_t* 
   const float avgt = ((last[2] + last[1]) + last[0]) / 3.0f;
   last[2] = last[1] = last[0];
   last[0] = avgt;
-  f3 vk[7];
+  {
+    f3 vk[7];
 #pragma unroll
-  for (int j = 0; j < 7; j++) vk[j] = cone_axis(C.axes + 3 * (3 + j), k, u, v);
-  for (int i = 0; i < C.counts[2]; i++, s++) {
-    const float4 e = sec[s];
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
-      const float amptau = gge(Q, ext, vmad(vk[j], track, pos), e.y) * e.w;
-      rays[j] += ((last[j] + amptau) * e.z) * C.ui_weight;
-      last[j] = amptau;
-    }
-    track += e.x;
+    for (int j = 0; j < 7; j++) vk[j] = cone_axis(C.axes + 3 * (3 + j), k, u, v);
+    cone_stage<7, 1>(Q, C, ext, sec, s, C.counts[2], track, vk, pos, rays, last);
   }
   float side = cvr_expf(-rays[1]);
 #pragma unroll
@@ -272,16 +398,37 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint16_t* 
 }
 
 // ---------------------------------------------------------------------------
-// The march
+// The march: one wave = one 8x8 tile, shading deferred into full-wave batches
 // ---------------------------------------------------------------------------
+//
+// The opacity of a sample, and with it the ERT break and the sample count, does
+// not depend on its shading (ShadeSample changes rgb only).  So each lane marches
+// its ray and, for every sample with alpha > 0, appends a shading job (position,
+// TF colour, alpha, 1 - dst.a before it) to its queue in LDS, advancing dst.a at
+// once.  When the wave holds >= 64 jobs (or no lane can march further) the jobs
+// are compacted and shaded 64 at a time, one per lane, so the 52 + 159 cone
+// fetches of a job run at full wave occupancy whatever the rays' divergence.
+// Each lane then folds its own results into dst.rgb in sample order with the
+// same fma as the sequential loop: the image is bit-identical to it.
 
-// One wave = one 8x8 tile (XCD b%8 takes a contiguous band of tiles).
+constexpr int kJobsPerLane = 4;
+constexpr int kJobSlots = 64 * kJobsPerLane;
+
+template <bool PHONG>
 __global__ void __launch_bounds__(64)
 dos_tile_kernel(DosArgs Q, const uint4* __restrict__ cells, const uint2* __restrict__ grad,
-                const float4* __restrict__ tf_g, const uint16_t* __restrict__ ext,
+                const float4* __restrict__ tf_g, const uint4* __restrict__ ext,
                 float4* __restrict__ out, uint32_t* __restrict__ samples,
+                unsigned long long* __restrict__ shade,
                 unsigned long long* __restrict__ tile_samples) {
   extern __shared__ float4 tfp[];
+  __shared__ float jpx[kJobSlots], jpy[kJobSlots], jpz[kJobSlots];   // tx_pos
+  __shared__ float jr[kJobSlots], jg[kJobSlots], jb[kJobSlots];      // TF rgb -> shaded rgb * a
+  __shared__ float ja[kJobSlots], jom[kJobSlots];                    // alpha, 1 - dst.a
+  __shared__ float jnx[PHONG ? kJobSlots : 1], jny[PHONG ? kJobSlots : 1],
+      jnz[PHONG ? kJobSlots : 1];                                     // gradient (Phong)
+  __shared__ uint16_t jlist[kJobSlots];
+  __shared__ float lane_up[3][64], lane_right[3][64];
   load_tf_lds(tfp, tf_g, Q.a.tf_n);
   const Rc1passArgs& A = Q.a;
   const int b = blockIdx.x, nt = A.ntiles;
@@ -292,31 +439,94 @@ dos_tile_kernel(DosArgs Q, const uint4* __restrict__ cells, const uint2* __restr
   tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
   const bool inside = px < A.W && py < A.H;
   float4 dst = make_float4(0.f, 0.f, 0.f, 0.f);
-  uint32_t cnt = 0;
+  uint32_t cnt = 0, nshade = 0, nlit = 0;
   Ray r;
-  if (inside && ray_setup(A, px, py, r)) {
-    const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
-    const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
-    const f3 light{A.light[0], A.light[1], A.light[2]};
+  bool active = inside && ray_setup(A, px, py, r);
+  if (active) {
+    // eye-space frame of the occlusion cones (:681-684)
     const f3 v_right = normalize3(cross3(r.cam, f3{0.0f, 1.0f, 0.0f}));
     const f3 v_up = normalize3(cross3(f3{-r.cam.x, -r.cam.y, -r.cam.z}, v_right));
-    const float step = A.step, D = r.D, fn = (float)A.tf_n;
-    const float inv_k = 1.0f / (Q.ka + Q.kd);
-    float s = 0.0f;
-    while (s < D) {
-      const float h = fminf(step, D - s);
-      const float tt = fmaf(h, 0.5f, s);
-      const SamplePos sp = sample_pos(fmaf(r.dt.x, tt, r.o.x), fmaf(r.dt.y, tt, r.o.y),
-                                      fmaf(r.dt.z, tt, r.o.z), A);
-      float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
-      cnt++;
-      if (sc.w > 0.0f) {
-        const f3 tx = vmad(r.dir, tt, r.tpos);        // tx_pos, box at [0, G]
+    lane_up[0][lane] = v_up.x; lane_up[1][lane] = v_up.y; lane_up[2][lane] = v_up.z;
+    lane_right[0][lane] = v_right.x; lane_right[1][lane] = v_right.y; lane_right[2][lane] = v_right.z;
+    active = 0.0f < r.D;
+  }
+  const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
+  const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
+  const f3 light{A.light[0], A.light[1], A.light[2]};
+  const float step = A.step, fn = (float)A.tf_n;
+  const float inv_k = 1.0f / (Q.ka + Q.kd);
+  float s = 0.0f;
+
+  for (;;) {
+    // ---- march until the wave holds a full batch of jobs --------------------
+    int n = 0;            // this lane's queued jobs
+    int queued = 0;       // the wave's (uniform)
+    for (;;) {
+      const bool can = active && n < kJobsPerLane;
+      if (__ballot(can) == 0) break;
+      bool pushed = false;
+      if (can) {
+        const float h = fminf(step, r.D - s);
+        const float tt = fmaf(h, 0.5f, s);
+        const SamplePos sp = sample_pos(fmaf(r.dt.x, tt, r.o.x), fmaf(r.dt.y, tt, r.o.y),
+                                        fmaf(r.dt.z, tt, r.o.z), A);
+        const float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
+        cnt++;
+        if (sc.w > 0.0f) {
+          const int slot = lane * kJobsPerLane + n;
+          const f3 tx = vmad(r.dir, tt, r.tpos);        // tx_pos, box at [0, G]
+          jpx[slot] = tx.x; jpy[slot] = tx.y; jpz[slot] = tx.z;
+          jr[slot] = sc.x; jg[slot] = sc.y; jb[slot] = sc.z;
+          const float a = 1.0f - cvr_expf(-(sc.w * h));
+          const float om = 1.0f - dst.w;
+          ja[slot] = a;
+          jom[slot] = om;
+          if (PHONG) {
+            Texel txl;
+            txl.ix = sp.ix; txl.iy = sp.iy; txl.iz = sp.iz;
+            txl.ax = sp.ax; txl.ay = sp.ay; txl.az = sp.az;
+            const f3 g = sample_gradient(grad, A.N, txl);
+            jnx[slot] = g.x; jny[slot] = g.y; jnz[slot] = g.z;
+          }
+          dst.w = fmaf(om, a, dst.w);
+          n++;
+          pushed = true;
+          if (dst.w > 0.99f) active = false;
+        }
+        if (active) {
+          s = s + h;
+          active = s < r.D;
+        }
+      }
+      queued += __popcll(__ballot(pushed));
+      if (queued >= 64) break;
+    }
+    if (queued == 0) break;   // nobody could march: every ray is done
+
+    // ---- compact the queues: exclusive prefix of n from its bit planes -----
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const unsigned long long b0 = __ballot(n & 1), b1 = __ballot(n & 2), b2 = __ballot(n & 4);
+    const int first = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+    for (int j = 0; j < kJobsPerLane; j++)
+      if (j < n) jlist[first + j] = (uint16_t)(lane * kJobsPerLane + j);
+    __syncthreads();
+
+    // ---- shade 64 jobs at a time (ShadeSample, :607-656) --------------------
+    for (int base = 0; base < queued; base += 64) {
+      const int f = base + lane;
+      if (f < queued) {
+        const int slot = jlist[f];
+        const int owner = slot / kJobsPerLane;
+        const f3 tx{jpx[slot], jpy[slot], jpz[slot]};
         const f3 wp{tx.x - hg.x, tx.y - hg.y, tx.z - hg.z};
+        float4 sc = make_float4(jr[slot], jg[slot], jb[slot], 0.0f);
+        const float a = ja[slot];
         float iocc = 0.0f, isdw = 0.0f;
         if (Q.apply_occlusion) {
           const f3 k = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
-          iocc = cone_trace(Q, Q.occ, ext, tx, k, v_up, v_right);
+          const f3 vu{lane_up[0][owner], lane_up[1][owner], lane_up[2][owner]};
+          const f3 vr{lane_right[0][owner], lane_right[1][owner], lane_right[2][owner]};
+          iocc = cone_trace(Q, Q.occ, ext, tx, k, vu, vr);
         }
         if (Q.apply_shadow) {
           f3 k, u, v;
@@ -333,42 +543,54 @@ dos_tile_kernel(DosArgs Q, const uint4* __restrict__ cells, const uint2* __restr
             if (Q.shadow_type == 1 && dot3(k, lf) < Q.spot_cos) lit = false;
           }
           // Cone1RayShadow(pos, k, v, u) is called as (pos, k, u, v): swapped (:559-561)
-          isdw = lit ? cone_trace(Q, Q.sdw, ext, tx, k, v, u) : 0.0f;
+          if (lit) {
+            isdw = cone_trace(Q, Q.sdw, ext, tx, k, v, u);
+            nlit++;
+          }
         }
-        if (Q.phong) {
-          Texel txl;
-          txl.ix = sp.ix; txl.iy = sp.iy; txl.iz = sp.iz;
-          txl.ax = sp.ax; txl.ay = sp.ay; txl.az = sp.az;
-          const f3 g = sample_gradient(grad, A.N, txl);
+        bool shaded = false;
+        if (PHONG) {
+          const f3 g{jnx[slot], jny[slot], jnz[slot]};
           if (g.x != 0.0f || g.y != 0.0f || g.z != 0.0f) {
-            const f3 n = normalize3(g);
+            const f3 nrm = normalize3(g);
             const f3 L = normalize3(f3{light.x - wp.x, light.y - wp.y, light.z - wp.z});
             const f3 Ve = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
             const f3 Hv = normalize3(f3{Ve.x + L.x, Ve.y + L.y, Ve.z + L.z});
-            const float dd = fmaxf(0.0f, dot3(n, L));
-            const float ds = fmaxf(0.0f, dot3(Hv, n));
+            const float dd = fmaxf(0.0f, dot3(nrm, L));
+            const float ds = fmaxf(0.0f, dot3(Hv, nrm));
             const float diff = inv_k * (iocc * Q.ka + (isdw * Q.kd) * dd);
             const float spec = (isdw * Q.ks) * cvr_powf(ds, A.shininess);
             sc.x = fmaf(A.ispec[0], spec, sc.x * diff);
             sc.y = fmaf(A.ispec[1], spec, sc.y * diff);
             sc.z = fmaf(A.ispec[2], spec, sc.z * diff);
           }
-        } else {
+          shaded = true;
+        }
+        if (!shaded) {
           sc.x = inv_k * ((sc.x * iocc) * Q.ka + (sc.x * isdw) * Q.kd);
           sc.y = inv_k * ((sc.y * iocc) * Q.ka + (sc.y * isdw) * Q.kd);
           sc.z = inv_k * ((sc.z * iocc) * Q.ka + (sc.z * isdw) * Q.kd);
         }
-        const float a = 1.0f - cvr_expf(-(sc.w * h));
-        const float om = 1.0f - dst.w;
-        dst.x = fmaf(om, sc.x * a, dst.x);
-        dst.y = fmaf(om, sc.y * a, dst.y);
-        dst.z = fmaf(om, sc.z * a, dst.z);
-        dst.w = fmaf(om, a, dst.w);
-        if (dst.w > 0.99f) break;
+        jr[slot] = sc.x * a;
+        jg[slot] = sc.y * a;
+        jb[slot] = sc.z * a;
       }
-      s = s + h;
     }
+    __syncthreads();
+
+    // ---- fold the results in sample order (front-to-back, :719-727) ---------
+    for (int j = 0; j < kJobsPerLane; j++)
+      if (j < n) {
+        const int slot = lane * kJobsPerLane + j;
+        const float om = jom[slot];
+        dst.x = fmaf(om, jr[slot], dst.x);
+        dst.y = fmaf(om, jg[slot], dst.y);
+        dst.z = fmaf(om, jb[slot], dst.z);
+      }
+    nshade += n;
+    __syncthreads();
   }
+
   if (inside || A.packed) {
     out[oidx] = dst;
     if (samples) samples[oidx] = cnt;
@@ -377,17 +599,29 @@ dos_tile_kernel(DosArgs Q, const uint4* __restrict__ cells, const uint2* __restr
     const unsigned long long v = wave_sum(cnt);
     if (lane == 0) tile_samples[t] = v;
   }
+  if (shade) {   // measurement only (secondary-fetch count of the roofline)
+    const unsigned long long sa = wave_sum(nshade), sl = wave_sum(nlit);
+    if (lane == 0) {
+      atomicAdd(&shade[0], sa);
+      atomicAdd(&shade[1], sl);
+    }
+  }
 }
 
 hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,
-                      unsigned long long* tile_samples, hipStream_t s) {
+                      unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
   if (q.a.ntiles <= 0) return hipSuccess;
   if (q.a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
   const size_t lds = (size_t)(q.a.tf_n + 2) * sizeof(float4);
   const uint4* cells = (const uint4*)c.d_cells + c.cells.linear_origin;
-  hipLaunchKernelGGL(dos_tile_kernel, dim3(q.a.ntiles), dim3(64), lds, s, q, cells,
-                     (const uint2*)c.d_grad, (const float4*)c.d_tf, (const uint16_t*)c.d_ext, out,
-                     samples, tile_samples);
+  if (q.phong)
+    hipLaunchKernelGGL(dos_tile_kernel<true>, dim3(q.a.ntiles), dim3(64), lds, s, q, cells,
+                       (const uint2*)c.d_grad, (const float4*)c.d_tf, c.d_ext_cells, out, samples,
+                       shade, tile_samples);
+  else
+    hipLaunchKernelGGL(dos_tile_kernel<false>, dim3(q.a.ntiles), dim3(64), lds, s, q, cells,
+                       (const uint2*)c.d_grad, (const float4*)c.d_tf, c.d_ext_cells, out, samples,
+                       shade, tile_samples);
   return hipGetLastError();
 }
 

@@ -199,7 +199,9 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                of the macro cells are empty for the current volume and TF
  *   "tile_stats" 1: record per-tile timing of every frame (diagnostics)
  *   "kernel_timing" N > 0: time the ray-march kernel of the last N frames
- *                (cvr_read_kernel_times); 0 off (default) */
+ *                (cvr_read_kernel_times); 0 off (default)
+ *   "shade_counters" 1: count shaded / shadow-lit samples of cvr_render_dosct
+ *                (cvr_read_shade_counters; one atomic per wave) */
 cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
 int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);
@@ -274,6 +276,13 @@ cvr_status  cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int*
  * launch) for the most recent min(N, frames since the last read, max_frames)
  * frames, oldest first.  Waits for those frames; resets the frame count. */
 cvr_status  cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* out_frames);
+
+/* Measurement (shade_counters option): samples of the last shaded frame
+ * (cvr_render_dosct) that ran the shading kernel (alpha > 0), and those of
+ * them whose shadow cone was traced (spot-light cut-off excluded).  Each
+ * traces counts[0] + 3 counts[1] + 7 counts[2] trilinear extinction fetches
+ * per cone: the secondary traffic of the roofline. */
+cvr_status  cvr_read_shade_counters(cvr_ctx* ctx, uint64_t out[2]);
 
 /* ----------------------------------------------------------------------------
  * Host-side helpers (native replacements for the reference's MSVC-only

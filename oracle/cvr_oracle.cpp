@@ -666,10 +666,12 @@ struct ExtVol {
     int d[3];
     ext_level_dims(res, L, d);
     Tex t{v + off[L], {d[0], d[1], d[2]}, 1};
-    const v3 u = mk(p.x / G.x, p.y / G.y, p.z / G.z);
+    // texel coordinate p/G*d - 0.5 as fma(p, d/G, -0.5) with d/G rounded once
+    // (the convention of the volume fetch, n_over_g in the march)
+    const v3 s = mk((float)d[0] / G.x, (float)d[1] / G.y, (float)d[2] / G.z);
     float rg;
-    t.sample(std::fmaf(u.x, (float)d[0], -0.5f), std::fmaf(u.y, (float)d[1], -0.5f),
-             std::fmaf(u.z, (float)d[2], -0.5f), &rg);
+    t.sample(std::fmaf(p.x, s.x, -0.5f), std::fmaf(p.y, s.y, -0.5f), std::fmaf(p.z, s.z, -0.5f),
+             &rg);
     if (p.x < 0.0f || p.x > G.x || p.y < 0.0f || p.y > G.y || p.z < 0.0f || p.z > G.z) {
       const float sg = std::ldexp(1.0f, (int)mip);   // pow(2.0, mip) of an integer level
       const v3 c = mk(std::fmin(std::fmax(p.x, 0.0f), G.x) - p.x, std::fmin(std::fmax(p.y, 0.0f), G.y) - p.y,
@@ -749,8 +751,9 @@ float cone_trace(const ExtVol& E, const OracleDosCone& C, v3 pos, v3 k, v3 u, v3
 
 }  // namespace
 
-ORACLE_API uint64_t oracle_render_dos(const OracleDos* Q, float* out_rgba, uint32_t* out_counts,
-                                      int nthreads) {
+// Rows [y0, y1) of the frame (the whole frame: 0, H).  out: W*H*4, counts: W*H.
+ORACLE_API uint64_t oracle_render_dos_rows(const OracleDos* Q, int y0, int y1, float* out_rgba,
+                                           uint32_t* out_counts, int nthreads) {
   const OracleRc1pass& P = Q->base;
   float V[16], tanf;
   oracle_lookat(P.eye, P.center, P.up, P.fovy_deg, V, &tanf);
@@ -784,8 +787,10 @@ ORACLE_API uint64_t oracle_render_dos(const OracleDos* Q, float* out_rgba, uint3
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
+  y0 = std::max(0, y0);
+  y1 = std::min(H, y1);
 #pragma omp parallel for schedule(dynamic, 1)
-  for (int py = 0; py < H; py++) {
+  for (int py = y0; py < y1; py++) {
     for (int px = 0; px < W; px++) {
       const int64_t pix = (int64_t)py * W + px;
       float dst[4] = {0, 0, 0, 0};
@@ -883,6 +888,11 @@ ORACLE_API uint64_t oracle_render_dos(const OracleDos* Q, float* out_rgba, uint3
     }
   }
   uint64_t total = 0;
-  for (int64_t i = 0; i < (int64_t)W * H; i++) total += counts[i];
+  for (int64_t i = (int64_t)y0 * W; i < (int64_t)y1 * W; i++) total += counts[i];
   return total;
+}
+
+ORACLE_API uint64_t oracle_render_dos(const OracleDos* Q, float* out_rgba, uint32_t* out_counts,
+                                      int nthreads) {
+  return oracle_render_dos_rows(Q, 0, Q->base.H, out_rgba, out_counts, nthreads);
 }

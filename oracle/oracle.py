@@ -80,6 +80,8 @@ def lib():
         L.oracle_ext_volume.restype = I
         L.oracle_render_dos.argtypes = [ctypes.POINTER(OracleDos), P, P, I]
         L.oracle_render_dos.restype = ctypes.c_uint64
+        L.oracle_render_dos_rows.argtypes = [ctypes.POINTER(OracleDos), I, I, P, P, I]
+        L.oracle_render_dos_rows.restype = ctypes.c_uint64
         _lib = L
     return _lib
 
@@ -258,9 +260,10 @@ def _cone(tables, keep):
 def render_dos(vol16, scale, tf_rgbt, ext_levels, camera, W, H, step, occ_tables, sdw_tables,
                apply_occlusion=True, apply_shadow=False, shadow_type=0, light=None,
                grad=None, phong=False, ka=0.5, kd=0.5, ks=0.8, shininess=30.0,
-               ispec=(1.0, 1.0, 1.0), threads: int = 0):
-    """Directional-occlusion shading frame (ray_bbox_marching.comp).  light = dict with
-    position/forward/up/right/spot_angle_deg.  Returns (rgba, counts, S)."""
+               ispec=(1.0, 1.0, 1.0), threads: int = 0, rows=None):
+    """Directional-occlusion shading frame (ray_bbox_marching.comp), or rows=(y0, y1) of
+    it.  light = dict with position/forward/up/right/spot_angle_deg.
+    Returns (rgba, counts, S)."""
     vol16 = np.ascontiguousarray(vol16, np.float32)
     tf = _q16_array(tf_rgbt)
     if grad is not None:
@@ -285,5 +288,7 @@ def render_dos(vol16, scale, tf_rgbt, ext_levels, camera, W, H, step, occ_tables
     Q.sdw = _cone(sdw_tables, keep)
     rgba = np.zeros((H, W, 4), np.float32)
     cnt = np.zeros((H, W), np.uint32)
-    S = lib().oracle_render_dos(ctypes.byref(Q), _p(rgba), _p(cnt), int(threads))
+    y0, y1 = rows if rows is not None else (0, H)
+    S = lib().oracle_render_dos_rows(ctypes.byref(Q), int(y0), int(y1), _p(rgba), _p(cnt),
+                                     int(threads))
     return rgba, cnt, int(S)

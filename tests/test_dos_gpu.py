@@ -189,3 +189,38 @@ def test_dosct_errors(bonsai_tf):
             d.set_extinction_volume(bonsai_tf, (0, 8, 8))
     finally:
         d.close()
+
+
+@pytest.mark.parametrize("nranks,tile", [(2, 32), (3, 16)])
+def test_dosct_screen_tiles_match_full_frame(dev, bonsai_tf, bonsai_tf_rgba, nranks, tile):
+    """Multi-GPU split of the shaded renderer: packed per-rank tiles equal the full frame."""
+    from cpp_volume_rendering_amd import screen_tiles as T
+    vol = D.marschner_lobb_u8(48)
+    scale = D.voxel_scale(48)
+    setup(dev, vol, scale, bonsai_tf, bonsai_tf_rgba, (64, 64, 64))
+    occ, sdw = default_cone_params(True), default_cone_params(False)
+    W, H = 100, 72
+    full, full_cnt, full_total = gpu_dos(dev, INITIAL, W, H, 0.0, occ, sdw, apply_shadow=True)
+    tpr = T.max_tiles_per_rank(W, H, tile, nranks)
+    packed = np.zeros((nranks, tpr, tile, tile, 4), np.float32)
+    tot = 0
+    for r in range(nranks):
+        p = N.DosParams()
+        p.ka, p.kd, p.ks, p.shininess = 0.5, 0.5, 0.8, 30.0
+        p.ispecular[:] = [1.0, 1.0, 1.0]
+        for f in ("position", "forward", "up", "right"):
+            getattr(p.light, f)[:] = list(LIGHT0[f])
+        p.light.spot_angle_deg = LIGHT0["spot_angle_deg"]
+        p.apply_occlusion, p.apply_shadow = 1, 1
+        p.occlusion, p.shadow = occ, sdw
+        k = T.tiles_for_rank(W, H, tile, r, nranks)
+        rgba = np.zeros((k, tile, tile, 4), np.float32)
+        total = np.zeros(1, np.uint64)
+        out = N.Output(rgba.ctypes.data, None, total.ctypes.data, 0)
+        fr = make_frame(Camera(**INITIAL), W, H, tile, r, nranks)
+        N.check(N.lib().cvr_render_dosct(dev.handle, ctypes.byref(fr), ctypes.byref(p),
+                                         ctypes.byref(out)), "dosct tiles", dev.handle)
+        packed[r, :k] = rgba
+        tot += int(total[0])
+    assert tot == full_total
+    assert_bitexact(T.unpack(packed, W, H, tile, nranks), full, "dos tiles")

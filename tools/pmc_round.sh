@@ -15,7 +15,12 @@ IFS=';' read -ra GRPS <<< "${PMC_GROUPS:-$DEFAULT_GROUPS}"
 i=0
 for grp in "${GRPS[@]}"; do
   i=$((i+1))
-  timeout -k 10 ${PMC_TIMEOUT:-90} rocprofv3 --kernel-trace --pmc $grp -d gpurun_out/pmc/g$i -o pmc --output-format csv -- python3 tools/ab_rc1pass.py --variants $VAR --rounds 1 --frames 5 $EXTRA > gpurun_out/pmc/g$i.log 2>&1
+  if [ -n "${PMC_CMD:-}" ]; then
+    # PMC_CMD: another workload, e.g. "bench.py --renderer dos --no-cpu-baseline --steps 1 --warmup 0"
+    timeout -k 10 ${PMC_TIMEOUT:-90} rocprofv3 --kernel-trace --pmc $grp -d gpurun_out/pmc/g$i -o pmc --output-format csv -- python3 $PMC_CMD > gpurun_out/pmc/g$i.log 2>&1
+  else
+    timeout -k 10 ${PMC_TIMEOUT:-90} rocprofv3 --kernel-trace --pmc $grp -d gpurun_out/pmc/g$i -o pmc --output-format csv -- python3 tools/ab_rc1pass.py --variants $VAR --rounds 1 --frames 5 $EXTRA > gpurun_out/pmc/g$i.log 2>&1
+  fi
   rc=$?
   if [ $rc -ne 0 ]; then
     echo "group $grp failed (rc $rc)"; tail -5 gpurun_out/pmc/g$i.log
