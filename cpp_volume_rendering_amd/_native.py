@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "cvr_tf1d_build_rgbt", "cvr_read_tf1d", "cvr_read_raw", "cvr_read_syn",
     "cvr_read_camera_state", "cvr_read_light_position", "cvr_read_light", "cvr_build_cone_tables",
     "cvr_set_extinction_volume", "cvr_copy_extinction_level", "cvr_render_dosct",
+    "cvr_tf1d_ext_lut", "cvr_set_extinction_sat", "cvr_copy_extinction_sat", "cvr_render_extbsd",
 )
 
 
@@ -94,6 +95,18 @@ class DosParams(ctypes.Structure):
                 ("occlusion", ConeParams), ("shadow", ConeParams)]
 
 
+class EbsParams(ctypes.Structure):
+    _fields_ = [("step", ctypes.c_float), ("apply_gradient_shading", ctypes.c_int),
+                ("ka", ctypes.c_float), ("kd", ctypes.c_float), ("ks", ctypes.c_float),
+                ("shininess", ctypes.c_float), ("ispecular", ctypes.c_float * 3),
+                ("light_pos", ctypes.c_float * 3), ("light_forward", ctypes.c_float * 3),
+                ("apply_occlusion", ctypes.c_int), ("occlusion_shells", ctypes.c_int),
+                ("occlusion_radius", ctypes.c_float), ("apply_shadow", ctypes.c_int),
+                ("shadow_type", ctypes.c_int), ("shadow_cone_angle_deg", ctypes.c_float),
+                ("shadow_sample_interval", ctypes.c_float), ("shadow_initial_step", ctypes.c_float),
+                ("shadow_ui_weight", ctypes.c_float), ("shadow_max_distance", ctypes.c_float)]
+
+
 _lib = None
 
 
@@ -153,6 +166,11 @@ def lib() -> ctypes.CDLL:
         "cvr_copy_extinction_level": ([P, I, FP, IP, IP], I),
         "cvr_render_dosct": ([P, ctypes.POINTER(Frame), ctypes.POINTER(DosParams),
                               ctypes.POINTER(Output)], I),
+        "cvr_tf1d_ext_lut": ([DP, I, DP, I, I, I, I, FP], I),
+        "cvr_set_extinction_sat": ([P, FP, I], I),
+        "cvr_copy_extinction_sat": ([P, FP, ctypes.c_size_t, IP], I),
+        "cvr_render_extbsd": ([P, ctypes.POINTER(Frame), ctypes.POINTER(EbsParams),
+                               ctypes.POINTER(Output)], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -123,12 +123,14 @@ float cvr_default_step(const float scale[3]) {
 
 // TransferFunction1D::BuildLinear + GenerateTexture_1D_RGBt
 // (transferfunction1d.cpp:319-358, 89-118; transferfunction.h:79-82).
-cvr_status cvr_tf1d_build_rgbt(const double* rgb_cp, int n_rgb, const double* a_cp, int n_a,
-                               int max_density, int extinction_input, float* out_rgbt) {
-  if (max_density < 1 || !out_rgbt || n_rgb < 0 || n_a < 0) return CVR_ERR_ARG;
+// TransferFunction1D::BuildLinear (transferfunction1d.cpp:319-358): the double
+// table m_transferfunction of max_density + 1 entries.
+static cvr_status build_tf_table(const double* rgb_cp, int n_rgb, const double* a_cp, int n_a,
+                                 int max_density, std::vector<double>& tab) {
+  if (max_density < 1 || n_rgb < 0 || n_a < 0) return CVR_ERR_ARG;
   if ((n_rgb > 0 && !rgb_cp) || (n_a > 0 && !a_cp)) return CVR_ERR_ARG;
   const int n = max_density + 1;
-  std::vector<double> tab((size_t)n * 4, 0.0);   // glm 0.9.5 dvec4 zero-init
+  tab.assign((size_t)n * 4, 0.0);   // glm 0.9.5 dvec4 zero-init
   for (int i = 0; i + 1 < n_rgb; i++) {
     // TransferControlPoint keeps its colour in a glm::vec4 (float)
     float c0[3], c1[3];
@@ -154,6 +156,18 @@ cvr_status cvr_tf1d_build_rgbt(const double* rgb_cp, int n_rgb, const double* a_
       tab[(size_t)x * 4 + 3] = (double)a0 + diff * k;
     }
   }
+  return CVR_OK;
+}
+
+// TransferFunction1D::BuildLinear + GenerateTexture_1D_RGBt
+// (transferfunction1d.cpp:319-358, 89-118; transferfunction.h:79-82).
+cvr_status cvr_tf1d_build_rgbt(const double* rgb_cp, int n_rgb, const double* a_cp, int n_a,
+                               int max_density, int extinction_input, float* out_rgbt) {
+  if (!out_rgbt) return CVR_ERR_ARG;
+  std::vector<double> tab;
+  cvr_status st = build_tf_table(rgb_cp, n_rgb, a_cp, n_a, max_density, tab);
+  if (st != CVR_OK) return st;
+  const int n = max_density + 1;
   for (int i = 0; i < n; i++) {
     out_rgbt[i * 4 + 0] = (float)tab[(size_t)i * 4 + 0];
     out_rgbt[i * 4 + 1] = (float)tab[(size_t)i * 4 + 1];
@@ -161,6 +175,35 @@ cvr_status cvr_tf1d_build_rgbt(const double* rgb_cp, int n_rgb, const double* a_
     float v4 = (float)tab[(size_t)i * 4 + 3];
     if (!extinction_input) v4 = (float)std::log(1.0 / (1.0 - (double)v4));
     out_rgbt[i * 4 + 3] = v4;
+  }
+  return CVR_OK;
+}
+
+// TransferFunction1D::GetExtN(StructuredGridVolume::GetNormalizedSample) for every
+// voxel value: Get(v / (2^bits - 1), 1.0).a (transferfunction1d.cpp:132-157) as
+// float, then MaterialOpacityToExtinction in double (:189-197), as float.
+cvr_status cvr_tf1d_ext_lut(const double* rgb_cp, int n_rgb, const double* a_cp, int n_a,
+                            int max_density, int extinction_input, int bytes_per_voxel,
+                            float* out_lut) {
+  if (!out_lut || (bytes_per_voxel != 1 && bytes_per_voxel != 2)) return CVR_ERR_ARG;
+  std::vector<double> tab;
+  cvr_status st = build_tf_table(rgb_cp, n_rgb, a_cp, n_a, max_density, tab);
+  if (st != CVR_OK) return st;
+  const int nv = bytes_per_voxel == 1 ? 256 : 65536;
+  const double den = bytes_per_voxel == 1 ? (256.0 - 1.0) : (65536.0 - 1.0);
+  for (int v = 0; v < nv; v++) {
+    double value = ((double)v / den) * ((double)max_density / 1.0);
+    float a;
+    if (value < 0.0f || value > (float)max_density) {
+      a = 0.0f;
+    } else if (std::fabs(value - (float)max_density) < 0.000001) {
+      a = (float)tab[(size_t)max_density * 4 + 3];
+    } else {
+      const int iv = (int)value;
+      const double t = value - iv;
+      a = (float)((1.0 - t) * tab[(size_t)iv * 4 + 3] + t * tab[(size_t)(iv + 1) * 4 + 3]);
+    }
+    out_lut[v] = extinction_input ? a : (float)std::log(1.0 / (1.0 - (double)a));
   }
   return CVR_OK;
 }
@@ -206,6 +249,7 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_ext; free_dev(p); c->d_ext = nullptr;
   p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr;
   p = c->d_ext_levels; free_dev(p); c->d_ext_levels = nullptr;
+  p = c->d_sat; free_dev(p); c->d_sat = nullptr;
   p = c->d_shade; free_dev(p); c->d_shade = nullptr;
   p = c->d_cones; free_dev(p); c->d_cones = nullptr;
   delete[] c->cone_tab;
@@ -407,6 +451,7 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
   c->occ_valid = 0;
   { void* p = c->d_ext; free_dev(p); c->d_ext = nullptr; c->ext_levels = 0; }
   { void* p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr; }
+  { void* p = c->d_sat; free_dev(p); c->d_sat = nullptr; }
   c->cone_valid = 0;
   HIP_TRY(c, hipMalloc((void**)&c->d_lut, nv * sizeof(uint16_t)));
   uint16_t* d_lut = c->d_lut;
@@ -814,6 +859,70 @@ cvr_status cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* f, const void*
 }
 
 
+
+// Output handling shared by the shaded renderers (device or host buffers, the
+// sample total through per-tile counts + the sum epilogue, kernel timing events,
+// shade counters).  launch(out, samples, shade, tile_samples, stream).
+extern "C++" {
+template <class Launch>
+static cvr_status render_shaded(Ctx* c, const cvr_output* o, int ntiles, size_t npix,
+                                const Launch& launch) {
+  hipStream_t s = c->stream;
+  float4* d_out;
+  uint32_t* d_samples;
+  unsigned long long* d_total;
+  const size_t rgba_bytes = npix * 16, smp_bytes = npix * 4;
+  if (o->on_device) {
+    d_out = (float4*)o->rgba;
+    d_samples = (uint32_t*)o->samples;
+    d_total = (unsigned long long*)o->total;
+  } else {
+    cvr_status st = ensure_scratch(c, rgba_bytes + (o->samples ? smp_bytes : 0));
+    if (st != CVR_OK) return st;
+    d_out = (float4*)c->d_scratch;
+    d_samples = o->samples ? (uint32_t*)((char*)c->d_scratch + rgba_bytes) : nullptr;
+    d_total = o->total ? c->d_total : nullptr;
+  }
+  if (d_total && !o->on_device) HIP_TRY(c, hipMemsetAsync(d_total, 0, sizeof(unsigned long long), s));
+  unsigned long long* tile_samples = nullptr;
+  if (d_total) {
+    if (c->tile_samples_n < ntiles) {
+      void* q = c->d_tile_samples; free_dev(q); c->d_tile_samples = nullptr; c->tile_samples_n = 0;
+      HIP_TRY(c, hipMalloc((void**)&c->d_tile_samples, (size_t)ntiles * 8));
+      HIP_TRY(c, hipMemsetAsync(c->d_tile_samples, 0, (size_t)ntiles * 8, s));
+      c->tile_samples_n = ntiles;
+    }
+    tile_samples = c->d_tile_samples;
+  }
+  unsigned long long* shade = nullptr;
+  if (c->shade_counters) {
+    if (!c->d_shade) HIP_TRY(c, hipMalloc((void**)&c->d_shade, 2 * sizeof(unsigned long long)));
+    HIP_TRY(c, hipMemsetAsync(c->d_shade, 0, 2 * sizeof(unsigned long long), s));
+    shade = c->d_shade;
+  }
+  const size_t nev = c->ev_start.size();
+  const size_t slot = nev ? (size_t)(c->timed_frames % (long long)nev) : 0;
+  if (nev) HIP_TRY(c, hipEventRecord(c->ev_start[slot], s));
+  HIP_TRY(c, launch(d_out, d_samples, shade, tile_samples, s));
+  if (nev) {
+    HIP_TRY(c, hipEventRecord(c->ev_stop[slot], s));
+    c->timed_frames++;
+  }
+  if (tile_samples) {
+    cvr::RenderPlan plan{};
+    plan.ntiles = ntiles;
+    HIP_TRY(c, cvr::launch_tile_epilogue(nullptr, tile_samples, d_total, plan, nullptr, s));
+  }
+  if (!o->on_device) {
+    HIP_TRY(c, hipMemcpyAsync(o->rgba, d_out, rgba_bytes, hipMemcpyDeviceToHost, s));
+    if (o->samples) HIP_TRY(c, hipMemcpyAsync(o->samples, d_samples, smp_bytes, hipMemcpyDeviceToHost, s));
+    if (o->total) HIP_TRY(c, hipMemcpyAsync(o->total, d_total, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return CVR_OK;
+}
+}  // extern "C++"
+
 // ---------------------------------------------------------------------------
 // Directional-occlusion shading (rc1pdosct)
 // ---------------------------------------------------------------------------
@@ -1000,58 +1109,130 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
     C.sections = c->d_cones + (size_t)k * CVR_MAX_CONE_SECTIONS;
   }
 
-  float4* d_out;
-  uint32_t* d_samples;
-  unsigned long long* d_total;
-  const size_t rgba_bytes = npix * 16, smp_bytes = npix * 4;
-  if (o->on_device) {
-    d_out = (float4*)o->rgba;
-    d_samples = (uint32_t*)o->samples;
-    d_total = (unsigned long long*)o->total;
-  } else {
-    cvr_status st = ensure_scratch(c, rgba_bytes + (o->samples ? smp_bytes : 0));
-    if (st != CVR_OK) return st;
-    d_out = (float4*)c->d_scratch;
-    d_samples = o->samples ? (uint32_t*)((char*)c->d_scratch + rgba_bytes) : nullptr;
-    d_total = o->total ? c->d_total : nullptr;
+  return render_shaded(c, o, ntiles, npix, [&](float4* out, uint32_t* smp, unsigned long long* shade,
+                                                unsigned long long* ts, hipStream_t st) {
+    return cvr::launch_dos(*c, Q, out, smp, shade, ts, st);
+  });
+}
+
+
+// ---------------------------------------------------------------------------
+// Extinction-based shading (rc1pextbsd)
+// ---------------------------------------------------------------------------
+
+cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!c->d_vox) return fail(c, CVR_ERR_STATE, "cvr_set_extinction_sat: no volume set");
+  const int nv = c->bpv == 1 ? 256 : 65536;
+  if (!ext_lut || lut_n != nv)
+    return fail(c, CVR_ERR_ARG, "cvr_set_extinction_sat: need one extinction per voxel value (%d)", nv);
+  const int w = c->N[0] + 2, h = c->N[1] + 2, d = c->N[2] + 2;
+  const size_t cells = (size_t)w * h * d;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  { void* p = c->d_sat; free_dev(p); c->d_sat = nullptr; }
+  float* d_lut = nullptr;
+  double* d_sd = nullptr;
+  hipError_t e = hipMalloc((void**)&d_lut, (size_t)nv * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(d_lut, ext_lut, (size_t)nv * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_sd, cells * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_sat, cells * sizeof(float));
+  if (e == hipSuccess) e = cvr::launch_sat_build(*c, d_lut, d_sd, c->d_sat, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_lut);
+  (void)hipFree(d_sd);
+  if (e != hipSuccess) {
+    void* p = c->d_sat; free_dev(p); c->d_sat = nullptr;
+    return fail(c, e == hipErrorOutOfMemory ? CVR_ERR_OOM : CVR_ERR_HIP,
+                "cvr_set_extinction_sat: %s", hipGetErrorString(e));
   }
-  if (d_total && !o->on_device) HIP_TRY(c, hipMemsetAsync(d_total, 0, sizeof(unsigned long long), s));
-  unsigned long long* tile_samples = nullptr;
-  if (d_total) {
-    if (c->tile_samples_n < ntiles) {
-      void* q = c->d_tile_samples; free_dev(q); c->d_tile_samples = nullptr; c->tile_samples_n = 0;
-      HIP_TRY(c, hipMalloc((void**)&c->d_tile_samples, (size_t)ntiles * 8));
-      HIP_TRY(c, hipMemsetAsync(c->d_tile_samples, 0, (size_t)ntiles * 8, s));
-      c->tile_samples_n = ntiles;
-    }
-    tile_samples = c->d_tile_samples;
-  }
-  const size_t nev = c->ev_start.size();
-  const size_t slot = nev ? (size_t)(c->timed_frames % (long long)nev) : 0;
-  if (nev) HIP_TRY(c, hipEventRecord(c->ev_start[slot], s));
-  unsigned long long* shade = nullptr;
-  if (c->shade_counters) {
-    if (!c->d_shade) HIP_TRY(c, hipMalloc((void**)&c->d_shade, 2 * sizeof(unsigned long long)));
-    HIP_TRY(c, hipMemsetAsync(c->d_shade, 0, 2 * sizeof(unsigned long long), s));
-    shade = c->d_shade;
-  }
-  HIP_TRY(c, cvr::launch_dos(*c, Q, d_out, d_samples, shade, tile_samples, s));
-  if (nev) {
-    HIP_TRY(c, hipEventRecord(c->ev_stop[slot], s));
-    c->timed_frames++;
-  }
-  if (tile_samples) {
-    cvr::RenderPlan plan{};
-    plan.ntiles = ntiles;
-    HIP_TRY(c, cvr::launch_tile_epilogue(nullptr, tile_samples, d_total, plan, nullptr, s));
-  }
-  if (!o->on_device) {
-    HIP_TRY(c, hipMemcpyAsync(o->rgba, d_out, rgba_bytes, hipMemcpyDeviceToHost, s));
-    if (o->samples) HIP_TRY(c, hipMemcpyAsync(o->samples, d_samples, smp_bytes, hipMemcpyDeviceToHost, s));
-    if (o->total) HIP_TRY(c, hipMemcpyAsync(o->total, d_total, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-  }
+  c->sat_dims[0] = w; c->sat_dims[1] = h; c->sat_dims[2] = d;
   return CVR_OK;
+}
+
+cvr_status cvr_copy_extinction_sat(cvr_ctx* ctx, float* out, size_t capacity, int dims[3]) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!c->d_sat) return fail(c, CVR_ERR_STATE, "cvr_copy_extinction_sat: no SAT built");
+  if (dims) for (int i = 0; i < 3; i++) dims[i] = c->sat_dims[i];
+  if (!out) return CVR_OK;
+  const size_t n = (size_t)c->sat_dims[0] * c->sat_dims[1] * c->sat_dims[2];
+  if (capacity < n) return fail(c, CVR_ERR_ARG, "cvr_copy_extinction_sat: buffer too small");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpy(out, c->d_sat, n * sizeof(float), hipMemcpyDeviceToHost));
+  return CVR_OK;
+}
+
+cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_params* p,
+                             const cvr_output* o) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: null argument");
+  if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
+    return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: bad viewport %dx%d", f->width, f->height);
+  if (!c->d_cells || !c->d_tf) return fail(c, CVR_ERR_STATE, "cvr_render_extbsd: no volume or TF");
+  if (!c->d_sat) return fail(c, CVR_ERR_STATE, "cvr_render_extbsd: needs cvr_set_extinction_sat");
+  const bool phong = p->apply_gradient_shading != 0;
+  if (phong && !c->d_grad) return fail(c, CVR_ERR_STATE, "cvr_render_extbsd: Phong needs cvr_set_gradient");
+  if (p->shadow_type < 0 || p->shadow_type > 1) return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: bad shadow type");
+  if (p->apply_occlusion && p->occlusion_shells < 1)
+    return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: need >= 1 occlusion shell");
+  if (p->apply_shadow && !(p->shadow_sample_interval > 0.0f))
+    return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: shadow sample interval must be positive");
+  if (f->nranks > 1 && (f->tile_size < 16 || f->tile_size % 16 != 0 || f->rank < 0 || f->rank >= f->nranks))
+    return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: bad tiling");
+  HIP_TRY(c, hipSetDevice(c->device));
+
+  cvr::EbsArgs Q{};
+  int ntiles = 0;
+  size_t npix = 0;
+  fill_frame_args(c, f, p->step, Q.a, ntiles, npix);
+  Q.a.ka = p->ka; Q.a.kd = p->kd; Q.a.ks = p->ks;
+  Q.a.shininess = p->shininess;
+  for (int i = 0; i < 3; i++) { Q.a.ispec[i] = p->ispecular[i]; Q.a.light[i] = p->light_pos[i]; }
+  for (int i = 0; i < 3; i++) {
+    Q.S[i] = c->scale[i];
+    Q.G[i] = (float)c->N[i] * c->scale[i];
+    Q.inv_vs[i] = 1.0f / (Q.G[i] + Q.S[i] * 2.0f);        // inv_vol_scaled (:75)
+    Q.sat_dims[i] = c->sat_dims[i];
+    Q.nsat[i] = (float)c->sat_dims[i];
+    Q.nsat_m1[i] = (float)(c->sat_dims[i] - 1);
+    Q.min_sat[i] = Q.S[i] * 0.5f;                        // MinSATPosition (:66)
+    Q.max_sat[i] = Q.G[i] + Q.S[i] * 1.5f;               // MaxSATPosition (:67)
+    Q.lfwd[i] = p->light_forward[i];
+  }
+  Q.apply_occlusion = p->apply_occlusion != 0;
+  Q.occ_shells = p->occlusion_shells;
+  Q.occ_radius = p->occlusion_radius;
+  Q.apply_shadow = p->apply_shadow != 0;
+  Q.shadow_type = p->shadow_type;
+  Q.phong = phong;
+  // DirSdwConeAngle = (float)(angle * pi / 180.0) (ebsrenderer.cpp:161); its cos / sin
+  const float ang = (float)(p->shadow_cone_angle_deg * 3.14159265358979323846 / 180.0);
+  Q.p_cs = std::cos(ang); Q.p_sn = std::sin(ang);
+  Q.n_cs = std::cos(-ang); Q.n_sn = std::sin(-ang);
+  Q.interval = p->shadow_sample_interval;
+  Q.initial_step = p->shadow_initial_step;
+  Q.ui_weight = p->shadow_ui_weight;
+  if (p->shadow_max_distance > 0.0f) {
+    Q.max_distance = p->shadow_max_distance;
+  } else {
+    // dir_cone_max_distance = 0.75f * Dv (ebsrenderer.cpp:98-105, float arithmetic)
+    const float vw = (float)((double)c->N[0] * (double)c->scale[0]);
+    const float vh = (float)((double)c->N[1] * (double)c->scale[1]);
+    const float vd = (float)((double)c->N[2] * (double)c->scale[2]);
+    Q.max_distance = 0.75f * std::sqrt((vw * vw + vh * vh) + vd * vd);
+  }
+  // ShadeSample (:502-518): ka only with occlusion, kd/ks only with shadows
+  Q.ka = Q.apply_occlusion ? p->ka : 0.0f;
+  Q.kd = Q.apply_shadow ? p->kd : 0.0f;
+  Q.ks = Q.apply_shadow ? p->ks : 0.0f;
+  return render_shaded(c, o, ntiles, npix, [&](float4* out, uint32_t* smp, unsigned long long* shade,
+                                                unsigned long long* ts, hipStream_t st) {
+    return cvr::launch_ebs(*c, Q, out, smp, shade, ts, st);
+  });
 }
 
 #pragma GCC visibility pop

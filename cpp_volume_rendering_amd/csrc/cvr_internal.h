@@ -87,6 +87,23 @@ struct DosArgs {
   DosCone occ, sdw;
 };
 
+// Extinction-based shading (ebs.hip): the SAT and the shader's uniforms.
+struct EbsArgs {
+  Rc1passArgs a;                     // ray, volume, TF, Blinn-Phong constants, tiles
+  float S[3], G[3];                  // VolumeScales, VolumeScaledSizes
+  float inv_vs[3];                   // 1 / (G + 2 S)
+  float nsat[3], nsat_m1[3];         // SAT dims as float, and dims - 1
+  int sat_dims[3];
+  float min_sat[3], max_sat[3];      // S / 2, G + 1.5 S
+  int apply_occlusion, occ_shells;
+  float occ_radius;
+  int apply_shadow, shadow_type, phong;
+  float p_cs, p_sn, n_cs, n_sn;      // cos / sin of +-DirSdwConeAngle
+  float interval, initial_step, ui_weight, max_distance;
+  float lfwd[3];
+  float ka, kd, ks;                  // Kambient if occlusion, Kdiffuse/Kspecular if shadow, else 0
+};
+
 // How one frame is cut into work: one 8x8 wave tile per workgroup.
 struct RenderPlan {
   int ntiles;                        // 8x8 wave tiles (one workgroup each)
@@ -177,6 +194,9 @@ struct Ctx {
   uint16_t* d_ext = nullptr;       // fp16 levels, concatenated (x-fastest)
   uint4* d_ext_cells = nullptr;    // the same levels as cell8 (8 fp16 corners per texel)
   ExtLevel* d_ext_levels = nullptr;  // [kMaxExtLevels] addressing of the levels
+  // extinction-based shading: the float SAT of (N+2) cells per axis
+  float* d_sat = nullptr;
+  int sat_dims[3] = {0, 0, 0};
   int ext_res[3] = {0, 0, 0};
   int ext_levels = 0;
   long long ext_off[kMaxExtLevels + 1] = {};
@@ -214,6 +234,10 @@ hipError_t launch_ext_volume(const Ctx& c, const float4* d_tf_rgba, int tf_n, co
                              float sigma0, int nlevels, const long long* off, uint16_t* d_ext,
                              uint4* d_ext_cells,
                              hipStream_t s);
+hipError_t launch_sat_build(const Ctx& c, const float* d_lut, double* d_sd, float* d_sf,
+                            hipStream_t s);
+hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* samples,
+                      unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s);
 hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade,
                       unsigned long long* tile_samples, hipStream_t s);

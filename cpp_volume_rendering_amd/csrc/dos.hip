@@ -18,6 +18,7 @@
 
 #include "cvr_device.h"
 #include "march_common.h"
+#include "shaded_march.h"
 
 namespace cvr {
 
@@ -254,15 +255,9 @@ __device__ __forceinline__ float ext_value(const DosArgs& Q, uint4 raw, const Ex
   return rg;
 }
 
-__device__ __forceinline__ f3 vmad(f3 d, float t, f3 p) {
-  return f3{fmaf(d.x, t, p.x), fmaf(d.y, t, p.y), fmaf(d.z, t, p.z)};
-}
 __device__ __forceinline__ f3 cone_axis(const float* a, f3 k, f3 u, f3 v) {
   return f3{fmaf(v.x, a[0], fmaf(u.x, a[1], k.x * a[2])), fmaf(v.y, a[0], fmaf(u.y, a[1], k.y * a[2])),
             fmaf(v.z, a[0], fmaf(u.z, a[1], k.z * a[2]))};
-}
-__device__ __forceinline__ f3 cross3(f3 x, f3 y) {   // glm / GLSL cross, no fma
-  return f3{x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y};
 }
 
 // The level of a section (uniform: every lane walks the same table entry).
@@ -398,231 +393,73 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
 }
 
 // ---------------------------------------------------------------------------
-// The march: one wave = one 8x8 tile, shading deferred into full-wave batches
+// ShadeSample (ray_bbox_marching.comp:607-656) for the deferred march
 // ---------------------------------------------------------------------------
-//
-// The opacity of a sample, and with it the ERT break and the sample count, does
-// not depend on its shading (ShadeSample changes rgb only).  So each lane marches
-// its ray and, for every sample with alpha > 0, appends a shading job (position,
-// TF colour, alpha, 1 - dst.a before it) to its queue in LDS, advancing dst.a at
-// once.  When the wave holds >= 64 jobs (or no lane can march further) the jobs
-// are compacted and shaded 64 at a time, one per lane, so the 52 + 159 cone
-// fetches of a job run at full wave occupancy whatever the rays' divergence.
-// Each lane then folds its own results into dst.rgb in sample order with the
-// same fma as the sequential loop: the image is bit-identical to it.
 
-constexpr int kJobsPerLane = 4;
-constexpr int kJobSlots = 64 * kJobsPerLane;
+struct DosShader {
+  using Args = DosArgs;
+  using Data = const uint4*;   // the cell8 extinction pyramid
 
-template <bool PHONG>
-__global__ void __launch_bounds__(64)
-dos_tile_kernel(DosArgs Q, const uint4* __restrict__ cells, const uint2* __restrict__ grad,
-                const float4* __restrict__ tf_g, const uint4* __restrict__ ext,
-                float4* __restrict__ out, uint32_t* __restrict__ samples,
-                unsigned long long* __restrict__ shade,
-                unsigned long long* __restrict__ tile_samples) {
-  extern __shared__ float4 tfp[];
-  __shared__ float jpx[kJobSlots], jpy[kJobSlots], jpz[kJobSlots];   // tx_pos
-  __shared__ float jr[kJobSlots], jg[kJobSlots], jb[kJobSlots];      // TF rgb -> shaded rgb * a
-  __shared__ float ja[kJobSlots], jom[kJobSlots];                    // alpha, 1 - dst.a
-  __shared__ float jnx[PHONG ? kJobSlots : 1], jny[PHONG ? kJobSlots : 1],
-      jnz[PHONG ? kJobSlots : 1];                                     // gradient (Phong)
-  __shared__ uint16_t jlist[kJobSlots];
-  __shared__ float lane_up[3][64], lane_right[3][64];
-  load_tf_lds(tfp, tf_g, Q.a.tf_n);
-  const Rc1passArgs& A = Q.a;
-  const int b = blockIdx.x, nt = A.ntiles;
-  const int t = (nt & 7) == 0 ? (b & 7) * (nt >> 3) + (b >> 3) : b;
-  const int lane = threadIdx.x;
-  int px, py;
-  long long oidx;
-  tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
-  const bool inside = px < A.W && py < A.H;
-  float4 dst = make_float4(0.f, 0.f, 0.f, 0.f);
-  uint32_t cnt = 0, nshade = 0, nlit = 0;
-  Ray r;
-  bool active = inside && ray_setup(A, px, py, r);
-  if (active) {
-    // eye-space frame of the occlusion cones (:681-684)
-    const f3 v_right = normalize3(cross3(r.cam, f3{0.0f, 1.0f, 0.0f}));
-    const f3 v_up = normalize3(cross3(f3{-r.cam.x, -r.cam.y, -r.cam.z}, v_right));
-    lane_up[0][lane] = v_up.x; lane_up[1][lane] = v_up.y; lane_up[2][lane] = v_up.z;
-    lane_right[0][lane] = v_right.x; lane_right[1][lane] = v_right.y; lane_right[2][lane] = v_right.z;
-    active = 0.0f < r.D;
-  }
-  const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
-  const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
-  const f3 light{A.light[0], A.light[1], A.light[2]};
-  const float step = A.step, fn = (float)A.tf_n;
-  const float inv_k = 1.0f / (Q.ka + Q.kd);
-  float s = 0.0f;
-
-  for (;;) {
-    // ---- march until the wave holds a full batch of jobs --------------------
-    int n = 0;            // this lane's queued jobs
-    int queued = 0;       // the wave's (uniform)
-    for (;;) {
-      const bool can = active && n < kJobsPerLane;
-      if (__ballot(can) == 0) break;
-      bool pushed = false;
-      if (can) {
-        const float h = fminf(step, r.D - s);
-        const float tt = fmaf(h, 0.5f, s);
-        const SamplePos sp = sample_pos(fmaf(r.dt.x, tt, r.o.x), fmaf(r.dt.y, tt, r.o.y),
-                                        fmaf(r.dt.z, tt, r.o.z), A);
-        const float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
-        cnt++;
-        if (sc.w > 0.0f) {
-          const int slot = lane * kJobsPerLane + n;
-          const f3 tx = vmad(r.dir, tt, r.tpos);        // tx_pos, box at [0, G]
-          jpx[slot] = tx.x; jpy[slot] = tx.y; jpz[slot] = tx.z;
-          jr[slot] = sc.x; jg[slot] = sc.y; jb[slot] = sc.z;
-          const float a = 1.0f - cvr_expf(-(sc.w * h));
-          const float om = 1.0f - dst.w;
-          ja[slot] = a;
-          jom[slot] = om;
-          if (PHONG) {
-            Texel txl;
-            txl.ix = sp.ix; txl.iy = sp.iy; txl.iz = sp.iz;
-            txl.ax = sp.ax; txl.ay = sp.ay; txl.az = sp.az;
-            const f3 g = sample_gradient(grad, A.N, txl);
-            jnx[slot] = g.x; jny[slot] = g.y; jnz[slot] = g.z;
-          }
-          dst.w = fmaf(om, a, dst.w);
-          n++;
-          pushed = true;
-          if (dst.w > 0.99f) active = false;
-        }
-        if (active) {
-          s = s + h;
-          active = s < r.D;
-        }
-      }
-      queued += __popcll(__ballot(pushed));
-      if (queued >= 64) break;
+  // Shaded colour of one job; `lit` counts the shadow cones traced.
+  __device__ static f3 shade(const DosArgs& Q, const uint4* __restrict__ ext, f3 tx, f3 wp,
+                             f3 cam, f3 rgb, const f3* g, uint32_t& lit) {
+    const Rc1passArgs& A = Q.a;
+    const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
+    const f3 light{A.light[0], A.light[1], A.light[2]};
+    float iocc = 0.0f, isdw = 0.0f;
+    if (Q.apply_occlusion) {
+      // eye-space frame of the occlusion cones (:681-684)
+      const f3 v_right = normalize3(cross3(cam, f3{0.0f, 1.0f, 0.0f}));
+      const f3 v_up = normalize3(cross3(f3{-cam.x, -cam.y, -cam.z}, v_right));
+      const f3 k = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
+      iocc = cone_trace(Q, Q.occ, ext, tx, k, v_up, v_right);
     }
-    if (queued == 0) break;   // nobody could march: every ray is done
-
-    // ---- compact the queues: exclusive prefix of n from its bit planes -----
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    const unsigned long long b0 = __ballot(n & 1), b1 = __ballot(n & 2), b2 = __ballot(n & 4);
-    const int first = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
-    for (int j = 0; j < kJobsPerLane; j++)
-      if (j < n) jlist[first + j] = (uint16_t)(lane * kJobsPerLane + j);
-    __syncthreads();
-
-    // ---- shade 64 jobs at a time (ShadeSample, :607-656) --------------------
-    for (int base = 0; base < queued; base += 64) {
-      const int f = base + lane;
-      if (f < queued) {
-        const int slot = jlist[f];
-        const int owner = slot / kJobsPerLane;
-        const f3 tx{jpx[slot], jpy[slot], jpz[slot]};
-        const f3 wp{tx.x - hg.x, tx.y - hg.y, tx.z - hg.z};
-        float4 sc = make_float4(jr[slot], jg[slot], jb[slot], 0.0f);
-        const float a = ja[slot];
-        float iocc = 0.0f, isdw = 0.0f;
-        if (Q.apply_occlusion) {
-          const f3 k = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
-          const f3 vu{lane_up[0][owner], lane_up[1][owner], lane_up[2][owner]};
-          const f3 vr{lane_right[0][owner], lane_right[1][owner], lane_right[2][owner]};
-          iocc = cone_trace(Q, Q.occ, ext, tx, k, vu, vr);
-        }
-        if (Q.apply_shadow) {
-          f3 k, u, v;
-          bool lit = true;
-          const f3 lf{Q.lfwd[0], Q.lfwd[1], Q.lfwd[2]};
-          if (Q.shadow_type == 2) {
-            k = lf;
-            v = f3{Q.lup[0], Q.lup[1], Q.lup[2]};
-            u = f3{Q.lright[0], Q.lright[1], Q.lright[2]};
-          } else {
-            k = normalize3(f3{light.x - wp.x, light.y - wp.y, light.z - wp.z});
-            u = normalize3(cross3(k, f3{Q.lright[0], Q.lright[1], Q.lright[2]}));
-            v = normalize3(cross3(k, u));
-            if (Q.shadow_type == 1 && dot3(k, lf) < Q.spot_cos) lit = false;
-          }
-          // Cone1RayShadow(pos, k, v, u) is called as (pos, k, u, v): swapped (:559-561)
-          if (lit) {
-            isdw = cone_trace(Q, Q.sdw, ext, tx, k, v, u);
-            nlit++;
-          }
-        }
-        bool shaded = false;
-        if (PHONG) {
-          const f3 g{jnx[slot], jny[slot], jnz[slot]};
-          if (g.x != 0.0f || g.y != 0.0f || g.z != 0.0f) {
-            const f3 nrm = normalize3(g);
-            const f3 L = normalize3(f3{light.x - wp.x, light.y - wp.y, light.z - wp.z});
-            const f3 Ve = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
-            const f3 Hv = normalize3(f3{Ve.x + L.x, Ve.y + L.y, Ve.z + L.z});
-            const float dd = fmaxf(0.0f, dot3(nrm, L));
-            const float ds = fmaxf(0.0f, dot3(Hv, nrm));
-            const float diff = inv_k * (iocc * Q.ka + (isdw * Q.kd) * dd);
-            const float spec = (isdw * Q.ks) * cvr_powf(ds, A.shininess);
-            sc.x = fmaf(A.ispec[0], spec, sc.x * diff);
-            sc.y = fmaf(A.ispec[1], spec, sc.y * diff);
-            sc.z = fmaf(A.ispec[2], spec, sc.z * diff);
-          }
-          shaded = true;
-        }
-        if (!shaded) {
-          sc.x = inv_k * ((sc.x * iocc) * Q.ka + (sc.x * isdw) * Q.kd);
-          sc.y = inv_k * ((sc.y * iocc) * Q.ka + (sc.y * isdw) * Q.kd);
-          sc.z = inv_k * ((sc.z * iocc) * Q.ka + (sc.z * isdw) * Q.kd);
-        }
-        jr[slot] = sc.x * a;
-        jg[slot] = sc.y * a;
-        jb[slot] = sc.z * a;
+    if (Q.apply_shadow) {
+      f3 k, u, v;
+      bool on = true;
+      const f3 lf{Q.lfwd[0], Q.lfwd[1], Q.lfwd[2]};
+      if (Q.shadow_type == 2) {
+        k = lf;
+        v = f3{Q.lup[0], Q.lup[1], Q.lup[2]};
+        u = f3{Q.lright[0], Q.lright[1], Q.lright[2]};
+      } else {
+        k = normalize3(f3{light.x - wp.x, light.y - wp.y, light.z - wp.z});
+        u = normalize3(cross3(k, f3{Q.lright[0], Q.lright[1], Q.lright[2]}));
+        v = normalize3(cross3(k, u));
+        if (Q.shadow_type == 1 && dot3(k, lf) < Q.spot_cos) on = false;
+      }
+      // Cone1RayShadow(pos, k, v, u) is called as (pos, k, u, v): swapped (:559-561)
+      if (on) {
+        isdw = cone_trace(Q, Q.sdw, ext, tx, k, v, u);
+        lit++;
       }
     }
-    __syncthreads();
-
-    // ---- fold the results in sample order (front-to-back, :719-727) ---------
-    for (int j = 0; j < kJobsPerLane; j++)
-      if (j < n) {
-        const int slot = lane * kJobsPerLane + j;
-        const float om = jom[slot];
-        dst.x = fmaf(om, jr[slot], dst.x);
-        dst.y = fmaf(om, jg[slot], dst.y);
-        dst.z = fmaf(om, jb[slot], dst.z);
+    const float inv_k = 1.0f / (Q.ka + Q.kd);
+    if (g) {   // ApplyPhongShading
+      if (g->x != 0.0f || g->y != 0.0f || g->z != 0.0f) {
+        const f3 nrm = normalize3(*g);
+        const f3 L = normalize3(f3{light.x - wp.x, light.y - wp.y, light.z - wp.z});
+        const f3 Ve = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
+        const f3 Hv = normalize3(f3{Ve.x + L.x, Ve.y + L.y, Ve.z + L.z});
+        const float dd = fmaxf(0.0f, dot3(nrm, L));
+        const float ds = fmaxf(0.0f, dot3(Hv, nrm));
+        const float diff = inv_k * (iocc * Q.ka + (isdw * Q.kd) * dd);
+        const float spec = (isdw * Q.ks) * cvr_powf(ds, A.shininess);
+        return f3{fmaf(A.ispec[0], spec, rgb.x * diff), fmaf(A.ispec[1], spec, rgb.y * diff),
+                  fmaf(A.ispec[2], spec, rgb.z * diff)};
       }
-    nshade += n;
-    __syncthreads();
-  }
-
-  if (inside || A.packed) {
-    out[oidx] = dst;
-    if (samples) samples[oidx] = cnt;
-  }
-  if (tile_samples) {
-    const unsigned long long v = wave_sum(cnt);
-    if (lane == 0) tile_samples[t] = v;
-  }
-  if (shade) {   // measurement only (secondary-fetch count of the roofline)
-    const unsigned long long sa = wave_sum(nshade), sl = wave_sum(nlit);
-    if (lane == 0) {
-      atomicAdd(&shade[0], sa);
-      atomicAdd(&shade[1], sl);
+      return rgb;
     }
+    return f3{inv_k * ((rgb.x * iocc) * Q.ka + (rgb.x * isdw) * Q.kd),
+              inv_k * ((rgb.y * iocc) * Q.ka + (rgb.y * isdw) * Q.kd),
+              inv_k * ((rgb.z * iocc) * Q.ka + (rgb.z * isdw) * Q.kd)};
   }
-}
+};
 
 hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
-  if (q.a.ntiles <= 0) return hipSuccess;
-  if (q.a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
-  const size_t lds = (size_t)(q.a.tf_n + 2) * sizeof(float4);
-  const uint4* cells = (const uint4*)c.d_cells + c.cells.linear_origin;
-  if (q.phong)
-    hipLaunchKernelGGL(dos_tile_kernel<true>, dim3(q.a.ntiles), dim3(64), lds, s, q, cells,
-                       (const uint2*)c.d_grad, (const float4*)c.d_tf, c.d_ext_cells, out, samples,
-                       shade, tile_samples);
-  else
-    hipLaunchKernelGGL(dos_tile_kernel<false>, dim3(q.a.ntiles), dim3(64), lds, s, q, cells,
-                       (const uint2*)c.d_grad, (const float4*)c.d_tf, c.d_ext_cells, out, samples,
-                       shade, tile_samples);
-  return hipGetLastError();
+  return launch_shaded_march<DosShader>(c, q, q.phong != 0, c.d_ext_cells, out, samples, shade,
+                                        tile_samples, s);
 }
 
 }  // namespace cvr

@@ -1,0 +1,254 @@
+// ebs.hip — extinction-based shading (cppvolrend rc1pextbsd) on gfx950.
+//
+// The march of shaded_march.h with ShadeSample of ebs_ray_bbox_marching.comp
+// (:498-550): an ambient occlusion from 15 concentric SAT boxes around the
+// sample (ExtinctionAmbientOcclusion :109-146, 120 SAT fetches) and a shadow
+// from a chain of SAT boxes along the dominant axis of the light direction,
+// widened by the cone angle (ExtinctionDirectionalShadows / ConeX|Y|ZAxis
+// :187-481; up to ~N/2 boxes of 8 fetches).  A SAT fetch is the GL_LINEAR
+// texture(TexVolumeSAT3D, p / (G + 2 s)) of the float SAT (sat.hip).
+// Arithmetic follows CVR-SPEC as oracle/cvr_oracle.cpp (oracle_render_ebs_rows)
+// does, op for op, so the images are bit-identical.  Compiled -ffp-contract=off.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "cvr_device.h"
+#include "march_common.h"
+#include "shaded_march.h"
+
+namespace cvr {
+
+namespace {
+
+// GetSummed3Density (:77-83): trilinear of the float SAT at u = p * inv_vol_scaled.
+__device__ __forceinline__ float sat_fetch(const EbsArgs& Q, const float* __restrict__ sat, float x,
+                                           float y, float z) {
+  const float tx = __builtin_amdgcn_fmed3f(fmaf(x * Q.inv_vs[0], Q.nsat[0], -0.5f), 0.0f, Q.nsat_m1[0]);
+  const float ty = __builtin_amdgcn_fmed3f(fmaf(y * Q.inv_vs[1], Q.nsat[1], -0.5f), 0.0f, Q.nsat_m1[1]);
+  const float tz = __builtin_amdgcn_fmed3f(fmaf(z * Q.inv_vs[2], Q.nsat[2], -0.5f), 0.0f, Q.nsat_m1[2]);
+  const int ix = (int)tx, iy = (int)ty, iz = (int)tz;
+  const float ax = __builtin_amdgcn_fractf(tx), ay = __builtin_amdgcn_fractf(ty),
+              az = __builtin_amdgcn_fractf(tz);
+  const int x1 = min(ix + 1, Q.sat_dims[0] - 1), y1 = min(iy + 1, Q.sat_dims[1] - 1),
+            z1 = min(iz + 1, Q.sat_dims[2] - 1);
+  const long long sy = Q.sat_dims[0], sz = (long long)Q.sat_dims[0] * Q.sat_dims[1];
+  const long long r00 = iz * sz + iy * sy, r10 = iz * sz + y1 * sy;
+  const long long r01 = z1 * sz + iy * sy, r11 = z1 * sz + y1 * sy;
+  const float c00 = lerpf(sat[r00 + ix], sat[r00 + x1], ax);
+  const float c10 = lerpf(sat[r10 + ix], sat[r10 + x1], ax);
+  const float c01 = lerpf(sat[r01 + ix], sat[r01 + x1], ax);
+  const float c11 = lerpf(sat[r11 + ix], sat[r11 + x1], ax);
+  return lerpf(lerpf(c00, c10, ay), lerpf(c01, c11, ay), az);
+}
+
+// EvaluateSAT3D (:85-99)
+__device__ __forceinline__ float sat_box(const EbsArgs& Q, const float* __restrict__ sat, f3 p1, f3 p2) {
+  const float V1 = sat_fetch(Q, sat, p2.x, p2.y, p2.z), V2 = sat_fetch(Q, sat, p1.x, p2.y, p2.z);
+  const float V3 = sat_fetch(Q, sat, p2.x, p2.y, p1.z), V4 = sat_fetch(Q, sat, p1.x, p2.y, p1.z);
+  const float V5 = sat_fetch(Q, sat, p2.x, p1.y, p2.z), V6 = sat_fetch(Q, sat, p1.x, p1.y, p2.z);
+  const float V7 = sat_fetch(Q, sat, p2.x, p1.y, p1.z), V8 = sat_fetch(Q, sat, p1.x, p1.y, p1.z);
+  return (V1 - V2 - V3 + V4 - V5 + V6 + V7 - V8);
+}
+
+// clamp(p + VolumeScales, MinSATPosition, MaxSATPosition)
+__device__ __forceinline__ f3 sat_offset(const EbsArgs& Q, f3 p) {
+  return f3{fminf(fmaxf(p.x + Q.S[0], Q.min_sat[0]), Q.max_sat[0]),
+            fminf(fmaxf(p.y + Q.S[1], Q.min_sat[1]), Q.max_sat[1]),
+            fminf(fmaxf(p.z + Q.S[2], Q.min_sat[2]), Q.max_sat[2])};
+}
+
+// EvaluateShadowSAT3D (:148-185, the texture path)
+__device__ __forceinline__ float shadow_box(const EbsArgs& Q, const float* __restrict__ sat, f3 p1, f3 p2) {
+  const float volquery = ((fabsf(p1.x - p2.x) / Q.S[0])) * ((fabsf(p1.y - p2.y) / Q.S[1])) *
+                         ((fabsf(p1.z - p2.z) / Q.S[2]));
+  return ((sat_box(Q, sat, sat_offset(Q, p1), sat_offset(Q, p2)) / volquery)) * Q.ui_weight;
+}
+
+// ExtinctionAmbientOcclusion (:109-146)
+__device__ float ebs_occlusion(const EbsArgs& Q, const float* __restrict__ sat, f3 tx) {
+  const float R = Q.occ_radius;
+  const f3 r0{R * Q.S[0], R * Q.S[1], R * Q.S[2]};
+  const float SAT_Sh0 = sat_box(Q, sat, sat_offset(Q, f3{tx.x - r0.x, tx.y - r0.y, tx.z - r0.z}),
+                                sat_offset(Q, f3{tx.x + r0.x, tx.y + r0.y, tx.z + r0.z}));
+  const float rsh0 = R;
+  const float tSh0 = SAT_Sh0 * (1.0f / (rsh0 * rsh0));
+  float SAT_Shi = SAT_Sh0, tshi = tSh0;
+  for (int i = 1; i < Q.occ_shells; i++) {
+    const float r1 = R * (float)(i + 1);
+    const f3 ri{r1 * Q.S[0], r1 * Q.S[1], r1 * Q.S[2]};
+    const float SAT_Shi_1 = sat_box(Q, sat, sat_offset(Q, f3{tx.x - ri.x, tx.y - ri.y, tx.z - ri.z}),
+                                    sat_offset(Q, f3{tx.x + ri.x, tx.y + ri.y, tx.z + ri.z}));
+    const float tshi_1 = tshi + (SAT_Shi_1 - SAT_Shi) * (1.0f / (r1 * r1));
+    SAT_Shi = SAT_Shi_1;
+    tshi = tshi_1;
+  }
+  const float rshi = R * (float)Q.occ_shells;
+  const float W_A = 1.0f / (rshi * rshi);
+  const float Stau = W_A * tshi;
+  return cvr_expf(-(Stau));
+}
+
+// ConeZAxis (:187-275)
+__device__ float cone_z(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv) {
+  float Stau = 0.0f;
+  float signal = 1.0f;
+  if (cv.z < 0) signal = -1.0f;
+  const float p_cs = Q.p_cs, p_sn = Q.p_sn, n_cs = Q.n_cs, n_sn = Q.n_sn;
+  const f3 proj_y = normalize3(f3{0.0f, cv.y, cv.z});
+  const f3 proj_x = normalize3(f3{cv.x, 0.0f, cv.z});
+  const f3 pj_x1 = normalize3(f3{proj_x.x * n_cs - proj_x.z * n_sn, 0.0f, proj_x.x * n_sn + proj_x.z * n_cs});
+  const f3 pj_x2 = normalize3(f3{proj_x.x * p_cs - proj_x.z * p_sn, 0.0f, proj_x.x * p_sn + proj_x.z * p_cs});
+  const f3 pj_y1 = normalize3(f3{0.0f, proj_y.y * n_cs - proj_y.z * n_sn, proj_y.y * n_sn + proj_y.z * n_cs});
+  const f3 pj_y2 = normalize3(f3{0.0f, proj_y.y * p_cs - proj_y.z * p_sn, proj_y.y * p_sn + proj_y.z * p_cs});
+  const float si = Q.interval * signal * Q.S[2];
+  float z_pos = Q.initial_step * signal * Q.S[2];
+  const float vmin = Q.S[2] * 0.5f, vmax = Q.G[2] - Q.S[2] * 0.5f;
+  while ((z_pos / cv.z) < Q.max_distance &&
+         (pos.z + (z_pos + si) > vmin && pos.z + (z_pos + si) < vmax)) {
+    const float z_mean = fabsf(z_pos + si * 0.5f);
+    const float p_x1 = pj_x1.x * (z_mean / fabsf(pj_x1.z));
+    const float p_x2 = pj_x2.x * (z_mean / fabsf(pj_x2.z));
+    const float p_y1 = pj_y1.y * (z_mean / fabsf(pj_y1.z));
+    const float p_y2 = pj_y2.y * (z_mean / fabsf(pj_y2.z));
+    float x1 = fminf(p_x1, p_x2), x2 = fmaxf(p_x1, p_x2);
+    float y1 = fminf(p_y1, p_y2), y2 = fmaxf(p_y1, p_y2);
+    const float xdiff = fabsf(x2 - x1), ydiff = fabsf(y2 - y1);
+    const float xs = (ceilf(xdiff / Q.S[0]) - (xdiff / Q.S[0])) * 0.5f;
+    const float ys = (ceilf(ydiff / Q.S[1]) - (ydiff / Q.S[1])) * 0.5f;
+    x1 = x1 - xs * Q.S[0]; x2 = x2 + xs * Q.S[0];
+    y1 = y1 - ys * Q.S[1]; y2 = y2 + ys * Q.S[1];
+    const float z1 = fminf(z_pos, z_pos + si), z2 = fmaxf(z_pos, z_pos + si);
+    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2});
+    z_pos = z_pos + si;
+  }
+  return Stau;
+}
+
+// ConeYAxis (:277-364)
+__device__ float cone_y(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv) {
+  float Stau = 0.0f;
+  float signal = 1.0f;
+  if (cv.y < 0) signal = -1.0f;
+  const float p_cs = Q.p_cs, p_sn = Q.p_sn, n_cs = Q.n_cs, n_sn = Q.n_sn;
+  const f3 proj_x = normalize3(f3{cv.x, cv.y, 0.0f});
+  const f3 proj_z = normalize3(f3{0.0f, cv.y, cv.z});
+  const f3 pj_x1 = normalize3(f3{proj_x.x * n_cs - proj_x.y * n_sn, proj_x.x * n_sn + proj_x.y * n_cs, 0.0f});
+  const f3 pj_x2 = normalize3(f3{proj_x.x * p_cs - proj_x.y * p_sn, proj_x.x * p_sn + proj_x.y * p_cs, 0.0f});
+  const f3 pj_z1 = normalize3(f3{0.0f, proj_z.z * n_sn + proj_z.y * n_cs, proj_z.z * n_cs - proj_z.y * n_sn});
+  const f3 pj_z2 = normalize3(f3{0.0f, proj_z.z * p_sn + proj_z.y * p_cs, proj_z.z * p_cs - proj_z.y * p_sn});
+  const float si = Q.interval * signal * Q.S[1];
+  float y_pos = Q.initial_step * signal * Q.S[1];
+  const float vmin = Q.S[1] * 0.5f, vmax = Q.G[1] - Q.S[1] * 0.5f;
+  while ((y_pos / cv.y) < Q.max_distance &&
+         (pos.y + (y_pos + si) > vmin && pos.y + (y_pos + si) < vmax)) {
+    const float y_mean = fabsf(y_pos + si * 0.5f);
+    const float p_x1 = pj_x1.x * (y_mean / fabsf(pj_x1.y));
+    const float p_x2 = pj_x2.x * (y_mean / fabsf(pj_x2.y));
+    const float p_z1 = pj_z1.z * (y_mean / fabsf(pj_z1.y));
+    const float p_z2 = pj_z2.z * (y_mean / fabsf(pj_z2.y));
+    float x1 = fminf(p_x1, p_x2), x2 = fmaxf(p_x1, p_x2);
+    float z1 = fminf(p_z1, p_z2), z2 = fmaxf(p_z1, p_z2);
+    const float xdiff = fabsf(x2 - x1), zdiff = fabsf(z2 - z1);
+    const float xs = (ceilf(xdiff / Q.S[0]) - (xdiff / Q.S[0])) * 0.5f;
+    const float zs = (ceilf(zdiff / Q.S[2]) - (zdiff / Q.S[2])) * 0.5f;
+    x1 = x1 - xs * Q.S[0]; x2 = x2 + xs * Q.S[0];
+    z1 = z1 - zs * Q.S[2]; z2 = z2 + zs * Q.S[2];
+    const float y1 = fminf(y_pos, y_pos + si), y2 = fmaxf(y_pos, y_pos + si);
+    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2});
+    y_pos = y_pos + si;
+  }
+  return Stau;
+}
+
+// ConeXAxis (:366-453)
+__device__ float cone_x(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv) {
+  float Stau = 0.0f;
+  float signal = 1.0f;
+  if (cv.x < 0) signal = -1.0f;
+  const float p_cs = Q.p_cs, p_sn = Q.p_sn, n_cs = Q.n_cs, n_sn = Q.n_sn;
+  const f3 proj_y = normalize3(f3{cv.x, cv.y, 0.0f});
+  const f3 proj_z = normalize3(f3{cv.x, 0.0f, cv.z});
+  const f3 pj_y1 = normalize3(f3{proj_y.y * n_sn + proj_y.x * n_cs, proj_y.y * n_cs - proj_y.x * n_sn, 0.0f});
+  const f3 pj_y2 = normalize3(f3{proj_y.y * p_sn + proj_y.x * p_cs, proj_y.y * p_cs - proj_y.x * p_sn, 0.0f});
+  const f3 pj_z1 = normalize3(f3{proj_z.z * n_sn + proj_z.x * n_cs, 0.0f, proj_z.z * n_cs - proj_z.x * n_sn});
+  const f3 pj_z2 = normalize3(f3{proj_z.z * p_sn + proj_z.x * p_cs, 0.0f, proj_z.z * p_cs - proj_z.x * p_sn});
+  const float si = Q.interval * signal * Q.S[0];
+  float x_pos = Q.initial_step * signal * Q.S[0];
+  const float vmin = Q.S[0] * 0.5f, vmax = Q.G[0] - Q.S[0] * 0.5f;
+  while ((x_pos / cv.x) < Q.max_distance &&
+         (pos.x + (x_pos + si) > vmin && pos.x + (x_pos + si) < vmax)) {
+    const float x_mean = fabsf(x_pos + si * 0.5f);
+    const float p_y1 = pj_y1.y * (x_mean / fabsf(pj_y1.x));
+    const float p_y2 = pj_y2.y * (x_mean / fabsf(pj_y2.x));
+    const float p_z1 = pj_z1.z * (x_mean / fabsf(pj_z1.x));
+    const float p_z2 = pj_z2.z * (x_mean / fabsf(pj_z2.x));
+    float y1 = fminf(p_y1, p_y2), y2 = fmaxf(p_y1, p_y2);
+    float z1 = fminf(p_z1, p_z2), z2 = fmaxf(p_z1, p_z2);
+    const float ydiff = fabsf(y2 - y1), zdiff = fabsf(z2 - z1);
+    const float ys = (ceilf(ydiff / Q.S[1]) - (ydiff / Q.S[1])) * 0.5f;
+    const float zs = (ceilf(zdiff / Q.S[2]) - (zdiff / Q.S[2])) * 0.5f;
+    y1 = y1 - ys * Q.S[1]; y2 = y2 + ys * Q.S[1];
+    z1 = z1 - zs * Q.S[2]; z2 = z2 + zs * Q.S[2];
+    const float x1 = fminf(x_pos, x_pos + si), x2 = fmaxf(x_pos, x_pos + si);
+    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2});
+    x_pos = x_pos + si;
+  }
+  return Stau;
+}
+
+}  // namespace
+
+struct EbsShader {
+  using Args = EbsArgs;
+  using Data = const float*;   // the float SAT
+
+  // ShadeSample (:498-550); `lit` counts the shadow box chains traced.
+  __device__ static f3 shade(const EbsArgs& Q, const float* __restrict__ sat, f3 tx, f3 wp, f3,
+                             f3 rgb, const f3* g, uint32_t& lit) {
+    const Rc1passArgs& A = Q.a;
+    const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
+    const f3 light{A.light[0], A.light[1], A.light[2]};
+    float iocc = 0.0f, isdw = 0.0f;
+    if (Q.apply_occlusion) iocc = ebs_occlusion(Q, sat, tx);
+    if (Q.apply_shadow) {
+      // ExtinctionDirectionalShadows (:455-481)
+      const f3 cv = Q.shadow_type == 0 ? normalize3(f3{light.x - wp.x, light.y - wp.y, light.z - wp.z})
+                                       : normalize3(f3{Q.lfwd[0], Q.lfwd[1], Q.lfwd[2]});
+      const f3 ac{fabsf(cv.x), fabsf(cv.y), fabsf(cv.z)};
+      float Stau;
+      if (ac.z > ac.x && ac.z > ac.y) Stau = cone_z(Q, sat, tx, cv);
+      else if (ac.y > ac.x) Stau = cone_y(Q, sat, tx, cv);
+      else Stau = cone_x(Q, sat, tx, cv);
+      isdw = cvr_expf(-Stau);
+      lit++;
+    }
+    const float inv_k = 1.0f / (Q.ka + Q.kd);
+    if (g) {   // ApplyPhongShading
+      if (g->x != 0.0f || g->y != 0.0f || g->z != 0.0f) {
+        const f3 nrm = normalize3(*g);
+        const f3 L = normalize3(f3{light.x - wp.x, light.y - wp.y, light.z - wp.z});
+        const f3 Ve = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
+        const f3 Hv = normalize3(f3{Ve.x + L.x, Ve.y + L.y, Ve.z + L.z});
+        const float dd = fmaxf(0.0f, dot3(nrm, L));
+        const float ds = fmaxf(0.0f, dot3(Hv, nrm));
+        const float pw = cvr_powf(ds, A.shininess);
+        // (1/(ka+kd)) * (L*IOcc*ka + IShadow*(L*kd*dot_diff)) + IShadow*(ks*Ispecular*pow) (:528-530)
+        return f3{inv_k * ((rgb.x * iocc) * Q.ka + isdw * ((rgb.x * Q.kd) * dd)) + isdw * ((Q.ks * A.ispec[0]) * pw),
+                  inv_k * ((rgb.y * iocc) * Q.ka + isdw * ((rgb.y * Q.kd) * dd)) + isdw * ((Q.ks * A.ispec[1]) * pw),
+                  inv_k * ((rgb.z * iocc) * Q.ka + isdw * ((rgb.z * Q.kd) * dd)) + isdw * ((Q.ks * A.ispec[2]) * pw)};
+      }
+      return rgb;
+    }
+    return f3{inv_k * ((rgb.x * iocc) * Q.ka + (rgb.x * isdw) * Q.kd),
+              inv_k * ((rgb.y * iocc) * Q.ka + (rgb.y * isdw) * Q.kd),
+              inv_k * ((rgb.z * iocc) * Q.ka + (rgb.z * isdw) * Q.kd)};
+  }
+};
+
+hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* samples,
+                      unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
+  return launch_shaded_march<EbsShader>(c, q, q.phong != 0, c.d_sat, out, samples, shade,
+                                        tile_samples, s);
+}
+
+}  // namespace cvr

@@ -1,0 +1,208 @@
+// shaded_march.h — the single-pass march of the shaded renderers (rc1pdosct,
+// rc1pextbsd) with their per-sample shading deferred into full-wave batches.
+//
+// ray_bbox_marching.comp:658-734 and ebs_ray_bbox_marching.comp:552-625 march
+// exactly as rc1pass does and, for every sample with alpha > 0, call an
+// expensive ShadeSample (cone tracing / SAT boxes: 10^2..10^3 fetches).  The
+// opacity of a sample, and with it the ERT break and the sample count, does not
+// depend on its shading (ShadeSample changes rgb only).  So each lane marches
+// its ray and, for every such sample, appends a shading job (position, TF
+// colour, alpha, 1 - dst.a before it) to its queue in LDS, advancing dst.a at
+// once.  When the wave holds >= 64 jobs (or no lane can march further) the jobs
+// are compacted and shaded 64 at a time, one per lane, so the shading runs at
+// full wave occupancy whatever the rays' divergence.  Each lane then folds its
+// own results into dst.rgb in sample order with the same fma as the sequential
+// loop: the image is bit-identical to it.
+//
+// A shader is a struct with
+//   using Args = ...;   // holds `Rc1passArgs a` (ray, volume, TF, tiles)
+//   using Data = ...;   // its device tables (passed by value)
+//   static f3 shade(const Args&, Data, f3 tx, f3 wp, f3 cam, f3 rgb, const f3* g, uint32_t& lit);
+// (tx: position in the [0, G] box, wp: world position, cam: the ray's camera
+// direction, g: the gradient sample when Phong shading is on, else null).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "cvr_device.h"
+#include "cvr_internal.h"
+#include "march_common.h"
+
+namespace cvr {
+
+constexpr int kJobsPerLane = 4;
+constexpr int kJobSlots = 64 * kJobsPerLane;
+
+__device__ __forceinline__ f3 vmad(f3 d, float t, f3 p) {
+  return f3{fmaf(d.x, t, p.x), fmaf(d.y, t, p.y), fmaf(d.z, t, p.z)};
+}
+__device__ __forceinline__ f3 cross3(f3 x, f3 y) {   // glm / GLSL cross, no fma
+  return f3{x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y};
+}
+
+// One wave = one 8x8 tile (XCD b%8 takes a contiguous band of tiles).
+template <class SH, bool PHONG>
+__global__ void __launch_bounds__(64)
+shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
+                    const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
+                    typename SH::Data data, float4* __restrict__ out,
+                    uint32_t* __restrict__ samples, unsigned long long* __restrict__ shade_ctr,
+                    unsigned long long* __restrict__ tile_samples) {
+  extern __shared__ float4 tfp[];
+  __shared__ float jpx[kJobSlots], jpy[kJobSlots], jpz[kJobSlots];   // tx_pos
+  __shared__ float jr[kJobSlots], jg[kJobSlots], jb[kJobSlots];      // TF rgb -> shaded rgb * a
+  __shared__ float ja[kJobSlots], jom[kJobSlots];                    // alpha, 1 - dst.a
+  __shared__ float jnx[PHONG ? kJobSlots : 1], jny[PHONG ? kJobSlots : 1],
+      jnz[PHONG ? kJobSlots : 1];                                     // gradient (Phong)
+  __shared__ uint16_t jlist[kJobSlots];
+  __shared__ float lane_cam[3][64];
+  load_tf_lds(tfp, tf_g, Q.a.tf_n);
+  const Rc1passArgs& A = Q.a;
+  const int b = blockIdx.x, nt = A.ntiles;
+  const int t = (nt & 7) == 0 ? (b & 7) * (nt >> 3) + (b >> 3) : b;
+  const int lane = threadIdx.x;
+  int px, py;
+  long long oidx;
+  tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
+  const bool inside = px < A.W && py < A.H;
+  float4 dst = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint32_t cnt = 0, nshade = 0, nlit = 0;
+  Ray r;
+  bool active = inside && ray_setup(A, px, py, r);
+  if (active) {
+    lane_cam[0][lane] = r.cam.x;
+    lane_cam[1][lane] = r.cam.y;
+    lane_cam[2][lane] = r.cam.z;
+    active = 0.0f < r.D;
+  }
+  const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
+  const float step = A.step, fn = (float)A.tf_n;
+  float s = 0.0f;
+
+  for (;;) {
+    // ---- march until the wave holds a full batch of jobs --------------------
+    int n = 0;            // this lane's queued jobs
+    int queued = 0;       // the wave's (uniform)
+    for (;;) {
+      const bool can = active && n < kJobsPerLane;
+      if (__ballot(can) == 0) break;
+      bool pushed = false;
+      if (can) {
+        const float h = fminf(step, r.D - s);
+        const float tt = fmaf(h, 0.5f, s);
+        const SamplePos sp = sample_pos(fmaf(r.dt.x, tt, r.o.x), fmaf(r.dt.y, tt, r.o.y),
+                                        fmaf(r.dt.z, tt, r.o.z), A);
+        const float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
+        cnt++;
+        if (sc.w > 0.0f) {
+          const int slot = lane * kJobsPerLane + n;
+          const f3 tx = vmad(r.dir, tt, r.tpos);        // tx_pos, box at [0, G]
+          jpx[slot] = tx.x; jpy[slot] = tx.y; jpz[slot] = tx.z;
+          jr[slot] = sc.x; jg[slot] = sc.y; jb[slot] = sc.z;
+          const float a = 1.0f - cvr_expf(-(sc.w * h));
+          const float om = 1.0f - dst.w;
+          ja[slot] = a;
+          jom[slot] = om;
+          if (PHONG) {
+            Texel txl;
+            txl.ix = sp.ix; txl.iy = sp.iy; txl.iz = sp.iz;
+            txl.ax = sp.ax; txl.ay = sp.ay; txl.az = sp.az;
+            const f3 g = sample_gradient(grad, A.N, txl);
+            jnx[slot] = g.x; jny[slot] = g.y; jnz[slot] = g.z;
+          }
+          dst.w = fmaf(om, a, dst.w);
+          n++;
+          pushed = true;
+          if (dst.w > 0.99f) active = false;
+        }
+        if (active) {
+          s = s + h;
+          active = s < r.D;
+        }
+      }
+      queued += __popcll(__ballot(pushed));
+      if (queued >= 64) break;
+    }
+    if (queued == 0) break;   // nobody could march: every ray is done
+
+    // ---- compact the queues: exclusive prefix of n from its bit planes -----
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const unsigned long long b0 = __ballot(n & 1), b1 = __ballot(n & 2), b2 = __ballot(n & 4);
+    const int first = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+    for (int j = 0; j < kJobsPerLane; j++)
+      if (j < n) jlist[first + j] = (uint16_t)(lane * kJobsPerLane + j);
+    __syncthreads();
+
+    // ---- shade 64 jobs at a time -------------------------------------------
+    for (int base = 0; base < queued; base += 64) {
+      const int f = base + lane;
+      if (f < queued) {
+        const int slot = jlist[f];
+        const int owner = slot / kJobsPerLane;
+        const f3 tx{jpx[slot], jpy[slot], jpz[slot]};
+        const f3 wp{tx.x - hg.x, tx.y - hg.y, tx.z - hg.z};
+        const f3 cam{lane_cam[0][owner], lane_cam[1][owner], lane_cam[2][owner]};
+        const f3 rgb{jr[slot], jg[slot], jb[slot]};
+        f3 g;
+        if (PHONG) g = f3{jnx[slot], jny[slot], jnz[slot]};
+        const f3 c = SH::shade(Q, data, tx, wp, cam, rgb, PHONG ? &g : nullptr, nlit);
+        const float a = ja[slot];
+        jr[slot] = c.x * a;
+        jg[slot] = c.y * a;
+        jb[slot] = c.z * a;
+      }
+    }
+    __syncthreads();
+
+    // ---- fold the results in sample order (front-to-back) -------------------
+    for (int j = 0; j < kJobsPerLane; j++)
+      if (j < n) {
+        const int slot = lane * kJobsPerLane + j;
+        const float om = jom[slot];
+        dst.x = fmaf(om, jr[slot], dst.x);
+        dst.y = fmaf(om, jg[slot], dst.y);
+        dst.z = fmaf(om, jb[slot], dst.z);
+      }
+    nshade += n;
+    __syncthreads();
+  }
+
+  if (inside || A.packed) {
+    out[oidx] = dst;
+    if (samples) samples[oidx] = cnt;
+  }
+  if (tile_samples) {
+    const unsigned long long v = wave_sum(cnt);
+    if (lane == 0) tile_samples[t] = v;
+  }
+  if (shade_ctr) {   // measurement only (secondary-fetch count of the roofline)
+    const unsigned long long sa = wave_sum(nshade), sl = wave_sum(nlit);
+    if (lane == 0) {
+      atomicAdd(&shade_ctr[0], sa);
+      atomicAdd(&shade_ctr[1], sl);
+    }
+  }
+}
+
+template <class SH>
+hipError_t launch_shaded_march(const Ctx& c, const typename SH::Args& q, bool phong,
+                               typename SH::Data data, float4* out, uint32_t* samples,
+                               unsigned long long* shade_ctr, unsigned long long* tile_samples,
+                               hipStream_t s) {
+  if (q.a.ntiles <= 0) return hipSuccess;
+  if (q.a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
+  const size_t lds = (size_t)(q.a.tf_n + 2) * sizeof(float4);
+  const uint4* cells = (const uint4*)c.d_cells + c.cells.linear_origin;
+  if (phong)
+    hipLaunchKernelGGL((shaded_march_kernel<SH, true>), dim3(q.a.ntiles), dim3(64), lds, s, q,
+                       cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, data, out, samples,
+                       shade_ctr, tile_samples);
+  else
+    hipLaunchKernelGGL((shaded_march_kernel<SH, false>), dim3(q.a.ntiles), dim3(64), lds, s, q,
+                       cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, data, out, samples,
+                       shade_ctr, tile_samples);
+  return hipGetLastError();
+}
+
+}  // namespace cvr

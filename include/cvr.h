@@ -30,8 +30,13 @@
  *   cvr_render_dosct             <- RC1PConeTracingDirOcclusionShading::Update + Redraw
  *                                   cppvolrend/structured/rc1pdosct/dosrcrenderer.cpp:134-260
  *                                   (the dispatch of ray_marching_1p_dosct.comp)
- *   (planned, not yet exported: cvr_render_extbsd <- RC1PExtinctionBasedShading,
- *    ebsrenderer.cpp:125-260)
+ *   cvr_set_extinction_sat       <- RC1PExtinctionBasedShading::GenerateExtinctionSAT3DTex +
+ *                                   SummedAreaTable3D<double>::BuildSAT
+ *                                   cppvolrend/structured/rc1pextbsd/ebsrenderer.cpp:624-716,
+ *                                   libs/vis_utils/summedareatable.h:218-278
+ *   cvr_render_extbsd            <- RC1PExtinctionBasedShading::Update + Redraw
+ *                                   cppvolrend/structured/rc1pextbsd/ebsrenderer.cpp:125-260
+ *                                   (the dispatch of ebs_ray_bbox_marching.comp)
  *   cvr_status (never exit())    <- gl::ExitOnGLError  libs/gl_utils/utils.cpp:11-30
  *
  * Threading: one context per device, externally synchronised (the reference
@@ -170,6 +175,27 @@ typedef struct cvr_dos_params {
   cvr_cone_params shadow;      /* sampler_shadow:    0.5 deg, packing 0, weight 1.0     */
 } cvr_dos_params;
 
+/* RC1PExtinctionBasedShading ("1-Pass - Extinction Based Shading", s_1rcebs):
+ * ebsrenderer.cpp:19-55, 125-260. */
+typedef struct cvr_ebs_params {
+  float step;                  /* <= 0: 0.5/sqrt(3)*|scale| (ebsrenderer.cpp:116-117)   */
+  int   apply_gradient_shading;/* ApplyPhongShading (needs cvr_set_gradient)           */
+  float ka, kd, ks, shininess; /* Blinn-Phong constants (renderingparameters.cpp:23-26) */
+  float ispecular[3];          /* Ispecular                                             */
+  float light_pos[3];          /* WorldLightingPos (point light)                        */
+  float light_forward[3];      /* LightCamForward (directional light)                   */
+  int   apply_occlusion;       /* apply_ambient_occlusion (default 1)                   */
+  int   occlusion_shells;      /* ambient_occlusion_shells (15)                         */
+  float occlusion_radius;      /* ambient_occlusion_radius (1.0, in voxels)             */
+  int   apply_shadow;          /* apply_directional_shadows (default 1)                 */
+  int   shadow_type;           /* type_of_shadow: 0 point light, 1 directional          */
+  float shadow_cone_angle_deg; /* dir_shadow_cone_angle (1.0)                           */
+  float shadow_sample_interval;/* dir_shadow_sample_interval (2.0 voxels)               */
+  float shadow_initial_step;   /* dir_shadow_initial_step (2.0 voxels)                  */
+  float shadow_ui_weight;      /* dir_shadow_user_interface_weight (1.0)                */
+  float shadow_max_distance;   /* <= 0: 0.75 * volume diagonal (ebsrenderer.cpp:98-105) */
+} cvr_ebs_params;
+
 /* ----------------------------------------------------------------------------
  * Context
  * -------------------------------------------------------------------------- */
@@ -201,7 +227,7 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *   "kernel_timing" N > 0: time the ray-march kernel of the last N frames
  *                (cvr_read_kernel_times); 0 off (default)
  *   "shade_counters" 1: count shaded / shadow-lit samples of cvr_render_dosct
- *                (cvr_read_shade_counters; one atomic per wave) */
+ *                and cvr_render_extbsd (cvr_read_shade_counters; one atomic per wave) */
 cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
 int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);
@@ -258,6 +284,22 @@ cvr_status  cvr_copy_extinction_level(cvr_ctx* ctx, int level, float* out, int d
 cvr_status  cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* frame,
                              const cvr_dos_params* params, const cvr_output* out);
 
+/* Extinction summed-area table of the current volume for the EBS renderer
+ * (GenerateExtinctionSAT3DTex, ebsrenderer.cpp:624-716): a (W+2)(H+2)(D+2)
+ * grid, zero on its border, holding ext_lut[voxel] inside, summed in double
+ * exactly as SummedAreaTable3D<double>::BuildSAT and stored as float.
+ * ext_lut: GetExtN(v / (2^bits - 1)) for every voxel value v (256 entries for
+ * 8-bit volumes, 65536 for 16-bit; cvr_tf1d_ext_lut builds it). */
+cvr_status  cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n);
+/* Copy the float SAT back (x-fastest); out = NULL: dims only. */
+cvr_status  cvr_copy_extinction_sat(cvr_ctx* ctx, float* out, size_t capacity, int dims[3]);
+
+/* One extinction-based shading frame: the ray-march with each sample shaded by
+ * a SAT ambient occlusion and a SAT box-chain shadow.  Needs
+ * cvr_set_extinction_sat. */
+cvr_status  cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* frame,
+                              const cvr_ebs_params* params, const cvr_output* out);
+
 /* Rank-0 side of the screen-tile split: `d_packed` holds nranks consecutive
  * blocks of `tiles_per_rank_max` packed tiles (rank r's block at offset
  * r*tiles_per_rank_max*tile_size^2 pixels); scatter them into the W x H
@@ -306,6 +348,13 @@ float       cvr_default_step(const float scale[3]);
  * out_rgbt receives (max_density+1) x 4 floats. */
 cvr_status  cvr_tf1d_build_rgbt(const double* rgb_cp, int n_rgb, const double* a_cp, int n_a,
                                 int max_density, int extinction_input, float* out_rgbt);
+
+/* TransferFunction1D::GetExtN (transferfunction1d.cpp:132-157, 189-197) of
+ * every voxel value v / (2^bits - 1), bits = 8 * bytes_per_voxel: the cell
+ * values of the EBS SAT.  out_lut receives 256 or 65536 floats. */
+cvr_status  cvr_tf1d_ext_lut(const double* rgb_cp, int n_rgb, const double* a_cp, int n_a,
+                             int max_density, int extinction_input, int bytes_per_voxel,
+                             float* out_lut);
 
 /* .tf1d reader (TransferFunctionReader::readtf1d, reader.cpp:744-814) and the
  * built table.  out_rgbt must hold 4*(max_density+1) floats; pass NULL to

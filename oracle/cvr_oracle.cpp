@@ -751,10 +751,16 @@ float cone_trace(const ExtVol& E, const OracleDosCone& C, v3 pos, v3 k, v3 u, v3
 
 }  // namespace
 
-// Rows [y0, y1) of the frame (the whole frame: 0, H).  out: W*H*4, counts: W*H.
-ORACLE_API uint64_t oracle_render_dos_rows(const OracleDos* Q, int y0, int y1, float* out_rgba,
-                                           uint32_t* out_counts, int nthreads) {
-  const OracleRc1pass& P = Q->base;
+namespace {
+
+// The single-pass march shared by the shaded renderers (ray_bbox_marching.comp
+// :658-734, ebs_ray_bbox_marching.comp:552-625): rows [y0, y1) of the frame.
+// For every sample with alpha > 0, shade(src, tx, wp, cam_dir, x, y, z) turns
+// src.rgb into the shaded colour (tx: position in the [0, G] box, wp: world
+// position, x/y/z: texel coordinates of the volume fetch).
+template <class Shade>
+uint64_t shaded_march_rows(const OracleRc1pass& P, int y0, int y1, float* out_rgba,
+                           uint32_t* out_counts, int nthreads, const Shade& shade) {
   float V[16], tanf;
   oracle_lookat(P.eye, P.center, P.up, P.fovy_deg, V, &tanf);
   const float aspect = P.aspect > 0 ? P.aspect : (float)P.W / (float)P.H;
@@ -762,24 +768,7 @@ ORACLE_API uint64_t oracle_render_dos_rows(const OracleDos* Q, int y0, int y1, f
   const v3 G = mk((float)P.N[0] * P.scale[0], (float)P.N[1] * P.scale[1], (float)P.N[2] * P.scale[2]);
   const v3 half = mk(G.x * 0.5f, G.y * 0.5f, G.z * 0.5f);
   const v3 NoG = mk((float)P.N[0] / G.x, (float)P.N[1] / G.y, (float)P.N[2] / G.z);
-  const v3 light = mk(P.light[0], P.light[1], P.light[2]);
-  const v3 lfwd = mk(Q->light_forward[0], Q->light_forward[1], Q->light_forward[2]);
-  const v3 lup = mk(Q->light_up[0], Q->light_up[1], Q->light_up[2]);
-  const v3 lright = mk(Q->light_right[0], Q->light_right[1], Q->light_right[2]);
   Tex vol{P.vol, {P.N[0], P.N[1], P.N[2]}, 1};
-  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3};
-  ExtVol E{Q->ext, {Q->ext_res[0], Q->ext_res[1], Q->ext_res[2]}, Q->ext_levels, G, {}};
-  E.off.assign(E.nl + 1, 0);
-  for (int L = 0; L < E.nl; L++) {
-    int d[3];
-    ext_level_dims(E.res, L, d);
-    E.off[L + 1] = E.off[L] + (int64_t)d[0] * d[1] * d[2];
-  }
-  // SpotLightMaxAngle uniform: glm::cos(glm::pi<float>() * angle / 180.f) (dosrcrenderer.cpp:158)
-  const float spot_cos = std::cos(3.14159265358979323846f * Q->spot_angle_deg / 180.0f);
-  const float ka = Q->apply_occlusion ? P.ka : 0.0f;
-  const float kd = Q->apply_shadow ? P.kd : 0.0f;
-  const float ks = Q->apply_shadow ? P.ks : 0.0f;
   const int W = P.W, H = P.H;
   std::vector<uint32_t> tmp;
   uint32_t* counts = out_counts;
@@ -811,9 +800,6 @@ ORACLE_API uint64_t oracle_render_dos_rows(const OracleDos* Q, int y0, int y1, f
       const bool hit = tfar > tnear;
       tnear = std::fmax(tnear, 0.0f);
       if (hit) {
-        // eye-space frame of the occlusion cones (:681-684)
-        const v3 v_right = normalize3(cross3(cam_dir, mk(0.0f, 1.0f, 0.0f)));
-        const v3 v_up = normalize3(cross3(mk(-cam_dir.x, -cam_dir.y, -cam_dir.z), v_right));
         const float D = std::fabs(tfar - tnear);
         const v3 tpos = mk(std::fmaf(dir.x, tnear, eye.x) + half.x, std::fmaf(dir.y, tnear, eye.y) + half.y,
                            std::fmaf(dir.z, tnear, eye.z) + half.z);
@@ -832,46 +818,7 @@ ORACLE_API uint64_t oracle_render_dos_rows(const OracleDos* Q, int y0, int y1, f
           if (src[3] > 0.0f) {
             const v3 tx = vmad(dir, t, tpos);              // tx_pos, volume box at [0, G]
             const v3 wp = mk(tx.x - half.x, tx.y - half.y, tx.z - half.z);
-            float iocc = 0.0f, isdw = 0.0f;
-            if (Q->apply_occlusion) {
-              const v3 k = normalize3(mk(eye.x - wp.x, eye.y - wp.y, eye.z - wp.z));
-              iocc = cone_trace(E, Q->occ, tx, k, v_up, v_right);
-            }
-            if (Q->apply_shadow) {
-              v3 k, u, v;
-              bool lit = true;
-              if (Q->shadow_type == 2) {
-                k = lfwd; v = lup; u = lright;
-              } else {
-                k = normalize3(mk(light.x - wp.x, light.y - wp.y, light.z - wp.z));
-                u = normalize3(cross3(k, lright));
-                v = normalize3(cross3(k, u));
-                if (Q->shadow_type == 1 && dot3(k, lfwd) < spot_cos) lit = false;
-              }
-              // Cone1RayShadow(pos, k, v, u) is called as (pos, k, u, v): swapped (:559-561)
-              isdw = lit ? cone_trace(E, Q->sdw, tx, k, v, u) : 0.0f;
-            }
-            const float inv_k = 1.0f / (ka + kd);
-            bool shaded_phong = false;
-            if (P.phong && P.grad) {
-              float g[3];
-              grd.sample(x, y, z, g);
-              if (g[0] != 0.0f || g[1] != 0.0f || g[2] != 0.0f) {
-                const v3 n = normalize3(mk(g[0], g[1], g[2]));
-                const v3 L = normalize3(mk(light.x - wp.x, light.y - wp.y, light.z - wp.z));
-                const v3 Ve = normalize3(mk(eye.x - wp.x, eye.y - wp.y, eye.z - wp.z));
-                const v3 Hv = normalize3(mk(Ve.x + L.x, Ve.y + L.y, Ve.z + L.z));
-                const float dd = std::fmax(0.0f, dot3(n, L));
-                const float ds = std::fmax(0.0f, dot3(Hv, n));
-                const float diff = inv_k * (iocc * ka + (isdw * kd) * dd);
-                const float spec = (isdw * ks) * cvr_powf(ds, P.shininess);
-                for (int q = 0; q < 3; q++) src[q] = std::fmaf(P.ispec[q], spec, src[q] * diff);
-                shaded_phong = true;
-              }
-            }
-            if (!shaded_phong && !(P.phong && P.grad)) {
-              for (int q = 0; q < 3; q++) src[q] = inv_k * ((src[q] * iocc) * ka + (src[q] * isdw) * kd);
-            }
+            shade(src, tx, wp, cam_dir, x, y, z);
             const float a = 1.0f - cvr_expf(-(src[3] * h));
             const float om = 1.0f - dst[3];
             dst[0] = std::fmaf(om, src[0] * a, dst[0]);
@@ -892,7 +839,389 @@ ORACLE_API uint64_t oracle_render_dos_rows(const OracleDos* Q, int y0, int y1, f
   return total;
 }
 
+}  // namespace
+
+// Rows [y0, y1) of the frame (the whole frame: 0, H).  out: W*H*4, counts: W*H.
+ORACLE_API uint64_t oracle_render_dos_rows(const OracleDos* Q, int y0, int y1, float* out_rgba,
+                                           uint32_t* out_counts, int nthreads) {
+  const OracleRc1pass& P = Q->base;
+  const v3 eye = mk(P.eye[0], P.eye[1], P.eye[2]);
+  const v3 G = mk((float)P.N[0] * P.scale[0], (float)P.N[1] * P.scale[1], (float)P.N[2] * P.scale[2]);
+  const v3 light = mk(P.light[0], P.light[1], P.light[2]);
+  const v3 lfwd = mk(Q->light_forward[0], Q->light_forward[1], Q->light_forward[2]);
+  const v3 lup = mk(Q->light_up[0], Q->light_up[1], Q->light_up[2]);
+  const v3 lright = mk(Q->light_right[0], Q->light_right[1], Q->light_right[2]);
+  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3};
+  ExtVol E{Q->ext, {Q->ext_res[0], Q->ext_res[1], Q->ext_res[2]}, Q->ext_levels, G, {}};
+  E.off.assign(E.nl + 1, 0);
+  for (int L = 0; L < E.nl; L++) {
+    int d[3];
+    ext_level_dims(E.res, L, d);
+    E.off[L + 1] = E.off[L] + (int64_t)d[0] * d[1] * d[2];
+  }
+  // SpotLightMaxAngle uniform: glm::cos(glm::pi<float>() * angle / 180.f) (dosrcrenderer.cpp:158)
+  const float spot_cos = std::cos(3.14159265358979323846f * Q->spot_angle_deg / 180.0f);
+  const float ka = Q->apply_occlusion ? P.ka : 0.0f;
+  const float kd = Q->apply_shadow ? P.kd : 0.0f;
+  const float ks = Q->apply_shadow ? P.ks : 0.0f;
+  auto shade = [&](float* src, v3 tx, v3 wp, v3 cam_dir, float x, float y, float z) {
+    // eye-space frame of the occlusion cones (:681-684)
+    const v3 v_right = normalize3(cross3(cam_dir, mk(0.0f, 1.0f, 0.0f)));
+    const v3 v_up = normalize3(cross3(mk(-cam_dir.x, -cam_dir.y, -cam_dir.z), v_right));
+    float iocc = 0.0f, isdw = 0.0f;
+    if (Q->apply_occlusion) {
+      const v3 k = normalize3(mk(eye.x - wp.x, eye.y - wp.y, eye.z - wp.z));
+      iocc = cone_trace(E, Q->occ, tx, k, v_up, v_right);
+    }
+    if (Q->apply_shadow) {
+      v3 k, u, v;
+      bool lit = true;
+      if (Q->shadow_type == 2) {
+        k = lfwd; v = lup; u = lright;
+      } else {
+        k = normalize3(mk(light.x - wp.x, light.y - wp.y, light.z - wp.z));
+        u = normalize3(cross3(k, lright));
+        v = normalize3(cross3(k, u));
+        if (Q->shadow_type == 1 && dot3(k, lfwd) < spot_cos) lit = false;
+      }
+      // Cone1RayShadow(pos, k, v, u) is called as (pos, k, u, v): swapped (:559-561)
+      isdw = lit ? cone_trace(E, Q->sdw, tx, k, v, u) : 0.0f;
+    }
+    const float inv_k = 1.0f / (ka + kd);
+    if (P.phong && P.grad) {
+      float g[3];
+      grd.sample(x, y, z, g);
+      if (g[0] != 0.0f || g[1] != 0.0f || g[2] != 0.0f) {
+        const v3 n = normalize3(mk(g[0], g[1], g[2]));
+        const v3 L = normalize3(mk(light.x - wp.x, light.y - wp.y, light.z - wp.z));
+        const v3 Ve = normalize3(mk(eye.x - wp.x, eye.y - wp.y, eye.z - wp.z));
+        const v3 Hv = normalize3(mk(Ve.x + L.x, Ve.y + L.y, Ve.z + L.z));
+        const float dd = std::fmax(0.0f, dot3(n, L));
+        const float ds = std::fmax(0.0f, dot3(Hv, n));
+        const float diff = inv_k * (iocc * ka + (isdw * kd) * dd);
+        const float spec = (isdw * ks) * cvr_powf(ds, P.shininess);
+        for (int q = 0; q < 3; q++) src[q] = std::fmaf(P.ispec[q], spec, src[q] * diff);
+      }
+    } else {
+      for (int q = 0; q < 3; q++) src[q] = inv_k * ((src[q] * iocc) * ka + (src[q] * isdw) * kd);
+    }
+  };
+  return shaded_march_rows(P, y0, y1, out_rgba, out_counts, nthreads, shade);
+}
+
 ORACLE_API uint64_t oracle_render_dos(const OracleDos* Q, float* out_rgba, uint32_t* out_counts,
                                       int nthreads) {
   return oracle_render_dos_rows(Q, 0, Q->base.H, out_rgba, out_counts, nthreads);
+}
+
+// ===========================================================================
+// Extinction-based shading (rc1pextbsd), SURVEY.md §8 rows A14-A15
+// ===========================================================================
+
+// GetExtN(v / (2^bits - 1)) for every voxel value v (transferfunction1d.cpp:
+// 132-157, 189-197; MaterialOpacityToExtinction, transferfunction.h:79-82):
+// Get(norm, 1.0).a as float, then log(1 / (1 - a)) in double, returned as float.
+ORACLE_API void oracle_ext_lut(const double* table, int max_density, int bpv, int extinction_input,
+                               float* out_lut) {
+  const int nv = bpv == 1 ? 256 : 65536;
+  const double den = bpv == 1 ? (256.0 - 1.0) : (65536.0 - 1.0);
+  for (int v = 0; v < nv; v++) {
+    float g[4];
+    oracle_tf_get(table, max_density, (double)v / den, 1.0, g);
+    const float a = g[3];
+    out_lut[v] = extinction_input ? a : (float)std::log(1.0 / (1.0 - (double)a));
+  }
+}
+
+// RC1PExtinctionBasedShading::GenerateExtinctionSAT3DTex (ebsrenderer.cpp:624-662) and
+// SummedAreaTable3D<double>::BuildSAT (summedareatable.h:218-278), literally: a
+// (W+2)(H+2)(D+2) grid with a zero border, the interior holding lut[voxel], summed in
+// double in the reference's order.  out: x-fastest doubles.
+ORACLE_API void oracle_sat_build(const void* vox, int bpv, int W, int H, int D, const float* lut,
+                                 double* out) {
+  const int w = W + 2, h = H + 2, d = D + 2;
+  auto at = [&](int x, int y, int z) -> double& { return out[x + (int64_t)w * y + (int64_t)w * h * z]; };
+  auto get = [&](int x, int y, int z) -> double {
+    if (x < 0 || y < 0 || z < 0) return 0.0;
+    if (x >= w) x = w - 1;
+    if (y >= h) y = h - 1;
+    if (z >= d) z = d - 1;
+    return at(x, y, z);
+  };
+  for (int x = 0; x < w; x++)
+    for (int y = 0; y < h; y++)
+      for (int z = 0; z < d; z++) {
+        double val;
+        if (x == 0 || y == 0 || z == 0 || x == w - 1 || y == h - 1 || z == d - 1) {
+          val = 0.0f;
+        } else {
+          const int64_t i = (int64_t)(x - 1) + (int64_t)(y - 1) * W + (int64_t)(z - 1) * W * H;
+          const int v = bpv == 1 ? ((const uint8_t*)vox)[i] : ((const uint16_t*)vox)[i];
+          val = lut[v];
+        }
+        at(x, y, z) = val;
+      }
+  at(0, 0, 0) = get(0, 0, 0);
+  for (int x = 1; x < w; x++) at(x, 0, 0) = get(x - 1, 0, 0) + get(x, 0, 0);
+  for (int y = 1; y < h; y++) at(0, y, 0) = get(0, y - 1, 0) + get(0, y, 0);
+  for (int z = 1; z < d; z++) at(0, 0, z) = get(0, 0, z - 1) + get(0, 0, z);
+  for (int x = 1; x < w; x++)
+    for (int z = 1; z < d; z++)
+      at(x, 0, z) = get(x - 1, 0, z) + get(x, 0, z - 1) - get(x - 1, 0, z - 1) + get(x, 0, z);
+  for (int x = 1; x < w; x++)
+    for (int y = 1; y < h; y++)
+      at(x, y, 0) = get(x - 1, y, 0) + get(x, y - 1, 0) - get(x - 1, y - 1, 0) + get(x, y, 0);
+  for (int y = 1; y < h; y++)
+    for (int z = 1; z < d; z++)
+      at(0, y, z) = get(0, y - 1, z) + get(0, y, z - 1) - get(0, y - 1, z - 1) + get(0, y, z);
+  for (int x = 1; x < w; x++)
+    for (int y = 1; y < h; y++)
+      for (int z = 1; z < d; z++) {
+        double val = get(x, y, z)
+                   + get(x - 1, y - 1, z - 1)
+                   + get(x, y, z - 1)
+                   + get(x, y - 1, z)
+                   + get(x - 1, y, z)
+                   - get(x - 1, y - 1, z)
+                   - get(x, y - 1, z - 1)
+                   - get(x - 1, y, z - 1);
+        at(x, y, z) = val;
+      }
+}
+
+struct OracleEbs {
+  OracleRc1pass base;
+  const float* sat; int sat_dims[3];   // the float SAT (W+2)(H+2)(D+2), x-fastest
+  int apply_occlusion, occ_shells; float occ_radius;
+  int apply_shadow, shadow_type;       // 0: point light, 1: LightCamForward
+  float cone_angle;                    // DirSdwConeAngle (radians, float)
+  float interval, initial_step, ui_weight, max_distance;
+  float light_forward[3];
+};
+
+namespace {
+
+struct Sat {
+  Tex t;            // comps = 1
+  v3 S, G, inv_vs, nsat, min_sat, max_sat;
+  // GetSummed3Density: texture(TexVolumeSAT3D, p * inv_vol_scaled).r
+  float f(float x, float y, float z) const {
+    const float ux = x * inv_vs.x, uy = y * inv_vs.y, uz = z * inv_vs.z;
+    float r;
+    t.sample(std::fmaf(ux, nsat.x, -0.5f), std::fmaf(uy, nsat.y, -0.5f), std::fmaf(uz, nsat.z, -0.5f), &r);
+    return r;
+  }
+  // EvaluateSAT3D (ebs_ray_bbox_marching.comp:85-99)
+  float box(v3 p1, v3 p2) const {
+    const float V1 = f(p2.x, p2.y, p2.z), V2 = f(p1.x, p2.y, p2.z);
+    const float V3 = f(p2.x, p2.y, p1.z), V4 = f(p1.x, p2.y, p1.z);
+    const float V5 = f(p2.x, p1.y, p2.z), V6 = f(p1.x, p1.y, p2.z);
+    const float V7 = f(p2.x, p1.y, p1.z), V8 = f(p1.x, p1.y, p1.z);
+    return (V1 - V2 - V3 + V4 - V5 + V6 + V7 - V8);
+  }
+  v3 offset_clamp(v3 p) const {   // clamp(p + VolumeScales, MinSATPosition, MaxSATPosition)
+    return mk(std::fmin(std::fmax(p.x + S.x, min_sat.x), max_sat.x),
+              std::fmin(std::fmax(p.y + S.y, min_sat.y), max_sat.y),
+              std::fmin(std::fmax(p.z + S.z, min_sat.z), max_sat.z));
+  }
+  float ao_box(v3 p1, v3 p2) const { return box(offset_clamp(p1), offset_clamp(p2)); }
+  // EvaluateShadowSAT3D (:148-185, texture path)
+  float shadow_box(v3 p1, v3 p2, float uiw) const {
+    const float volquery = ((std::fabs(p1.x - p2.x) / S.x)) * ((std::fabs(p1.y - p2.y) / S.y)) *
+                           ((std::fabs(p1.z - p2.z) / S.z));
+    return ((box(offset_clamp(p1), offset_clamp(p2)) / volquery)) * uiw;
+  }
+};
+
+// ExtinctionAmbientOcclusion (:109-146)
+float ebs_occlusion(const Sat& T, v3 tx, int shells, float R) {
+  const v3 r0 = mk(R * T.S.x, R * T.S.y, R * T.S.z);
+  const float SAT_Sh0 = T.ao_box(mk(tx.x - r0.x, tx.y - r0.y, tx.z - r0.z),
+                                 mk(tx.x + r0.x, tx.y + r0.y, tx.z + r0.z));
+  const float rsh0 = R;
+  const float tSh0 = SAT_Sh0 * (1.0f / (rsh0 * rsh0));
+  float SAT_Shi = SAT_Sh0, tshi = tSh0;
+  for (int i = 1; i < shells; i++) {
+    const float r1 = R * (float)(i + 1);
+    const v3 ri = mk(r1 * T.S.x, r1 * T.S.y, r1 * T.S.z);
+    const float SAT_Shi_1 = T.ao_box(mk(tx.x - ri.x, tx.y - ri.y, tx.z - ri.z),
+                                     mk(tx.x + ri.x, tx.y + ri.y, tx.z + ri.z));
+    const float tshi_1 = tshi + (SAT_Shi_1 - SAT_Shi) * (1.0f / (r1 * r1));
+    SAT_Shi = SAT_Shi_1;
+    tshi = tshi_1;
+  }
+  const float rshi = R * (float)shells;
+  const float W_A = 1.0f / (rshi * rshi);
+  const float Stau = W_A * tshi;
+  return cvr_expf(-(Stau));
+}
+
+struct ConeCS { float p_cs, p_sn, n_cs, n_sn; };
+
+// One box chain along the dominant axis a (ConeZAxis :187-275, ConeYAxis :277-364,
+// ConeXAxis :366-453).  The three are written out as the reference has them.
+float cone_z(const Sat& T, const OracleEbs& Q, const ConeCS& c, v3 pos, v3 cv) {
+  float Stau = 0.0f;
+  float signal = 1.0f;
+  if (cv.z < 0) signal = -1.0f;
+  const v3 proj_y = normalize3(mk(0.0f, cv.y, cv.z));
+  const v3 proj_x = normalize3(mk(cv.x, 0.0f, cv.z));
+  const v3 pj_x1 = normalize3(mk(proj_x.x * c.n_cs - proj_x.z * c.n_sn, 0.0f, proj_x.x * c.n_sn + proj_x.z * c.n_cs));
+  const v3 pj_x2 = normalize3(mk(proj_x.x * c.p_cs - proj_x.z * c.p_sn, 0.0f, proj_x.x * c.p_sn + proj_x.z * c.p_cs));
+  const v3 pj_y1 = normalize3(mk(0.0f, proj_y.y * c.n_cs - proj_y.z * c.n_sn, proj_y.y * c.n_sn + proj_y.z * c.n_cs));
+  const v3 pj_y2 = normalize3(mk(0.0f, proj_y.y * c.p_cs - proj_y.z * c.p_sn, proj_y.y * c.p_sn + proj_y.z * c.p_cs));
+  const float si = Q.interval * signal * T.S.z;
+  float z_pos = Q.initial_step * signal * T.S.z;
+  const float vmin = T.S.z * 0.5f, vmax = T.G.z - T.S.z * 0.5f;
+  while ((z_pos / cv.z) < Q.max_distance &&
+         (pos.z + (z_pos + si) > vmin && pos.z + (z_pos + si) < vmax)) {
+    const float z_mean = std::fabs(z_pos + si * 0.5f);
+    const float p_x1 = pj_x1.x * (z_mean / std::fabs(pj_x1.z));
+    const float p_x2 = pj_x2.x * (z_mean / std::fabs(pj_x2.z));
+    const float p_y1 = pj_y1.y * (z_mean / std::fabs(pj_y1.z));
+    const float p_y2 = pj_y2.y * (z_mean / std::fabs(pj_y2.z));
+    float x1 = std::fmin(p_x1, p_x2), x2 = std::fmax(p_x1, p_x2);
+    float y1 = std::fmin(p_y1, p_y2), y2 = std::fmax(p_y1, p_y2);
+    const float xdiff = std::fabs(x2 - x1), ydiff = std::fabs(y2 - y1);
+    const float xs = (std::ceil(xdiff / T.S.x) - (xdiff / T.S.x)) * 0.5f;
+    const float ys = (std::ceil(ydiff / T.S.y) - (ydiff / T.S.y)) * 0.5f;
+    x1 = x1 - xs * T.S.x; x2 = x2 + xs * T.S.x;
+    y1 = y1 - ys * T.S.y; y2 = y2 + ys * T.S.y;
+    const float z1 = std::fmin(z_pos, z_pos + si), z2 = std::fmax(z_pos, z_pos + si);
+    Stau += T.shadow_box(mk(pos.x + x1, pos.y + y1, pos.z + z1), mk(pos.x + x2, pos.y + y2, pos.z + z2),
+                         Q.ui_weight);
+    z_pos = z_pos + si;
+  }
+  return Stau;
+}
+
+float cone_y(const Sat& T, const OracleEbs& Q, const ConeCS& c, v3 pos, v3 cv) {
+  float Stau = 0.0f;
+  float signal = 1.0f;
+  if (cv.y < 0) signal = -1.0f;
+  const v3 proj_x = normalize3(mk(cv.x, cv.y, 0.0f));
+  const v3 proj_z = normalize3(mk(0.0f, cv.y, cv.z));
+  const v3 pj_x1 = normalize3(mk(proj_x.x * c.n_cs - proj_x.y * c.n_sn, proj_x.x * c.n_sn + proj_x.y * c.n_cs, 0.0f));
+  const v3 pj_x2 = normalize3(mk(proj_x.x * c.p_cs - proj_x.y * c.p_sn, proj_x.x * c.p_sn + proj_x.y * c.p_cs, 0.0f));
+  const v3 pj_z1 = normalize3(mk(0.0f, proj_z.z * c.n_sn + proj_z.y * c.n_cs, proj_z.z * c.n_cs - proj_z.y * c.n_sn));
+  const v3 pj_z2 = normalize3(mk(0.0f, proj_z.z * c.p_sn + proj_z.y * c.p_cs, proj_z.z * c.p_cs - proj_z.y * c.p_sn));
+  const float si = Q.interval * signal * T.S.y;
+  float y_pos = Q.initial_step * signal * T.S.y;
+  const float vmin = T.S.y * 0.5f, vmax = T.G.y - T.S.y * 0.5f;
+  while ((y_pos / cv.y) < Q.max_distance &&
+         (pos.y + (y_pos + si) > vmin && pos.y + (y_pos + si) < vmax)) {
+    const float y_mean = std::fabs(y_pos + si * 0.5f);
+    const float p_x1 = pj_x1.x * (y_mean / std::fabs(pj_x1.y));
+    const float p_x2 = pj_x2.x * (y_mean / std::fabs(pj_x2.y));
+    const float p_z1 = pj_z1.z * (y_mean / std::fabs(pj_z1.y));
+    const float p_z2 = pj_z2.z * (y_mean / std::fabs(pj_z2.y));
+    float x1 = std::fmin(p_x1, p_x2), x2 = std::fmax(p_x1, p_x2);
+    float z1 = std::fmin(p_z1, p_z2), z2 = std::fmax(p_z1, p_z2);
+    const float xdiff = std::fabs(x2 - x1), zdiff = std::fabs(z2 - z1);
+    const float xs = (std::ceil(xdiff / T.S.x) - (xdiff / T.S.x)) * 0.5f;
+    const float zs = (std::ceil(zdiff / T.S.z) - (zdiff / T.S.z)) * 0.5f;
+    x1 = x1 - xs * T.S.x; x2 = x2 + xs * T.S.x;
+    z1 = z1 - zs * T.S.z; z2 = z2 + zs * T.S.z;
+    const float y1 = std::fmin(y_pos, y_pos + si), y2 = std::fmax(y_pos, y_pos + si);
+    Stau += T.shadow_box(mk(pos.x + x1, pos.y + y1, pos.z + z1), mk(pos.x + x2, pos.y + y2, pos.z + z2),
+                         Q.ui_weight);
+    y_pos = y_pos + si;
+  }
+  return Stau;
+}
+
+float cone_x(const Sat& T, const OracleEbs& Q, const ConeCS& c, v3 pos, v3 cv) {
+  float Stau = 0.0f;
+  float signal = 1.0f;
+  if (cv.x < 0) signal = -1.0f;
+  const v3 proj_y = normalize3(mk(cv.x, cv.y, 0.0f));
+  const v3 proj_z = normalize3(mk(cv.x, 0.0f, cv.z));
+  const v3 pj_y1 = normalize3(mk(proj_y.y * c.n_sn + proj_y.x * c.n_cs, proj_y.y * c.n_cs - proj_y.x * c.n_sn, 0.0f));
+  const v3 pj_y2 = normalize3(mk(proj_y.y * c.p_sn + proj_y.x * c.p_cs, proj_y.y * c.p_cs - proj_y.x * c.p_sn, 0.0f));
+  const v3 pj_z1 = normalize3(mk(proj_z.z * c.n_sn + proj_z.x * c.n_cs, 0.0f, proj_z.z * c.n_cs - proj_z.x * c.n_sn));
+  const v3 pj_z2 = normalize3(mk(proj_z.z * c.p_sn + proj_z.x * c.p_cs, 0.0f, proj_z.z * c.p_cs - proj_z.x * c.p_sn));
+  const float si = Q.interval * signal * T.S.x;
+  float x_pos = Q.initial_step * signal * T.S.x;
+  const float vmin = T.S.x * 0.5f, vmax = T.G.x - T.S.x * 0.5f;
+  while ((x_pos / cv.x) < Q.max_distance &&
+         (pos.x + (x_pos + si) > vmin && pos.x + (x_pos + si) < vmax)) {
+    const float x_mean = std::fabs(x_pos + si * 0.5f);
+    const float p_y1 = pj_y1.y * (x_mean / std::fabs(pj_y1.x));
+    const float p_y2 = pj_y2.y * (x_mean / std::fabs(pj_y2.x));
+    const float p_z1 = pj_z1.z * (x_mean / std::fabs(pj_z1.x));
+    const float p_z2 = pj_z2.z * (x_mean / std::fabs(pj_z2.x));
+    float y1 = std::fmin(p_y1, p_y2), y2 = std::fmax(p_y1, p_y2);
+    float z1 = std::fmin(p_z1, p_z2), z2 = std::fmax(p_z1, p_z2);
+    const float ydiff = std::fabs(y2 - y1), zdiff = std::fabs(z2 - z1);
+    const float ys = (std::ceil(ydiff / T.S.y) - (ydiff / T.S.y)) * 0.5f;
+    const float zs = (std::ceil(zdiff / T.S.z) - (zdiff / T.S.z)) * 0.5f;
+    y1 = y1 - ys * T.S.y; y2 = y2 + ys * T.S.y;
+    z1 = z1 - zs * T.S.z; z2 = z2 + zs * T.S.z;
+    const float x1 = std::fmin(x_pos, x_pos + si), x2 = std::fmax(x_pos, x_pos + si);
+    Stau += T.shadow_box(mk(pos.x + x1, pos.y + y1, pos.z + z1), mk(pos.x + x2, pos.y + y2, pos.z + z2),
+                         Q.ui_weight);
+    x_pos = x_pos + si;
+  }
+  return Stau;
+}
+
+}  // namespace
+
+ORACLE_API uint64_t oracle_render_ebs_rows(const OracleEbs* Q, int y0, int y1, float* out_rgba,
+                                           uint32_t* out_counts, int nthreads) {
+  const OracleRc1pass& P = Q->base;
+  const v3 eye = mk(P.eye[0], P.eye[1], P.eye[2]);
+  const v3 light = mk(P.light[0], P.light[1], P.light[2]);
+  Sat T;
+  T.t = Tex{Q->sat, {Q->sat_dims[0], Q->sat_dims[1], Q->sat_dims[2]}, 1};
+  T.S = mk(P.scale[0], P.scale[1], P.scale[2]);
+  T.G = mk((float)P.N[0] * P.scale[0], (float)P.N[1] * P.scale[1], (float)P.N[2] * P.scale[2]);
+  // inv_vol_scaled = 1.0f / (VolumeScaledSizes + VolumeScales * 2.0) (:75)
+  T.inv_vs = mk(1.0f / (T.G.x + T.S.x * 2.0f), 1.0f / (T.G.y + T.S.y * 2.0f), 1.0f / (T.G.z + T.S.z * 2.0f));
+  T.nsat = mk((float)Q->sat_dims[0], (float)Q->sat_dims[1], (float)Q->sat_dims[2]);
+  T.min_sat = mk(T.S.x * 0.5f, T.S.y * 0.5f, T.S.z * 0.5f);
+  T.max_sat = mk(T.G.x + T.S.x * 1.5f, T.G.y + T.S.y * 1.5f, T.G.z + T.S.z * 1.5f);
+  ConeCS cs{std::cos(Q->cone_angle), std::sin(Q->cone_angle), std::cos(-Q->cone_angle),
+            std::sin(-Q->cone_angle)};
+  const v3 lfwd = mk(Q->light_forward[0], Q->light_forward[1], Q->light_forward[2]);
+  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3};
+  const float ka = Q->apply_occlusion ? P.ka : 0.0f;
+  const float kd = Q->apply_shadow ? P.kd : 0.0f;
+  const float ks = Q->apply_shadow ? P.ks : 0.0f;
+  auto shade = [&](float* src, v3 tx, v3 wp, v3, float x, float y, float z) {
+    float iocc = 0.0f, isdw = 0.0f;
+    if (Q->apply_occlusion) iocc = ebs_occlusion(T, tx, Q->occ_shells, Q->occ_radius);
+    if (Q->apply_shadow) {
+      // ExtinctionDirectionalShadows (:455-481)
+      const v3 cv = Q->shadow_type == 0 ? normalize3(mk(light.x - wp.x, light.y - wp.y, light.z - wp.z))
+                                        : normalize3(lfwd);
+      const v3 ac = mk(std::fabs(cv.x), std::fabs(cv.y), std::fabs(cv.z));
+      float Stau;
+      if (ac.z > ac.x && ac.z > ac.y) Stau = cone_z(T, *Q, cs, tx, cv);
+      else if (ac.y > ac.x) Stau = cone_y(T, *Q, cs, tx, cv);
+      else Stau = cone_x(T, *Q, cs, tx, cv);
+      isdw = cvr_expf(-Stau);
+    }
+    const float inv_k = 1.0f / (ka + kd);
+    if (P.phong && P.grad) {
+      float g[3];
+      grd.sample(x, y, z, g);
+      if (g[0] != 0.0f || g[1] != 0.0f || g[2] != 0.0f) {
+        const v3 n = normalize3(mk(g[0], g[1], g[2]));
+        const v3 L = normalize3(mk(light.x - wp.x, light.y - wp.y, light.z - wp.z));
+        const v3 Ve = normalize3(mk(eye.x - wp.x, eye.y - wp.y, eye.z - wp.z));
+        const v3 Hv = normalize3(mk(Ve.x + L.x, Ve.y + L.y, Ve.z + L.z));
+        const float dd = std::fmax(0.0f, dot3(n, L));
+        const float ds = std::fmax(0.0f, dot3(Hv, n));
+        const float pw = cvr_powf(ds, P.shininess);
+        // (1/(ka+kd)) * (L*IOcc*ka + IShadow*(L*kd*dot_diff)) + IShadow*(ks*Ispecular*pow) (:528-530)
+        for (int q = 0; q < 3; q++)
+          src[q] = inv_k * ((src[q] * iocc) * ka + isdw * ((src[q] * kd) * dd)) +
+                   isdw * ((ks * P.ispec[q]) * pw);
+      }
+    } else {
+      for (int q = 0; q < 3; q++) src[q] = inv_k * ((src[q] * iocc) * ka + (src[q] * isdw) * kd);
+    }
+  };
+  return shaded_march_rows(P, y0, y1, out_rgba, out_counts, nthreads, shade);
 }

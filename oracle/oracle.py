@@ -4,6 +4,7 @@ TEST INFRASTRUCTURE ONLY."""
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import subprocess
 
@@ -47,6 +48,16 @@ class OracleDos(ctypes.Structure):
                 ("occ", OracleDosCone), ("sdw", OracleDosCone)]
 
 
+class OracleEbs(ctypes.Structure):
+    _fields_ = [("base", OracleRc1pass), ("sat", ctypes.c_void_p), ("sat_dims", ctypes.c_int * 3),
+                ("apply_occlusion", ctypes.c_int), ("occ_shells", ctypes.c_int),
+                ("occ_radius", ctypes.c_float), ("apply_shadow", ctypes.c_int),
+                ("shadow_type", ctypes.c_int), ("cone_angle", ctypes.c_float),
+                ("interval", ctypes.c_float), ("initial_step", ctypes.c_float),
+                ("ui_weight", ctypes.c_float), ("max_distance", ctypes.c_float),
+                ("light_forward", ctypes.c_float * 3)]
+
+
 def build() -> None:
     subprocess.run(["make", "-C", HERE, "-s"], check=True)
 
@@ -82,6 +93,12 @@ def lib():
         L.oracle_render_dos.restype = ctypes.c_uint64
         L.oracle_render_dos_rows.argtypes = [ctypes.POINTER(OracleDos), I, I, P, P, I]
         L.oracle_render_dos_rows.restype = ctypes.c_uint64
+        L.oracle_ext_lut.argtypes = [P, I, I, I, P]
+        L.oracle_ext_lut.restype = None
+        L.oracle_sat_build.argtypes = [P, I, I, I, I, P, P]
+        L.oracle_sat_build.restype = None
+        L.oracle_render_ebs_rows.argtypes = [ctypes.POINTER(OracleEbs), I, I, P, P, I]
+        L.oracle_render_ebs_rows.restype = ctypes.c_uint64
         _lib = L
     return _lib
 
@@ -291,4 +308,63 @@ def render_dos(vol16, scale, tf_rgbt, ext_levels, camera, W, H, step, occ_tables
     y0, y1 = rows if rows is not None else (0, H)
     S = lib().oracle_render_dos_rows(ctypes.byref(Q), int(y0), int(y1), _p(rgba), _p(cnt),
                                      int(threads))
+    return rgba, cnt, int(S)
+
+
+def ext_lut(table: np.ndarray, bpv: int = 1, extinction_input: bool = False) -> np.ndarray:
+    """GetExtN(v / (2^bits - 1)) for every voxel value (the EBS SAT cell values)."""
+    t = np.ascontiguousarray(table, np.float64)
+    out = np.zeros(256 if bpv == 1 else 65536, np.float32)
+    lib().oracle_ext_lut(_p(t), t.shape[0] - 1, int(bpv), int(extinction_input), _p(out))
+    return out
+
+
+def sat_build(vox: np.ndarray, lut: np.ndarray) -> np.ndarray:
+    """GenerateExtinctionSAT3DTex + SummedAreaTable3D<double>::BuildSAT, literally.
+    Returns the (D+2, H+2, W+2) double SAT."""
+    v = np.ascontiguousarray(vox)
+    d, h, w = v.shape
+    lut = np.ascontiguousarray(lut, np.float32)
+    out = np.zeros((d + 2, h + 2, w + 2), np.float64)
+    lib().oracle_sat_build(_p(v), v.dtype.itemsize, w, h, d, _p(lut), _p(out))
+    return out
+
+
+def ebs_max_distance(n_xyz, scale) -> float:
+    """dir_cone_max_distance = 0.75f * Dv (ebsrenderer.cpp:98-105), float arithmetic."""
+    f = np.float32
+    vw = f(n_xyz[0] * float(scale[0])); vh = f(n_xyz[1] * float(scale[1])); vd = f(n_xyz[2] * float(scale[2]))
+    dv = np.sqrt(f(f(vw * vw + vh * vh) + vd * vd), dtype=np.float32)
+    return float(f(f(0.75) * dv))
+
+
+def render_ebs(vol16, scale, tf_rgbt, sat_f32, camera, W, H, step, apply_occlusion=True,
+               occ_shells=15, occ_radius=1.0, apply_shadow=True, shadow_type=0,
+               cone_angle_deg=1.0, interval=2.0, initial_step=2.0, ui_weight=1.0,
+               max_distance=None, light=(0.0, 0.0, 0.0), light_forward=(0.0, 0.0, -1.0),
+               grad=None, phong=False, ka=0.5, kd=0.5, ks=0.8, shininess=30.0,
+               ispec=(1.0, 1.0, 1.0), threads: int = 0, rows=None):
+    """Extinction-based shading frame (ebs_ray_bbox_marching.comp).  Returns (rgba, counts, S)."""
+    vol16 = np.ascontiguousarray(vol16, np.float32)
+    tf = _q16_array(tf_rgbt)
+    sat = np.ascontiguousarray(sat_f32, np.float32)
+    if grad is not None:
+        grad = np.ascontiguousarray(grad, np.float32)
+    Q = OracleEbs()
+    Q.base = _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shininess,
+                     ispec, light)
+    Q.sat = _p(sat)
+    Q.sat_dims[:] = list(sat.shape[::-1])
+    Q.apply_occlusion, Q.occ_shells, Q.occ_radius = int(apply_occlusion), int(occ_shells), float(occ_radius)
+    Q.apply_shadow, Q.shadow_type = int(apply_shadow), int(shadow_type)
+    # DirSdwConeAngle uniform: (float)(angle * glm::pi<double>() / 180.0) (ebsrenderer.cpp:161)
+    Q.cone_angle = float(np.float32(cone_angle_deg * math.pi / 180.0))
+    Q.interval, Q.initial_step, Q.ui_weight = float(interval), float(initial_step), float(ui_weight)
+    d, h, w = vol16.shape
+    Q.max_distance = ebs_max_distance((w, h, d), scale) if max_distance is None else float(max_distance)
+    Q.light_forward[:] = [float(v) for v in light_forward]
+    rgba = np.zeros((H, W, 4), np.float32)
+    cnt = np.zeros((H, W), np.uint32)
+    y0, y1 = rows if rows is not None else (0, H)
+    S = lib().oracle_render_ebs_rows(ctypes.byref(Q), int(y0), int(y1), _p(rgba), _p(cnt), int(threads))
     return rgba, cnt, int(S)
