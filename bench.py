@@ -2,7 +2,8 @@
 """Headline benchmark: rc1pass ray-march, Msamples/s at 1024^2 on a 512^3 volume.
 
 (--renderer dos: BASELINE.json config 4 instead, the directional-occlusion renderer
-with cone AO + cone shadows at 2048^2; a secondary line, not the headline.)
+with cone AO + cone shadows at 2048^2; --renderer ebs: config 5, the extinction-SAT
+precompute + extinction-based shading on 1024^3.  Secondary lines, not the headline.)
 
 Workload (BASELINE.json metric, SURVEY.md §8d "512^3 EA"): Marschner-Lobb field
 (alpha 0.25, f_M 6) quantised to u8, 512^3, voxel scale 1 (world box +-256),
@@ -40,7 +41,8 @@ from cpp_volume_rendering_amd import datasets as D  # noqa: E402
 from cpp_volume_rendering_amd import screen_tiles as T  # noqa: E402
 from cpp_volume_rendering_amd.renderer import (Camera, DataManager, RayCasting1Pass,  # noqa: E402
                                                RC1PConeTracingDirOcclusionShading,
-                                               RenderingParameters, build_tf_rgbt, make_frame)
+                                               RC1PExtinctionBasedShading, RenderingParameters,
+                                               build_ext_lut, build_tf_rgbt, make_frame)
 
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md (spec)
 
@@ -50,9 +52,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=0, help="default 50 (dos: 5)")
     p.add_argument("--warmup", type=int, default=-1, help="default 5 (dos: 1)")
-    p.add_argument("--size", type=int, default=512)
+    p.add_argument("--size", type=int, default=0, help="volume N^3 (default 512; ebs 1024)")
     p.add_argument("--res", type=int, default=0, help="viewport (default 1024; dos 2048)")
-    p.add_argument("--renderer", choices=["rc1pass", "dos"], default="rc1pass")
+    p.add_argument("--renderer", choices=["rc1pass", "dos", "ebs"], default="rc1pass")
     p.add_argument("--tile", type=int, default=32)
     p.add_argument("--field", choices=["ml", "blobs"], default="ml")
     p.add_argument("--phong", action="store_true")
@@ -62,7 +64,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None):
+def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None):
     """The CPU oracle (C++/OpenMP restatement of ray_marching_1p.comp; the reference has
     no CPU ray-caster) on the host cores: whole frames of the same workload, repeated
     until `seconds` of wall time are spent (each frame starts from the centre band of
@@ -72,17 +74,21 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     v16 = O.volume_r16f(vol)
     step = O.default_step(scale)
-    rows_per_chunk = 16 if dos is None else 2
+    rows_per_chunk = 16
     if dos is not None:
         levels = O.ext_volume(v16, scale, dos["tf_rgba"], dos["res"], threads=threads)
 
     def render_rows(y0, y1, nthreads):
-        if dos is None:
-            return O.render_rc1pass(v16, scale, tf, cam, W, H, step, rows=(y0, y1),
-                                    threads=nthreads)[2]
-        return O.render_dos(v16, scale, tf, levels, cam, W, H, step, dos["occ"], dos["sdw"],
-                            apply_shadow=True, light=dos["light"], rows=(y0, y1),
-                            threads=nthreads)[2]
+        if dos is not None:
+            return O.render_dos(v16, scale, tf, levels, cam, W, H, step, dos["occ"], dos["sdw"],
+                                apply_shadow=True, light=dos["light"], rows=(y0, y1),
+                                threads=nthreads)[2]
+        if ebs is not None:
+            return O.render_ebs(v16, scale, tf, ebs["sat"], cam, W, H, step,
+                                light=ebs["light"], light_forward=ebs["forward"],
+                                rows=(y0, y1), threads=nthreads)[2]
+        return O.render_rc1pass(v16, scale, tf, cam, W, H, step, rows=(y0, y1),
+                                threads=nthreads)[2]
     y = H // 2 - rows_per_chunk // 2
     order = []
     for k in range(H // rows_per_chunk + 2):
@@ -103,12 +109,25 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None):
 
     S, rows, dt = run(threads, seconds)
     S1, rows1, dt1 = run(1, max(2.0, seconds / 4))
-    return {"value": round(S / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads,
+    extra = {}
+    if ebs is not None:
+        # the reference's SAT build (serial BuildSAT, restated) on a 256^3 sub-volume
+        sub = np.ascontiguousarray(vol[:256, :256, :256])
+        t0 = time.perf_counter()
+        O.sat_build(sub, ebs["lut"])
+        dts = time.perf_counter() - t0
+        extra = {"sat_build_Mcells_s": round((sub.shape[0] + 2) * (sub.shape[1] + 2) *
+                                             (sub.shape[2] + 2) / dts / 1e6, 2),
+                 "sat_build_sample": f"serial BuildSAT restatement, {sub.shape[::-1]} voxels "
+                                     f"in {dts:.2f} s (1 thread, as the reference)"}
+    return {**extra, "value": round(S / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads,
             "kind": "port",
             "sample": f"{rows} image rows ({rows / H:.1f} frames, centre band outward) of the "
                       f"same {W}x{H} frame, {S} samples in {dt:.1f} s on {threads} threads; "
                       f"C++/OpenMP oracle (no CPU ray-caster exists in the reference)"
-                      + ("; extinction pyramid built outside the timed sample" if dos else ""),
+                      + ("; extinction pyramid built outside the timed sample" if dos else "")
+                      + ("; shading only, on the GPU-built SAT (bit-identical to the oracle's, "
+                         "tests/test_ebs_gpu.py)" if ebs else ""),
             "single_thread_value": round(S1 / dt1 / 1e6, 3),
             "single_thread_sample": f"{rows1} rows, {S1} samples in {dt1:.1f} s"}
 
@@ -156,9 +175,11 @@ def main():
         torch.cuda.set_device(0)
 
     dos = a.renderer == "dos"
-    a.steps = a.steps or (5 if dos else 50)
-    a.warmup = a.warmup if a.warmup >= 0 else (1 if dos else 5)
-    n, W = a.size, a.res or (2048 if dos else 1024)
+    ebs = a.renderer == "ebs"
+    shaded = dos or ebs
+    a.steps = a.steps or (5 if dos else (2 if ebs else 50))
+    a.warmup = a.warmup if a.warmup >= 0 else (1 if shaded else 5)
+    n, W = a.size or (1024 if ebs else 512), a.res or (2048 if dos else 1024)
     H = W
     vol = D.marschner_lobb_u8(n) if a.field == "ml" else D.blobs_u8(n)
     scale = D.voxel_scale(n)
@@ -173,15 +194,25 @@ def main():
     if a.phong:
         dm.SetGradientType(N.GRADIENT_FINITE_DIFFERENCES)
     rp = RenderingParameters(W, H, light_position=D.LIGHT_LIST0_POSITION)
+    sat_ms = None
     if dos:
         r = RC1PConeTracingDirOcclusionShading(local if world > 1 else 0)
         r.glsl_apply_shadow = True        # config 4: cone AO + cone shadows (point light)
+    elif ebs:
+        dm.SetExtinctionTable(build_ext_lut(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
+        r = RC1PExtinctionBasedShading(local if world > 1 else 0)
     else:
         r = RayCasting1Pass(local if world > 1 else 0)
     r.m_apply_gradient_shading = a.phong
     r.SetExternalResources(dm, rp)
     assert r.Init(W, H)
     r.PrepareRender(cam)
+    if ebs:
+        # the SAT precompute on its own (Init built it once already): GPU wall time
+        torch.cuda.synchronize()
+        t_sat = time.perf_counter()
+        r.device.set_extinction_sat(dm.ext_lut)
+        sat_ms = (time.perf_counter() - t_sat) * 1e3
 
     dev = torch.device("cuda", local if world > 1 else 0)
     stream = torch.cuda.current_stream(dev)
@@ -202,7 +233,7 @@ def main():
     L = N.lib()
     fptr, pptr = ctypes.byref(frame), ctypes.byref(r._params)
     out = N.Output(out_buf.data_ptr(), None, total.data_ptr(), 1)
-    render = L.cvr_render_dosct if dos else L.cvr_render_rc1pass
+    render = L.cvr_render_dosct if dos else (L.cvr_render_extbsd if ebs else L.cvr_render_rc1pass)
 
     def step_once():
         N.check(render(r.device.handle, fptr, pptr, ctypes.byref(out)), "render",
@@ -217,13 +248,13 @@ def main():
 
     # samples per frame (this rank), counted by the kernel; for the shaded renderer
     # also the shaded / shadow-lit samples (each traces a fixed number of cone fetches)
-    if dos:
+    if shaded:
         N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 1), "opt", r.device.handle)
     step_once()
     torch.cuda.synchronize(dev)
     S_rank = int(total.item())
-    shade = (ctypes.c_uint64 * 2)()
-    if dos:
+    shade = (ctypes.c_uint64 * 3)()
+    if shaded:
         N.check(L.cvr_read_shade_counters(r.device.handle, shade), "shade", r.device.handle)
         N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 0), "opt", r.device.handle)
 
@@ -289,19 +320,23 @@ def main():
         # per sample + float4 output per pixel (+ 48 B per sample for the Phong gradient,
         # counted on every sample as an upper bound of the shaded ones)
         b_alg = 8 * 1 * S_rank + 16 * pixels + (48 * S_rank if a.phong else 0)
+        fetches = int(shade[2])
         if dos:
             # + 8 fp16 corners (16 B) per trilinear extinction fetch of the cones
             f_occ, f_sdw = cone_fetches(r, n, scale)
-            fetches = shade[0] * f_occ + shade[1] * f_sdw
+            assert fetches == shade[0] * f_occ + shade[1] * f_sdw
             b_alg += 16 * fetches
+        elif ebs:
+            # + 8 float corners (32 B) per trilinear SAT fetch
+            b_alg += 32 * fetches
         achieved = b_alg / (kern_ms * 1e-3) / 1e9
         wkey = f"{a.renderer}_{a.field}{n}_{W}x{H}{'_phong' if a.phong else ''}"
-        kname = ("dos_tile_kernel" if dos else
+        kname = ("shaded_march_kernel<DosShader>" if dos else
+                 "shaded_march_kernel<EbsShader>" if ebs else
                  f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, *, false, true>")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic(a.pmc if not dos else a.pmc.replace("rc1pass", "dos"),
-                                        wkey),
+                "traffic": load_traffic(a.pmc.replace("rc1pass", a.renderer), wkey),
                 "kernel": kname,
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank}
@@ -309,10 +344,15 @@ def main():
             roof.update({"shaded_samples": shade[0], "shadow_lit_samples": shade[1],
                          "cone_fetches_per_shaded": [f_occ, f_sdw],
                          "secondary_fetches": fetches})
-        metric = ("Msamples/s (rays x steps), rc1pass ray-march, 512^3 volume at 1024^2"
-                  if not dos else
-                  "Msamples/s (rays x steps), Dir. Occlusion Shading (cone AO + cone shadows), "
-                  "512^3 volume at 2048^2")
+        elif ebs:
+            roof.update({"shaded_samples": shade[0], "shadow_chains": shade[1],
+                         "sat_fetches": fetches,
+                         "sat_fetches_per_shaded": round(fetches / max(1, shade[0]), 1)})
+        metric = ("Msamples/s (rays x steps), Dir. Occlusion Shading (cone AO + cone shadows), "
+                  f"{n}^3 volume at {W}^2" if dos else
+                  "Msamples/s (rays x steps), Extinction-Based Shading (SAT AO + SAT shadows), "
+                  f"{n}^3 volume at {W}^2" if ebs else
+                  f"Msamples/s (rays x steps), rc1pass ray-march, {n}^3 volume at {W}^2")
         res = {
             "metric": metric,
             "value": round(msps, 2),
@@ -327,9 +367,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": (f"rc1pass emission-absorption, " if not dos else
-                                    f"rc1pdosct cone AO (20 deg, <=3 rays) + point-light cone "
-                                    f"shadows (0.5 deg), extinction pyramid 128^3, ")
+            "config": {"workload": (f"rc1pdosct cone AO (20 deg, <=3 rays) + point-light cone "
+                                    f"shadows (0.5 deg), extinction pyramid 128^3, " if dos else
+                                    f"rc1pextbsd SAT AO (15 shells) + point-light SAT box-chain "
+                                    f"shadows (1 deg cone), extinction SAT {n + 2}^3, " if ebs else
+                                    f"rc1pass emission-absorption, ")
                                    + f"Marschner-Lobb {n}^3 u8 "
                                    f"({a.field}), {W}x{H}, bonsai_01.tf1d, camera "
                                    f"'Initial State', step 0.5, ERT 0.99"
@@ -342,6 +384,12 @@ def main():
                                            if macro > 0 else "off"},
             "roofline": roof,
         }
+        if ebs:
+            cells = (n + 2) ** 3
+            res["precompute"] = {"sat_ms": round(sat_ms, 2), "sat_cells": cells,
+                                 "sat_Mcells_s": round(cells / (sat_ms * 1e-3) / 1e6, 1),
+                                 "what": "GenerateExtinctionSAT3DTex + BuildSAT on the GPU "
+                                         "(double, reference recurrence, bit-exact), wall time"}
         if world == 1 and not a.no_cpu_baseline:
             dos_cfg = None
             if dos:
@@ -352,8 +400,12 @@ def main():
                                      "forward": rp.light_forward, "up": rp.light_up,
                                      "right": rp.light_right,
                                      "spot_angle_deg": rp.spot_light_angle}}
+            ebs_cfg = None
+            if ebs:
+                ebs_cfg = {"sat": r.device.extinction_sat(), "lut": dm.ext_lut,
+                           "light": rp.light_position, "forward": rp.light_forward}
             res["cpu_baseline"] = cpu_baseline(vol, scale, tf, D.INITIAL_STATE_CAMERA, W, H,
-                                               a.cpu_seconds, dos_cfg)
+                                               a.cpu_seconds, dos_cfg, ebs_cfg)
         print(json.dumps(res))
     if world > 1:
         dist.barrier()

@@ -817,13 +817,13 @@ cvr_status cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int* 
   return CVR_OK;
 }
 
-cvr_status cvr_read_shade_counters(cvr_ctx* ctx, uint64_t out[2]) {
+cvr_status cvr_read_shade_counters(cvr_ctx* ctx, uint64_t out[3]) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c || !out) return CVR_ERR_ARG;
   if (!c->d_shade) return fail(c, CVR_ERR_STATE, "shade_counters option was not enabled");
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  HIP_TRY(c, hipMemcpy(out, c->d_shade, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(out, c->d_shade, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return CVR_OK;
 }
 
@@ -896,8 +896,8 @@ static cvr_status render_shaded(Ctx* c, const cvr_output* o, int ntiles, size_t 
   }
   unsigned long long* shade = nullptr;
   if (c->shade_counters) {
-    if (!c->d_shade) HIP_TRY(c, hipMalloc((void**)&c->d_shade, 2 * sizeof(unsigned long long)));
-    HIP_TRY(c, hipMemsetAsync(c->d_shade, 0, 2 * sizeof(unsigned long long), s));
+    if (!c->d_shade) HIP_TRY(c, hipMalloc((void**)&c->d_shade, 3 * sizeof(unsigned long long)));
+    HIP_TRY(c, hipMemsetAsync(c->d_shade, 0, 3 * sizeof(unsigned long long), s));
     shade = c->d_shade;
   }
   const size_t nev = c->ev_start.size();

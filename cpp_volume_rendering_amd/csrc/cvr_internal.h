@@ -159,7 +159,7 @@ struct Ctx {
   int boost_pct = 5;               // % of every band's longest entries run at raised priority
   int quad_pct = 0;                // % of every band's longest tiles marched 4 lanes per ray
   int shade_counters = 0;          // DOS/EBS: count shaded and shadow-lit samples
-  unsigned long long* d_shade = nullptr;   // [2]: shaded, lit (last frame)
+  unsigned long long* d_shade = nullptr;   // [3]: shaded, lit, secondary fetches (last frame)
   int tile_stats = 0;              // record per-tile timing (diagnostics)
   unsigned long long* d_tile_stats = nullptr;
   int tile_stats_n = 0;

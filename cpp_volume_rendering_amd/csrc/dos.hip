@@ -402,7 +402,7 @@ struct DosShader {
 
   // Shaded colour of one job; `lit` counts the shadow cones traced.
   __device__ static f3 shade(const DosArgs& Q, const uint4* __restrict__ ext, f3 tx, f3 wp,
-                             f3 cam, f3 rgb, const f3* g, uint32_t& lit) {
+                             f3 cam, f3 rgb, const f3* g, uint32_t& lit, uint32_t& fetches) {
     const Rc1passArgs& A = Q.a;
     const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
     const f3 light{A.light[0], A.light[1], A.light[2]};
@@ -413,6 +413,7 @@ struct DosShader {
       const f3 v_up = normalize3(cross3(f3{-cam.x, -cam.y, -cam.z}, v_right));
       const f3 k = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
       iocc = cone_trace(Q, Q.occ, ext, tx, k, v_up, v_right);
+      fetches += Q.occ.counts[0] + 3 * Q.occ.counts[1] + 7 * Q.occ.counts[2];
     }
     if (Q.apply_shadow) {
       f3 k, u, v;
@@ -432,6 +433,7 @@ struct DosShader {
       if (on) {
         isdw = cone_trace(Q, Q.sdw, ext, tx, k, v, u);
         lit++;
+        fetches += Q.sdw.counts[0] + 3 * Q.sdw.counts[1] + 7 * Q.sdw.counts[2];
       }
     }
     const float inv_k = 1.0f / (Q.ka + Q.kd);

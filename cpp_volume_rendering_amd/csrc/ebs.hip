@@ -89,7 +89,8 @@ __device__ float ebs_occlusion(const EbsArgs& Q, const float* __restrict__ sat, 
 }
 
 // ConeZAxis (:187-275)
-__device__ float cone_z(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv) {
+__device__ float cone_z(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv,
+                        uint32_t& boxes) {
   float Stau = 0.0f;
   float signal = 1.0f;
   if (cv.z < 0) signal = -1.0f;
@@ -119,13 +120,15 @@ __device__ float cone_z(const EbsArgs& Q, const float* __restrict__ sat, f3 pos,
     y1 = y1 - ys * Q.S[1]; y2 = y2 + ys * Q.S[1];
     const float z1 = fminf(z_pos, z_pos + si), z2 = fmaxf(z_pos, z_pos + si);
     Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2});
+    boxes++;
     z_pos = z_pos + si;
   }
   return Stau;
 }
 
 // ConeYAxis (:277-364)
-__device__ float cone_y(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv) {
+__device__ float cone_y(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv,
+                        uint32_t& boxes) {
   float Stau = 0.0f;
   float signal = 1.0f;
   if (cv.y < 0) signal = -1.0f;
@@ -155,13 +158,15 @@ __device__ float cone_y(const EbsArgs& Q, const float* __restrict__ sat, f3 pos,
     z1 = z1 - zs * Q.S[2]; z2 = z2 + zs * Q.S[2];
     const float y1 = fminf(y_pos, y_pos + si), y2 = fmaxf(y_pos, y_pos + si);
     Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2});
+    boxes++;
     y_pos = y_pos + si;
   }
   return Stau;
 }
 
 // ConeXAxis (:366-453)
-__device__ float cone_x(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv) {
+__device__ float cone_x(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv,
+                        uint32_t& boxes) {
   float Stau = 0.0f;
   float signal = 1.0f;
   if (cv.x < 0) signal = -1.0f;
@@ -191,6 +196,7 @@ __device__ float cone_x(const EbsArgs& Q, const float* __restrict__ sat, f3 pos,
     z1 = z1 - zs * Q.S[2]; z2 = z2 + zs * Q.S[2];
     const float x1 = fminf(x_pos, x_pos + si), x2 = fmaxf(x_pos, x_pos + si);
     Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2});
+    boxes++;
     x_pos = x_pos + si;
   }
   return Stau;
@@ -204,21 +210,26 @@ struct EbsShader {
 
   // ShadeSample (:498-550); `lit` counts the shadow box chains traced.
   __device__ static f3 shade(const EbsArgs& Q, const float* __restrict__ sat, f3 tx, f3 wp, f3,
-                             f3 rgb, const f3* g, uint32_t& lit) {
+                             f3 rgb, const f3* g, uint32_t& lit, uint32_t& fetches) {
     const Rc1passArgs& A = Q.a;
     const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
     const f3 light{A.light[0], A.light[1], A.light[2]};
     float iocc = 0.0f, isdw = 0.0f;
-    if (Q.apply_occlusion) iocc = ebs_occlusion(Q, sat, tx);
+    if (Q.apply_occlusion) {
+      iocc = ebs_occlusion(Q, sat, tx);
+      fetches += 8 * Q.occ_shells;
+    }
     if (Q.apply_shadow) {
       // ExtinctionDirectionalShadows (:455-481)
       const f3 cv = Q.shadow_type == 0 ? normalize3(f3{light.x - wp.x, light.y - wp.y, light.z - wp.z})
                                        : normalize3(f3{Q.lfwd[0], Q.lfwd[1], Q.lfwd[2]});
       const f3 ac{fabsf(cv.x), fabsf(cv.y), fabsf(cv.z)};
       float Stau;
-      if (ac.z > ac.x && ac.z > ac.y) Stau = cone_z(Q, sat, tx, cv);
-      else if (ac.y > ac.x) Stau = cone_y(Q, sat, tx, cv);
-      else Stau = cone_x(Q, sat, tx, cv);
+      uint32_t boxes = 0;
+      if (ac.z > ac.x && ac.z > ac.y) Stau = cone_z(Q, sat, tx, cv, boxes);
+      else if (ac.y > ac.x) Stau = cone_y(Q, sat, tx, cv, boxes);
+      else Stau = cone_x(Q, sat, tx, cv, boxes);
+      fetches += 8 * boxes;
       isdw = cvr_expf(-Stau);
       lit++;
     }

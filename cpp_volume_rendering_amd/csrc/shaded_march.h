@@ -17,9 +17,12 @@
 // A shader is a struct with
 //   using Args = ...;   // holds `Rc1passArgs a` (ray, volume, TF, tiles)
 //   using Data = ...;   // its device tables (passed by value)
-//   static f3 shade(const Args&, Data, f3 tx, f3 wp, f3 cam, f3 rgb, const f3* g, uint32_t& lit);
+//   static f3 shade(const Args&, Data, f3 tx, f3 wp, f3 cam, f3 rgb, const f3* g, uint32_t& lit,
+//                   uint32_t& fetches);
 // (tx: position in the [0, G] box, wp: world position, cam: the ray's camera
-// direction, g: the gradient sample when Phong shading is on, else null).
+// direction, g: the gradient sample when Phong shading is on, else null; lit
+// and fetches count the shadow traces and the secondary texture fetches, for the
+// roofline).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -67,7 +70,7 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
   tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
   const bool inside = px < A.W && py < A.H;
   float4 dst = make_float4(0.f, 0.f, 0.f, 0.f);
-  uint32_t cnt = 0, nshade = 0, nlit = 0;
+  uint32_t cnt = 0, nshade = 0, nlit = 0, nfetch = 0;
   Ray r;
   bool active = inside && ray_setup(A, px, py, r);
   if (active) {
@@ -146,7 +149,7 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
         const f3 rgb{jr[slot], jg[slot], jb[slot]};
         f3 g;
         if (PHONG) g = f3{jnx[slot], jny[slot], jnz[slot]};
-        const f3 c = SH::shade(Q, data, tx, wp, cam, rgb, PHONG ? &g : nullptr, nlit);
+        const f3 c = SH::shade(Q, data, tx, wp, cam, rgb, PHONG ? &g : nullptr, nlit, nfetch);
         const float a = ja[slot];
         jr[slot] = c.x * a;
         jg[slot] = c.y * a;
@@ -177,10 +180,11 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
     if (lane == 0) tile_samples[t] = v;
   }
   if (shade_ctr) {   // measurement only (secondary-fetch count of the roofline)
-    const unsigned long long sa = wave_sum(nshade), sl = wave_sum(nlit);
+    const unsigned long long sa = wave_sum(nshade), sl = wave_sum(nlit), sf = wave_sum(nfetch);
     if (lane == 0) {
       atomicAdd(&shade_ctr[0], sa);
       atomicAdd(&shade_ctr[1], sl);
+      atomicAdd(&shade_ctr[2], sf);
     }
   }
 }

@@ -9,6 +9,8 @@ tests) read like the reference:
     RC1PConeTracingDirOcclusionShading
                                 -> RC1PConeTracingDirOcclusionShading
                                                         (cppvolrend/structured/rc1pdosct/dosrcrenderer.*)
+    RC1PExtinctionBasedShading  -> RC1PExtinctionBasedShading
+                                                        (cppvolrend/structured/rc1pextbsd/ebsrenderer.*)
 
 Per frame: ``PrepareRender(camera)`` (calls ``Update`` when outdated) then
 ``Redraw()``, exactly as RenderingManager::Display does
@@ -96,6 +98,7 @@ class DataManager:
         self.scale = (1.0, 1.0, 1.0)
         self.tf_rgbt: Optional[np.ndarray] = None  # (n, 4) float32: r, g, b, extinction
         self.tf_rgba: Optional[np.ndarray] = None  # (n, 4) float32: r, g, b, opacity
+        self.ext_lut: Optional[np.ndarray] = None  # GetExtN per voxel value (EBS SAT cells)
         self.gradient_type = N.GRADIENT_NONE        # datamanager.cpp:27 (NONE by default)
         self.name = ""
 
@@ -139,6 +142,10 @@ class DataManager:
             raise ValueError(f"unsupported volume format: {path}")
         self.SetVolume(vox, scale or (1.0, 1.0, 1.0), name=path)
 
+    def SetExtinctionTable(self, ext_lut: np.ndarray):
+        """GetExtN(v / (2^bits - 1)) for every voxel value (build_ext_lut)."""
+        self.ext_lut = np.ascontiguousarray(ext_lut, dtype=np.float32)
+
     def ReadTransferFunction(self, path: str):
         self.SetTransferFunction(read_tf1d(path))
 
@@ -156,6 +163,18 @@ def read_tf1d(path: str) -> np.ndarray:
     N.check(L.cvr_read_tf1d(path.encode(), None, n), "cvr_read_tf1d")
     out = np.empty((n.value, 4), dtype=np.float32)
     N.check(L.cvr_read_tf1d(path.encode(), N.fptr(out), n), "cvr_read_tf1d")
+    return out
+
+
+def build_ext_lut(rgb_cp, alpha_cp, bytes_per_voxel: int = 1, max_density: int = 255,
+                  extinction_input: bool = False) -> np.ndarray:
+    """TransferFunction1D::GetExtN of every voxel value: the EBS SAT cell values."""
+    rgb = np.ascontiguousarray(np.asarray(rgb_cp, dtype=np.float64).reshape(-1, 4))
+    a = np.ascontiguousarray(np.asarray(alpha_cp, dtype=np.float64).reshape(-1, 2))
+    out = np.empty(256 if bytes_per_voxel == 1 else 65536, dtype=np.float32)
+    N.check(N.lib().cvr_tf1d_ext_lut(N.dptr(rgb), rgb.shape[0], N.dptr(a), a.shape[0],
+                                     max_density, int(extinction_input), int(bytes_per_voxel),
+                                     N.fptr(out)), "cvr_tf1d_ext_lut")
     return out
 
 
@@ -256,6 +275,22 @@ class Device:
         N.check(N.lib().cvr_set_extinction_volume(self.handle, N.fptr(t), t.shape[0], r,
                                                   float(sigma0)),
                 "cvr_set_extinction_volume", self.handle)
+
+    def set_extinction_sat(self, ext_lut: np.ndarray):
+        t = np.ascontiguousarray(ext_lut, dtype=np.float32)
+        N.check(N.lib().cvr_set_extinction_sat(self.handle, N.fptr(t), t.shape[0]),
+                "cvr_set_extinction_sat", self.handle)
+
+    def extinction_sat(self) -> np.ndarray:
+        """The float SAT as a (D+2, H+2, W+2) array."""
+        L = N.lib()
+        dims = (ctypes.c_int * 3)()
+        N.check(L.cvr_copy_extinction_sat(self.handle, None, 0, dims), "cvr_copy_extinction_sat",
+                self.handle)
+        a = np.zeros((dims[2], dims[1], dims[0]), np.float32)
+        N.check(L.cvr_copy_extinction_sat(self.handle, N.fptr(a), a.size, dims),
+                "cvr_copy_extinction_sat", self.handle)
+        return a
 
     def extinction_levels(self) -> list:
         """Every level of the extinction pyramid as (d, h, w) float32 arrays."""
@@ -514,6 +549,80 @@ class RC1PConeTracingDirOcclusionShading(RayCasting1Pass):
         N.check(N.lib().cvr_render_dosct(self.device.handle, ctypes.byref(self._frame),
                                          ctypes.byref(self._params), ctypes.byref(out)),
                 "cvr_render_dosct", self.device.handle)
+
+
+class RC1PExtinctionBasedShading(RayCasting1Pass):
+    """HIP implementation of RC1PExtinctionBasedShading
+    (cppvolrend/structured/rc1pextbsd/ebsrenderer.cpp): the single-pass march with a
+    summed-area-table ambient occlusion and a SAT box-chain shadow per sample."""
+
+    POINT_LIGHT, DIRECTIONAL_LIGHT = 0, 1
+
+    def __init__(self, device: int = 0):
+        super().__init__(device)
+        self.apply_ambient_occlusion = True          # ebsrenderer.cpp:27-31
+        self.ambient_occlusion_shells = 15
+        self.ambient_occlusion_radius = 1.0
+        self.apply_directional_shadows = True        # :33-42
+        self.dir_shadow_cone_angle = 1.0
+        self.dir_shadow_sample_interval = 2.0
+        self.dir_shadow_initial_step = 2.0
+        self.dir_shadow_user_interface_weight = 1.0
+        self.dir_cone_max_distance = 0.0             # 0: 0.75 * diagonal, set at Init (:98-105)
+        self.type_of_shadow = self.POINT_LIGHT
+        self._params = N.EbsParams()
+
+    def GetName(self): return "1-Pass - Ray Casting - Extinction Based Shading"
+    def GetAbbreviationName(self): return "s_1rc_ebs"
+
+    def Init(self, swidth: int, sheight: int) -> bool:
+        dm = self.m_ext_data_manager
+        if dm is None or dm.ext_lut is None:
+            return False
+        if not super().Init(swidth, sheight):
+            return False
+        self.device.set_extinction_sat(dm.ext_lut)   # GenerateExtinctionSAT3DTex (:88-90)
+        return True
+
+    def Update(self, camera: Camera) -> bool:
+        rp = self.m_ext_rendering_parameters or RenderingParameters()
+        self._frame = make_frame(camera, self.width, self.height)
+        p = self._params
+        p.step = float(self.m_u_step_size)
+        p.apply_gradient_shading = int(bool(self.m_apply_gradient_shading) and
+                                       self.m_ext_data_manager.gradient_type != N.GRADIENT_NONE)
+        p.ka, p.kd = rp.blinnphong_ka, rp.blinnphong_kd
+        p.ks, p.shininess = rp.blinnphong_ks, rp.blinnphong_shininess
+        p.ispecular[:] = [float(v) for v in rp.light_specular]
+        p.light_pos[:] = [float(v) for v in rp.light_position]
+        p.light_forward[:] = [float(v) for v in rp.light_forward]
+        p.apply_occlusion = int(bool(self.apply_ambient_occlusion))
+        p.occlusion_shells = int(self.ambient_occlusion_shells)
+        p.occlusion_radius = float(self.ambient_occlusion_radius)
+        p.apply_shadow = int(bool(self.apply_directional_shadows))
+        p.shadow_type = int(self.type_of_shadow)
+        p.shadow_cone_angle_deg = float(self.dir_shadow_cone_angle)
+        p.shadow_sample_interval = float(self.dir_shadow_sample_interval)
+        p.shadow_initial_step = float(self.dir_shadow_initial_step)
+        p.shadow_ui_weight = float(self.dir_shadow_user_interface_weight)
+        p.shadow_max_distance = float(self.dir_cone_max_distance)
+        return True
+
+    def Redraw(self, stream: Optional[torch.cuda.Stream] = None, count_samples: bool = True):
+        if self._frame is None:
+            raise N.CvrError(N.CVR_ERR_STATE, "RC1PExtinctionBasedShading.Redraw",
+                             "Update() not called")
+        s = stream if stream is not None else torch.cuda.current_stream(self._device_index)
+        self.device.set_stream(s.cuda_stream)
+        if count_samples:
+            with torch.cuda.stream(s):
+                self.total.zero_()
+        out = N.Output(self.rgba.data_ptr(),
+                       self.samples.data_ptr() if count_samples else None,
+                       self.total.data_ptr() if count_samples else None, 1)
+        N.check(N.lib().cvr_render_extbsd(self.device.handle, ctypes.byref(self._frame),
+                                          ctypes.byref(self._params), ctypes.byref(out)),
+                "cvr_render_extbsd", self.device.handle)
 
 
 def composite_over_white(rgba: np.ndarray) -> np.ndarray:

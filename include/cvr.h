@@ -319,12 +319,12 @@ cvr_status  cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int*
  * frames, oldest first.  Waits for those frames; resets the frame count. */
 cvr_status  cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* out_frames);
 
-/* Measurement (shade_counters option): samples of the last shaded frame
- * (cvr_render_dosct) that ran the shading kernel (alpha > 0), and those of
- * them whose shadow cone was traced (spot-light cut-off excluded).  Each
- * traces counts[0] + 3 counts[1] + 7 counts[2] trilinear extinction fetches
- * per cone: the secondary traffic of the roofline. */
-cvr_status  cvr_read_shade_counters(cvr_ctx* ctx, uint64_t out[2]);
+/* Measurement (shade_counters option), for the last shaded frame
+ * (cvr_render_dosct / cvr_render_extbsd): out[0] samples that ran the shading
+ * (alpha > 0), out[1] those whose shadow was traced (spot cut-off excluded),
+ * out[2] the secondary trilinear fetches (extinction pyramid / SAT): the
+ * secondary traffic of the roofline. */
+cvr_status  cvr_read_shade_counters(cvr_ctx* ctx, uint64_t out[3]);
 
 /* ----------------------------------------------------------------------------
  * Host-side helpers (native replacements for the reference's MSVC-only
