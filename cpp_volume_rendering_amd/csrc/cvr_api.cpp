@@ -250,6 +250,7 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr;
   p = c->d_ext_levels; free_dev(p); c->d_ext_levels = nullptr;
   p = c->d_sat; free_dev(p); c->d_sat = nullptr;
+  p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr;
   p = c->d_shade; free_dev(p); c->d_shade = nullptr;
   p = c->d_cones; free_dev(p); c->d_cones = nullptr;
   delete[] c->cone_tab;
@@ -452,6 +453,7 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
   { void* p = c->d_ext; free_dev(p); c->d_ext = nullptr; c->ext_levels = 0; }
   { void* p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr; }
   { void* p = c->d_sat; free_dev(p); c->d_sat = nullptr; }
+  { void* p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr; }
   c->cone_valid = 0;
   HIP_TRY(c, hipMalloc((void**)&c->d_lut, nv * sizeof(uint16_t)));
   uint16_t* d_lut = c->d_lut;
@@ -1129,9 +1131,13 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
     return fail(c, CVR_ERR_ARG, "cvr_set_extinction_sat: need one extinction per voxel value (%d)", nv);
   const int w = c->N[0] + 2, h = c->N[1] + 2, d = c->N[2] + 2;
   const size_t cells = (size_t)w * h * d;
+  // the shader indexes texels with 32-bit / 24-bit products
+  if (w > 4096 || h > 4096 || d > 4096 || cells >= ((size_t)1 << 31))
+    return fail(c, CVR_ERR_ARG, "cvr_set_extinction_sat: volume too large for the SAT");
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   { void* p = c->d_sat; free_dev(p); c->d_sat = nullptr; }
+  { void* p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr; }
   float* d_lut = nullptr;
   double* d_sd = nullptr;
   hipError_t e = hipMalloc((void**)&d_lut, (size_t)nv * sizeof(float));
@@ -1142,8 +1148,12 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   (void)hipFree(d_lut);
   (void)hipFree(d_sd);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_sat_cells, cells * 2 * sizeof(float4));
+  if (e == hipSuccess) e = cvr::launch_sat_cells(*c, c->d_sat, c->d_sat_cells, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     void* p = c->d_sat; free_dev(p); c->d_sat = nullptr;
+    p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr;
     return fail(c, e == hipErrorOutOfMemory ? CVR_ERR_OOM : CVR_ERR_HIP,
                 "cvr_set_extinction_sat: %s", hipGetErrorString(e));
   }

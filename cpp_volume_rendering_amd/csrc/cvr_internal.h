@@ -196,6 +196,7 @@ struct Ctx {
   ExtLevel* d_ext_levels = nullptr;  // [kMaxExtLevels] addressing of the levels
   // extinction-based shading: the float SAT of (N+2) cells per axis
   float* d_sat = nullptr;
+  float4* d_sat_cells = nullptr;   // the same SAT as cell8 (8 float corners per texel)
   int sat_dims[3] = {0, 0, 0};
   int ext_res[3] = {0, 0, 0};
   int ext_levels = 0;
@@ -236,6 +237,7 @@ hipError_t launch_ext_volume(const Ctx& c, const float4* d_tf_rgba, int tf_n, co
                              hipStream_t s);
 hipError_t launch_sat_build(const Ctx& c, const float* d_lut, double* d_sd, float* d_sf,
                             hipStream_t s);
+hipError_t launch_sat_cells(const Ctx& c, const float* d_sf, float4* d_cells, hipStream_t s);
 hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s);
 hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,

@@ -20,29 +20,27 @@ namespace cvr {
 
 namespace {
 
-// GetSummed3Density (:77-83): trilinear of the float SAT at u = p * inv_vol_scaled.
-__device__ __forceinline__ float sat_fetch(const EbsArgs& Q, const float* __restrict__ sat, float x,
+// GetSummed3Density (:77-83): trilinear of the float SAT at u = p * inv_vol_scaled,
+// from the cell8 copy (two float4 per texel: the 8 corners, x fastest).
+__device__ __forceinline__ float sat_fetch(const EbsArgs& Q, const float4* __restrict__ sat, float x,
                                            float y, float z) {
   const float tx = __builtin_amdgcn_fmed3f(fmaf(x * Q.inv_vs[0], Q.nsat[0], -0.5f), 0.0f, Q.nsat_m1[0]);
   const float ty = __builtin_amdgcn_fmed3f(fmaf(y * Q.inv_vs[1], Q.nsat[1], -0.5f), 0.0f, Q.nsat_m1[1]);
   const float tz = __builtin_amdgcn_fmed3f(fmaf(z * Q.inv_vs[2], Q.nsat[2], -0.5f), 0.0f, Q.nsat_m1[2]);
-  const int ix = (int)tx, iy = (int)ty, iz = (int)tz;
+  // < 2^31 texels (checked on the host): 32-bit index, 24-bit row products
+  const uint32_t row = __umul24((uint32_t)tz, (uint32_t)Q.sat_dims[1]) + (uint32_t)ty;
+  const uint32_t idx = __umul24(row, (uint32_t)Q.sat_dims[0]) + (uint32_t)tx;
+  const float4* cell = sat + 2 * (size_t)idx;
+  const float4 lo = cell[0], hi = cell[1];
   const float ax = __builtin_amdgcn_fractf(tx), ay = __builtin_amdgcn_fractf(ty),
               az = __builtin_amdgcn_fractf(tz);
-  const int x1 = min(ix + 1, Q.sat_dims[0] - 1), y1 = min(iy + 1, Q.sat_dims[1] - 1),
-            z1 = min(iz + 1, Q.sat_dims[2] - 1);
-  const long long sy = Q.sat_dims[0], sz = (long long)Q.sat_dims[0] * Q.sat_dims[1];
-  const long long r00 = iz * sz + iy * sy, r10 = iz * sz + y1 * sy;
-  const long long r01 = z1 * sz + iy * sy, r11 = z1 * sz + y1 * sy;
-  const float c00 = lerpf(sat[r00 + ix], sat[r00 + x1], ax);
-  const float c10 = lerpf(sat[r10 + ix], sat[r10 + x1], ax);
-  const float c01 = lerpf(sat[r01 + ix], sat[r01 + x1], ax);
-  const float c11 = lerpf(sat[r11 + ix], sat[r11 + x1], ax);
+  const float c00 = lerpf(lo.x, lo.y, ax), c10 = lerpf(lo.z, lo.w, ax);
+  const float c01 = lerpf(hi.x, hi.y, ax), c11 = lerpf(hi.z, hi.w, ax);
   return lerpf(lerpf(c00, c10, ay), lerpf(c01, c11, ay), az);
 }
 
 // EvaluateSAT3D (:85-99)
-__device__ __forceinline__ float sat_box(const EbsArgs& Q, const float* __restrict__ sat, f3 p1, f3 p2) {
+__device__ __forceinline__ float sat_box(const EbsArgs& Q, const float4* __restrict__ sat, f3 p1, f3 p2) {
   const float V1 = sat_fetch(Q, sat, p2.x, p2.y, p2.z), V2 = sat_fetch(Q, sat, p1.x, p2.y, p2.z);
   const float V3 = sat_fetch(Q, sat, p2.x, p2.y, p1.z), V4 = sat_fetch(Q, sat, p1.x, p2.y, p1.z);
   const float V5 = sat_fetch(Q, sat, p2.x, p1.y, p2.z), V6 = sat_fetch(Q, sat, p1.x, p1.y, p2.z);
@@ -58,14 +56,14 @@ __device__ __forceinline__ f3 sat_offset(const EbsArgs& Q, f3 p) {
 }
 
 // EvaluateShadowSAT3D (:148-185, the texture path)
-__device__ __forceinline__ float shadow_box(const EbsArgs& Q, const float* __restrict__ sat, f3 p1, f3 p2) {
+__device__ __forceinline__ float shadow_box(const EbsArgs& Q, const float4* __restrict__ sat, f3 p1, f3 p2) {
   const float volquery = ((fabsf(p1.x - p2.x) / Q.S[0])) * ((fabsf(p1.y - p2.y) / Q.S[1])) *
                          ((fabsf(p1.z - p2.z) / Q.S[2]));
   return ((sat_box(Q, sat, sat_offset(Q, p1), sat_offset(Q, p2)) / volquery)) * Q.ui_weight;
 }
 
 // ExtinctionAmbientOcclusion (:109-146)
-__device__ float ebs_occlusion(const EbsArgs& Q, const float* __restrict__ sat, f3 tx) {
+__device__ float ebs_occlusion(const EbsArgs& Q, const float4* __restrict__ sat, f3 tx) {
   const float R = Q.occ_radius;
   const f3 r0{R * Q.S[0], R * Q.S[1], R * Q.S[2]};
   const float SAT_Sh0 = sat_box(Q, sat, sat_offset(Q, f3{tx.x - r0.x, tx.y - r0.y, tx.z - r0.z}),
@@ -89,7 +87,7 @@ __device__ float ebs_occlusion(const EbsArgs& Q, const float* __restrict__ sat, 
 }
 
 // ConeZAxis (:187-275)
-__device__ float cone_z(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv,
+__device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
   float Stau = 0.0f;
   float signal = 1.0f;
@@ -127,7 +125,7 @@ __device__ float cone_z(const EbsArgs& Q, const float* __restrict__ sat, f3 pos,
 }
 
 // ConeYAxis (:277-364)
-__device__ float cone_y(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv,
+__device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
   float Stau = 0.0f;
   float signal = 1.0f;
@@ -165,7 +163,7 @@ __device__ float cone_y(const EbsArgs& Q, const float* __restrict__ sat, f3 pos,
 }
 
 // ConeXAxis (:366-453)
-__device__ float cone_x(const EbsArgs& Q, const float* __restrict__ sat, f3 pos, f3 cv,
+__device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
   float Stau = 0.0f;
   float signal = 1.0f;
@@ -206,10 +204,10 @@ __device__ float cone_x(const EbsArgs& Q, const float* __restrict__ sat, f3 pos,
 
 struct EbsShader {
   using Args = EbsArgs;
-  using Data = const float*;   // the float SAT
+  using Data = const float4*;   // the float SAT, cell8
 
   // ShadeSample (:498-550); `lit` counts the shadow box chains traced.
-  __device__ static f3 shade(const EbsArgs& Q, const float* __restrict__ sat, f3 tx, f3 wp, f3,
+  __device__ static f3 shade(const EbsArgs& Q, const float4* __restrict__ sat, f3 tx, f3 wp, f3,
                              f3 rgb, const f3* g, uint32_t& lit, uint32_t& fetches) {
     const Rc1passArgs& A = Q.a;
     const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
@@ -258,7 +256,7 @@ struct EbsShader {
 
 hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
-  return launch_shaded_march<EbsShader>(c, q, q.phong != 0, c.d_sat, out, samples, shade,
+  return launch_shaded_march<EbsShader>(c, q, q.phong != 0, c.d_sat_cells, out, samples, shade,
                                         tile_samples, s);
 }
 
