@@ -64,7 +64,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None):
+def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgba=None):
     """The CPU oracle (C++/OpenMP restatement of ray_marching_1p.comp; the reference has
     no CPU ray-caster) on the host cores: whole frames of the same workload, repeated
     until `seconds` of wall time are spent (each frame starts from the centre band of
@@ -78,17 +78,20 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None):
     if dos is not None:
         levels = O.ext_volume(v16, scale, dos["tf_rgba"], dos["res"], threads=threads)
 
-    def render_rows(y0, y1, nthreads):
+    def render_rows_full(y0, y1, nthreads):
         if dos is not None:
             return O.render_dos(v16, scale, tf, levels, cam, W, H, step, dos["occ"], dos["sdw"],
                                 apply_shadow=True, light=dos["light"], rows=(y0, y1),
-                                threads=nthreads)[2]
+                                threads=nthreads)
         if ebs is not None:
             return O.render_ebs(v16, scale, tf, ebs["sat"], cam, W, H, step,
                                 light=ebs["light"], light_forward=ebs["forward"],
-                                rows=(y0, y1), threads=nthreads)[2]
+                                rows=(y0, y1), threads=nthreads)
         return O.render_rc1pass(v16, scale, tf, cam, W, H, step, rows=(y0, y1),
-                                threads=nthreads)[2]
+                                threads=nthreads)
+
+    def render_rows(y0, y1, nthreads):
+        return render_rows_full(y0, y1, nthreads)[2]
     y = H // 2 - rows_per_chunk // 2
     order = []
     for k in range(H // rows_per_chunk + 2):
@@ -120,6 +123,24 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None):
                                              (sub.shape[2] + 2) / dts / 1e6, 2),
                  "sat_build_sample": f"serial BuildSAT restatement, {sub.shape[::-1]} voxels "
                                      f"in {dts:.2f} s (1 thread, as the reference)"}
+    if gpu_rgba is not None:
+        # the checker: this frame's GPU image against the oracle on a band of rows
+        # (the whole frame for rc1pass), as float bits and as eval.py's SSIM
+        from cpp_volume_rendering_amd.ssim import ssim_rgba
+        band = H if (dos is None and ebs is None) else (64 if dos is not None else 32)
+        y0 = H // 2 - band // 2
+        ref = render_rows_full(y0, y0 + band, threads)[0][y0:y0 + band]
+        got = gpu_rgba[y0:y0 + band]
+        extra["parity"] = {
+            "rows": [y0, y0 + band],
+            "bit_exact": bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32))),
+            "max_abs_diff": float(np.nan_to_num(np.abs(got.astype(np.float64) - ref), nan=0.0,
+                                                posinf=0.0).max()),
+            # non-finite pixels (NaN/inf in the same channels on both sides count as equal)
+            "nonfinite_px": int((~np.isfinite(ref)).any(-1).sum()),
+            "ssim_rgb8_vs_oracle": round(ssim_rgba(got, ref), 6),
+            "what": "GPU frame vs the CPU oracle (CVR-SPEC) on these rows; SSIM as eval.py "
+                    "(magick compare -metric SSIM, tests/test_ssim.py) of the screenshots"}
     return {**extra, "value": round(S / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads,
             "kind": "port",
             "sample": f"{rows} image rows ({rows / H:.1f} frames, centre band outward) of the "
@@ -404,8 +425,11 @@ def main():
             if ebs:
                 ebs_cfg = {"sat": r.device.extinction_sat(), "lut": dm.ext_lut,
                            "light": rp.light_position, "forward": rp.light_forward}
+            gpu_img = out_buf.float().cpu().numpy() if world == 1 else None
             res["cpu_baseline"] = cpu_baseline(vol, scale, tf, D.INITIAL_STATE_CAMERA, W, H,
-                                               a.cpu_seconds, dos_cfg, ebs_cfg)
+                                               a.cpu_seconds, dos_cfg, ebs_cfg, gpu_img)
+            if "parity" in res["cpu_baseline"]:
+                res["parity"] = res["cpu_baseline"].pop("parity")
         print(json.dumps(res))
     if world > 1:
         dist.barrier()
