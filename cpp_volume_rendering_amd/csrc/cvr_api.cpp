@@ -428,6 +428,8 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
     return fail(c, CVR_ERR_ARG, "cvr_set_volume: scale must be positive");
   if ((size_t)(w + 4) * (h + 4) * (d + 4) >= (size_t)1 << 32)
     return fail(c, CVR_ERR_ARG, "cvr_set_volume: volume too large for 32-bit cell indexing");
+  if ((size_t)(w + 1) * (h + 1) >= (size_t)1 << 23)
+    return fail(c, CVR_ERR_ARG, "cvr_set_volume: slice too large for 24-bit cell addressing");
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   free_dev(c->d_vox); c->vox_bytes = 0;

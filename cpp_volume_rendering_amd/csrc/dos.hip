@@ -169,7 +169,7 @@ hipError_t launch_ext_volume(const Ctx& c, const float4* d_tf_rgba, int tf_n, co
     E.G[i] = (float)c.N[i] * c.scale[i];
   }
   E.tf_n = tf_n;
-  const uint4* cells = (const uint4*)c.d_cells + c.cells.linear_origin;
+  const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
   for (int L = 0; L < nlevels; L++) {
     E.L = L;
     for (int i = 0; i < 3; i++) {

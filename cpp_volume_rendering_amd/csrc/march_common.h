@@ -41,25 +41,37 @@ __device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lx, 
 // Sampling
 // ---------------------------------------------------------------------------
 
-// One sample's cell address + weights.  Texel coordinates are clamped to
-// [0, N-1]: under CLAMP_TO_EDGE a coordinate in [-1, 0) blends texel 0 with
-// itself and the clamped one weights texel 0 by exactly 1 — both give v0
-// bit-exactly (fmaf(a, 0, v0) = fmaf(0, d, v0) = v0 for v0 >= 0) — and with
-// x >= 0 the floor is the truncating convert and the weight one v_fract.
+// floor(x) as int in one instruction (x finite and in int range).
+__device__ __forceinline__ int cvt_flr(float x) {
+  int r;
+  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// One sample's cell address + weights.  Along each axis the texel coordinate x
+// lies in [-0.5, N-0.5] (a sample inside the box); cell floor(x)+1 of the
+// (N+1)^3 cell grid holds texels (floor(x), floor(x)+1) clamped to the edge, so
+// for x in [-1, 0) and [N-1, N) it holds one texel twice and any weight gives
+// that texel exactly (fmaf(a, 0, v) = v for v >= 0) — the value GL's
+// CLAMP_TO_EDGE and the oracle's clamped floor give.  Weight = v_fract(x).
 struct SamplePos { uint32_t idx; float ax, ay, az; int ix, iy, iz; };
 
 __device__ __forceinline__ SamplePos sample_pos(float x, float y, float z, const Rc1passArgs& A) {
-  x = __builtin_amdgcn_fmed3f(x, 0.0f, A.nm1[0]);
-  y = __builtin_amdgcn_fmed3f(y, 0.0f, A.nm1[1]);
-  z = __builtin_amdgcn_fmed3f(z, 0.0f, A.nm1[2]);
   SamplePos p;
   p.ax = __builtin_amdgcn_fractf(x); p.ay = __builtin_amdgcn_fractf(y); p.az = __builtin_amdgcn_fractf(z);
-  p.ix = (int)x; p.iy = (int)y; p.iz = (int)z;
-  // cell (ix+1, iy+1, iz+1) of the (N+1)^3 x-fastest grid; the +1 offsets live
-  // in the base pointer
-  p.idx = __umul24((uint32_t)p.iz, (uint32_t)A.cells.pitch_z) +
-          __umul24((uint32_t)p.iy, (uint32_t)A.cells.pitch_y) + (uint32_t)p.ix;
+  p.ix = cvt_flr(x); p.iy = cvt_flr(y); p.iz = cvt_flr(z);
+  // cell (ix+1, iy+1, iz+1), counted from the grid's first cell (ix, iy, iz >= -1)
+  p.idx = (uint32_t)(__mul24(p.iz, A.cells.pitch_z) + __mul24(p.iy, A.cells.pitch_y) +
+                     (p.ix + (int)A.cells.linear_origin));
   return p;
+}
+
+// The same for a position that may lie anywhere (not a live sample of a hit
+// ray): clamped into the grid first, so the load stays in bounds.
+__device__ __forceinline__ SamplePos sample_pos_clamped(float x, float y, float z,
+                                                       const Rc1passArgs& A) {
+  return sample_pos(__builtin_amdgcn_fmed3f(x, 0.0f, A.nm1[0]), __builtin_amdgcn_fmed3f(y, 0.0f, A.nm1[1]),
+                    __builtin_amdgcn_fmed3f(z, 0.0f, A.nm1[2]), A);
 }
 
 // (float)hi - (float)lo of a packed fp16 pair, in ONE mixed-precision FMA
@@ -135,6 +147,7 @@ struct Ray {
   f3 dir, tpos, o, dt;   // direction, entry point (texture space), texel-space origin/step
   f3 inv_dt;             // 1 / dt (macro-cell exits)
   float D;               // distance to evaluate, |tfar - tnear|
+  bool outside;          // box behind the eye (tfar < 0): the march runs outside the grid
 };
 
 // Ray generation + slab test, ray_marching_1p.comp:93-121 and
@@ -157,6 +170,11 @@ __device__ __forceinline__ bool ray_setup(const Rc1passArgs& A, int px, int py, 
   float tnear = fmaxf(fmaxf(fminf(ta.x, tb.x), fminf(ta.y, tb.y)), fminf(ta.z, tb.z));
   float tfar = fminf(fminf(fmaxf(ta.x, tb.x), fmaxf(ta.y, tb.y)), fmaxf(ta.z, tb.z));
   bool hit = tfar > tnear;
+  // With tfar >= 0 the marched segment [max(tnear, 0), tfar] lies in the box;
+  // a box behind the eye is still "hit" and marched from the eye outward
+  // (the reference samples the clamped texture there), so those positions
+  // must be clamped before addressing cells.
+  r.outside = !(tfar >= 0.0f);
   tnear = fmaxf(tnear, 0.0f);
   r.dir = dir;
   r.D = fabsf(tfar - tnear);

@@ -89,6 +89,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
   float s = 0.0f;
   bool done = !(s < D);
   bool probe = true;
+  const bool wave_in_box = __ballot(r.outside) == 0;   // the usual case: no clamps
   while (!done) {
     // Empty-space skipping (bit-exact): if the macro cell holding the next
     // sample is transparent for the current TF (every density its texels can
@@ -105,21 +106,55 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
         continue;
       }
     }
-    // stage 1: the next K sample positions (sequential s += h) and their loads
+    // stage 1: the next K sample positions (sequential s += h) and their loads.
+    // Away from the ray's end every h is the full step: when D - s_(K-1) >=
+    // step for every active lane (s_j = s + step + ... + step, the same adds),
+    // the min / compare of each step are skipped (wave-uniform branch).
     float hj[K], tj[K];
     bool vj[K];
     SamplePos sp[K];
     uint4 raw[K];
-    float ss = s;
+    float ss;
+    {
+      float c[K + 1];
+      c[0] = s;
 #pragma unroll
-    for (int j = 0; j < K; j++) {
-      vj[j] = ss < D;
-      hj[j] = fminf(step, D - ss);
-      tj[j] = fmaf(hj[j], 0.5f, ss);
-      ss = ss + hj[j];
-      sp[j] = sample_pos(fmaf(r.dt.x, tj[j], r.o.x), fmaf(r.dt.y, tj[j], r.o.y),
-                                 fmaf(r.dt.z, tj[j], r.o.z), A);
-      raw[j] = cells[sp[j].idx];
+      for (int j = 0; j < K; j++) c[j + 1] = c[j] + step;
+      if (__ballot(!(D - c[K - 1] >= step)) == 0) {
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+          vj[j] = true;
+          hj[j] = step;
+          tj[j] = fmaf(step, 0.5f, c[j]);
+        }
+        ss = c[K];
+      } else {
+        ss = s;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+          vj[j] = ss < D;
+          hj[j] = fminf(step, D - ss);
+          // a sample past the ray's end is not composited; its (discarded) load
+          // goes to the entry point so that it stays inside the grid
+          tj[j] = vj[j] ? fmaf(hj[j], 0.5f, ss) : 0.0f;
+          ss = ss + hj[j];
+        }
+      }
+    }
+    if (wave_in_box) {
+#pragma unroll
+      for (int j = 0; j < K; j++) {
+        sp[j] = sample_pos(fmaf(r.dt.x, tj[j], r.o.x), fmaf(r.dt.y, tj[j], r.o.y),
+                           fmaf(r.dt.z, tj[j], r.o.z), A);
+        raw[j] = cells[sp[j].idx];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; j++) {
+        sp[j] = sample_pos_clamped(fmaf(r.dt.x, tj[j], r.o.x), fmaf(r.dt.y, tj[j], r.o.y),
+                                   fmaf(r.dt.z, tj[j], r.o.z), A);
+        raw[j] = cells[sp[j].idx];
+      }
     }
     // stage 2: density and transfer-function classification
     float4 src[K];
@@ -238,7 +273,8 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
 #pragma unroll
     for (int k = 0; k < K; k++) {
       tj[k] = fmaf(hj[k], 0.5f, sj[k]);
-      sp[k] = sample_pos(fmaf(r.dt.x, tj[k], r.o.x), fmaf(r.dt.y, tj[k], r.o.y),
+      // quad lanes of dead rays or past a ray's end load too (results dropped)
+      sp[k] = sample_pos_clamped(fmaf(r.dt.x, tj[k], r.o.x), fmaf(r.dt.y, tj[k], r.o.y),
                                  fmaf(r.dt.z, tj[k], r.o.z), A);
       raw[k] = cells[sp[k].idx];
     }
@@ -577,7 +613,7 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
   size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
   if (c.max_waves_cu > 0) lds = std::max(lds, (size_t)(160 * 1024 / c.max_waves_cu) & ~(size_t)255);
   // cell (1,1,1) <-> texel (0,0,0)
-  const uint4* cells = (const uint4*)c.d_cells + c.cells.linear_origin;
+  const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
   int grid = order ? plan.order_slots : plan.ntiles;
   hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF>), dim3(grid), dim3(64), lds, s,
                      a, cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples,

@@ -82,6 +82,7 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
   const f3 hg{A.half_grid[0], A.half_grid[1], A.half_grid[2]};
   const float step = A.step, fn = (float)A.tf_n;
   float s = 0.0f;
+  const bool wave_in_box = __ballot(active && r.outside) == 0;   // else clamp positions
 
   for (;;) {
     // ---- march until the wave holds a full batch of jobs --------------------
@@ -94,8 +95,9 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
       if (can) {
         const float h = fminf(step, r.D - s);
         const float tt = fmaf(h, 0.5f, s);
-        const SamplePos sp = sample_pos(fmaf(r.dt.x, tt, r.o.x), fmaf(r.dt.y, tt, r.o.y),
-                                        fmaf(r.dt.z, tt, r.o.z), A);
+        const float x = fmaf(r.dt.x, tt, r.o.x), y = fmaf(r.dt.y, tt, r.o.y),
+                    z = fmaf(r.dt.z, tt, r.o.z);
+        const SamplePos sp = wave_in_box ? sample_pos(x, y, z, A) : sample_pos_clamped(x, y, z, A);
         const float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
         cnt++;
         if (sc.w > 0.0f) {
@@ -197,7 +199,7 @@ hipError_t launch_shaded_march(const Ctx& c, const typename SH::Args& q, bool ph
   if (q.a.ntiles <= 0) return hipSuccess;
   if (q.a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
   const size_t lds = (size_t)(q.a.tf_n + 2) * sizeof(float4);
-  const uint4* cells = (const uint4*)c.d_cells + c.cells.linear_origin;
+  const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
   if (phong)
     hipLaunchKernelGGL((shaded_march_kernel<SH, true>), dim3(q.a.ntiles), dim3(64), lds, s, q,
                        cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, data, out, samples,
