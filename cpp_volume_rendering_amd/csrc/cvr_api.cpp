@@ -305,6 +305,11 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     for (auto& o : c->oslot) o.valid = 0;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "sat_chunk")) {
+    if (value < 1 || value > 64) return fail(c, CVR_ERR_ARG, "sat_chunk must be 1..64");
+    c->sat_chunk = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "shade_counters")) {
     c->shade_counters = value ? 1 : 0;
     return CVR_OK;
@@ -400,6 +405,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
     return c->occ_valid ? (int)(c->occ_empty * 1000.0f + 0.5f) : -1;
   if (!std::strcmp(key, "tile_stats")) return c->tile_stats;
   if (!std::strcmp(key, "shade_counters")) return c->shade_counters;
+  if (!std::strcmp(key, "sat_chunk")) return c->sat_chunk;
   if (!std::strcmp(key, "quad")) return c->quad_pct;
   if (!std::strcmp(key, "kernel_timing")) return (int)c->ev_start.size();
   return -1;

@@ -195,6 +195,7 @@ struct Ctx {
   uint4* d_ext_cells = nullptr;    // the same levels as cell8 (8 fp16 corners per texel)
   ExtLevel* d_ext_levels = nullptr;  // [kMaxExtLevels] addressing of the levels
   // extinction-based shading: the float SAT of (N+2) cells per axis
+  int sat_chunk = 32;                // z planes per SAT work item (option "sat_chunk")
   float* d_sat = nullptr;
   float4* d_sat_cells = nullptr;   // the same SAT as cell8 (8 float corners per texel)
   int sat_dims[3] = {0, 0, 0};

@@ -11,14 +11,21 @@
 // after those seven reproduces every double bit for bit, so:
 //   * the (x, y) plane is cut into 8x8 column tiles, one wave each; tiles on one
 //     anti-diagonal tx + ty = k are independent (one launch per k);
-//   * inside a tile, lane (lx, ly) owns a column and visits z at time
-//     t = z - 1 + lx + ly (a skewed pipeline): its left / upper / diagonal
+//   * the z axis is cut into chunks; work item (tile, chunk) depends only on
+//     the left / upper / diagonal tiles' same chunk and on its own previous
+//     chunk, so items with tx + ty + chunk = k are independent: one launch per k
+//     (critical path ~ (tiles along x + along y + chunks) x chunk length instead
+//     of tiles x depth);
+//   * inside an item, lane (lx, ly) owns a column and visits z at time
+//     t = z - z0 + lx + ly (a skewed pipeline): its left / upper / diagonal
 //     neighbours reached the same z one or two steps earlier, so their values
 //     come by cross-lane shuffles of a 3-deep history, no barrier per step;
 //   * the tile's left face, upper face and corner column (finished by earlier
-//     launches) and its voxel extinctions are staged in LDS 64 steps at a time.
-// Only the tile's last row / column is kept in double (what later tiles read);
-// every cell is stored as float, the texture the shader samples (GL_R32F).
+//     launches), its own column below the chunk, and its voxel extinctions are
+//     staged in LDS / registers when the item starts.
+// Double values are kept for what later items read (the tiles' last row /
+// column, the chunks' last two planes); every cell is stored as float, the
+// texture the shader samples (GL_R32F).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -28,81 +35,91 @@ namespace cvr {
 
 namespace {
 
-constexpr int kSatCh = 64;                    // steps per staging chunk
+constexpr int kSatChMax = 64;                 // largest z chunk
 constexpr int kSatSkew = 14;                  // max lx + ly
-constexpr int kSatBnd = kSatCh + kSatSkew + 1;  // boundary window (z and z - 1)
-constexpr int kSatVal = kSatCh + kSatSkew;    // voxel window
 
 struct SatArgs {
   int W, H, D;          // volume
   int w, h, d;          // SAT grid (W+2, H+2, D+2)
-  int TY, k;            // tile rows; this launch's anti-diagonal
+  int TX, TY, NC, C;    // tiles along x / y, z chunks of C planes
+  int k;                // this launch's anti-diagonal tx + ty + chunk
   int bpv;
   const void* vox;
   const float* lut;     // extinction per voxel value
-  double* sd;           // double values of the tiles' last row / column
+  double* sd;           // double values read back by later items
   float* sf;            // the float SAT
 };
 
 template <int BPV>
 __global__ void __launch_bounds__(64) sat_tile_kernel(SatArgs P) {
-  __shared__ double bnd[17][kSatBnd];   // left face (8), upper face (8), corner
-  __shared__ float val[kSatVal][64];    // V(x, y, z) of the tile's columns
+  __shared__ double bnd[17][kSatChMax + 1];   // left face (8), upper face (8), corner; z0-1 .. z1
+  __shared__ float val[kSatChMax][64];        // V(x, y, z) of the tile's columns, z0 .. z1
+  const int tx = (int)blockIdx.x % P.TX, cz = (int)blockIdx.x / P.TX;
+  const int ty = P.k - tx - cz;
+  if (ty < 0 || ty >= P.TY) return;           // not on this anti-diagonal (whole wave)
   const int lane = threadIdx.x, lx = lane & 7, ly = lane >> 3;
-  const int tx = max(0, P.k - (P.TY - 1)) + (int)blockIdx.x, ty = P.k - tx;
   const int x0 = 1 + 8 * tx, y0 = 1 + 8 * ty;
   const int x = x0 + lx, y = y0 + ly;
+  const int z0 = 1 + cz * P.C, z1 = min(z0 + P.C - 1, P.d - 1);
+  const int nz = z1 - z0 + 1;
   const bool in_xy = x <= P.w - 1 && y <= P.h - 1;
   const long long sy = P.w, sz = (long long)P.w * P.h;
-  const int nsteps = P.d + kSatSkew - 1;   // lane with skew 14 reaches z = d - 1
-  const bool keep = (lx == 7 || ly == 7);  // read back by the next tiles
-  double h0 = 0.0, h1 = 0.0, h2 = 0.0;     // own column at z-1, z-2, z-3
-  for (int t0 = 0; t0 < nsteps; t0 += kSatCh) {
-    __syncthreads();
-    // boundary columns, z in [t0 - 14, t0 + 64]
-    for (int i = lane; i < 17 * kSatBnd; i += 64) {
-      const int col = i / kSatBnd, zi = i - col * kSatBnd, z = t0 - kSatSkew + zi;
-      const int cx = col < 8 ? x0 - 1 : (col < 16 ? x0 + col - 8 : x0 - 1);
-      const int cy = col < 8 ? y0 + col : y0 - 1;
-      double v = 0.0;
-      if (z >= 1 && z <= P.d - 1 && cx >= 1 && cy >= 1 && cx <= P.w - 1 && cy <= P.h - 1)
-        v = P.sd[cx + cy * sy + z * sz];
-      bnd[col][zi] = v;
+  // the own column below the chunk (z0 - 1, z0 - 2): the history's start
+  double h0 = 0.0, h1 = 0.0, h2 = 0.0;
+  if (in_xy) {
+    if (z0 - 1 >= 1) h0 = P.sd[x + y * sy + (z0 - 1) * sz];
+    if (z0 - 2 >= 1) h1 = P.sd[x + y * sy + (z0 - 2) * sz];
+  }
+  // boundary columns, z in [z0 - 1, z1]
+  for (int i = lane; i < 17 * (nz + 1); i += 64) {
+    const int col = i / (nz + 1), zi = i - col * (nz + 1), z = z0 - 1 + zi;
+    const int cx = col < 8 ? x0 - 1 : (col < 16 ? x0 + col - 8 : x0 - 1);
+    const int cy = col < 8 ? y0 + col : y0 - 1;
+    double v = 0.0;
+    if (z >= 1 && cx >= 1 && cy >= 1 && cx <= P.w - 1 && cy <= P.h - 1)
+      v = P.sd[cx + cy * sy + z * sz];
+    bnd[col][zi] = v;
+  }
+  // voxel extinctions of the tile's columns, z in [z0, z1]
+  for (int zi = 0; zi < nz; zi++) {
+    const int z = z0 + zi;
+    float v = 0.0f;
+    if (in_xy && z <= P.D && x <= P.W && y <= P.H) {
+      const long long i = (long long)(x - 1) + (long long)(y - 1) * P.W +
+                          (long long)(z - 1) * P.W * P.H;
+      const uint32_t q = BPV == 1 ? ((const uint8_t*)P.vox)[i] : ((const uint16_t*)P.vox)[i];
+      v = P.lut[q];
     }
-    // voxel extinctions of the tile's columns, z in [t0 - 13, t0 + 64]
-    for (int zi = 0; zi < kSatVal; zi++) {
-      const int z = t0 - (kSatSkew - 1) + zi;
-      float v = 0.0f;
-      if (in_xy && z >= 1 && z <= P.D && x <= P.W && y <= P.H) {
-        const long long i = (long long)(x - 1) + (long long)(y - 1) * P.W +
-                            (long long)(z - 1) * P.W * P.H;
-        const uint32_t q = BPV == 1 ? ((const uint8_t*)P.vox)[i] : ((const uint16_t*)P.vox)[i];
-        v = P.lut[q];
-      }
-      val[zi][lane] = v;
+    val[zi][lane] = v;
+  }
+  __syncthreads();
+  const bool keep_col = (lx == 7 || ly == 7);   // read by the next tiles (all z)
+  const int nsteps = nz + kSatSkew;
+  for (int t = 0; t < nsteps; t++) {
+    const int z = z0 + t - (lx + ly);
+    double L0 = __shfl(h0, lane - 1, 64), L1 = __shfl(h1, lane - 1, 64);
+    double T0 = __shfl(h0, lane - 8, 64), T1 = __shfl(h1, lane - 8, 64);
+    double D1 = __shfl(h1, lane - 9, 64), D2 = __shfl(h2, lane - 9, 64);
+    double nh;
+    if (in_xy && z >= z0 && z <= z1) {
+      const int zb = z - (z0 - 1);
+      if (lx == 0) { L0 = bnd[ly][zb]; L1 = bnd[ly][zb - 1]; }
+      if (ly == 0) { T0 = bnd[8 + lx][zb]; T1 = bnd[8 + lx][zb - 1]; }
+      if (lx == 0 && ly == 0) { D1 = bnd[16][zb]; D2 = bnd[16][zb - 1]; }
+      else if (lx == 0) { D1 = bnd[ly - 1][zb]; D2 = bnd[ly - 1][zb - 1]; }
+      else if (ly == 0) { D1 = bnd[8 + lx - 1][zb]; D2 = bnd[8 + lx - 1][zb - 1]; }
+      const double v = (double)val[z - z0][lane];
+      const double s = v + D2 + h0 + T0 + L0 - D1 - T1 - L1;
+      const long long o = x + y * sy + z * sz;
+      P.sf[o] = (float)s;
+      if (keep_col || z >= z1 - 1) P.sd[o] = s;
+      nh = s;
+    } else {
+      // before its first z the lane's history is the column below the chunk
+      // (already in h0, h1); after its last z nothing reads it
+      nh = z < z0 ? h0 : 0.0;
     }
-    __syncthreads();
-    const int tend = min(t0 + kSatCh, nsteps);
-    for (int t = t0; t < tend; t++) {
-      const int z = 1 + t - (lx + ly);
-      double L0 = __shfl(h0, lane - 1, 64), L1 = __shfl(h1, lane - 1, 64);
-      double T0 = __shfl(h0, lane - 8, 64), T1 = __shfl(h1, lane - 8, 64);
-      double D1 = __shfl(h1, lane - 9, 64), D2 = __shfl(h2, lane - 9, 64);
-      double nh = 0.0;
-      if (in_xy && z >= 1 && z <= P.d - 1) {
-        const int zb = z - (t0 - kSatSkew);
-        if (lx == 0) { L0 = bnd[ly][zb]; L1 = bnd[ly][zb - 1]; }
-        if (ly == 0) { T0 = bnd[8 + lx][zb]; T1 = bnd[8 + lx][zb - 1]; }
-        if (lx == 0 && ly == 0) { D1 = bnd[16][zb]; D2 = bnd[16][zb - 1]; }
-        else if (lx == 0) { D1 = bnd[ly - 1][zb]; D2 = bnd[ly - 1][zb - 1]; }
-        else if (ly == 0) { D1 = bnd[8 + lx - 1][zb]; D2 = bnd[8 + lx - 1][zb - 1]; }
-        const double v = (double)val[z - (t0 - (kSatSkew - 1))][lane];
-        const double s = v + D2 + h0 + T0 + L0 - D1 - T1 - L1;
-        const long long o = x + y * sy + z * sz;
-        P.sf[o] = (float)s;
-        if (keep) P.sd[o] = s;
-        nh = s;
-      }
+    if (z >= z0 || !in_xy) {
       h2 = h1;
       h1 = h0;
       h0 = nh;
@@ -146,21 +163,19 @@ hipError_t launch_sat_build(const Ctx& c, const float* d_lut, double* d_sd, floa
   P.lut = d_lut;
   P.sd = d_sd;
   P.sf = d_sf;
-  const int TX = (P.w - 1 + 7) / 8;   // columns x in [1, w-1] (the far border plane included)
-  const int TY = (P.h - 1 + 7) / 8;
-  P.TY = TY;
+  P.TX = (P.w - 1 + 7) / 8;   // columns x in [1, w-1] (the far border plane included)
+  P.TY = (P.h - 1 + 7) / 8;
+  P.C = c.sat_chunk > 0 && c.sat_chunk <= kSatChMax ? c.sat_chunk : 32;
+  P.NC = (P.d - 1 + P.C - 1) / P.C;   // planes z in [1, d-1]
   hipError_t e = hipMemsetAsync(d_sf, 0, (size_t)P.w * P.h * P.d * sizeof(float), s);
   if (e != hipSuccess) return e;
-  for (int k = 0; k <= TX + TY - 2; k++) {
+  const unsigned grid = (unsigned)(P.TX * P.NC);
+  for (int k = 0; k <= P.TX + P.TY + P.NC - 3; k++) {
     P.k = k;
-    const int lo = k - (TY - 1) > 0 ? k - (TY - 1) : 0;
-    const int hi = k < TX - 1 ? k : TX - 1;
-    const int n = hi - lo + 1;
-    if (n <= 0) continue;
     if (c.bpv == 1)
-      hipLaunchKernelGGL(sat_tile_kernel<1>, dim3(n), dim3(64), 0, s, P);
+      hipLaunchKernelGGL(sat_tile_kernel<1>, dim3(grid), dim3(64), 0, s, P);
     else
-      hipLaunchKernelGGL(sat_tile_kernel<2>, dim3(n), dim3(64), 0, s, P);
+      hipLaunchKernelGGL(sat_tile_kernel<2>, dim3(grid), dim3(64), 0, s, P);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

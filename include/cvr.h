@@ -226,6 +226,7 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *   "tile_stats" 1: record per-tile timing of every frame (diagnostics)
  *   "kernel_timing" N > 0: time the ray-march kernel of the last N frames
  *                (cvr_read_kernel_times); 0 off (default)
+ *   "sat_chunk"  z planes per work item of the EBS SAT build (1..64, default 32)
  *   "shade_counters" 1: count shaded / shadow-lit samples of cvr_render_dosct
  *                and cvr_render_extbsd (cvr_read_shade_counters; one atomic per wave) */
 cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
