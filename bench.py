@@ -64,7 +64,8 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgba=None):
+def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgba=None,
+                 phong=None):
     """The CPU oracle (C++/OpenMP restatement of ray_marching_1p.comp; the reference has
     no CPU ray-caster) on the host cores: whole frames of the same workload, repeated
     until `seconds` of wall time are spent (each frame starts from the centre band of
@@ -77,6 +78,7 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgb
     rows_per_chunk = 16
     if dos is not None:
         levels = O.ext_volume(v16, scale, dos["tf_rgba"], dos["res"], threads=threads)
+    grad = O.gradient(vol, "fd") if phong is not None else None
 
     def render_rows_full(y0, y1, nthreads):
         if dos is not None:
@@ -87,6 +89,9 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgb
             return O.render_ebs(v16, scale, tf, ebs["sat"], cam, W, H, step,
                                 light=ebs["light"], light_forward=ebs["forward"],
                                 rows=(y0, y1), threads=nthreads)
+        if phong is not None:
+            return O.render_rc1pass(v16, scale, tf, cam, W, H, step, grad=grad, phong=True,
+                                    light=phong["light"], rows=(y0, y1), threads=nthreads)
         return O.render_rc1pass(v16, scale, tf, cam, W, H, step, rows=(y0, y1),
                                 threads=nthreads)
 
@@ -269,13 +274,14 @@ def main():
 
     # samples per frame (this rank), counted by the kernel; for the shaded renderer
     # also the shaded / shadow-lit samples (each traces a fixed number of cone fetches)
-    if shaded:
+    count_shaded = shaded or a.phong
+    if count_shaded:
         N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 1), "opt", r.device.handle)
     step_once()
     torch.cuda.synchronize(dev)
     S_rank = int(total.item())
     shade = (ctypes.c_uint64 * 3)()
-    if shaded:
+    if count_shaded:
         N.check(L.cvr_read_shade_counters(r.device.handle, shade), "shade", r.device.handle)
         N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 0), "opt", r.device.handle)
 
@@ -338,9 +344,9 @@ def main():
         msps = S_all * a.steps / elapsed / 1e6
         ms_per_step = elapsed / a.steps * 1e3
         # algorithmic bytes per launch: 8 trilinear corners x 1 B (u8 input)
-        # per sample + float4 output per pixel (+ 48 B per sample for the Phong gradient,
-        # counted on every sample as an upper bound of the shaded ones)
-        b_alg = 8 * 1 * S_rank + 16 * pixels + (48 * S_rank if a.phong else 0)
+        # per sample + float4 output per pixel (+ 48 B per shaded sample for the Phong
+        # gradient: 8 corners x 3 fp16, counted by the kernel)
+        b_alg = 8 * 1 * S_rank + 16 * pixels + (48 * int(shade[0]) if a.phong else 0)
         fetches = int(shade[2])
         if dos:
             # + 8 fp16 corners (16 B) per trilinear extinction fetch of the cones
@@ -361,6 +367,8 @@ def main():
                 "kernel": kname,
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank}
+        if a.phong:
+            roof["phong_shaded_samples"] = int(shade[0])
         if dos:
             roof.update({"shaded_samples": shade[0], "shadow_lit_samples": shade[1],
                          "cone_fetches_per_shaded": [f_occ, f_sdw],
@@ -426,8 +434,9 @@ def main():
                 ebs_cfg = {"sat": r.device.extinction_sat(), "lut": dm.ext_lut,
                            "light": rp.light_position, "forward": rp.light_forward}
             gpu_img = out_buf.float().cpu().numpy() if world == 1 else None
+            phong_cfg = {"light": rp.light_position} if a.phong else None
             res["cpu_baseline"] = cpu_baseline(vol, scale, tf, D.INITIAL_STATE_CAMERA, W, H,
-                                               a.cpu_seconds, dos_cfg, ebs_cfg, gpu_img)
+                                               a.cpu_seconds, dos_cfg, ebs_cfg, gpu_img, phong_cfg)
             if "parity" in res["cpu_baseline"]:
                 res["parity"] = res["cpu_baseline"].pop("parity")
         print(json.dumps(res))

@@ -539,10 +539,18 @@ cvr_status cvr_set_gradient(cvr_ctx* ctx, int mode) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   free_dev(c->d_grad); c->grad_bytes = 0; c->grad_mode = 0;
   if (mode == 0) return CVR_OK;
-  c->grad_bytes = (size_t)c->N[0] * c->N[1] * c->N[2] * 8;
+  c->grad_bytes = cvr::cell_count(c->cells) * 48;
   HIP_TRY(c, hipMalloc(&c->d_grad, c->grad_bytes));
-  HIP_TRY(c, cvr::launch_gradient(*c, mode, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  uint2* tmp = nullptr;
+  hipError_t e = hipMalloc((void**)&tmp, (size_t)c->N[0] * c->N[1] * c->N[2] * 8);
+  if (e == hipSuccess) e = cvr::launch_gradient(*c, mode, tmp, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(tmp);
+  if (e != hipSuccess) {
+    free_dev(c->d_grad); c->grad_bytes = 0;
+    return fail(c, e == hipErrorOutOfMemory ? CVR_ERR_OOM : CVR_ERR_HIP, "cvr_set_gradient: %s",
+                hipGetErrorString(e));
+  }
   c->grad_mode = mode;
   return CVR_OK;
 }
@@ -687,6 +695,12 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
       c->tile_stats_n = plan.ntiles;
     }
     A.tile_stats = c->d_tile_stats;
+  }
+  A.shade_ctr = nullptr;
+  if (c->shade_counters && phong) {   // measurement: shaded samples (gradient fetches)
+    if (!c->d_shade) HIP_TRY(c, hipMalloc((void**)&c->d_shade, 3 * sizeof(unsigned long long)));
+    HIP_TRY(c, hipMemsetAsync(c->d_shade, 0, 3 * sizeof(unsigned long long), c->stream));
+    A.shade_ctr = c->d_shade;
   }
   plan.quad_pct = c->quad_pct;
   {

@@ -105,50 +105,6 @@ __device__ __forceinline__ f3 normalize3(f3 v) {
   return f3{v.x * inv, v.y * inv, v.z * inv};
 }
 
-// Corner indices + weights of one trilinear sample (texel space).
-struct Texel { int ix, iy, iz; float ax, ay, az; };
-
-// Gradient: 4 x fp16 (x, y, z, 0) per voxel, x-fastest, trilinear per channel.
-__device__ __forceinline__ f3 sample_gradient(const uint2* __restrict__ grad, const int N[3],
-                                              const Texel& t) {
-  int x0 = max(t.ix, 0), x1 = min(t.ix + 1, N[0] - 1);
-  int y0 = max(t.iy, 0), y1 = min(t.iy + 1, N[1] - 1);
-  int z0 = max(t.iz, 0), z1 = min(t.iz + 1, N[2] - 1);
-  size_t sx = 1, sy = (size_t)N[0], sz = (size_t)N[0] * N[1];
-  uint2 q[8];
-  q[0] = grad[x0 * sx + y0 * sy + z0 * sz];
-  q[1] = grad[x1 * sx + y0 * sy + z0 * sz];
-  q[2] = grad[x0 * sx + y1 * sy + z0 * sz];
-  q[3] = grad[x1 * sx + y1 * sy + z0 * sz];
-  q[4] = grad[x0 * sx + y0 * sy + z1 * sz];
-  q[5] = grad[x1 * sx + y0 * sy + z1 * sz];
-  q[6] = grad[x0 * sx + y1 * sy + z1 * sz];
-  q[7] = grad[x1 * sx + y1 * sy + z1 * sz];
-  float vx[8], vy[8], vz[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    float dummy;
-    h2f2(q[i].x, vx[i], vy[i]);
-    h2f2(q[i].y, vz[i], dummy);
-  }
-  f3 r;
-  {
-    float c00 = lerpf(vx[0], vx[1], t.ax), c10 = lerpf(vx[2], vx[3], t.ax);
-    float c01 = lerpf(vx[4], vx[5], t.ax), c11 = lerpf(vx[6], vx[7], t.ax);
-    r.x = lerpf(lerpf(c00, c10, t.ay), lerpf(c01, c11, t.ay), t.az);
-  }
-  {
-    float c00 = lerpf(vy[0], vy[1], t.ax), c10 = lerpf(vy[2], vy[3], t.ax);
-    float c01 = lerpf(vy[4], vy[5], t.ax), c11 = lerpf(vy[6], vy[7], t.ax);
-    r.y = lerpf(lerpf(c00, c10, t.ay), lerpf(c01, c11, t.ay), t.az);
-  }
-  {
-    float c00 = lerpf(vz[0], vz[1], t.ax), c10 = lerpf(vz[2], vz[3], t.ax);
-    float c01 = lerpf(vz[4], vz[5], t.ax), c11 = lerpf(vz[6], vz[7], t.ax);
-    r.z = lerpf(lerpf(c00, c10, t.ay), lerpf(c01, c11, t.ay), t.az);
-  }
-  return r;
-}
 
 
 // Branch-free CVR-SPEC exp: same values as cvr_expf (selects instead of the

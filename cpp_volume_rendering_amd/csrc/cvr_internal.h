@@ -48,6 +48,7 @@ struct Rc1passArgs {
   int packed;
   int ntiles;                        // 8x8 wave tiles of this launch
   unsigned long long* tile_stats;    // diagnostics (tile_stats option) or null
+  unsigned long long* shade_ctr;     // measurement (shade_counters): [0] += shaded samples (Phong)
   int cost_time;                     // LPT cost = measured tile time (1) or longest ray (0)
   // empty-space skipping: occupancy byte per macro cell (null = off)
   const uint8_t* occ;
@@ -147,7 +148,7 @@ struct Ctx {
   int tf_n = 0;
   float tf_max_alpha = 0.0f;         // largest (fp16-rounded) TF opacity; NaN if any is not finite
   // gradient (4 x fp16 per voxel, x-fastest)
-  void* d_grad = nullptr;
+  void* d_grad = nullptr;          // gradient cell8: 3 uint4 (x, y, z fp16 pairs) per volume cell
   size_t grad_bytes = 0;
   int grad_mode = 0;
   // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
@@ -219,7 +220,7 @@ struct Ctx {
 // kernels / launchers (raymarch.hip)
 hipError_t launch_build_cells_impl(const void* vox, int bpv, const uint16_t* lut, const int N[3],
                                    const CellGrid& g, void* cells, hipStream_t s);
-hipError_t launch_gradient(const Ctx& c, int mode, hipStream_t s);
+hipError_t launch_gradient(const Ctx& c, int mode, uint2* tmp, hipStream_t s);
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
                           uint32_t* samples, unsigned long long* tile_samples, const int* order,
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s);

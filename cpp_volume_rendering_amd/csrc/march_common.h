@@ -114,14 +114,22 @@ __device__ __forceinline__ float4 classify(const float4* __restrict__ tfp, float
                      lerpf(t0.w, t1.w, a));
 }
 
+// The gradient at a sample, from the gradient cell8 grid (precompute.hip:
+// gradient_cells_kernel) at the volume cell's index: three 16-B loads, the same
+// corners and lerp order as the per-voxel trilinear fetch.
+__device__ __forceinline__ f3 sample_gradient_cell(const uint4* __restrict__ gcells,
+                                                   const SamplePos& sp) {
+  const uint4* g = gcells + 3 * (size_t)sp.idx;
+  const uint4 gx = g[0], gy = g[1], gz = g[2];
+  return f3{trilerp_cell(gx, sp.ax, sp.ay, sp.az), trilerp_cell(gy, sp.ax, sp.ay, sp.az),
+            trilerp_cell(gz, sp.ax, sp.ay, sp.az)};
+}
+
 // Blinn-Phong (ray_marching_1p.comp:48-81), CVR-SPEC arithmetic.
-__device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint2* __restrict__ grad,
+__device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint4* __restrict__ grad,
                                             const SamplePos& sp, f3 dir, float t, f3 tpos, f3 hg,
                                             f3 eye, float4& src) {
-  Texel tx;
-  tx.ix = sp.ix; tx.iy = sp.iy; tx.iz = sp.iz;
-  tx.ax = sp.ax; tx.ay = sp.ay; tx.az = sp.az;
-  f3 g = sample_gradient(grad, A.N, tx);
+  f3 g = sample_gradient_cell(grad, sp);
   if (g.x != 0.0f || g.y != 0.0f || g.z != 0.0f) {
     f3 wp{fmaf(dir.x, t, tpos.x) - hg.x, fmaf(dir.y, t, tpos.y) - hg.y, fmaf(dir.z, t, tpos.z) - hg.z};
     f3 n = normalize3(g);

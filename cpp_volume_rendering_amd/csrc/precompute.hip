@@ -106,18 +106,52 @@ __global__ void gradient_kernel(const VT* __restrict__ vox, int nx, int ny, int 
   grad[idx] = o;
 }
 
-hipError_t launch_gradient(const Ctx& c, int mode, hipStream_t s) {
+// The gradient in the volume's cell8 grid: cell i holds, per component, the 8
+// corners the trilinear fetch of cell i reads (same convention as
+// build_cells_kernel), as three uint4 of packed fp16 pairs (x, y, z).  One
+// shaded sample reads 48 contiguous bytes at the volume cell's index.
+__global__ void gradient_cells_kernel(const uint2* __restrict__ grad, int nx, int ny, int nz,
+                                      CellGrid g, uint4* __restrict__ gcells, size_t ncells) {
+  size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= ncells) return;
+  uint32_t i = (uint32_t)idx;
+  const int a = (int)(i % (uint32_t)g.cx);
+  const uint32_t rest = i / (uint32_t)g.cx;
+  const int b = (int)(rest % (uint32_t)g.cy);
+  const int c = (int)(rest / (uint32_t)g.cy);
+  const int x0 = max(a - 1, 0), x1 = min(a, nx - 1);
+  const int y0 = max(b - 1, 0), y1 = min(b, ny - 1);
+  const int z0 = max(c - 1, 0), z1 = min(c, nz - 1);
+  auto q = [&](int x, int y, int z) { return grad[(size_t)x + (size_t)y * nx + (size_t)z * nx * ny]; };
+  const uint2 g000 = q(x0, y0, z0), g100 = q(x1, y0, z0), g010 = q(x0, y1, z0), g110 = q(x1, y1, z0);
+  const uint2 g001 = q(x0, y0, z1), g101 = q(x1, y0, z1), g011 = q(x0, y1, z1), g111 = q(x1, y1, z1);
+  auto lo = [](uint32_t w) { return w & 0xffffu; };
+  auto hi = [](uint32_t w) { return w >> 16; };
+  // component x: low half of .x; y: high half of .x; z: low half of .y
+  gcells[3 * idx + 0] = make_uint4(lo(g000.x) | (lo(g100.x) << 16), lo(g010.x) | (lo(g110.x) << 16),
+                                   lo(g001.x) | (lo(g101.x) << 16), lo(g011.x) | (lo(g111.x) << 16));
+  gcells[3 * idx + 1] = make_uint4(hi(g000.x) | (hi(g100.x) << 16), hi(g010.x) | (hi(g110.x) << 16),
+                                   hi(g001.x) | (hi(g101.x) << 16), hi(g011.x) | (hi(g111.x) << 16));
+  gcells[3 * idx + 2] = make_uint4(lo(g000.y) | (lo(g100.y) << 16), lo(g010.y) | (lo(g110.y) << 16),
+                                   lo(g001.y) | (lo(g101.y) << 16), lo(g011.y) | (lo(g111.y) << 16));
+}
+
+// Per-voxel gradient (RGB16F + pad) into `tmp`, then its cell8 form into c.d_grad.
+hipError_t launch_gradient(const Ctx& c, int mode, uint2* tmp, hipStream_t s) {
   size_t n = (size_t)c.N[0] * c.N[1] * c.N[2];
   int bs = 256;
   size_t nb = (n + bs - 1) / bs;
   if (c.bpv == 1)
     hipLaunchKernelGGL(gradient_kernel<uint8_t>, dim3((unsigned)nb), dim3(bs), 0, s,
-                       (const uint8_t*)c.d_vox, c.N[0], c.N[1], c.N[2], mode, 255.0,
-                       (uint2*)c.d_grad);
+                       (const uint8_t*)c.d_vox, c.N[0], c.N[1], c.N[2], mode, 255.0, tmp);
   else
     hipLaunchKernelGGL(gradient_kernel<uint16_t>, dim3((unsigned)nb), dim3(bs), 0, s,
-                       (const uint16_t*)c.d_vox, c.N[0], c.N[1], c.N[2], mode, 65535.0,
-                       (uint2*)c.d_grad);
+                       (const uint16_t*)c.d_vox, c.N[0], c.N[1], c.N[2], mode, 65535.0, tmp);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t nc = cell_count(c.cells);
+  hipLaunchKernelGGL(gradient_cells_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, tmp,
+                     c.N[0], c.N[1], c.N[2], c.cells, (uint4*)c.d_grad, nc);
   return hipGetLastError();
 }
 

@@ -76,9 +76,9 @@ __device__ __forceinline__ bool skip_empty(const Rc1passArgs& A, const Ray& r, f
 // accumulates h one step at a time); batching only changes when loads issue.
 template <int K, bool PHONG, bool SKIP, bool XF>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
-                                          const uint2* __restrict__ grad,
+                                          const uint4* __restrict__ grad,
                                           const float4* __restrict__ tfp, int px, int py,
-                                          float4& dst, uint32_t& cnt) {
+                                          float4& dst, uint32_t& cnt, uint32_t& nshade) {
   dst = make_float4(0.f, 0.f, 0.f, 0.f);
   cnt = 0;
   Ray r;
@@ -176,7 +176,10 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
           float4 sc = src[j];
           if (sc.w > 0.0f) {
             visible = true;
-            if (PHONG) shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
+            if (PHONG) {
+              shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
+              nshade++;
+            }
             const float x = -(sc.w * hj[j]);
             const float a = 1.0f - (XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
             const float om = 1.0f - dst.w;
@@ -239,7 +242,7 @@ __device__ __forceinline__ void quad_composite(const QSample& q, bool valid, boo
 template <int K, bool PHONG, bool XF>
 __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
                                                const uint4* __restrict__ cells,
-                                               const uint2* __restrict__ grad,
+                                               const uint4* __restrict__ grad,
                                                const float4* __restrict__ tfp, int px, int py,
                                                bool active, float4& dst, uint32_t& cnt) {
   const int j = threadIdx.x & 3;
@@ -317,7 +320,7 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
 template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF>
 __global__ void __launch_bounds__(64)
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
-                    const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
+                    const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
                     float4* __restrict__ out, uint32_t* __restrict__ samples,
                     unsigned long long* __restrict__ tile_samples, const int* __restrict__ order,
                     uint32_t* __restrict__ tile_cost, int boost) {
@@ -342,14 +345,14 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   int px, py;
   long long oidx;
   float4 dst;
-  uint32_t cnt;
+  uint32_t cnt, nshade = 0;
   bool writer;
   if (!QUAD || quarter < 0) {   // whole tile, one lane per ray
     tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
     const bool inside = px < A.W && py < A.H;
     dst = make_float4(0.f, 0.f, 0.f, 0.f);
     cnt = 0;
-    if (inside) march_ray<K, PHONG, SKIP, XF>(A, cells, grad, tfp, px, py, dst, cnt);
+    if (inside) march_ray<K, PHONG, SKIP, XF>(A, cells, grad, tfp, px, py, dst, cnt, nshade);
     writer = inside || A.packed;
   } else {                    // quarter of a tile, four lanes per ray
     const int ray = lane >> 2;
@@ -363,6 +366,10 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   if (writer) {
     out[oidx] = dst;
     if (samples) samples[oidx] = cnt;
+  }
+  if (PHONG && A.shade_ctr) {   // measurement only: shaded samples (the gradient's bytes)
+    const unsigned long long v = wave_sum(nshade);
+    if (lane == 0 && v) atomicAdd(&A.shade_ctr[0], v);
   }
   if (tile_samples) {   // per-tile sample count; summed by tile_order_kernel (no hot atomic)
     unsigned long long v = wave_sum(cnt);
@@ -616,7 +623,7 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
   const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
   int grid = order ? plan.order_slots : plan.ntiles;
   hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF>), dim3(grid), dim3(64), lds, s,
-                     a, cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, out, samples,
+                     a, cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, out, samples,
                      tile_samples, order, tile_cost, order ? plan.boost : 0);
   return hipGetLastError();
 }

@@ -48,7 +48,7 @@ __device__ __forceinline__ f3 cross3(f3 x, f3 y) {   // glm / GLSL cross, no fma
 template <class SH, bool PHONG>
 __global__ void __launch_bounds__(64)
 shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
-                    const uint2* __restrict__ grad, const float4* __restrict__ tf_g,
+                    const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
                     typename SH::Data data, float4* __restrict__ out,
                     uint32_t* __restrict__ samples, unsigned long long* __restrict__ shade_ctr,
                     unsigned long long* __restrict__ tile_samples) {
@@ -110,10 +110,7 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
           ja[slot] = a;
           jom[slot] = om;
           if (PHONG) {
-            Texel txl;
-            txl.ix = sp.ix; txl.iy = sp.iy; txl.iz = sp.iz;
-            txl.ax = sp.ax; txl.ay = sp.ay; txl.az = sp.az;
-            const f3 g = sample_gradient(grad, A.N, txl);
+            const f3 g = sample_gradient_cell(grad, sp);
             jnx[slot] = g.x; jny[slot] = g.y; jnz[slot] = g.z;
           }
           dst.w = fmaf(om, a, dst.w);
@@ -202,11 +199,11 @@ hipError_t launch_shaded_march(const Ctx& c, const typename SH::Args& q, bool ph
   const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
   if (phong)
     hipLaunchKernelGGL((shaded_march_kernel<SH, true>), dim3(q.a.ntiles), dim3(64), lds, s, q,
-                       cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, data, out, samples,
+                       cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, data, out, samples,
                        shade_ctr, tile_samples);
   else
     hipLaunchKernelGGL((shaded_march_kernel<SH, false>), dim3(q.a.ntiles), dim3(64), lds, s, q,
-                       cells, (const uint2*)c.d_grad, (const float4*)c.d_tf, data, out, samples,
+                       cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, data, out, samples,
                        shade_ctr, tile_samples);
   return hipGetLastError();
 }

@@ -321,7 +321,8 @@ cvr_status  cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int*
 cvr_status  cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* out_frames);
 
 /* Measurement (shade_counters option), for the last shaded frame
- * (cvr_render_dosct / cvr_render_extbsd): out[0] samples that ran the shading
+ * (cvr_render_dosct / cvr_render_extbsd; cvr_render_rc1pass with Blinn-Phong
+ * fills out[0] only): out[0] samples that ran the shading
  * (alpha > 0), out[1] those whose shadow was traced (spot cut-off excluded),
  * out[2] the secondary trilinear fetches (extinction pyramid / SAT): the
  * secondary traffic of the roofline. */
