@@ -30,8 +30,15 @@ import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
+
+# Frames in flight run on separate HIP streams; HIP maps streams onto at most
+# GPU_MAX_HW_QUEUES hardware queues per process (4 by default), and streams that
+# share a queue serialise.  8 queues keep 4 render streams + RCCL's apart.  Set
+# before torch initialises HIP.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -60,12 +67,21 @@ def parse():
     p.add_argument("--phong", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--format", choices=["rgba16f", "rgba32f"], default="rgba16f",
+                   help="frame format: RGBA16F (the reference's framebuffer) or RGBA32F")
+    p.add_argument("--streams", type=int, default=4,
+                   help="frames in flight (render streams rotated per frame)")
+    p.add_argument("--quad", type=int, default=-1,
+                   help="quad (4 lanes per ray) share of the longest tiles, %% "
+                        "(default: 10 at >= 8 GPUs, else 0)")
+    p.add_argument("--transport", choices=["rccl", "torch"], default="rccl",
+                   help="N > 1 gather: the library's RCCL communicator or dist.gather")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_rc1pass.json"))
     return p.parse_args()
 
 
 def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgba=None,
-                 phong=None):
+                 phong=None, half=False):
     """The CPU oracle (C++/OpenMP restatement of ray_marching_1p.comp; the reference has
     no CPU ray-caster) on the host cores: whole frames of the same workload, repeated
     until `seconds` of wall time are spent (each frame starts from the centre band of
@@ -135,6 +151,8 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgb
         band = H if (dos is None and ebs is None) else (64 if dos is not None else 32)
         y0 = H // 2 - band // 2
         ref = render_rows_full(y0, y0 + band, threads)[0][y0:y0 + band]
+        if half:   # the RGBA16F frame: the oracle's float composite rounded to nearest even
+            ref = ref.astype(np.float16).astype(np.float32)
         got = gpu_rgba[y0:y0 + band]
         extra["parity"] = {
             "rows": [y0, y0 + band],
@@ -144,7 +162,8 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgb
             # non-finite pixels (NaN/inf in the same channels on both sides count as equal)
             "nonfinite_px": int((~np.isfinite(ref)).any(-1).sum()),
             "ssim_rgb8_vs_oracle": round(ssim_rgba(got, ref), 6),
-            "what": "GPU frame vs the CPU oracle (CVR-SPEC) on these rows; SSIM as eval.py "
+            "what": "GPU frame vs the CPU oracle (CVR-SPEC" + (", rounded to RGBA16F" if half else "")
+                    + ") on these rows; SSIM as eval.py "
                     "(magick compare -metric SSIM, tests/test_ssim.py) of the screenshots"}
     return {**extra, "value": round(S / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads,
             "kind": "port",
@@ -244,33 +263,38 @@ def main():
     stream = torch.cuda.current_stream(dev)
     r.device.set_stream(stream.cuda_stream)
     tile = a.tile
+    fmt = N.FORMAT_RGBA16F if a.format == "rgba16f" else N.FORMAT_RGBA32F
+    # the frame (its tiles on this rank at N > 1): render, RCCL gather to rank 0, unpack
+    # the per-GPU share of the frame shrinks with N: at 8 GPUs the longest rays set
+    # a rank's frame time, and 4 lanes per ray on the longest 10 % of tiles pay off
+    quad = a.quad if a.quad >= 0 else (10 if world >= 8 else 0)
+    if not shaded:
+        N.check(N.lib().cvr_set_option(r.device.handle, b"quad", quad), "quad", r.device.handle)
+    try:
+        split = T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev,
+                                  transport=a.transport if world > 1 else None, streams=a.streams)
+    except N.CvrError as e:     # no native communicator: torch's dist.gather instead
+        if world == 1 or a.transport != "rccl":
+            raise
+        print(f"rank {rank}: native RCCL gather unavailable ({e}); using dist.gather",
+              file=sys.stderr)
+        a.transport = "torch"
+        split = T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev, transport="torch")
     if world > 1:
         frame = make_frame(cam, W, H, tile, rank, world)
         k = T.tiles_for_rank(W, H, tile, rank, world)
-        tpr = T.max_tiles_per_rank(W, H, tile, world)
-        out_buf = torch.zeros((tpr, tile, tile, 4), dtype=torch.float32, device=dev)
-        image = torch.zeros((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
         pixels = k * tile * tile
+        out_buf = split.packed[0]
     else:
         frame = make_frame(cam, W, H)
-        out_buf = r.rgba
         pixels = W * H
+        out_buf = split.image
     total = torch.zeros((1,), dtype=torch.int64, device=dev)
     L = N.lib()
-    fptr, pptr = ctypes.byref(frame), ctypes.byref(r._params)
-    out = N.Output(out_buf.data_ptr(), None, total.data_ptr(), 1)
-    render = L.cvr_render_dosct if dos else (L.cvr_render_extbsd if ebs else L.cvr_render_rc1pass)
+    out = N.Output(out_buf.data_ptr(), None, total.data_ptr(), 1, fmt)
 
     def step_once():
-        N.check(render(r.device.handle, fptr, pptr, ctypes.byref(out)), "render",
-                r.device.handle)
-
-    def gather_once():
-        if world > 1:
-            allp = T.gather_to_root(out_buf, tpr)
-            if rank == 0:
-                N.check(L.cvr_unpack_tiles_device(r.device.handle, fptr, allp.data_ptr(), tpr,
-                                                  image.data_ptr()), "unpack", r.device.handle)
+        r.render_to(frame, out)
 
     # samples per frame (this rank), counted by the kernel; for the shaded renderer
     # also the shaded / shadow-lit samples (each traces a fixed number of cone fetches)
@@ -286,31 +310,36 @@ def main():
         N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 0), "opt", r.device.handle)
 
     for _ in range(a.warmup):
-        step_once()
-        gather_once()
+        split.submit(cam)
+    split.flush()
     torch.cuda.synchronize(dev)
 
     # The timed region renders without the sample counter (S is the kernel's own
     # count from the frame above, checked again after timing) and without the
     # library's timing events (an event record between kernels costs ~5 us).
-    out_nt = N.Output(out_buf.data_ptr(), None, None, 1)
-    fptr_nt = ctypes.byref(out_nt)
-
-    def step_timed():
-        N.check(render(r.device.handle, fptr, pptr, fptr_nt), "render", r.device.handle)
-
+    # Frames are pipelined at N > 1: frame i+1 renders while frame i is gathered.
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step_timed()
-        gather_once()
+        split.submit(cam)
+    split.flush()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+
+    # multi-GPU check: rank 0 renders the whole frame itself; the gathered image
+    # must equal it bit for bit
+    split_exact = None
+    if world > 1 and rank == 0:
+        full = torch.zeros_like(split.image)
+        r.render_to(make_frame(cam, W, H), N.Output(full.data_ptr(), None, None, 1, fmt))
+        torch.cuda.synchronize(dev)
+        split_exact = bool(torch.equal(full.view(torch.int16 if fmt else torch.int32),
+                                       split.image.view(torch.int16 if fmt else torch.int32)))
 
     # Kernel-only time for the roofline: HIP events the library records on its
     # own stream around the ray-march launch (kernel_timing), in a separate pass.
@@ -344,9 +373,10 @@ def main():
         msps = S_all * a.steps / elapsed / 1e6
         ms_per_step = elapsed / a.steps * 1e3
         # algorithmic bytes per launch: 8 trilinear corners x 1 B (u8 input)
-        # per sample + float4 output per pixel (+ 48 B per shaded sample for the Phong
-        # gradient: 8 corners x 3 fp16, counted by the kernel)
-        b_alg = 8 * 1 * S_rank + 16 * pixels + (48 * int(shade[0]) if a.phong else 0)
+        # per sample + the output pixel (RGBA16F 8 B, RGBA32F 16 B) (+ 48 B per shaded
+        # sample for the Phong gradient: 8 corners x 3 fp16, counted by the kernel)
+        px_bytes = 8 if fmt == N.FORMAT_RGBA16F else 16
+        b_alg = 8 * 1 * S_rank + px_bytes * pixels + (48 * int(shade[0]) if a.phong else 0)
         fetches = int(shade[2])
         if dos:
             # + 8 fp16 corners (16 B) per trilinear extinction fetch of the cones
@@ -409,10 +439,17 @@ def main():
                        "parallelism": f"screen tiles {tile}x{tile} over {world} GPU(s)"
                                       if world > 1 else "1 GPU",
                        "storage": "cell8 fp16 (16 B/cell, x-fastest)",
+                       "frame_format": a.format,
+                       "frames_in_flight": split.nstreams,
+                       "quad_pct": quad if not shaded else 0,
                        "empty_space_skip": f"macro cells 2^{macro}, auto (on at >= 15 % empty)"
                                            if macro > 0 else "off"},
             "roofline": roof,
         }
+        if world > 1:
+            res["config"]["gather"] = (f"{a.transport}: packed {a.format} tiles to rank 0 + "
+                                       f"unpack, pipelined one frame deep")
+            res["multi_gpu_bit_exact_vs_1gpu_frame"] = split_exact
         if ebs:
             cells = (n + 2) ** 3
             res["precompute"] = {"sat_ms": round(sat_ms, 2), "sat_cells": cells,
@@ -433,13 +470,15 @@ def main():
             if ebs:
                 ebs_cfg = {"sat": r.device.extinction_sat(), "lut": dm.ext_lut,
                            "light": rp.light_position, "forward": rp.light_forward}
-            gpu_img = out_buf.float().cpu().numpy() if world == 1 else None
+            gpu_img = split.image.float().cpu().numpy() if world == 1 else None
             phong_cfg = {"light": rp.light_position} if a.phong else None
             res["cpu_baseline"] = cpu_baseline(vol, scale, tf, D.INITIAL_STATE_CAMERA, W, H,
-                                               a.cpu_seconds, dos_cfg, ebs_cfg, gpu_img, phong_cfg)
+                                               a.cpu_seconds, dos_cfg, ebs_cfg, gpu_img, phong_cfg,
+                                               half=fmt == N.FORMAT_RGBA16F)
             if "parity" in res["cpu_baseline"]:
                 res["parity"] = res["cpu_baseline"].pop("parity")
         print(json.dumps(res))
+    split.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

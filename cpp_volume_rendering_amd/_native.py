@@ -32,7 +32,10 @@ EXPORTED_SYMBOLS = (
     "cvr_read_camera_state", "cvr_read_light_position", "cvr_read_light", "cvr_build_cone_tables",
     "cvr_set_extinction_volume", "cvr_copy_extinction_level", "cvr_render_dosct",
     "cvr_tf1d_ext_lut", "cvr_set_extinction_sat", "cvr_copy_extinction_sat", "cvr_render_extbsd",
+    "cvr_comm_unique_id", "cvr_comm_init", "cvr_comm_destroy", "cvr_gather_tiles",
+    "cvr_gather_sync",
 )
+COMM_ID_BYTES = 128
 
 
 class CvrError(RuntimeError):
@@ -52,9 +55,14 @@ class Frame(ctypes.Structure):
                 ("tile_size", ctypes.c_int), ("rank", ctypes.c_int), ("nranks", ctypes.c_int)]
 
 
+FORMAT_RGBA32F = 0
+FORMAT_RGBA16F = 1   # the reference's RGBA16F frame (imageStore rounding: nearest even)
+
+
 class Output(ctypes.Structure):
     _fields_ = [("rgba", ctypes.c_void_p), ("samples", ctypes.c_void_p),
-                ("total", ctypes.c_void_p), ("on_device", ctypes.c_int)]
+                ("total", ctypes.c_void_p), ("on_device", ctypes.c_int),
+                ("format", ctypes.c_int)]
 
 
 class Rc1passParams(ctypes.Structure):
@@ -147,7 +155,12 @@ def lib() -> ctypes.CDLL:
         "cvr_tiles_for_rank": ([ctypes.POINTER(Frame), I], I),
         "cvr_render_rc1pass": ([P, ctypes.POINTER(Frame), ctypes.POINTER(Rc1passParams),
                                 ctypes.POINTER(Output)], I),
-        "cvr_unpack_tiles_device": ([P, ctypes.POINTER(Frame), P, I, P], I),
+        "cvr_unpack_tiles_device": ([P, ctypes.POINTER(Frame), P, I, I, P], I),
+        "cvr_comm_unique_id": ([ctypes.c_char_p], I),
+        "cvr_comm_init": ([P, I, I, ctypes.c_char_p], I),
+        "cvr_comm_destroy": ([P], I),
+        "cvr_gather_tiles": ([P, ctypes.POINTER(Frame), P, I, I, P, P], I),
+        "cvr_gather_sync": ([P], I),
         "cvr_copy_tile_stats": ([P, P, I, IP], I),
         "cvr_read_kernel_times": ([P, FP, I, IP], I),
         "cvr_read_shade_counters": ([P, ctypes.POINTER(ctypes.c_uint64)], I),

@@ -238,6 +238,7 @@ void cvr_destroy(cvr_ctx* ctx) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  cvr::comm_release(c);
   free_dev(c->d_vox);
   free_dev(c->d_cells);
   void* p = c->d_tf; free_dev(p); c->d_tf = nullptr;
@@ -358,6 +359,11 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->max_waves_cu = value;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "split_streams")) {
+    if (value < 1 || value > 8) return fail(c, CVR_ERR_ARG, "split_streams must be 1..8");
+    c->split_streams = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "async_order")) {
     if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "async_order must be 0 or 1");
     if (c->side) HIP_TRY(c, hipStreamSynchronize(c->side));
@@ -399,6 +405,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "debug_keep")) return c->debug_keep;
   if (!std::strcmp(key, "debug_epi_stop")) return c->epi_stop;
   if (!std::strcmp(key, "async_order")) return c->async_order;
+  if (!std::strcmp(key, "split_streams")) return c->split_streams;
   if (!std::strcmp(key, "order_interval")) return c->order_interval;
   if (!std::strcmp(key, "skip_min_pct")) return c->skip_min_pct;
   if (!std::strcmp(key, "occ_empty_permille"))   // read-only: empty macro cells (after a render)
@@ -656,6 +663,8 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: null argument");
+  if (o->format != CVR_FORMAT_RGBA32F && o->format != CVR_FORMAT_RGBA16F)
+    return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: unknown output format %d", o->format);
   if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
     return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: bad viewport %dx%d", f->width, f->height);
   if (!c->d_cells) return fail(c, CVR_ERR_STATE, "cvr_render_rc1pass: no volume set");
@@ -722,7 +731,8 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   float4* d_out;
   uint32_t* d_samples;
   unsigned long long* d_total;
-  size_t rgba_bytes = npix * 16, smp_bytes = npix * 4;
+  A.out_half = o->format == CVR_FORMAT_RGBA16F;
+  size_t rgba_bytes = npix * (A.out_half ? 8 : 16), smp_bytes = npix * 4;
   if (o->on_device) {
     d_out = (float4*)o->rgba;
     d_samples = (uint32_t*)o->samples;
@@ -747,9 +757,28 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
                   (packed ? (f->rank << 8) ^ (f->nranks << 12) ^ 1 : 0);
   const int* order = nullptr;
   uint32_t* tile_cost = nullptr;
-  Ctx::OrderSlot& os = c->oslot[c->async_order ? c->frame_no % Ctx::kOrderSlots : 0];
+  // One slot per render stream: frames issued on different streams may overlap
+  // on the device (the screen-tile split alternates two), and a slot's order,
+  // costs and rebuilds stay in its stream's order.  async_order: slots rotate.
+  int si = -1;
+  if (c->async_order) {
+    si = (int)(c->frame_no % 3);
+  } else {
+    for (int i = 0; i < Ctx::kOrderSlots; i++)
+      if (c->oslot[i].owned && c->oslot[i].stream == s) si = i;
+    if (si < 0) {
+      si = c->slot_rr++ % Ctx::kOrderSlots;
+      Ctx::OrderSlot& o = c->oslot[si];
+      if (o.owned) HIP_TRY(c, hipDeviceSynchronize());   // the slot's last frame is done
+      o.stream = s;
+      o.owned = true;
+      o.valid = 0;
+      o.frames = 0;
+    }
+  }
+  Ctx::OrderSlot& os = c->oslot[si];
   if (can_order) {
-    if (!c->side) {
+    if (c->async_order && !c->side) {   // side stream + events only for side-stream sorts
       int lo = 0, hi = 0;
       HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
       HIP_TRY(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi));
@@ -760,7 +789,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     // and overwrites its costs (it ran alongside the previous frame)
     if (os.pending) HIP_TRY(c, hipStreamWaitEvent(s, os.done, 0));
     if (os.units < plan.order_slots || os.ntiles < plan.ntiles) {
-      HIP_TRY(c, hipStreamSynchronize(c->side));
+      if (c->side) HIP_TRY(c, hipStreamSynchronize(c->side));
       void* p = os.d_order; free_dev(p); os.d_order = nullptr;
       p = os.d_cost; free_dev(p); os.d_cost = nullptr;
       os.units = os.ntiles = 0;
@@ -799,7 +828,8 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   // missing or stale for this plan): costs shift slowly between frames, and
   // the rebuild (~15 us on the frame's stream) would otherwise cost ~10 %.
   const bool rebuild = tile_cost && !c->async_order &&
-                       (!order || c->frame_no % std::max(1, c->order_interval) == 0);
+                       (!order || os.frames % std::max(1, c->order_interval) == 0);
+  os.frames++;
   if (rebuild) {
     // one epilogue on the frame's stream: sum + order for the next frame
     HIP_TRY(c, cvr::launch_tile_epilogue(tile_cost, tile_samples, d_total, plan, os.d_order, s));
@@ -871,13 +901,14 @@ cvr_status cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* o
 }
 
 cvr_status cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* f, const void* d_packed,
-                                   int tpr_max, void* d_rgba) {
+                                   int tpr_max, int format, void* d_rgba) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
-  if (!f || !d_packed || !d_rgba || f->nranks < 1 || f->tile_size < 16 || tpr_max < 0)
+  if (!f || !d_packed || !d_rgba || f->nranks < 1 || f->tile_size < 16 || tpr_max < 0 ||
+      (format != CVR_FORMAT_RGBA32F && format != CVR_FORMAT_RGBA16F))
     return fail(c, CVR_ERR_ARG, "cvr_unpack_tiles_device: bad arguments");
   HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, cvr::launch_unpack_tiles((const float4*)d_packed, (float4*)d_rgba, f->width, f->height,
+  HIP_TRY(c, cvr::launch_unpack_tiles(d_packed, d_rgba, format == CVR_FORMAT_RGBA16F, f->width, f->height,
                                       f->tile_size, f->nranks, tpr_max, c->stream));
   return CVR_OK;
 }
@@ -895,7 +926,7 @@ static cvr_status render_shaded(Ctx* c, const cvr_output* o, int ntiles, size_t 
   float4* d_out;
   uint32_t* d_samples;
   unsigned long long* d_total;
-  const size_t rgba_bytes = npix * 16, smp_bytes = npix * 4;
+  const size_t rgba_bytes = npix * (o->format == CVR_FORMAT_RGBA16F ? 8 : 16), smp_bytes = npix * 4;
   if (o->on_device) {
     d_out = (float4*)o->rgba;
     d_samples = (uint32_t*)o->samples;
@@ -1053,6 +1084,8 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_dosct: null argument");
+  if (o->format != CVR_FORMAT_RGBA32F && o->format != CVR_FORMAT_RGBA16F)
+    return fail(c, CVR_ERR_ARG, "cvr_render_dosct: unknown output format %d", o->format);
   if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
     return fail(c, CVR_ERR_ARG, "cvr_render_dosct: bad viewport %dx%d", f->width, f->height);
   if (!c->d_cells || !c->d_tf) return fail(c, CVR_ERR_STATE, "cvr_render_dosct: no volume or TF");
@@ -1098,6 +1131,7 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   int ntiles = 0;
   size_t npix = 0;
   fill_frame_args(c, f, p->step, Q.a, ntiles, npix);
+  Q.a.out_half = o->format == CVR_FORMAT_RGBA16F;
   Q.a.ka = p->ka;   // Phong ambient/diffuse/specular weights of the surface term
   Q.a.kd = p->kd;
   Q.a.ks = p->ks;
@@ -1202,6 +1236,8 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: null argument");
+  if (o->format != CVR_FORMAT_RGBA32F && o->format != CVR_FORMAT_RGBA16F)
+    return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: unknown output format %d", o->format);
   if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
     return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: bad viewport %dx%d", f->width, f->height);
   if (!c->d_cells || !c->d_tf) return fail(c, CVR_ERR_STATE, "cvr_render_extbsd: no volume or TF");
@@ -1221,6 +1257,7 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
   int ntiles = 0;
   size_t npix = 0;
   fill_frame_args(c, f, p->step, Q.a, ntiles, npix);
+  Q.a.out_half = o->format == CVR_FORMAT_RGBA16F;
   Q.a.ka = p->ka; Q.a.kd = p->kd; Q.a.ks = p->ks;
   Q.a.shininess = p->shininess;
   for (int i = 0; i < 3; i++) { Q.a.ispec[i] = p->ispecular[i]; Q.a.light[i] = p->light_pos[i]; }

@@ -1,0 +1,192 @@
+// cvr_comm.cpp — the screen-tile split's one exchange step:
+// rank 0 gathers every rank's packed tiles over RCCL (xGMI) and unpacks them
+// into the frame.  Native, so a frame costs two C calls on the host (render +
+// gather) instead of a Python collective: at 8 GPUs a rank's share of a
+// 1024^2 frame renders in tens of microseconds.
+//
+// Pipelining: the gather runs on the context's communication stream after the
+// render that produced its tiles; the render stream only waits for the gather
+// issued one call earlier.  With two packed buffers used alternately, frame
+// n+1 renders while frame n is in flight (cvr.h, cvr_gather_tiles).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "cvr_internal.h"
+
+using cvr::Ctx;
+
+namespace {
+
+struct Comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0;
+  hipStream_t stream = nullptr;        // communication stream (gathers + rank-0 unpack)
+  hipEvent_t ev_render = nullptr;      // end of the render whose tiles are gathered
+  hipEvent_t ev_gather[2] = {nullptr, nullptr};
+  long long ngather = 0;
+};
+
+cvr_status cfail(Ctx* c, cvr_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  c->err = buf;
+  return st;
+}
+
+#define CHIP(ctx, expr)                                                                  \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      return cfail(ctx, CVR_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e),     \
+                   __FILE__, __LINE__);                                                  \
+  } while (0)
+
+#define CNCCL(ctx, expr)                                                                 \
+  do {                                                                                   \
+    ncclResult_t _r = (expr);                                                            \
+    if (_r != ncclSuccess)                                                               \
+      return cfail(ctx, CVR_ERR_HIP, "%s: %s (%s:%d)", #expr, ncclGetErrorString(_r),    \
+                   __FILE__, __LINE__);                                                  \
+  } while (0)
+
+Comm* comm_of(Ctx* c) { return static_cast<Comm*>(c->comm); }
+
+}  // namespace
+
+namespace cvr {
+// called by cvr_destroy
+void comm_release(Ctx* c) {
+  Comm* m = comm_of(c);
+  if (!m) return;
+  (void)hipSetDevice(c->device);
+  if (m->stream) (void)hipStreamSynchronize(m->stream);
+  if (m->comm) (void)ncclCommDestroy(m->comm);
+  if (m->ev_render) (void)hipEventDestroy(m->ev_render);
+  for (hipEvent_t e : m->ev_gather)
+    if (e) (void)hipEventDestroy(e);
+  if (m->stream) (void)hipStreamDestroy(m->stream);
+  delete m;
+  c->comm = nullptr;
+}
+}  // namespace cvr
+
+#pragma GCC visibility push(default)
+extern "C" {
+
+cvr_status cvr_comm_unique_id(unsigned char out_id[CVR_COMM_ID_BYTES]) {
+  if (!out_id) return CVR_ERR_ARG;
+  static_assert(sizeof(ncclUniqueId) == CVR_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return CVR_ERR_HIP;
+  std::memcpy(out_id, &id, sizeof(id));
+  return CVR_OK;
+}
+
+cvr_status cvr_comm_init(cvr_ctx* ctx, int nranks, int rank,
+                         const unsigned char id[CVR_COMM_ID_BYTES]) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!id || nranks < 1 || rank < 0 || rank >= nranks)
+    return cfail(c, CVR_ERR_ARG, "cvr_comm_init: bad rank %d of %d", rank, nranks);
+  if (c->comm) return cfail(c, CVR_ERR_STATE, "cvr_comm_init: already initialised");
+  CHIP(c, hipSetDevice(c->device));
+  Comm* m = new Comm();
+  c->comm = m;
+  m->nranks = nranks;
+  m->rank = rank;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclResult_t r = ncclCommInitRank(&m->comm, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    m->comm = nullptr;
+    cvr::comm_release(c);
+    return cfail(c, CVR_ERR_HIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  }
+  int lo = 0, hi = 0;
+  CHIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+  CHIP(c, hipStreamCreateWithPriority(&m->stream, hipStreamNonBlocking, hi));
+  CHIP(c, hipEventCreateWithFlags(&m->ev_render, hipEventDisableTiming));
+  for (hipEvent_t& e : m->ev_gather) CHIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return CVR_OK;
+}
+
+cvr_status cvr_comm_destroy(cvr_ctx* ctx) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  cvr::comm_release(c);
+  return CVR_OK;
+}
+
+cvr_status cvr_gather_tiles(cvr_ctx* ctx, const cvr_frame* f, const void* d_packed,
+                            int tpr_max, int format, void* d_gathered, void* d_rgba) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  Comm* m = comm_of(c);
+  if (!m) return cfail(c, CVR_ERR_STATE, "cvr_gather_tiles: cvr_comm_init not called");
+  if (!f || !d_packed || tpr_max < 0 || f->tile_size < 16 ||
+      (format != CVR_FORMAT_RGBA32F && format != CVR_FORMAT_RGBA16F))
+    return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: bad arguments");
+  if (f->nranks != m->nranks || f->rank != m->rank)
+    return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: frame rank %d/%d, communicator %d/%d",
+                 f->rank, f->nranks, m->rank, m->nranks);
+  if (m->rank == 0 && (!d_gathered || !d_rgba))
+    return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: rank 0 needs the gather buffer and image");
+  if (cvr_tiles_for_rank(f, f->rank) > tpr_max)
+    return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: tiles_per_rank_max too small");
+  CHIP(c, hipSetDevice(c->device));
+  const size_t px = format == CVR_FORMAT_RGBA16F ? 8 : 16;
+  const size_t bytes = (size_t)tpr_max * f->tile_size * f->tile_size * px;
+  hipStream_t s = c->stream;
+  CHIP(c, hipEventRecord(m->ev_render, s));
+  CHIP(c, hipStreamWaitEvent(m->stream, m->ev_render, 0));
+  if (m->rank == 0) {
+    char* g = static_cast<char*>(d_gathered);
+    // rank 0's own block: skipped when it rendered straight into it
+    if (d_packed != d_gathered)
+      CHIP(c, hipMemcpyAsync(g, d_packed, bytes, hipMemcpyDeviceToDevice, m->stream));
+    if (m->nranks > 1) {
+      CNCCL(c, ncclGroupStart());
+      for (int r = 1; r < m->nranks; r++)
+        CNCCL(c, ncclRecv(g + (size_t)r * bytes, bytes, ncclChar, r, m->comm, m->stream));
+      CNCCL(c, ncclGroupEnd());
+    }
+    CHIP(c, cvr::launch_unpack_tiles(g, d_rgba, format == CVR_FORMAT_RGBA16F, f->width, f->height,
+                                     f->tile_size, m->nranks, tpr_max, m->stream));
+  } else {
+    CNCCL(c, ncclSend(d_packed, bytes, ncclChar, 0, m->comm, m->stream));
+  }
+  const int k = (int)(m->ngather & 1);
+  CHIP(c, hipEventRecord(m->ev_gather[k], m->stream));
+  // One render stream and two buffers: the next render reuses the buffers of frame
+  // n-1, so the stream waits for the previous gather (this gather overlaps the next
+  // render).  D >= 2 streams rotated with D buffers: the next render on this stream
+  // is frame n+D in this frame's buffers, so it waits for this gather (the other
+  // streams render the next frames meanwhile, overlapping this frame's tail too).
+  if (c->split_streams >= 2)
+    CHIP(c, hipStreamWaitEvent(s, m->ev_gather[k], 0));
+  else if (m->ngather > 0)
+    CHIP(c, hipStreamWaitEvent(s, m->ev_gather[k ^ 1], 0));
+  m->ngather++;
+  return CVR_OK;
+}
+
+cvr_status cvr_gather_sync(cvr_ctx* ctx) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  Comm* m = comm_of(c);
+  if (!m) return cfail(c, CVR_ERR_STATE, "cvr_gather_sync: cvr_comm_init not called");
+  if (m->ngather == 0) return CVR_OK;
+  CHIP(c, hipSetDevice(c->device));
+  CHIP(c, hipStreamWaitEvent(c->stream, m->ev_gather[(m->ngather - 1) & 1], 0));
+  return CVR_OK;
+}
+
+}  // extern "C"
+#pragma GCC visibility pop

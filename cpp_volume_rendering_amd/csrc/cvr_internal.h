@@ -46,6 +46,7 @@ struct Rc1passArgs {
   // screen-tile split (cvr_frame)
   int tile, rank, nranks, ntx, my_tiles;
   int packed;
+  int out_half;                      // 1: store RGBA16F (uint2 per pixel), 0: float4
   int ntiles;                        // 8x8 wave tiles of this launch
   unsigned long long* tile_stats;    // diagnostics (tile_stats option) or null
   unsigned long long* shade_ctr;     // measurement (shade_counters): [0] += shaded samples (Phong)
@@ -182,11 +183,15 @@ struct Ctx {
     int valid = 0;
     hipEvent_t done = nullptr;     // the side-stream sort of this slot has finished
     bool pending = false;
+    hipStream_t stream = nullptr;  // render stream that owns the slot (async_order 0)
+    bool owned = false;
+    long long frames = 0;          // frames rendered with this slot
   };
-  static constexpr int kOrderSlots = 3;
+  static constexpr int kOrderSlots = 8;   // async_order uses the first 3
   int async_order = 0;             // option "async_order": 1 = sort on a side stream (lag 3)
   int order_interval = 8;          // option "order_interval": rebuild the order every n-th frame
   OrderSlot oslot[kOrderSlots];
+  int slot_rr = 0;                 // next slot handed to a new render stream
   long long frame_no = 0;
   hipStream_t side = nullptr;      // high-priority stream for the order builds
   hipEvent_t ev_frame = nullptr;   // end of a frame's ray-march (the side stream waits on it)
@@ -211,11 +216,16 @@ struct Ctx {
   cvr_cone_tables* cone_tab = nullptr;   // host copies [2]
   unsigned long long* d_tile_samples = nullptr;   // per-wave-tile sample counts (zeroed)
   int tile_samples_n = 0;
+  // multi-GPU gather (cvr_comm.cpp): RCCL communicator, its stream and events
+  void* comm = nullptr;
+  int split_streams = 1;           // option "split_streams": render streams the caller rotates
   // scratch
   unsigned long long* d_total = nullptr;
   void* d_scratch = nullptr;      // host-output staging
   size_t scratch_bytes = 0;
 };
+
+void comm_release(Ctx* c);   // cvr_comm.cpp
 
 // kernels / launchers (raymarch.hip)
 hipError_t launch_build_cells_impl(const void* vox, int bpv, const uint16_t* lut, const int N[3],
@@ -245,8 +255,8 @@ hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* sam
 hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade,
                       unsigned long long* tile_samples, hipStream_t s);
-hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
-                               int nranks, int tiles_per_rank_max, hipStream_t s);
+hipError_t launch_unpack_tiles(const void* packed, void* out, int half, int W, int H, int tile,
+                               int nranks, int tpr_max, hipStream_t s);
 
 inline CellGrid make_cell_grid(const int N[3]) {
   CellGrid g;

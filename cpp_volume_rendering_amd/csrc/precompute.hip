@@ -156,7 +156,9 @@ hipError_t launch_gradient(const Ctx& c, int mode, uint2* tmp, hipStream_t s) {
 }
 
 // Scatter packed per-rank tiles (screen-tile split) into the W x H image.
-__global__ void unpack_tiles_kernel(const float4* __restrict__ packed, float4* __restrict__ out,
+// PX = float4 (RGBA32F) or uint2 (RGBA16F): pixels are moved, not converted.
+template <typename PX>
+__global__ void unpack_tiles_kernel(const PX* __restrict__ packed, PX* __restrict__ out,
                                     int W, int H, int tile, int nranks, int tpr_max, int ntx,
                                     size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -171,15 +173,19 @@ __global__ void unpack_tiles_kernel(const float4* __restrict__ packed, float4* _
   if (px < W && py < H && ty * tile < H) out[(size_t)py * W + px] = packed[i];
 }
 
-hipError_t launch_unpack_tiles(const float4* packed, float4* out, int W, int H, int tile,
+hipError_t launch_unpack_tiles(const void* packed, void* out, int half, int W, int H, int tile,
                                int nranks, int tpr_max, hipStream_t s) {
   int ntx = (W + tile - 1) / tile;
   size_t n = (size_t)nranks * tpr_max * tile * tile;
   int bs = 256;
   size_t nb = (n + bs - 1) / bs;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(unpack_tiles_kernel, dim3((unsigned)nb), dim3(bs), 0, s, packed, out, W, H,
-                     tile, nranks, tpr_max, ntx, n);
+  if (half)
+    hipLaunchKernelGGL(unpack_tiles_kernel<uint2>, dim3((unsigned)nb), dim3(bs), 0, s,
+                       (const uint2*)packed, (uint2*)out, W, H, tile, nranks, tpr_max, ntx, n);
+  else
+    hipLaunchKernelGGL(unpack_tiles_kernel<float4>, dim3((unsigned)nb), dim3(bs), 0, s,
+                       (const float4*)packed, (float4*)out, W, H, tile, nranks, tpr_max, ntx, n);
   return hipGetLastError();
 }
 

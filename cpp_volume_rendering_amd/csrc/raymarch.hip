@@ -364,7 +364,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     if ((lane & 3) != 0) cnt = 0;           // one count per ray
   }
   if (writer) {
-    out[oidx] = dst;
+    store_rgba(out, oidx, dst, A.out_half);
     if (samples) samples[oidx] = cnt;
   }
   if (PHONG && A.shade_ctr) {   // measurement only: shaded samples (the gradient's bytes)

@@ -171,7 +171,7 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
   }
 
   if (inside || A.packed) {
-    out[oidx] = dst;
+    store_rgba(out, oidx, dst, A.out_half);
     if (samples) samples[oidx] = cnt;
   }
   if (tile_samples) {

@@ -439,7 +439,7 @@ class RayCasting1Pass(BaseVolumeRenderer):
     def Redraw(self, stream: Optional[torch.cuda.Stream] = None, count_samples: bool = True):
         """Dispatch the ray-march into self.rgba (asynchronous on `stream`)."""
         if self._frame is None:
-            raise N.CvrError(N.CVR_ERR_STATE, "RayCasting1Pass.Redraw", "Update() not called")
+            raise N.CvrError(N.CVR_ERR_STATE, f"{type(self).__name__}.Redraw", "Update() not called")
         s = stream if stream is not None else torch.cuda.current_stream(self._device_index)
         self.device.set_stream(s.cuda_stream)
         if count_samples:
@@ -448,9 +448,17 @@ class RayCasting1Pass(BaseVolumeRenderer):
         out = N.Output(self.rgba.data_ptr(),
                        self.samples.data_ptr() if count_samples else None,
                        self.total.data_ptr() if count_samples else None, 1)
-        N.check(N.lib().cvr_render_rc1pass(self.device.handle, ctypes.byref(self._frame),
-                                           ctypes.byref(self._params), ctypes.byref(out)),
-                "cvr_render_rc1pass", self.device.handle)
+        self.render_to(self._frame, out)
+
+    # C entry of this renderer's frame (cvr_render_rc1pass / _dosct / _extbsd)
+    _ENTRY = "cvr_render_rc1pass"
+
+    def render_to(self, frame: N.Frame, out: N.Output):
+        """One frame (or this rank's screen tiles of it) into `out`, with the parameters
+        of the last Update(), asynchronous on the device's current stream."""
+        N.check(getattr(N.lib(), self._ENTRY)(self.device.handle, ctypes.byref(frame),
+                                              ctypes.byref(self._params), ctypes.byref(out)),
+                self._ENTRY, self.device.handle)
 
     def FillParameterSpace(self, pspace: dict):
         pspace.clear()
@@ -534,21 +542,7 @@ class RC1PConeTracingDirOcclusionShading(RayCasting1Pass):
         p.shadow = self.sampler_shadow
         return True
 
-    def Redraw(self, stream: Optional[torch.cuda.Stream] = None, count_samples: bool = True):
-        if self._frame is None:
-            raise N.CvrError(N.CVR_ERR_STATE, "RC1PConeTracingDirOcclusionShading.Redraw",
-                             "Update() not called")
-        s = stream if stream is not None else torch.cuda.current_stream(self._device_index)
-        self.device.set_stream(s.cuda_stream)
-        if count_samples:
-            with torch.cuda.stream(s):
-                self.total.zero_()
-        out = N.Output(self.rgba.data_ptr(),
-                       self.samples.data_ptr() if count_samples else None,
-                       self.total.data_ptr() if count_samples else None, 1)
-        N.check(N.lib().cvr_render_dosct(self.device.handle, ctypes.byref(self._frame),
-                                         ctypes.byref(self._params), ctypes.byref(out)),
-                "cvr_render_dosct", self.device.handle)
+    _ENTRY = "cvr_render_dosct"
 
 
 class RC1PExtinctionBasedShading(RayCasting1Pass):
@@ -608,21 +602,7 @@ class RC1PExtinctionBasedShading(RayCasting1Pass):
         p.shadow_max_distance = float(self.dir_cone_max_distance)
         return True
 
-    def Redraw(self, stream: Optional[torch.cuda.Stream] = None, count_samples: bool = True):
-        if self._frame is None:
-            raise N.CvrError(N.CVR_ERR_STATE, "RC1PExtinctionBasedShading.Redraw",
-                             "Update() not called")
-        s = stream if stream is not None else torch.cuda.current_stream(self._device_index)
-        self.device.set_stream(s.cuda_stream)
-        if count_samples:
-            with torch.cuda.stream(s):
-                self.total.zero_()
-        out = N.Output(self.rgba.data_ptr(),
-                       self.samples.data_ptr() if count_samples else None,
-                       self.total.data_ptr() if count_samples else None, 1)
-        N.check(N.lib().cvr_render_extbsd(self.device.handle, ctypes.byref(self._frame),
-                                          ctypes.byref(self._params), ctypes.byref(out)),
-                "cvr_render_extbsd", self.device.handle)
+    _ENTRY = "cvr_render_extbsd"
 
 
 def composite_over_white(rgba: np.ndarray) -> np.ndarray:

@@ -83,43 +83,281 @@ def gather_to_root(packed: torch.Tensor, tpr_max: int, group=None) -> torch.Tens
     return None
 
 
-class TiledRc1pass:
-    """Renders one frame of a RayCasting1Pass split over the ranks of a process group.
+class ScreenTileSplit:
+    """One renderer's frames split over the ranks of a process group.
 
-    Each rank owns a replica of the renderer's device data; ``render`` launches this
-    rank's tiles, gathers to rank 0 over the default group and unpacks there."""
+    Every rank holds a replica of the renderer's device data (volume, TF, gradient,
+    extinction pyramid or SAT) and renders its interleaved ``tile`` x ``tile`` screen
+    tiles packed contiguously; rank 0 gathers the packed buffers (RCCL over xGMI; gloo
+    on CPU) and unpacks them into ``image``.  Pixels travel as ``fmt``: RGBA16F by
+    default, the reference's own frame format (imageStore into the RGBA16F image,
+    ray_marching_1p.comp:174-176), which halves the gather; RGBA32F keeps the exact
+    composite.
+
+    Frames are pipelined.  ``submit`` launches frame n's tiles and its gather
+    (asynchronous); buffer sets rotate (see ``streams``).  ``flush`` completes everything
+    submitted (the current stream waits for it); afterwards ``image`` holds frame
+    ``completed`` for work queued on the current stream.  ``render`` = submit + flush.
+    (With the torch transport, frame n-1 is already complete after submit(n).)
+
+    ``streams`` = D (default 4 on GPUs): frame n renders on stream n % D with buffer
+    set n % D, so D consecutive frames also overlap on the device (a frame's longest
+    tiles no longer idle the GPU at its end).  At world 1 the frames rotate D images.
+    Streams sharing a hardware queue serialise: give the process enough queues
+    (GPU_MAX_HW_QUEUES, bench.py sets 8).
+
+    Transport ``"rccl"`` (default on GPUs at world > 1): the library's own
+    communicator (cvr_comm_init, id broadcast over the process group) and
+    cvr_gather_tiles, two C calls per frame; rank 0 renders straight into its block
+    of the gather buffer.  ``"torch"``: ``dist.gather`` of the process group (any
+    backend; the gloo tests), one stream, with ``render_fn(frame, out_tensor,
+    total_tensor_or_None)`` and ``unpack_fn(frame, gathered, image)`` defaulting to
+    the library (renderer.render_to, cvr_unpack_tiles_device); the CPU tests pass
+    host mirrors."""
+
+    def __init__(self, renderer=None, width: int = None, height: int = None, tile: int = 32,
+                 fmt: int = N.FORMAT_RGBA16F, group=None, device=None, render_fn=None,
+                 unpack_fn=None, count_samples: bool = False, transport: str = None,
+                 streams: int = None):
+        self.r = renderer
+        self.width = width if width is not None else renderer.width
+        self.height = height if height is not None else renderer.height
+        self.tile = tile
+        self.fmt = fmt
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if device is None:
+            device = torch.device("cuda", renderer._device_index)
+        self.device = torch.device(device)
+        self.render_fn = render_fn or self._render_lib
+        self.unpack_fn = unpack_fn or self._unpack_lib
+        dtype = torch.float16 if fmt == N.FORMAT_RGBA16F else torch.float32
+        w, h = self.width, self.height
+        self.split = self.world > 1
+        custom = render_fn is not None or unpack_fn is not None
+        if transport is None:
+            transport = "rccl" if self.device.type == "cuda" and not custom else "torch"
+        self.transport = transport if self.split else "none"
+        if streams is None:
+            streams = 4 if self.device.type == "cuda" and self.transport != "torch" else 1
+        if self.transport == "torch":
+            streams = 1
+        self.nstreams = streams
+        self.streams = ([torch.cuda.Stream(self.device) for _ in range(streams)]
+                        if streams > 1 else None)
+        self.k = tiles_for_rank(w, h, tile, self.rank, self.world) if self.split else 0
+        self.tpr_max = max_tiles_per_rank(w, h, tile, self.world) if self.split else 0
+        nimg = streams if not self.split else 1
+        self._images = ([torch.zeros((h, w, 4), dtype=dtype, device=self.device)
+                         for _ in range(nimg)] if self.rank == 0 else None)
+        # buffer sets: frame n uses set n % nbuf (one per stream; two for one stream)
+        self.nbuf = max(2, streams)
+        if self.split:
+            # padded to tpr_max tiles (gather needs equal sizes); padding stays zero
+            self.packed = [torch.zeros((self.tpr_max, tile, tile, 4), dtype=dtype,
+                                       device=self.device) for _ in range(self.nbuf)]
+            self.gathered = ([torch.zeros((self.world, self.tpr_max, tile, tile, 4), dtype=dtype,
+                                          device=self.device) for _ in range(self.nbuf)]
+                             if self.rank == 0 else None)
+        self.total = (torch.zeros((1,), dtype=torch.int64, device=self.device)
+                      if count_samples else None)
+        self.submitted = 0
+        self.completed = -1
+        self._pending = []          # [(frame_no, slot, work, frame)]
+        self._fkey = None
+        self._fresh = True          # next submit makes the render streams wait for the caller
+        self._comm = False
+        if self.transport == "rccl":
+            self._init_comm()
+        # fast path (library render + RCCL gather): per-slot C arguments built once,
+        # so a frame costs a few ctypes calls on the host
+        self._fast = None
+        if self.transport == "rccl" and render_fn is None and self.streams is not None:
+            L = N.lib()
+            h = self.r.device.handle
+            slots = []
+            for i in range(self.nbuf):
+                g = self.gathered[i] if self.rank == 0 else None
+                buf = g[0] if self.rank == 0 else self.packed[i]
+                out = N.Output(buf.data_ptr(), None,
+                               self.total.data_ptr() if self.total is not None else None, 1,
+                               fmt)
+                slots.append((self.streams[i % self.nstreams].cuda_stream, out, buf.data_ptr(),
+                              g.data_ptr() if g is not None else None))
+            self._fast = (L, h, getattr(L, self.r._ENTRY), ctypes.byref(self.r._params),
+                          self._images[0].data_ptr() if self.rank == 0 else None, slots)
+
+    @property
+    def image(self):
+        """Rank 0: the frame ``completed`` (None on other ranks)."""
+        if self._images is None:
+            return None
+        return self._images[max(self.completed, 0) % len(self._images)]
+
+    def _init_comm(self):
+        L = N.lib()
+        buf = ctypes.create_string_buffer(N.COMM_ID_BYTES)
+        if self.rank == 0:
+            N.check(L.cvr_comm_unique_id(buf), "cvr_comm_unique_id")
+        on_dev = dist.get_backend(self.group) == "nccl"
+        t = torch.tensor(list(buf.raw), dtype=torch.uint8,
+                         device=self.device if on_dev else "cpu")
+        dist.broadcast(t, src=0, group=self.group)
+        uid = bytes(t.cpu().tolist())
+        h = self.r.device.handle
+        N.check(L.cvr_comm_init(h, self.world, self.rank, uid), "cvr_comm_init", h)
+        self._comm = True
+        N.check(L.cvr_set_option(h, b"split_streams", self.nstreams), "split_streams", h)
+
+    def close(self):
+        if self._comm:
+            self.flush()
+            N.check(N.lib().cvr_comm_destroy(self.r.device.handle), "cvr_comm_destroy",
+                    self.r.device.handle)
+            self._comm = False
+
+    # -- library defaults ---------------------------------------------------
+    def _render_lib(self, frame, out_tensor, total):
+        out = N.Output(out_tensor.data_ptr(), None,
+                       total.data_ptr() if total is not None else None, 1, self.fmt)
+        self.r.render_to(frame, out)
+
+    def _unpack_lib(self, frame, gathered, image):
+        N.check(N.lib().cvr_unpack_tiles_device(self.r.device.handle, ctypes.byref(frame),
+                                                gathered.data_ptr(), self.tpr_max, self.fmt,
+                                                image.data_ptr()),
+                "cvr_unpack_tiles_device", self.r.device.handle)
+
+    # -- frames ---------------------------------------------------------------
+    def _stream_for(self, n):
+        """The render stream of frame n, made current on the renderer's context."""
+        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        if self.streams is None:
+            s = cur
+        else:
+            if self._fresh:
+                for st in self.streams:     # see everything the caller queued before
+                    st.wait_stream(cur)
+                self._fresh = False
+            s = self.streams[n % self.nstreams]
+        if s is not None and self.r is not None:
+            self.r.device.set_stream(s.cuda_stream)
+        return s
+
+    def submit(self, camera):
+        """Render this rank's tiles of one frame and start their gather."""
+        n = self.submitted
+        frame = self._frame_for(camera)
+        self._stream_for(n)
+        if not self.split:
+            self.render_fn(frame, self._images[n % len(self._images)], self.total)
+            self.submitted += 1
+            self.completed = n if self.streams is None else n - 1
+            return
+        slot = n % self.nbuf
+        if self._fast is not None:
+            L, h, entry, params, img, slots = self._fast
+            if self._fresh:
+                self._stream_for(n)
+            sptr, out, buf, g = slots[slot]
+            L.cvr_set_stream(h, sptr)
+            fr = ctypes.byref(frame)
+            st = entry(h, fr, params, ctypes.byref(out))
+            if st:
+                N.check(st, self.r._ENTRY, h)
+            st = L.cvr_gather_tiles(h, fr, buf, self.tpr_max, self.fmt, g, img)
+            if st:
+                N.check(st, "cvr_gather_tiles", h)
+            self.submitted += 1
+            self.completed = n - 1
+            return
+        if self.transport == "rccl":
+            # the library orders this render after the gather of frame n-2 (same slot)
+            h = self.r.device.handle
+            g = self.gathered[slot] if self.rank == 0 else None
+            buf = g[0] if self.rank == 0 else self.packed[slot]
+            self.render_fn(frame, buf, self.total)
+            N.check(N.lib().cvr_gather_tiles(h, ctypes.byref(frame), buf.data_ptr(), self.tpr_max,
+                                             self.fmt, g.data_ptr() if g is not None else None,
+                                             self._images[0].data_ptr() if self.rank == 0
+                                             else None),
+                    "cvr_gather_tiles", h)
+            self.submitted += 1
+            self.completed = n - 1
+            return
+        # the slot's previous frame (n-2) was completed before frame n-1 was submitted
+        # returned, so its gather no longer reads packed[slot]
+        self.render_fn(frame, self.packed[slot], self.total)
+        gl = list(self.gathered[slot].unbind(0)) if self.rank == 0 else None
+        work = dist.gather(self.packed[slot], gather_list=gl, dst=0, group=self.group,
+                           async_op=True)
+        self._pending.append((n, slot, work, frame))
+        self.submitted += 1
+        while len(self._pending) > 1:
+            self._complete_oldest()
+
+    def _frame_for(self, camera):
+        """This rank's cvr_frame for `camera` (cached while the camera is unchanged)."""
+        key = (tuple(camera.eye), tuple(camera.center), tuple(camera.up), camera.fovy_deg,
+               camera.aspect)
+        if key != self._fkey:
+            self._frame = (make_frame(camera, self.width, self.height, self.tile, self.rank,
+                                      self.world) if self.split else
+                           make_frame(camera, self.width, self.height))
+            self._fkey = key
+        return self._frame
+
+    def _complete_oldest(self):
+        n, slot, work, frame = self._pending.pop(0)
+        work.wait()       # the current stream waits for the gather (RCCL) / host waits (gloo)
+        if self.rank == 0:
+            self.unpack_fn(frame, self.gathered[slot], self._images[0])
+        self.completed = n
+
+    def flush(self):
+        """Complete every submitted frame: work queued on the current stream afterwards
+        sees the last frame in `image`."""
+        if self.device.type == "cuda":
+            cur = torch.cuda.current_stream(self.device)
+            if self.streams is not None:
+                for st in self.streams:
+                    cur.wait_stream(st)
+            if self.r is not None:
+                self.r.device.set_stream(cur.cuda_stream)
+            if self.transport == "rccl" and self.submitted:
+                N.check(N.lib().cvr_gather_sync(self.r.device.handle), "cvr_gather_sync",
+                        self.r.device.handle)
+        self._fresh = True
+        while self._pending:
+            self._complete_oldest()
+        self.completed = self.submitted - 1
+        return self.image
+
+    def render(self, camera):
+        self.submit(camera)
+        return self.flush()
+
+
+class TiledRc1pass(ScreenTileSplit):
+    """ScreenTileSplit of a RayCasting1Pass with RGBA32F pixels (the exact composite)
+    and a per-frame sample total; ``render(camera)`` returns the image on rank 0 and
+    this rank's packed tiles elsewhere."""
 
     def __init__(self, renderer, tile: int = 32):
-        self.r = renderer
-        self.tile = tile
-        self.world = dist.get_world_size() if dist.is_initialized() else 1
-        self.rank = dist.get_rank() if dist.is_initialized() else 0
-        w, h = renderer.width, renderer.height
-        self.k = tiles_for_rank(w, h, tile, self.rank, self.world)
-        self.tpr_max = max_tiles_per_rank(w, h, tile, self.world)
-        dev = torch.device("cuda", renderer._device_index)
-        self.packed = torch.zeros((self.tpr_max, tile, tile, 4), dtype=torch.float32, device=dev)
-        self.total = torch.zeros((1,), dtype=torch.int64, device=dev)
-        self.image = (torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
-                      if self.rank == 0 else None)
+        super().__init__(renderer, tile=tile, fmt=N.FORMAT_RGBA32F, count_samples=True,
+                         streams=1)
 
     def render(self, camera, stream=None, gather: bool = True):
-        r = self.r
-        s = stream if stream is not None else torch.cuda.current_stream(r._device_index)
-        frame = make_frame(camera, r.width, r.height, self.tile, self.rank, self.world)
-        r.Update(camera)
-        r.device.set_stream(s.cuda_stream)
-        out = N.Output(self.packed.data_ptr(), None, self.total.data_ptr(), 1)
-        N.check(N.lib().cvr_render_rc1pass(r.device.handle, ctypes.byref(frame),
-                                           ctypes.byref(r._params), ctypes.byref(out)),
-                "cvr_render_rc1pass", r.device.handle)
-        if not gather or self.world == 1:
-            return self.packed
-        allp = gather_to_root(self.packed, self.tpr_max)
-        if self.rank == 0:
-            N.check(N.lib().cvr_unpack_tiles_device(r.device.handle, ctypes.byref(frame),
-                                                    allp.data_ptr(), self.tpr_max,
-                                                    self.image.data_ptr()),
-                    "cvr_unpack_tiles_device", r.device.handle)
-            self._keep = allp      # keep the gather buffer alive until the stream passes it
-        return self.image
+        s = stream if stream is not None else torch.cuda.current_stream(self.r._device_index)
+        self.r.Update(camera)
+        self.r.device.set_stream(s.cuda_stream)
+        with torch.cuda.stream(s):
+            self.total.zero_()
+            if not gather and self.split:
+                frame = make_frame(camera, self.width, self.height, self.tile, self.rank,
+                                   self.world)
+                self.render_fn(frame, self.packed[0], self.total)
+                return self.packed[0][:self.k]
+            img = super().render(camera)
+        return img if self.rank == 0 else self.packed[(self.submitted - 1) % self.nbuf][:self.k]

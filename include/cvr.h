@@ -94,19 +94,25 @@ typedef struct cvr_frame {
   int nranks;
 } cvr_frame;
 
-/* Output buffers.  rgba: float RGBA, premultiplied, W*H*4 floats (or the
- * packed tile buffer).  samples (optional): per-pixel loop-iteration count of
+/* Output buffers.  rgba: premultiplied RGBA, W*H pixels (or the packed tile
+ * buffer), in `format`: CVR_FORMAT_RGBA32F (0, 16 B/pixel, the exact
+ * composite) or CVR_FORMAT_RGBA16F (1, 8 B/pixel: binary16 rounded to nearest
+ * even, the reference's own framebuffer, imageStore into the RGBA16F
+ * OutputFrag image, ray_marching_1p.comp:174-176 / renderoutputframe.cpp:64-87).  samples (optional): per-pixel loop-iteration count of
  * ray_marching_1p.comp:124-172 (transparent samples included, stopping at the
  * ERT break).  total (optional): the sum of all iteration counts (uint64).
  * on_device = 1: all three are device pointers and the call is asynchronous
  * on the context stream; the frame's count is atomically ADDED to *total, so
  * the caller zeroes it (one counter can accumulate many frames).
  * on_device = 0: host pointers, *total is overwritten, the call blocks.      */
+#define CVR_FORMAT_RGBA32F 0
+#define CVR_FORMAT_RGBA16F 1
 typedef struct cvr_output {
   void* rgba;
   void* samples;
   void* total;
   int on_device;
+  int format;       /* CVR_FORMAT_RGBA32F | CVR_FORMAT_RGBA16F */
 } cvr_output;
 
 /* ----------------------------------------------------------------------------
@@ -304,10 +310,54 @@ cvr_status  cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* frame,
 /* Rank-0 side of the screen-tile split: `d_packed` holds nranks consecutive
  * blocks of `tiles_per_rank_max` packed tiles (rank r's block at offset
  * r*tiles_per_rank_max*tile_size^2 pixels); scatter them into the W x H
- * device image `d_rgba`.  Asynchronous on the context stream. */
+ * device image `d_rgba`.  Both buffers hold pixels of `format`
+ * (CVR_FORMAT_RGBA32F or CVR_FORMAT_RGBA16F).  Asynchronous on the context
+ * stream. */
 cvr_status  cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* frame,
                                     const void* d_packed, int tiles_per_rank_max,
-                                    void* d_rgba);
+                                    int format, void* d_rgba);
+
+/* ----------------------------------------------------------------------------
+ * Multi-GPU: the screen-tile split's gather, native RCCL over xGMI
+ * (the reference renders on one GPU, so this has no reference
+ * counterpart beyond the Redraw it feeds, rc1prenderer.cpp:140-151).
+ * One context per GPU, one process (or thread) per context.
+ * -------------------------------------------------------------------------- */
+
+#define CVR_COMM_ID_BYTES 128
+
+/* Rank 0 creates the communicator id (ncclGetUniqueId) and hands it to every
+ * rank out of band (e.g. torch.distributed broadcast). */
+cvr_status  cvr_comm_unique_id(unsigned char out_id[CVR_COMM_ID_BYTES]);
+
+/* Collective over the nranks contexts: joins this context to the communicator. */
+cvr_status  cvr_comm_init(cvr_ctx* ctx, int nranks, int rank,
+                          const unsigned char id[CVR_COMM_ID_BYTES]);
+cvr_status  cvr_comm_destroy(cvr_ctx* ctx);
+
+/* Gather one frame's packed tiles on rank 0 and unpack them into the image.
+ * Every rank calls it right after rendering its tiles (frame->rank/nranks
+ * must match the communicator) into `d_packed` (tiles_per_rank_max tiles,
+ * padding allowed).  Rank 0 also passes `d_gathered` (nranks blocks of
+ * tiles_per_rank_max tiles; when d_packed == d_gathered, rank 0 rendered
+ * straight into its block 0 and no copy is made) and the W x H image `d_rgba`.
+ * Asynchronous: the gather and unpack run on the context's communication
+ * stream after the render.  Callers alternate two packed (and, on rank 0, two
+ * gather) buffers, frame n using buffer n % 2 (see split_streams for more).  With option split_streams = 1
+ * (default) the context stream then waits only for the PREVIOUS gather, so the
+ * next render overlaps this gather.  With split_streams = D >= 2 the caller
+ * rotates D streams and D buffer sets (frame n on stream n % D, cvr_set_stream
+ * before each render) and the stream waits for THIS gather, so D consecutive
+ * frames overlap on the device as well.
+ * Frames on different streams each use their own LPT order state; frames that
+ * count samples (cvr_output.total) must not overlap.  Before reading the image
+ * on the context stream, call cvr_gather_sync. */
+cvr_status  cvr_gather_tiles(cvr_ctx* ctx, const cvr_frame* frame, const void* d_packed,
+                             int tiles_per_rank_max, int format, void* d_gathered,
+                             void* d_rgba);
+
+/* The context stream waits for every gather issued so far. */
+cvr_status  cvr_gather_sync(cvr_ctx* ctx);
 
 /* Diagnostics (tile_stats option): for each 8x8 tile of the last frame, four
  * uint64: start and end stamp (s_memrealtime, 100 MHz), its longest ray's

@@ -85,3 +85,81 @@ def test_tile_partition_covers_frame():
         owned = sum(T.tiles_for_rank(W, H, tile, r, world) for r in range(world))
         assert owned == ntx * nty
         assert T.max_tiles_per_rank(W, H, tile, world) == -(-ntx * nty // world)
+
+
+CAMS = [dict(D.INITIAL_STATE_CAMERA),
+        dict(D.INITIAL_STATE_CAMERA, eye=(-300.0, 120.0, 380.0)),
+        dict(D.INITIAL_STATE_CAMERA, eye=(0.0, -400.0, 200.0))]
+
+
+def _frames(W, H):
+    import oracle as O
+    vol = D.marschner_lobb_u8(24)
+    scale = D.voxel_scale(24)
+    table = O.tf_table_double(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA)
+    out = {}
+    for c in CAMS:
+        rgba, _, _ = O.render_rc1pass(O.volume_r16f(vol), scale, O.tf_rgbt(table), c, W, H,
+                                      O.default_step(scale))
+        out[tuple(c["eye"])] = rgba.astype(np.float16)
+    return out
+
+
+def _split_worker(rank, world, port, W, H, tile, q):
+    """ScreenTileSplit (torch transport, RGBA16F) over gloo with host mirrors of the
+    render (pack_rank of an oracle frame) and the unpack: frames are pipelined, so
+    after submit(n) rank 0's image must hold frame n-1, and after flush frame n."""
+    from cpp_volume_rendering_amd import _native as N
+    from cpp_volume_rendering_amd.renderer import Camera
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        imgs = _frames(W, H)
+
+        def render_fn(frame, out, total):
+            eye = tuple(float(v) for v in frame.camera.eye)
+            assert frame.rank == rank and frame.nranks == world
+            p = T.pack_rank(imgs[eye], tile, rank, world)
+            out.zero_()
+            out[:p.shape[0]] = torch.from_numpy(p)
+
+        def unpack_fn(frame, gathered, image):
+            image.copy_(torch.from_numpy(T.unpack(gathered.numpy(), W, H, tile, world)))
+
+        sp = T.ScreenTileSplit(None, W, H, tile=tile, fmt=N.FORMAT_RGBA16F, device="cpu",
+                               render_fn=render_fn, unpack_fn=unpack_fn)
+        assert sp.transport == "torch"
+        seq = [0, 1, 2, 1, 0]
+        ok = True
+        for n, ci in enumerate(seq):
+            sp.submit(Camera(**CAMS[ci]))
+            assert sp.completed == n - 1
+            if rank == 0 and n > 0:
+                want = imgs[tuple(CAMS[seq[n - 1]]["eye"])]
+                ok &= np.array_equal(sp.image.numpy().view(np.uint16), want.view(np.uint16))
+        img = sp.flush()
+        assert sp.completed == len(seq) - 1
+        if rank == 0:
+            want = imgs[tuple(CAMS[seq[-1]]["eye"])]
+            ok &= np.array_equal(img.numpy().view(np.uint16), want.view(np.uint16))
+            q.put("ok" if ok else "mismatch")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H,tile", [(2, 96, 80, 32), (3, 70, 45, 16)])
+def test_screen_tile_split_pipeline_gloo(world, W, H, tile):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, W, H, tile, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    codes = [p.exitcode for p in procs]
+    assert codes == [0] * world, f"worker exit codes {codes}"
+    assert q.get(timeout=10) == "ok"

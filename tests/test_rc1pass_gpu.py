@@ -183,7 +183,8 @@ def test_screen_tiles_match_full_frame(dev, bonsai_tf, nranks, tile):
     frame = make_frame(Camera(**INITIAL), W, H, tile, 0, nranks)
     dev.set_stream(torch.cuda.current_stream().cuda_stream)
     N.check(N.lib().cvr_unpack_tiles_device(dev.handle, ctypes.byref(frame), d_packed.data_ptr(),
-                                            tpr, d_img.data_ptr()), "unpack", dev.handle)
+                                            tpr, N.FORMAT_RGBA32F, d_img.data_ptr()), "unpack",
+            dev.handle)
     torch.cuda.synchronize()
     dev.set_stream(None)
     assert_bitexact(d_img.cpu().numpy(), full, "device unpack")
