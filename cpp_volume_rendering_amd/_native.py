@@ -33,8 +33,12 @@ EXPORTED_SYMBOLS = (
     "cvr_set_extinction_volume", "cvr_copy_extinction_level", "cvr_render_dosct",
     "cvr_tf1d_ext_lut", "cvr_set_extinction_sat", "cvr_copy_extinction_sat", "cvr_render_extbsd",
     "cvr_comm_unique_id", "cvr_comm_init", "cvr_comm_destroy", "cvr_gather_tiles",
-    "cvr_gather_sync",
+    "cvr_gather_sync", "cvr_multiscale_resolution", "cvr_multiscale_filter",
+    "cvr_screenshot_rgb8",
 )
+SINGLE_RAY_PER_PIXEL, MULTIPLE_RAYS_PER_PIXEL, DOWN_SCALING_RENDER, UP_SCALING_RENDER = range(4)
+(FILTER_BOX, FILTER_HAT, FILTER_CATMULL_ROM, FILTER_MITCHELL_NETRAVALI, FILTER_CARDINAL_BSPLINE_3,
+ FILTER_CARDINAL_OMOMS3) = range(6)
 COMM_ID_BYTES = 128
 
 
@@ -161,6 +165,9 @@ def lib() -> ctypes.CDLL:
         "cvr_comm_destroy": ([P], I),
         "cvr_gather_tiles": ([P, ctypes.POINTER(Frame), P, I, I, P, P], I),
         "cvr_gather_sync": ([P], I),
+        "cvr_multiscale_resolution": ([I, I, I, IP, IP], I),
+        "cvr_multiscale_filter": ([P, I, I, P, I, I, P, I, I], I),
+        "cvr_screenshot_rgb8": ([P, P, I, I, I, P], I),
         "cvr_copy_tile_stats": ([P, P, I, IP], I),
         "cvr_read_kernel_times": ([P, FP, I, IP], I),
         "cvr_read_shade_counters": ([P, ctypes.POINTER(ctypes.c_uint64)], I),

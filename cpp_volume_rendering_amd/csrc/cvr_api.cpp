@@ -900,6 +900,45 @@ cvr_status cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* o
   return CVR_OK;
 }
 
+cvr_status cvr_multiscale_resolution(int mode, int sw, int sh, int* rw, int* rh) {
+  if (!rw || !rh || sw < 1 || sh < 1 || mode < 0 || mode > 3) return CVR_ERR_ARG;
+  // UpdateScreenResolutionMultiScaling, multiplier (2, 2) or (-2, -2)
+  if (mode == CVR_SINGLE_RAY_PER_PIXEL) { *rw = sw; *rh = sh; }
+  else if (mode == CVR_UP_SCALING_RENDER) { *rw = sw / 2; *rh = sh / 2; }
+  else { *rw = sw * 2; *rh = sh * 2; }
+  return (*rw >= 1 && *rh >= 1) ? CVR_OK : CVR_ERR_ARG;
+}
+
+cvr_status cvr_multiscale_filter(cvr_ctx* ctx, int mode, int kernel, void* d_frame, int fw, int fh,
+                                 void* d_screen, int sw, int sh) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!d_frame || !d_screen || mode < 1 || mode > 3 || kernel < 0 || kernel > 5 || fw < 1 ||
+      fh < 1 || sw < 1 || sh < 1 || d_frame == d_screen)
+    return fail(c, CVR_ERR_ARG, "cvr_multiscale_filter: bad arguments");
+  const bool cardinal = kernel == CVR_FILTER_CARDINAL_BSPLINE_3 || kernel == CVR_FILTER_CARDINAL_OMOMS3;
+  // the digital filter's pre-factored LU needs lines longer than its 8/9 factors
+  if (cardinal && mode != CVR_MULTIPLE_RAYS_PER_PIXEL &&
+      (mode == CVR_DOWN_SCALING_RENDER ? (sw < 16 || sh < 16) : (fw < 16 || fh < 16)))
+    return fail(c, CVR_ERR_ARG, "cvr_multiscale_filter: cardinal kernels need >= 16 px lines");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, cvr::launch_multiscale(mode, kernel, d_frame, fw, fh, d_screen, sw, sh, c->stream));
+  return CVR_OK;
+}
+
+cvr_status cvr_screenshot_rgb8(cvr_ctx* ctx, const void* d_frame, int format, int w, int h,
+                               void* d_rgb) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!d_frame || !d_rgb || w < 1 || h < 1 ||
+      (format != CVR_FORMAT_RGBA32F && format != CVR_FORMAT_RGBA16F))
+    return fail(c, CVR_ERR_ARG, "cvr_screenshot_rgb8: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, cvr::launch_screenshot(d_frame, format == CVR_FORMAT_RGBA16F, w, h, (uint8_t*)d_rgb,
+                                    c->stream));
+  return CVR_OK;
+}
+
 cvr_status cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* f, const void* d_packed,
                                    int tpr_max, int format, void* d_rgba) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);

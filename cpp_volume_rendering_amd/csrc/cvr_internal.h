@@ -227,6 +227,12 @@ struct Ctx {
 
 void comm_release(Ctx* c);   // cvr_comm.cpp
 
+// postpass.hip: multiscaling filters (mode 1-3, kernel 0-5) and the screenshot
+hipError_t launch_multiscale(int mode, int kernel, void* frame, int fw, int fh, void* screen, int sw,
+                             int sh, hipStream_t s);
+hipError_t launch_screenshot(const void* frame, int half, int w, int h, uint8_t* rgb,
+                             hipStream_t s);
+
 // kernels / launchers (raymarch.hip)
 hipError_t launch_build_cells_impl(const void* vox, int bpv, const uint16_t* lut, const int N[3],
                                    const CellGrid& g, void* cells, hipStream_t s);

@@ -1,0 +1,322 @@
+// postpass.hip — the step after the ray-march: the pixel
+// multiscaling filters of RenderFrameToScreen and the screenshot composite.
+//
+//   MULTIPLE_RAYS_PER_PIXEL  render at (2w, 2h), bilinear texture() fetch at the
+//                            screen pixel centres (multisample_filter.comp)
+//   DOWN_SCALING_RENDER      render at (2w, 2h), kernel-filtered decimation
+//                            (downscaling_filter.comp + <kernel>_filter.comp), then
+//                            for the cardinal kernels the recursive digital filter
+//                            over the result (cbs/comoms_digital_filter.comp)
+//   UP_SCALING_RENDER        render at (w/2, h/2), digital prefilter IN PLACE on the
+//                            rendered frame for the cardinal kernels, then kernel-
+//                            filtered interpolation (upscaling_filter.comp)
+//   screenshot               the RGBA16F frame drawn with SRC_ALPHA /
+//                            ONE_MINUS_SRC_ALPHA over the white clear colour, read
+//                            back as RGB8 (renderingmanager.cpp:103-112, 476-492)
+//
+// Every image is RGBA16F, as the reference's textures: each imageStore rounds to
+// binary16 (nearest even), and the digital filter's recursion re-reads its own
+// rounded stores.  The GLSL float expressions are evaluated in the shaders' order
+// without contraction (-ffp-contract=off); texelFetch outside the image reads 0
+// (robust access), texture() clamps to the edge (GL_CLAMP_TO_EDGE).  These are
+// small HBM-bound passes (8 B per pixel in, 8 B out, x the kernel's footprint
+// served from L2).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "cvr_internal.h"
+
+namespace cvr {
+namespace {
+
+__device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+
+__device__ __forceinline__ float4 load_px(const uint2* img, int w, int x, int y) {
+  const uint2 p = img[(size_t)y * w + x];
+  return make_float4(h2f((uint16_t)(p.x & 0xffffu)), h2f((uint16_t)(p.x >> 16)),
+                     h2f((uint16_t)(p.y & 0xffffu)), h2f((uint16_t)(p.y >> 16)));
+}
+__device__ __forceinline__ void store_px(uint2* img, int w, int x, int y, float4 v) {
+  img[(size_t)y * w + x] = make_uint2((uint32_t)f2h(v.x) | ((uint32_t)f2h(v.y) << 16),
+                                      (uint32_t)f2h(v.z) | ((uint32_t)f2h(v.w) << 16));
+}
+// texelFetch with robust access: 0 outside the image
+__device__ __forceinline__ float4 fetch_px(const uint2* img, int w, int h, int x, int y) {
+  if (x < 0 || y < 0 || x >= w || y >= h) return make_float4(0.f, 0.f, 0.f, 0.f);
+  return load_px(img, w, x, y);
+}
+
+// ---- kernels of renderoutputframe/<name>_filter.comp ------------------------
+struct KBox {      // box_filter.comp
+  static constexpr float support = 1.0f;
+  __device__ static float w(float x) { return x <= -0.5f || x > 0.5f ? 0.0f : 1.0f; }
+};
+struct KHat {      // hat_filter.comp
+  static constexpr float support = 2.0f;
+  __device__ static float w(float x) {
+    x = fabsf(x);
+    return x > 1.0f ? 0.0f : 1.0f - x;
+  }
+};
+struct KCatmullRom {   // catmullrom_filter.comp
+  static constexpr float support = 4.0f;
+  __device__ static float k0(float u) { return ((0.5f * u - 0.5f) * u) * u; }
+  __device__ static float k1(float u) { return ((-1.5f * u + 2.0f) * u + 0.5f) * u; }
+  __device__ static float w(float x) {
+    x = fabsf(x);
+    return x > 2.0f ? 0.0f : x > 1.0f ? k0(2.0f - x) : k1(1.0f - x);
+  }
+};
+struct KMitchell {     // mitchellnetravali_filter.comp
+  static constexpr float support = 4.0f;
+  __device__ static float k0(float u) { return (((7 / 18.0f) * u - 1 / 3.0f) * u) * u; }
+  __device__ static float k1(float u) {
+    return (((-7 / 6.0f) * u + 1.5f) * u + 0.5f) * u + 1 / 18.0f;
+  }
+  __device__ static float w(float x) {
+    x = fabsf(x);
+    return x > 2.0f ? 0.0f : x > 1.0f ? k0(2.0f - x) : k1(1.0f - x);
+  }
+};
+struct KCardinalBSpline3 {   // cardinalbspline_filter.comp
+  static constexpr float support = 4.0f;
+  __device__ static float k0(float u) { return ((u)*u) * u; }
+  __device__ static float k1(float u) { return ((-3.0f * u + 3.0f) * u + 3.0f) * u + 1.0f; }
+  __device__ static float w(float x) {
+    x = fabsf(x);
+    return x > 2.0f ? 0.0f : x > 1.0f ? k0(2.0f - x) : k1(1.0f - x);
+  }
+};
+struct KCardinalOmoms3 {     // cardinalomoms_filter.comp
+  static constexpr float support = 4.0f;
+  __device__ static float k0(float u) { return ((0.875f * u) * u + 0.125f) * u; }
+  __device__ static float k1(float u) {
+    return ((-2.625f * u + 2.625f) * u + 2.25f) * u + 1.0f;
+  }
+  __device__ static float w(float x) {
+    x = fabsf(x);
+    return x > 2.0f ? 0.0f : x > 1.0f ? k0(2.0f - x) : k1(1.0f - x);
+  }
+};
+
+__device__ __forceinline__ float4 madd(float4 acc, float wgt, float4 t) {
+  return make_float4(acc.x + wgt * t.x, acc.y + wgt * t.y, acc.z + wgt * t.z, acc.w + wgt * t.w);
+}
+
+// multisample_filter.comp: texture(TexGeneratedFrame, (p + 0.5) / size), bilinear,
+// clamp to edge, texel centres at (i + 0.5) / n
+__global__ void multisample_kernel(const uint2* __restrict__ src, int sw, int sh,
+                                   uint2* __restrict__ dst, int tw, int th) {
+  const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (x >= tw || y >= th) return;
+  const float u = ((float)x + 0.5f) / (float)tw, v = ((float)y + 0.5f) / (float)th;
+  const float fx = u * (float)sw - 0.5f, fy = v * (float)sh - 0.5f;
+  const float flx = floorf(fx), fly = floorf(fy);
+  const float ax = fx - flx, ay = fy - fly;
+  const int x0 = min(max((int)flx, 0), sw - 1), x1 = min(max((int)flx + 1, 0), sw - 1);
+  const int y0 = min(max((int)fly, 0), sh - 1), y1 = min(max((int)fly + 1, 0), sh - 1);
+  const float4 a = load_px(src, sw, x0, y0), b = load_px(src, sw, x1, y0);
+  const float4 c = load_px(src, sw, x0, y1), d = load_px(src, sw, x1, y1);
+  auto lerp4 = [](float4 p, float4 q, float t) {
+    return make_float4(fmaf(t, q.x - p.x, p.x), fmaf(t, q.y - p.y, p.y), fmaf(t, q.z - p.z, p.z),
+                       fmaf(t, q.w - p.w, p.w));
+  };
+  store_px(dst, tw, x, y, lerp4(lerp4(a, b, ax), lerp4(c, d, ax), ay));
+}
+
+// downscaling_filter.comp
+template <class K>
+__global__ void downscale_kernel(const uint2* __restrict__ src, int sw, int sh,
+                                 uint2* __restrict__ dst, int tw, int th) {
+  const int jc = blockIdx.x * 16 + (threadIdx.x & 15), jr = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (jc >= tw || jr >= th) return;
+  const float s_r = (float)th / (float)sh;
+  const float s_c = (float)tw / (float)sw;
+  const float kr = 0.5f * K::support;
+  const float x_r = ((float)jr + 0.5f) / (float)th;
+  const int il_r = (int)ceilf((x_r - kr / (float)th) * (float)sh - 0.5f);
+  const int ir_r = (int)floorf((x_r + kr / (float)th) * (float)sh - 0.5f);
+  const float x_c = ((float)jc + 0.5f) / (float)tw;
+  const int il_c = (int)ceilf((x_c - kr / (float)tw) * (float)sw - 0.5f);
+  const int ir_c = (int)floorf((x_c + kr / (float)tw) * (float)sw - 0.5f);
+  float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int ir = il_r; ir <= ir_r; ir++) {
+    const float wr = K::w((x_r - ((float)ir + 0.5f) / (float)sh) * (float)th);
+    for (int ic = il_c; ic <= ir_c; ic++) {
+      const float wc = K::w((x_c - ((float)ic + 0.5f) / (float)sw) * (float)tw);
+      f = madd(f, wr * wc, fetch_px(src, sw, sh, ic, ir));
+    }
+  }
+  const float s = s_r * s_c;
+  store_px(dst, tw, jc, jr, make_float4(f.x * s, f.y * s, f.z * s, f.w * s));
+}
+
+// upscaling_filter.comp
+template <class K>
+__global__ void upscale_kernel(const uint2* __restrict__ src, int sw, int sh,
+                               uint2* __restrict__ dst, int tw, int th) {
+  const int jc = blockIdx.x * 16 + (threadIdx.x & 15), jr = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (jc >= tw || jr >= th) return;
+  const float kr = 0.5f * K::support;
+  const float x_r = ((float)jr + 0.5f) / (float)th;
+  const float xi_r = x_r * (float)sh - 0.5f;
+  const int il_r = (int)ceilf(xi_r - kr), ir_r = (int)floorf(xi_r + kr);
+  const float x_c = ((float)jc + 0.5f) / (float)tw;
+  const float xi_c = x_c * (float)sw - 0.5f;
+  const int il_c = (int)ceilf(xi_c - kr), ir_c = (int)floorf(xi_c + kr);
+  float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int ir = il_r; ir <= ir_r; ir++) {
+    const float wr = K::w(xi_r - (float)ir);
+    for (int ic = il_c; ic <= ir_c; ic++)
+      f = madd(f, wr * K::w(xi_c - (float)ic), fetch_px(src, sw, sh, ic, ir));
+  }
+  store_px(dst, tw, jc, jr, f);
+}
+
+// cbs_digital_filter.comp / comoms_digital_filter.comp: the pre-factored LU
+// solve of the cardinal kernel's sampled convolution, one thread per row (dir 0)
+// or column (dir 1), in place, every step stored as RGBA16F.
+struct LCbs {
+  static constexpr int m = 8;
+  __device__ static float L(int i) {
+    constexpr float t[8] = {.2f, .26315789f, .26760563f, .26792453f,
+                            .26794742f, .26794907f, .26794918f, .26794919f};
+    return t[i];
+  }
+};
+struct LOmoms {
+  static constexpr int m = 9;
+  __device__ static float L(int i) {
+    constexpr float t[9] = {.23529412f, .33170732f, .34266611f, .34395774f, .34411062f,
+                            .34412872f, .34413087f, .34413112f, .34413115f};
+    return t[i];
+  }
+};
+
+template <class LU>
+__global__ void digital_filter_kernel(uint2* __restrict__ img, int w, int h, int dir) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lines = dir == 0 ? h : w;
+  if (t >= lines) return;
+  const int nn = dir == 0 ? w : h;
+  auto at = [&](int i, int& x, int& y) {
+    if (dir == 0) { x = i; y = t; } else { x = t; y = i; }
+  };
+  const int m = LU::m;
+  const float p_inv = 1.0f;
+  const float L_inf = LU::L(m - 1), v_inv = L_inf / (1.f + L_inf);
+  int x, y;
+  // forward pass: f[i] -= L * f[i-1]
+  at(0, x, y);
+  float4 prev = load_px(img, w, x, y);
+  for (int i = 1; i < nn; i++) {
+    at(i, x, y);
+    const float l = i < m ? LU::L(i - 1) : L_inf;
+    const float4 c = load_px(img, w, x, y);
+    float4 r = make_float4(c.x - l * prev.x, c.y - l * prev.y, c.z - l * prev.z, c.w - l * prev.w);
+    store_px(img, w, x, y, r);
+    prev = load_px(img, w, x, y);     // the stored (rounded) value
+  }
+  // f[nn-1] *= p_inv * v_inv
+  at(nn - 1, x, y);
+  {
+    const float4 c = load_px(img, w, x, y);
+    const float s = p_inv * v_inv;
+    store_px(img, w, x, y, make_float4(c.x * s, c.y * s, c.z * s, c.w * s));
+    prev = load_px(img, w, x, y);
+  }
+  // reverse pass: f[i] = L * (p_inv * f[i] - f[i+1])
+  for (int i = nn - 2; i >= 0; i--) {
+    at(i, x, y);
+    const float l = i >= m - 1 ? L_inf : LU::L(i);
+    const float4 c = load_px(img, w, x, y);
+    const float4 r = make_float4(l * (p_inv * c.x - prev.x), l * (p_inv * c.y - prev.y),
+                                 l * (p_inv * c.z - prev.z), l * (p_inv * c.w - prev.w));
+    store_px(img, w, x, y, r);
+    prev = load_px(img, w, x, y);
+  }
+}
+
+// Screenshot: FragColor = texture(frame) blended SRC_ALPHA / ONE_MINUS_SRC_ALPHA over
+// white, stored to an 8-bit unorm back buffer, read as RGB (row 0 = bottom).
+template <bool HALF>
+__global__ void screenshot_kernel(const void* __restrict__ src, int w, int h,
+                                  uint8_t* __restrict__ rgb) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)w * h) return;
+  float4 p;
+  if (HALF) p = load_px((const uint2*)src, w, (int)(i % w), (int)(i / w));
+  else p = ((const float4*)src)[i];
+  const float c[3] = {p.x, p.y, p.z};
+  for (int k = 0; k < 3; k++) {
+    const float v = c[k] * p.w + (1.0f - p.w);
+    const float q = floorf(v * 255.0f + 0.5f);
+    rgb[i * 3 + k] = (uint8_t)(q < 0.0f ? 0.0f : (q > 255.0f ? 255.0f : q));
+  }
+}
+
+#define CVR_KERNEL_SWITCH(KFN, kernel, g, b, s, ...)                                  \
+  switch (kernel) {                                                                 \
+    case 0: hipLaunchKernelGGL(KFN<KBox>, g, b, 0, s, __VA_ARGS__); break;          \
+    case 1: hipLaunchKernelGGL(KFN<KHat>, g, b, 0, s, __VA_ARGS__); break;          \
+    case 2: hipLaunchKernelGGL(KFN<KCatmullRom>, g, b, 0, s, __VA_ARGS__); break;   \
+    case 3: hipLaunchKernelGGL(KFN<KMitchell>, g, b, 0, s, __VA_ARGS__); break;     \
+    case 4: hipLaunchKernelGGL(KFN<KCardinalBSpline3>, g, b, 0, s, __VA_ARGS__); break; \
+    case 5: hipLaunchKernelGGL(KFN<KCardinalOmoms3>, g, b, 0, s, __VA_ARGS__); break;   \
+    default: return hipErrorInvalidValue;                                           \
+  }
+
+hipError_t launch_digital(int kernel, uint2* img, int w, int h, hipStream_t s) {
+  for (int dir = 0; dir < 2; dir++) {
+    const int lines = dir == 0 ? h : w;
+    const dim3 g((lines + 63) / 64), b(64);
+    if (kernel == 4) hipLaunchKernelGGL(digital_filter_kernel<LCbs>, g, b, 0, s, img, w, h, dir);
+    else hipLaunchKernelGGL(digital_filter_kernel<LOmoms>, g, b, 0, s, img, w, h, dir);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t launch_multiscale(int mode, int kernel, void* frame, int fw, int fh, void* screen, int sw,
+                             int sh, hipStream_t s) {
+  const dim3 g((sw + 15) / 16, (sh + 15) / 16), b(256);
+  uint2* src = (uint2*)frame;
+  uint2* dst = (uint2*)screen;
+  if (mode == 1) {
+    hipLaunchKernelGGL(multisample_kernel, g, b, 0, s, src, fw, fh, dst, sw, sh);
+    return hipGetLastError();
+  }
+  const bool cardinal = kernel == 4 || kernel == 5;
+  if (mode == 2) {
+    CVR_KERNEL_SWITCH(downscale_kernel, kernel, g, b, s, src, fw, fh, dst, sw, sh);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !cardinal) return e;
+    return launch_digital(kernel, dst, sw, sh, s);        // over the filtered screen
+  }
+  if (mode == 3) {
+    if (cardinal) {
+      hipError_t e = launch_digital(kernel, src, fw, fh, s);   // in place on the frame
+      if (e != hipSuccess) return e;
+    }
+    CVR_KERNEL_SWITCH(upscale_kernel, kernel, g, b, s, src, fw, fh, dst, sw, sh);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_screenshot(const void* frame, int half, int w, int h, uint8_t* rgb,
+                             hipStream_t s) {
+  const size_t n = (size_t)w * h;
+  if (n == 0) return hipSuccess;
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+  if (half) hipLaunchKernelGGL(screenshot_kernel<true>, g, b, 0, s, frame, w, h, rgb);
+  else hipLaunchKernelGGL(screenshot_kernel<false>, g, b, 0, s, frame, w, h, rgb);
+  return hipGetLastError();
+}
+
+}  // namespace cvr

@@ -329,11 +329,14 @@ def tiles_for_rank(frame: N.Frame, rank: int) -> int:
 class BaseVolumeRenderer:
     """cppvolrend/volrenderbase.h:25-96 (GL-free)."""
 
-    SINGLE_RAY_PER_PIXEL = 0
+    # volrenderbase.h:28-33
+    SINGLE_RAY_PER_PIXEL, MULTIPLE_RAYS_PER_PIXEL, DOWN_SCALING_RENDER, UP_SCALING_RENDER = range(4)
 
     def __init__(self):
         self.vr_built = False
         self.vr_outdated = True
+        self.vr_pixel_multiscaling_support = False
+        self.vr_pixel_multiscaling_mode = 0
         self.m_ext_data_manager: Optional[DataManager] = None
         self.m_ext_rendering_parameters: Optional[RenderingParameters] = None
 
@@ -351,8 +354,19 @@ class BaseVolumeRenderer:
     def IsOutdated(self): return self.vr_outdated
     def IsBuilt(self): return self.vr_built
     def SetBuilt(self, b: bool): self.vr_built = bool(b)
-    def IsPixelMultiScalingSupported(self): return False
-    def GetCurrentMultiScalingMode(self): return self.SINGLE_RAY_PER_PIXEL
+    def IsPixelMultiScalingSupported(self): return self.vr_pixel_multiscaling_support
+
+    def GetCurrentMultiScalingMode(self):      # volrenderbase.cpp:106-109
+        return self.vr_pixel_multiscaling_mode if self.IsPixelMultiScalingSupported() else 0
+
+    def SetCurrentMultiScalingMode(self, f: int):
+        self.vr_pixel_multiscaling_mode = int(f)
+
+    # multiscaling entry points (volrenderbase.h:50-52); RenderingManager::Display
+    # dispatches on GetCurrentMultiScalingMode (renderingmanager.cpp:199-208, 1200-1217)
+    def MultiSampleRedraw(self): pass
+    def DownScalingRedraw(self): pass
+    def UpScalingRedraw(self): pass
 
     # virtual API
     def GetName(self) -> str: raise NotImplementedError
@@ -383,7 +397,11 @@ class RayCasting1Pass(BaseVolumeRenderer):
         self._frame: Optional[N.Frame] = None
         self._params = N.Rc1passParams()
         self.width = self.height = 0
-        self.rgba: Optional[torch.Tensor] = None    # (H, W, 4) float32, device
+        self.rgba: Optional[torch.Tensor] = None    # (H, W, 4) float32 (float16 when multiscaling)
+        self.screen: Optional[torch.Tensor] = None  # the screen image (rgba, or the filtered frame)
+        self.screen_width = self.screen_height = 0
+        self.m_kernel_filter = N.FILTER_HAT         # renderoutputframe.cpp:34
+        self.vr_pixel_multiscaling_support = True   # rc1prenderer.cpp:25
         self.samples: Optional[torch.Tensor] = None  # (H, W) int32 iteration counts
         self.total: Optional[torch.Tensor] = None   # (1,) int64 sum of samples
 
@@ -416,16 +434,48 @@ class RayCasting1Pass(BaseVolumeRenderer):
         return True
 
     def Reshape(self, w: int, h: int):
-        self.width, self.height = int(w), int(h)
+        """Screen size (w, h).  The frame is rendered at the multiscaling mode's resolution
+        (BaseVolumeRenderer::Reshape, volrenderbase.cpp:42-66): float32 RGBA for a single
+        ray per pixel, else the RGBA16F render target the post-pass filters into
+        ``screen`` (RGBA16F, w x h)."""
+        self.screen_width, self.screen_height = int(w), int(h)
+        mode = self.GetCurrentMultiScalingMode()
+        rw, rh = ctypes.c_int(), ctypes.c_int()
+        N.check(N.lib().cvr_multiscale_resolution(mode, int(w), int(h), ctypes.byref(rw),
+                                                  ctypes.byref(rh)), "cvr_multiscale_resolution")
+        self.width, self.height = rw.value, rh.value
         dev = torch.device("cuda", self._device_index)
-        self.rgba = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
-        self.samples = torch.zeros((h, w), dtype=torch.int32, device=dev)
+        self.rgba = torch.zeros((self.height, self.width, 4),
+                                dtype=torch.float16 if mode else torch.float32, device=dev)
+        self.samples = torch.zeros((self.height, self.width), dtype=torch.int32, device=dev)
         self.total = torch.zeros((1,), dtype=torch.int64, device=dev)
+        self.screen = (torch.zeros((h, w, 4), dtype=torch.float16, device=dev) if mode
+                       else self.rgba)
         super().Reshape(w, h)
+
+    def SetCurrentMultiScalingMode(self, f: int):
+        """Switch the multiscaling mode (AddImGuiMultiSampleOptions, volrenderbase.cpp:
+        119-171): the render target is resized for it."""
+        super().SetCurrentMultiScalingMode(f)
+        if self.rgba is not None:
+            self.Reshape(self.screen_width, self.screen_height)
+
+    def SetImageKernelFilter(self, k: int):
+        """RenderFrameToScreen::SetImageKernelFilter (vis::IMAGE_FILTER_KERNEL, default
+        K2_HAT, renderoutputframe.cpp:34, 541-545)."""
+        self.m_kernel_filter = int(k)
+
+    def _camera_frame(self, camera: Camera) -> N.Frame:
+        """The frame at the render resolution; the aspect stays the screen's
+        (Camera::GetAspectRatio, passed as a uniform, rc1prenderer.cpp:100-101)."""
+        if camera.aspect == 0 and self.GetCurrentMultiScalingMode():
+            camera = Camera(camera.eye, camera.center, camera.up, camera.fovy_deg,
+                            self.screen_width / self.screen_height)
+        return make_frame(camera, self.width, self.height)
 
     def Update(self, camera: Camera) -> bool:
         rp = self.m_ext_rendering_parameters or RenderingParameters()
-        self._frame = make_frame(camera, self.width, self.height)
+        self._frame = self._camera_frame(camera)
         p = self._params
         p.step = float(self.m_u_step_size)
         p.apply_gradient_shading = int(bool(self.m_apply_gradient_shading) and
@@ -445,10 +495,44 @@ class RayCasting1Pass(BaseVolumeRenderer):
         if count_samples:
             with torch.cuda.stream(s):
                 self.total.zero_()                  # the kernel accumulates into it
+        mode = self.GetCurrentMultiScalingMode()
         out = N.Output(self.rgba.data_ptr(),
                        self.samples.data_ptr() if count_samples else None,
-                       self.total.data_ptr() if count_samples else None, 1)
+                       self.total.data_ptr() if count_samples else None, 1,
+                       N.FORMAT_RGBA16F if mode else N.FORMAT_RGBA32F)
         self.render_to(self._frame, out)
+        if mode:    # the post-pass of RenderFrameToScreen, same stream
+            N.check(N.lib().cvr_multiscale_filter(self.device.handle, mode, self.m_kernel_filter,
+                                                  self.rgba.data_ptr(), self.width, self.height,
+                                                  self.screen.data_ptr(), self.screen_width,
+                                                  self.screen_height),
+                    "cvr_multiscale_filter", self.device.handle)
+
+    # rc1prenderer.cpp:153-190: the same dispatch, then the mode's filter (Redraw does both)
+    def MultiSampleRedraw(self, stream=None, count_samples: bool = True):
+        assert self.GetCurrentMultiScalingMode() == self.MULTIPLE_RAYS_PER_PIXEL
+        self.Redraw(stream, count_samples)
+
+    def DownScalingRedraw(self, stream=None, count_samples: bool = True):
+        assert self.GetCurrentMultiScalingMode() == self.DOWN_SCALING_RENDER
+        self.Redraw(stream, count_samples)
+
+    def UpScalingRedraw(self, stream=None, count_samples: bool = True):
+        assert self.GetCurrentMultiScalingMode() == self.UP_SCALING_RENDER
+        self.Redraw(stream, count_samples)
+
+    def Screenshot(self) -> np.ndarray:
+        """RenderingManager::SaveScreenshot's pixels: the screen image blended over white,
+        RGB8, row 0 = bottom (renderingmanager.cpp:103-112, 476-492).  Synchronises."""
+        w, h = self.screen_width, self.screen_height
+        rgb = torch.empty((h, w, 3), dtype=torch.uint8, device=self.screen.device)
+        s = torch.cuda.current_stream(self._device_index)
+        self.device.set_stream(s.cuda_stream)
+        N.check(N.lib().cvr_screenshot_rgb8(self.device.handle, self.screen.data_ptr(),
+                                            N.FORMAT_RGBA16F if self.screen.dtype == torch.float16
+                                            else N.FORMAT_RGBA32F, w, h, rgb.data_ptr()),
+                "cvr_screenshot_rgb8", self.device.handle)
+        return rgb.cpu().numpy()
 
     # C entry of this renderer's frame (cvr_render_rc1pass / _dosct / _extbsd)
     _ENTRY = "cvr_render_rc1pass"
@@ -522,7 +606,7 @@ class RC1PConeTracingDirOcclusionShading(RayCasting1Pass):
 
     def Update(self, camera: Camera) -> bool:
         rp = self.m_ext_rendering_parameters or RenderingParameters()
-        self._frame = make_frame(camera, self.width, self.height)
+        self._frame = self._camera_frame(camera)
         p = self._params
         p.step = float(self.m_u_step_size)
         p.apply_gradient_shading = int(bool(self.m_apply_gradient_shading) and
@@ -580,7 +664,7 @@ class RC1PExtinctionBasedShading(RayCasting1Pass):
 
     def Update(self, camera: Camera) -> bool:
         rp = self.m_ext_rendering_parameters or RenderingParameters()
-        self._frame = make_frame(camera, self.width, self.height)
+        self._frame = self._camera_frame(camera)
         p = self._params
         p.step = float(self.m_u_step_size)
         p.apply_gradient_shading = int(bool(self.m_apply_gradient_shading) and

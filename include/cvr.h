@@ -318,6 +318,47 @@ cvr_status  cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* frame,
                                     int format, void* d_rgba);
 
 /* ----------------------------------------------------------------------------
+ * After the march: pixel multiscaling and the screenshot
+ * (libs/vis_utils/renderoutputframe.cpp:89-146, 265-539 and its
+ * shader/renderoutputframe/ compute shaders; renderingmanager.cpp:103-112,
+ * 476-492)
+ * -------------------------------------------------------------------------- */
+
+/* BaseVolumeRenderer multiscaling modes (volrenderbase.h:28-33) */
+#define CVR_SINGLE_RAY_PER_PIXEL    0
+#define CVR_MULTIPLE_RAYS_PER_PIXEL 1
+#define CVR_DOWN_SCALING_RENDER     2
+#define CVR_UP_SCALING_RENDER       3
+/* vis::IMAGE_FILTER_KERNEL (libs/vis_utils/filters/utils.hpp:8-15); K2_HAT is
+ * RenderFrameToScreen's default (renderoutputframe.cpp:34) */
+#define CVR_FILTER_BOX                0
+#define CVR_FILTER_HAT                1
+#define CVR_FILTER_CATMULL_ROM        2
+#define CVR_FILTER_MITCHELL_NETRAVALI 3
+#define CVR_FILTER_CARDINAL_BSPLINE_3 4
+#define CVR_FILTER_CARDINAL_OMOMS3    5
+
+/* Render resolution of a mode at screen size (w, h): 2w x 2h for modes 1-2,
+ * w/2 x h/2 for mode 3 (UpdateScreenResolutionMultiScaling with the 2 x 2
+ * multiplier of cppvolrend/defines.h:16-17). */
+cvr_status  cvr_multiscale_resolution(int mode, int screen_w, int screen_h, int* render_w,
+                                      int* render_h);
+
+/* Filter a rendered RGBA16F frame (fw x fh, device) to the RGBA16F screen
+ * image (sw x sh, device): mode 1 = multisample_filter (bilinear), 2 = kernel
+ * downscale (+ the digital filter over the result for the cardinal kernels),
+ * 3 = kernel upscale (the cardinal kernels' digital prefilter runs IN PLACE on
+ * d_frame first, as the reference does).  Asynchronous on the context stream. */
+cvr_status  cvr_multiscale_filter(cvr_ctx* ctx, int mode, int kernel, void* d_frame, int fw,
+                                  int fh, void* d_screen, int sw, int sh);
+
+/* Screenshot: the frame (device, CVR_FORMAT_*) blended over the white clear
+ * colour with SRC_ALPHA / ONE_MINUS_SRC_ALPHA and stored as RGB8, row 0 =
+ * bottom as glReadPixels returns it (w*h*3 bytes, device).  Asynchronous. */
+cvr_status  cvr_screenshot_rgb8(cvr_ctx* ctx, const void* d_frame, int format, int w, int h,
+                                void* d_rgb);
+
+/* ----------------------------------------------------------------------------
  * Multi-GPU: the screen-tile split's gather, native RCCL over xGMI
  * (the reference renders on one GPU, so this has no reference
  * counterpart beyond the Redraw it feeds, rc1prenderer.cpp:140-151).

@@ -1225,3 +1225,198 @@ ORACLE_API uint64_t oracle_render_ebs_rows(const OracleEbs* Q, int y0, int y1, f
   };
   return shaded_march_rows(P, y0, y1, out_rgba, out_counts, nthreads, shade);
 }
+
+// ===========================================================================
+// Post-pass: pixel multiscaling filters and the screenshot composite
+//   RenderFrameToScreen::DrawMultiSampleHigherResolutionMode / ...WithDownScale /
+//   ...WithUpScale ........... libs/vis_utils/renderoutputframe.cpp:265-539
+//   multisample_filter.comp, downscaling_filter.comp, upscaling_filter.comp,
+//   box/hat/catmullrom/mitchellnetravali/cardinalbspline/cardinalomoms_filter.comp,
+//   cbs/comoms_digital_filter.comp .. libs/vis_utils/shader/renderoutputframe/
+//   blend over white + glReadPixels .. cppvolrend/renderingmanager.cpp:103-112, 476-492
+// Images are RGBA16F (uint16 x 4 per pixel, row 0 = bottom); every imageStore
+// rounds to binary16; texelFetch outside the image reads 0; texture() is
+// bilinear with clamp-to-edge (CVR-SPEC lerp).
+// ===========================================================================
+namespace post {
+
+struct Px { float c[4]; };
+
+inline Px load(const uint16_t* img, int w, int x, int y) {
+  Px p;
+  for (int k = 0; k < 4; k++) p.c[k] = half_to_float(img[((size_t)y * w + x) * 4 + k]);
+  return p;
+}
+inline void store(uint16_t* img, int w, int x, int y, const Px& p) {
+  for (int k = 0; k < 4; k++) img[((size_t)y * w + x) * 4 + k] = float_to_half(p.c[k]);
+}
+inline Px fetch(const uint16_t* img, int w, int h, int x, int y) {
+  if (x < 0 || y < 0 || x >= w || y >= h) return Px{{0.f, 0.f, 0.f, 0.f}};
+  return load(img, w, x, y);
+}
+
+// kernel_support / kernel_weight of <name>_filter.comp
+float support(int k) { return k == 0 ? 1.0f : (k == 1 ? 2.0f : 4.0f); }
+float cubic(int k, float x) {
+  x = std::fabs(x);
+  if (x > 2.0f) return 0.0f;
+  const bool far = x > 1.0f;
+  const float u = far ? 2.0f - x : 1.0f - x;
+  switch (k) {
+    case 2: return far ? ((0.5f * u - 0.5f) * u) * u : ((-1.5f * u + 2.0f) * u + 0.5f) * u;
+    case 3: return far ? (((7 / 18.0f) * u - 1 / 3.0f) * u) * u
+                       : (((-7 / 6.0f) * u + 1.5f) * u + 0.5f) * u + 1 / 18.0f;
+    case 4: return far ? ((u)*u) * u : ((-3.0f * u + 3.0f) * u + 3.0f) * u + 1.0f;
+    default: return far ? ((0.875f * u) * u + 0.125f) * u
+                        : ((-2.625f * u + 2.625f) * u + 2.25f) * u + 1.0f;
+  }
+}
+float weight(int k, float x) {
+  if (k == 0) return x <= -0.5f || x > 0.5f ? 0.0f : 1.0f;
+  if (k == 1) { x = std::fabs(x); return x > 1.0f ? 0.0f : 1.0f - x; }
+  return cubic(k, x);
+}
+
+void multisample(const uint16_t* src, int sw, int sh, uint16_t* dst, int tw, int th) {
+  for (int y = 0; y < th; y++)
+    for (int x = 0; x < tw; x++) {
+      const float u = ((float)x + 0.5f) / (float)tw, v = ((float)y + 0.5f) / (float)th;
+      const float fx = u * (float)sw - 0.5f, fy = v * (float)sh - 0.5f;
+      const float flx = std::floor(fx), fly = std::floor(fy);
+      const float ax = fx - flx, ay = fy - fly;
+      auto cl = [](int i, int n) { return i < 0 ? 0 : (i > n - 1 ? n - 1 : i); };
+      const int x0 = cl((int)flx, sw), x1 = cl((int)flx + 1, sw);
+      const int y0 = cl((int)fly, sh), y1 = cl((int)fly + 1, sh);
+      const Px a = load(src, sw, x0, y0), b = load(src, sw, x1, y0);
+      const Px c = load(src, sw, x0, y1), d = load(src, sw, x1, y1);
+      Px r;
+      for (int k = 0; k < 4; k++) {
+        const float top = std::fma(ax, b.c[k] - a.c[k], a.c[k]);
+        const float bot = std::fma(ax, d.c[k] - c.c[k], c.c[k]);
+        r.c[k] = std::fma(ay, bot - top, top);
+      }
+      store(dst, tw, x, y, r);
+    }
+}
+
+void downscale(int K, const uint16_t* src, int sw, int sh, uint16_t* dst, int tw, int th) {
+  const float s_r = (float)th / (float)sh, s_c = (float)tw / (float)sw;
+  const float kr = 0.5f * support(K);
+  for (int jr = 0; jr < th; jr++)
+    for (int jc = 0; jc < tw; jc++) {
+      const float x_r = ((float)jr + 0.5f) / (float)th;
+      const int il_r = (int)std::ceil((x_r - kr / (float)th) * (float)sh - 0.5f);
+      const int ir_r = (int)std::floor((x_r + kr / (float)th) * (float)sh - 0.5f);
+      const float x_c = ((float)jc + 0.5f) / (float)tw;
+      const int il_c = (int)std::ceil((x_c - kr / (float)tw) * (float)sw - 0.5f);
+      const int ir_c = (int)std::floor((x_c + kr / (float)tw) * (float)sw - 0.5f);
+      Px f{{0.f, 0.f, 0.f, 0.f}};
+      for (int ir = il_r; ir <= ir_r; ir++)
+        for (int ic = il_c; ic <= ir_c; ic++) {
+          const float wgt = weight(K, (x_r - ((float)ir + 0.5f) / (float)sh) * (float)th) *
+                            weight(K, (x_c - ((float)ic + 0.5f) / (float)sw) * (float)tw);
+          const Px t = fetch(src, sw, sh, ic, ir);
+          for (int k = 0; k < 4; k++) f.c[k] = f.c[k] + wgt * t.c[k];
+        }
+      const float s = s_r * s_c;
+      for (int k = 0; k < 4; k++) f.c[k] = f.c[k] * s;
+      store(dst, tw, jc, jr, f);
+    }
+}
+
+void upscale(int K, const uint16_t* src, int sw, int sh, uint16_t* dst, int tw, int th) {
+  const float kr = 0.5f * support(K);
+  for (int jr = 0; jr < th; jr++)
+    for (int jc = 0; jc < tw; jc++) {
+      const float x_r = ((float)jr + 0.5f) / (float)th;
+      const float xi_r = x_r * (float)sh - 0.5f;
+      const int il_r = (int)std::ceil(xi_r - kr), ir_r = (int)std::floor(xi_r + kr);
+      const float x_c = ((float)jc + 0.5f) / (float)tw;
+      const float xi_c = x_c * (float)sw - 0.5f;
+      const int il_c = (int)std::ceil(xi_c - kr), ir_c = (int)std::floor(xi_c + kr);
+      Px f{{0.f, 0.f, 0.f, 0.f}};
+      for (int ir = il_r; ir <= ir_r; ir++)
+        for (int ic = il_c; ic <= ir_c; ic++) {
+          const float wgt = weight(K, xi_r - (float)ir) * weight(K, xi_c - (float)ic);
+          const Px t = fetch(src, sw, sh, ic, ir);
+          for (int k = 0; k < 4; k++) f.c[k] = f.c[k] + wgt * t.c[k];
+        }
+      store(dst, tw, jc, jr, f);
+    }
+}
+
+// cbs/comoms_digital_filter.comp: direction 0 (rows), then direction 1 (columns),
+// in place; imageLoad re-reads the rounded stores.
+void digital(int K, uint16_t* img, int w, int h) {
+  static const float Lc[8] = {.2f, .26315789f, .26760563f, .26792453f,
+                              .26794742f, .26794907f, .26794918f, .26794919f};
+  static const float Lo[9] = {.23529412f, .33170732f, .34266611f, .34395774f, .34411062f,
+                              .34412872f, .34413087f, .34413112f, .34413115f};
+  const float* L = K == 4 ? Lc : Lo;
+  const int m = K == 4 ? 8 : 9;
+  const float p_inv = 1.0f;
+  const float L_inf = L[m - 1], v_inv = L_inf / (1.f + L_inf);
+  for (int dir = 0; dir < 2; dir++) {
+    const int lines = dir == 0 ? h : w, nn = dir == 0 ? w : h;
+    for (int t = 0; t < lines; t++) {
+      auto X = [&](int i) { return dir == 0 ? i : t; };
+      auto Y = [&](int i) { return dir == 0 ? t : i; };
+      auto ld = [&](int i) { return load(img, w, X(i), Y(i)); };
+      auto st = [&](int i, const Px& p) { store(img, w, X(i), Y(i), p); };
+      for (int i = 1; i < nn; i++) {
+        const float l = i < m ? L[i - 1] : L_inf;
+        const Px c = ld(i), p = ld(i - 1);
+        Px r;
+        for (int k = 0; k < 4; k++) r.c[k] = c.c[k] - l * p.c[k];
+        st(i, r);
+      }
+      {
+        Px c = ld(nn - 1);
+        for (int k = 0; k < 4; k++) c.c[k] = c.c[k] * p_inv * v_inv;
+        st(nn - 1, c);
+      }
+      for (int i = nn - 2; i >= 0; i--) {
+        const float l = i >= m - 1 ? L_inf : L[i];
+        const Px c = ld(i), n1 = ld(i + 1);
+        Px r;
+        for (int k = 0; k < 4; k++) r.c[k] = l * (p_inv * c.c[k] - n1.c[k]);
+        st(i, r);
+      }
+    }
+  }
+}
+
+}  // namespace post
+
+// mode 1 multisample, 2 downscale, 3 upscale; kernel = vis::IMAGE_FILTER_KERNEL.
+// `frame` is modified in place by mode 3 with a cardinal kernel (as the reference).
+ORACLE_API int oracle_multiscale_filter(int mode, int kernel, uint16_t* frame, int fw, int fh,
+                                        uint16_t* screen, int sw, int sh) {
+  const bool cardinal = kernel == 4 || kernel == 5;
+  if (mode == 1) {
+    post::multisample(frame, fw, fh, screen, sw, sh);
+  } else if (mode == 2) {
+    post::downscale(kernel, frame, fw, fh, screen, sw, sh);
+    if (cardinal) post::digital(kernel, screen, sw, sh);
+  } else if (mode == 3) {
+    if (cardinal) post::digital(kernel, frame, fw, fh);
+    post::upscale(kernel, frame, fw, fh, screen, sw, sh);
+  } else {
+    return 1;
+  }
+  return 0;
+}
+
+// RGBA (float, or binary16 when `half`) over white -> RGB8 (glReadPixels order)
+ORACLE_API void oracle_screenshot_rgb8(const void* frame, int half, int w, int h, uint8_t* rgb) {
+  for (size_t i = 0; i < (size_t)w * h; i++) {
+    float p[4];
+    for (int k = 0; k < 4; k++)
+      p[k] = half ? half_to_float(((const uint16_t*)frame)[i * 4 + k]) : ((const float*)frame)[i * 4 + k];
+    for (int k = 0; k < 3; k++) {
+      const float v = p[k] * p[3] + (1.0f - p[3]);
+      const float q = std::floor(v * 255.0f + 0.5f);
+      rgb[i * 3 + k] = (uint8_t)(q < 0.0f ? 0.0f : (q > 255.0f ? 255.0f : q));
+    }
+  }
+}

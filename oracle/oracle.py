@@ -99,6 +99,10 @@ def lib():
         L.oracle_sat_build.restype = None
         L.oracle_render_ebs_rows.argtypes = [ctypes.POINTER(OracleEbs), I, I, P, P, I]
         L.oracle_render_ebs_rows.restype = ctypes.c_uint64
+        L.oracle_multiscale_filter.argtypes = [I, I, P, I, I, P, I, I]
+        L.oracle_multiscale_filter.restype = I
+        L.oracle_screenshot_rgb8.argtypes = [P, I, I, I, P]
+        L.oracle_screenshot_rgb8.restype = None
         _lib = L
     return _lib
 
@@ -205,7 +209,7 @@ def render_rc1pass(vol16: np.ndarray, scale, tf: np.ndarray, camera: dict, W: in
     if grad is not None:
         grad = np.ascontiguousarray(grad, np.float32)
     P = _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shininess, ispec,
-                light)
+                light, aspect=camera.get("aspect", 0.0))
     rgba = np.zeros((H, W, 4), np.float32)
     cnt = np.zeros((H, W), np.uint32)
     if rows is None:
@@ -368,3 +372,26 @@ def render_ebs(vol16, scale, tf_rgbt, sat_f32, camera, W, H, step, apply_occlusi
     y0, y1 = rows if rows is not None else (0, H)
     S = lib().oracle_render_ebs_rows(ctypes.byref(Q), int(y0), int(y1), _p(rgba), _p(cnt), int(threads))
     return rgba, cnt, int(S)
+
+
+def multiscale_filter(mode: int, kernel: int, frame_f16: np.ndarray, screen_w: int,
+                      screen_h: int) -> np.ndarray:
+    """RenderFrameToScreen's multiscaling post-pass on an RGBA16F frame (h, w, 4) float16.
+    Returns the (screen_h, screen_w, 4) float16 screen image.  Mode 3 with a cardinal
+    kernel prefilters `frame_f16` in place, as the reference does."""
+    assert frame_f16.dtype == np.float16 and frame_f16.flags.c_contiguous
+    fh, fw = frame_f16.shape[:2]
+    out = np.zeros((screen_h, screen_w, 4), np.float16)
+    st = lib().oracle_multiscale_filter(mode, kernel, _p(frame_f16), fw, fh, _p(out), screen_w,
+                                        screen_h)
+    assert st == 0
+    return out
+
+
+def screenshot_rgb8(frame: np.ndarray) -> np.ndarray:
+    """The frame blended over white (SRC_ALPHA, ONE_MINUS_SRC_ALPHA) as RGB8."""
+    frame = np.ascontiguousarray(frame)
+    h, w = frame.shape[:2]
+    out = np.zeros((h, w, 3), np.uint8)
+    lib().oracle_screenshot_rgb8(_p(frame), int(frame.dtype == np.float16), w, h, _p(out))
+    return out

@@ -1,0 +1,119 @@
+"""GPU parity of the multiscaling post-pass and the screenshot (postpass.hip via
+the C-ABI) against the oracle restatement, bit for bit: every mode x every
+kernel on random RGBA16F images and on a rendered frame, and the renderer-level
+path (RayCasting1Pass in each multiscaling mode: the frame rendered at the
+mode's resolution, filtered to the screen) against oracle frame + oracle filter."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from cpp_volume_rendering_amd import _native as N
+from cpp_volume_rendering_amd import datasets as D
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = list(range(6))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+    from cpp_volume_rendering_amd.renderer import Device
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    d = Device(0)
+    yield d
+    d.close()
+
+
+def gpu_filter(dev, mode, k, frame, sw, sh):
+    import torch
+    f = torch.from_numpy(frame.copy()).cuda()
+    out = torch.zeros((sh, sw, 4), dtype=torch.float16, device="cuda")
+    dev.set_stream(torch.cuda.current_stream().cuda_stream)
+    N.check(N.lib().cvr_multiscale_filter(dev.handle, mode, k, f.data_ptr(), frame.shape[1],
+                                          frame.shape[0], out.data_ptr(), sw, sh),
+            "cvr_multiscale_filter", dev.handle)
+    torch.cuda.synchronize()
+    dev.set_stream(None)
+    return out.cpu().numpy(), f.cpu().numpy()
+
+
+def _eq16(a, b):
+    return np.array_equal(a.view(np.uint16), b.view(np.uint16))
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("k", KERNELS)
+def test_filters_match_oracle_random(dev, oracle, mode, k):
+    rng = np.random.default_rng(10 * mode + k)
+    sw, sh = 72, 56
+    fw, fh = (sw * 2, sh * 2) if mode < 3 else (sw // 2, sh // 2)
+    frame = (rng.random((fh, fw, 4)) * 1.5 - 0.25).astype(np.float16)
+    got, gframe = gpu_filter(dev, mode, k, frame, sw, sh)
+    oframe = frame.copy()
+    want = oracle.multiscale_filter(mode, k, oframe, sw, sh)
+    assert _eq16(got, want)
+    assert _eq16(gframe, oframe)      # the in-place prefilter (mode 3, cardinal) as well
+
+
+def test_bad_filter_arguments(dev):
+    import torch
+    f = torch.zeros((8, 8, 4), dtype=torch.float16, device="cuda")
+    o = torch.zeros((16, 16, 4), dtype=torch.float16, device="cuda")
+    L = N.lib()
+    assert L.cvr_multiscale_filter(dev.handle, 4, 0, f.data_ptr(), 8, 8, o.data_ptr(), 16, 16) != 0
+    assert L.cvr_multiscale_filter(dev.handle, 3, 9, f.data_ptr(), 8, 8, o.data_ptr(), 16, 16) != 0
+    # cardinal prefilter on lines shorter than its LU factors
+    assert L.cvr_multiscale_filter(dev.handle, 3, 4, f.data_ptr(), 8, 8, o.data_ptr(), 16, 16) != 0
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("k", [N.FILTER_HAT, N.FILTER_CATMULL_ROM, N.FILTER_CARDINAL_OMOMS3])
+def test_renderer_multiscaling_matches_oracle(oracle, bonsai_tf, mode, k):
+    """RayCasting1Pass in a multiscaling mode == oracle frame (at the render
+    resolution, RGBA16F) through the oracle post-pass; its Screenshot == oracle's."""
+    import torch
+    from cpp_volume_rendering_amd.renderer import (Camera, DataManager, RayCasting1Pass,
+                                                   RenderingParameters)
+    n, W, H = 64, 96, 80
+    vol = D.marschner_lobb_u8(n)
+    dm = DataManager()
+    dm.SetVolume(vol, D.voxel_scale(n))
+    dm.SetTransferFunction(bonsai_tf)
+    r = RayCasting1Pass(0)
+    r.SetExternalResources(dm, RenderingParameters(W, H))
+    r.SetCurrentMultiScalingMode(mode)
+    r.SetImageKernelFilter(k)
+    assert r.Init(W, H)
+    cam = Camera(**D.INITIAL_STATE_CAMERA)
+    r.PrepareRender(cam)
+    r.Redraw()
+    torch.cuda.synchronize()
+    rw, rh = (2 * W, 2 * H) if mode < 3 else (W // 2, H // 2)
+    assert (r.width, r.height) == (rw, rh)
+    frame = r.rgba.cpu().numpy()
+    cam_o = dict(D.INITIAL_STATE_CAMERA, aspect=W / H)
+    ref, _, _ = oracle.render_rc1pass(oracle.volume_r16f(vol), D.voxel_scale(n), bonsai_tf, cam_o,
+                                      rw, rh, oracle.default_step(D.voxel_scale(n)))
+    ref16 = ref.astype(np.float16)
+    want = oracle.multiscale_filter(mode, k, ref16.copy(), W, H)
+    assert _eq16(r.screen.cpu().numpy(), want)
+    if mode != 3 or k < 4:
+        assert _eq16(frame, ref16)
+    assert np.array_equal(r.Screenshot(), oracle.screenshot_rgb8(want))
+    r.Clean()
+
+
+def test_screenshot_rgba32f(dev, oracle):
+    import torch
+    rng = np.random.default_rng(5)
+    f = rng.random((33, 47, 4)).astype(np.float32)
+    d = torch.from_numpy(f).cuda()
+    rgb = torch.zeros((33, 47, 3), dtype=torch.uint8, device="cuda")
+    dev.set_stream(torch.cuda.current_stream().cuda_stream)
+    N.check(N.lib().cvr_screenshot_rgb8(dev.handle, d.data_ptr(), N.FORMAT_RGBA32F, 47, 33,
+                                        rgb.data_ptr()), "screenshot", dev.handle)
+    torch.cuda.synchronize()
+    dev.set_stream(None)
+    assert np.array_equal(rgb.cpu().numpy(), oracle.screenshot_rgb8(f))
