@@ -76,6 +76,8 @@ def parse():
                         "(default: 10 at >= 8 GPUs, else 0)")
     p.add_argument("--transport", choices=["rccl", "torch"], default="rccl",
                    help="N > 1 gather: the library's RCCL communicator or dist.gather")
+    p.add_argument("--postpass", action="store_true",
+                   help="also time the multiscaling post-pass filters on this workload's frame")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_rc1pass.json"))
     return p.parse_args()
 
@@ -206,6 +208,46 @@ def load_traffic(path, workload_key):
         return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+def postpass_bench(r, dev, W, H, reps):
+    """The step after the march: RenderFrameToScreen's multiscaling
+    filters, timed with HIP events on the context stream.  Modes 1-2 filter a (2W, 2H)
+    RGBA16F frame of this workload to the W x H screen, mode 3 a (W/2, H/2) one; the
+    frames are rendered here by the same renderer.  Algorithmic bytes: 8 B per frame pixel
+    read + 8 B per screen pixel written (+ 2 x 16 B per pixel of the image the cardinal
+    kernels' digital filter sweeps in place, twice)."""
+    L = N.lib()
+    cur = torch.cuda.current_stream(dev)
+    r.device.set_stream(cur.cuda_stream)
+    cam = Camera(**D.INITIAL_STATE_CAMERA, aspect=W / H)
+    out = []
+    screen = torch.zeros((H, W, 4), dtype=torch.float16, device=dev)
+    for mode, kern in [(1, 1), (2, 1), (2, 2), (2, 4), (3, 1), (3, 2), (3, 5)]:
+        fw, fh = (2 * W, 2 * H) if mode < 3 else (W // 2, H // 2)
+        frame = torch.zeros((fh, fw, 4), dtype=torch.float16, device=dev)
+        r.render_to(make_frame(cam, fw, fh), N.Output(frame.data_ptr(), None, None, 1,
+                                                      N.FORMAT_RGBA16F))
+        work = frame.clone()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for i in range(reps + 2):
+            if i == 2:
+                ev[0].record(cur)
+            if mode == 3 and kern >= 4:      # the prefilter runs in place: restore the frame
+                work.copy_(frame)
+            N.check(L.cvr_multiscale_filter(r.device.handle, mode, kern, work.data_ptr(), fw, fh,
+                                            screen.data_ptr(), W, H), "filter", r.device.handle)
+        ev[1].record(cur)
+        torch.cuda.synchronize(dev)
+        ms = ev[0].elapsed_time(ev[1]) / reps
+        swept = (W * H if mode == 2 else fw * fh) if kern >= 4 else 0
+        b = 8 * fw * fh + 8 * W * H + 2 * 16 * swept
+        out.append({"mode": mode, "kernel": kern, "frame": [fw, fh], "ms": round(ms, 4),
+                    "bytes_alg": b, "GB_s": round(b / (ms * 1e-3) / 1e9, 1)})
+    return {"screen": [W, H], "filters": out,
+            "what": "cvr_multiscale_filter (postpass.hip); mode 1 multisample, 2 downscale, "
+                    "3 upscale; kernel 1 hat, 2 Catmull-Rom, 4 cardinal B-spline, 5 o-MOMS; "
+                    "mode 3 with a cardinal kernel includes restoring the frame (in-place prefilter)"}
 
 
 def main():
@@ -456,6 +498,8 @@ def main():
                                  "sat_Mcells_s": round(cells / (sat_ms * 1e-3) / 1e6, 1),
                                  "what": "GenerateExtinctionSAT3DTex + BuildSAT on the GPU "
                                          "(double, reference recurrence, bit-exact), wall time"}
+        if a.postpass and world == 1:
+            res["postpass"] = postpass_bench(r, dev, W, H, a.steps)
         if world == 1 and not a.no_cpu_baseline:
             dos_cfg = None
             if dos:
