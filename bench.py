@@ -494,10 +494,15 @@ def main():
             res["multi_gpu_bit_exact_vs_1gpu_frame"] = split_exact
         if ebs:
             cells = (n + 2) ** 3
+            sat_gpu_ms = N.lib().cvr_get_option(r.device.handle, b"sat_build_us") / 1e3
             res["precompute"] = {"sat_ms": round(sat_ms, 2), "sat_cells": cells,
-                                 "sat_Mcells_s": round(cells / (sat_ms * 1e-3) / 1e6, 1),
+                                 "sat_gpu_ms": round(sat_gpu_ms, 2),
+                                 "sat_Mcells_s": round(cells / (sat_gpu_ms * 1e-3) / 1e6, 1),
                                  "what": "GenerateExtinctionSAT3DTex + BuildSAT on the GPU "
-                                         "(double, reference recurrence, bit-exact), wall time"}
+                                         "(double, reference recurrence, bit-exact): sat_ms = wall "
+                                         "time of cvr_set_extinction_sat incl. freeing and "
+                                         "allocating the SAT buffers, sat_gpu_ms = HIP-event time "
+                                         "of the build + cell8 expansion kernels"}
         if a.postpass and world == 1:
             res["postpass"] = postpass_bench(r, dev, W, H, a.steps)
         if world == 1 and not a.no_cpu_baseline:

@@ -252,6 +252,7 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_ext_levels; free_dev(p); c->d_ext_levels = nullptr;
   p = c->d_sat; free_dev(p); c->d_sat = nullptr;
   p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr;
+  p = c->d_sat_scratch; free_dev(p); c->d_sat_scratch = nullptr;
   p = c->d_shade; free_dev(p); c->d_shade = nullptr;
   p = c->d_cones; free_dev(p); c->d_cones = nullptr;
   delete[] c->cone_tab;
@@ -406,6 +407,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "debug_epi_stop")) return c->epi_stop;
   if (!std::strcmp(key, "async_order")) return c->async_order;
   if (!std::strcmp(key, "split_streams")) return c->split_streams;
+  if (!std::strcmp(key, "sat_build_us")) return c->sat_build_us;   // read-only
   if (!std::strcmp(key, "order_interval")) return c->order_interval;
   if (!std::strcmp(key, "skip_min_pct")) return c->skip_min_pct;
   if (!std::strcmp(key, "occ_empty_permille"))   // read-only: empty macro cells (after a render)
@@ -469,6 +471,8 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
   { void* p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr; }
   { void* p = c->d_sat; free_dev(p); c->d_sat = nullptr; }
   { void* p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr; }
+  { void* p = c->d_sat_scratch; free_dev(p); c->d_sat_scratch = nullptr; }
+  c->sat_dims[0] = c->sat_dims[1] = c->sat_dims[2] = 0;
   c->cone_valid = 0;
   HIP_TRY(c, hipMalloc((void**)&c->d_lut, nv * sizeof(uint16_t)));
   uint16_t* d_lut = c->d_lut;
@@ -1231,24 +1235,51 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
     return fail(c, CVR_ERR_ARG, "cvr_set_extinction_sat: volume too large for the SAT");
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  { void* p = c->d_sat; free_dev(p); c->d_sat = nullptr; }
-  { void* p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr; }
+  // Same grid as the last build (a TF change): rebuild into the existing buffers.
+  // Freeing and re-allocating the ~50 GB of a 1024^3 SAT costs seconds.
+  const bool reuse = c->d_sat && c->d_sat_cells && c->d_sat_scratch &&
+                     c->sat_dims[0] == w && c->sat_dims[1] == h && c->sat_dims[2] == d;
+  if (!reuse) {
+    void* p = c->d_sat; free_dev(p); c->d_sat = nullptr;
+    p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr;
+    p = c->d_sat_scratch; free_dev(p); c->d_sat_scratch = nullptr;
+    c->sat_dims[0] = c->sat_dims[1] = c->sat_dims[2] = 0;
+  }
   float* d_lut = nullptr;
-  double* d_sd = nullptr;
   hipError_t e = hipMalloc((void**)&d_lut, (size_t)nv * sizeof(float));
   if (e == hipSuccess) e = hipMemcpy(d_lut, ext_lut, (size_t)nv * sizeof(float), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc((void**)&d_sd, cells * sizeof(double));
-  if (e == hipSuccess) e = hipMalloc((void**)&c->d_sat, cells * sizeof(float));
+  // the double recurrence's grid stays allocated with the SAT (for rebuilds)
+  if (e == hipSuccess && !reuse) e = hipMalloc(&c->d_sat_scratch, cells * sizeof(double));
+  double* d_sd = (double*)c->d_sat_scratch;
+  if (e == hipSuccess && !reuse) e = hipMalloc((void**)&c->d_sat, cells * sizeof(float));
+  // GPU time of the two compute phases (option "sat_build_us"): the wall time of
+  // this call also holds the allocations of ~50 GB at 1024^3
+  hipEvent_t ev[4] = {};
+  for (hipEvent_t& x : ev)
+    if (e == hipSuccess) e = hipEventCreate(&x);
+  if (e == hipSuccess) e = hipEventRecord(ev[0], c->stream);
   if (e == hipSuccess) e = cvr::launch_sat_build(*c, d_lut, d_sd, c->d_sat, c->stream);
+  if (e == hipSuccess) e = hipEventRecord(ev[1], c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   (void)hipFree(d_lut);
-  (void)hipFree(d_sd);
-  if (e == hipSuccess) e = hipMalloc((void**)&c->d_sat_cells, cells * 2 * sizeof(float4));
+  if (e == hipSuccess && !reuse) e = hipMalloc((void**)&c->d_sat_cells, cells * 2 * sizeof(float4));
+  if (e == hipSuccess) e = hipEventRecord(ev[2], c->stream);
   if (e == hipSuccess) e = cvr::launch_sat_cells(*c, c->d_sat, c->d_sat_cells, c->stream);
+  if (e == hipSuccess) e = hipEventRecord(ev[3], c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) {
+    float a = 0.f, b = 0.f;
+    if (hipEventElapsedTime(&a, ev[0], ev[1]) == hipSuccess &&
+        hipEventElapsedTime(&b, ev[2], ev[3]) == hipSuccess)
+      c->sat_build_us = (int)((a + b) * 1000.0f);
+  }
+  for (hipEvent_t x : ev)
+    if (x) (void)hipEventDestroy(x);
   if (e != hipSuccess) {
     void* p = c->d_sat; free_dev(p); c->d_sat = nullptr;
     p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr;
+    p = c->d_sat_scratch; free_dev(p); c->d_sat_scratch = nullptr;
+    c->sat_dims[0] = c->sat_dims[1] = c->sat_dims[2] = 0;
     return fail(c, e == hipErrorOutOfMemory ? CVR_ERR_OOM : CVR_ERR_HIP,
                 "cvr_set_extinction_sat: %s", hipGetErrorString(e));
   }

@@ -202,8 +202,10 @@ struct Ctx {
   ExtLevel* d_ext_levels = nullptr;  // [kMaxExtLevels] addressing of the levels
   // extinction-based shading: the float SAT of (N+2) cells per axis
   int sat_chunk = 32;                // z planes per SAT work item (option "sat_chunk")
+  int sat_build_us = 0;              // GPU time of the last SAT build (option "sat_build_us")
   float* d_sat = nullptr;
   float4* d_sat_cells = nullptr;   // the same SAT as cell8 (8 float corners per texel)
+  void* d_sat_scratch = nullptr;   // the double grid of the build (kept for rebuilds)
   int sat_dims[3] = {0, 0, 0};
   int ext_res[3] = {0, 0, 0};
   int ext_levels = 0;

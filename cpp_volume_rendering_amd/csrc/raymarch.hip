@@ -317,11 +317,15 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
 // (four lanes per ray).  Without an order, block b -> tile in XCD bands
 // (blocks b and b+8 share an XCD, so XCD b%8 gets one contiguous band).
 // Waves of the `boost` longest tiles of each band raise their priority.
-#ifndef CVR_RC1_WAVES_PER_EU
-#define CVR_RC1_WAVES_PER_EU 7
+// (CVR_RC1_WAVES_PER_EU: residency experiments only, tools/build_variant.sh; the
+// default leaves register allocation to the compiler per variant)
+#ifdef CVR_RC1_WAVES_PER_EU
+#define CVR_RC1_OCC __attribute__((amdgpu_waves_per_eu(CVR_RC1_WAVES_PER_EU)))
+#else
+#define CVR_RC1_OCC
 #endif
 template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CVR_RC1_WAVES_PER_EU)))
+__global__ void __launch_bounds__(64) CVR_RC1_OCC
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
                     float4* __restrict__ out, uint32_t* __restrict__ samples,
