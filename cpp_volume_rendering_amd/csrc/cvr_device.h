@@ -14,6 +14,16 @@ typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float lerpf(float a, float b, float t) { return fmaf(t, b - a, a); }
 
+// float -> binary16 bits, round to nearest even, as an opaque instruction: a
+// plain (_Float16) cast lets the backend fold a preceding multiply or fma into
+// v_fma_mixlo_f16 (one rounding straight to f16 instead of f32 then f16, which
+// differs in the last f16 bit now and then, -ffp-contract=off notwithstanding).
+__device__ __forceinline__ uint32_t f32_to_h16(float f) {
+  uint32_t r;
+  asm volatile("v_cvt_f16_f32 %0, %1" : "=v"(r) : "v"(f));
+  return r & 0xffffu;
+}
+
 __device__ __forceinline__ void h2f2(uint32_t w, float& lo, float& hi) {
   half2_t p = __builtin_bit_cast(half2_t, w);
   lo = (float)p.x;

@@ -29,7 +29,7 @@ namespace cvr {
 __device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 
 // float -> binary16, round to nearest even (v_cvt_f16_f32)
-__device__ __forceinline__ uint16_t f2h_rne(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+__device__ __forceinline__ uint16_t f2h_rne(float f) { return (uint16_t)f32_to_h16(f); }
 
 // x, y, z in texel space of a d[0] x d[1] x d[2] level.  Clamping to [0, d-1]
 // gives the same values as GL's CLAMP_TO_EDGE on [-1, d-1] (see sample_pos).

@@ -14,10 +14,8 @@ namespace cvr {
 // the reference's RGBA16F frame) packed in one uint2.
 __device__ __forceinline__ void store_rgba(float4* out, long long i, float4 v, int half) {
   if (half) {
-    const uint32_t x = __builtin_bit_cast(uint16_t, (_Float16)v.x);
-    const uint32_t y = __builtin_bit_cast(uint16_t, (_Float16)v.y);
-    const uint32_t z = __builtin_bit_cast(uint16_t, (_Float16)v.z);
-    const uint32_t w = __builtin_bit_cast(uint16_t, (_Float16)v.w);
+    const uint32_t x = f32_to_h16(v.x), y = f32_to_h16(v.y);
+    const uint32_t z = f32_to_h16(v.z), w = f32_to_h16(v.w);
     reinterpret_cast<uint2*>(out)[i] = make_uint2(x | (y << 16), z | (w << 16));
   } else {
     out[i] = v;

@@ -25,13 +25,14 @@
 
 #include <cstdint>
 
+#include "cvr_device.h"
 #include "cvr_internal.h"
 
 namespace cvr {
 namespace {
 
 __device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
-__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+__device__ __forceinline__ uint16_t f2h(float f) { return (uint16_t)f32_to_h16(f); }
 
 __device__ __forceinline__ float4 load_px(const uint2* img, int w, int x, int y) {
   const uint2 p = img[(size_t)y * w + x];
@@ -195,47 +196,88 @@ struct LOmoms {
   }
 };
 
+// One lane per (line, channel): the channels of a pixel are independent in the
+// recursion, so a line's four channels run on four adjacent lanes.  The value a
+// step stores is kept in a register as the binary16 round trip (what imageLoad
+// would read back).  The recursion is sequential along a line, so the line is
+// streamed through registers in batches of kDigitalBatch, software-pipelined:
+// the next batch's loads are issued before the current batch's updates and
+// stores (the forward pass reads values no earlier step has written; the
+// reverse pass reads values this lane stored in the forward pass).
+constexpr int kDigitalBatch = 32;
+
+__device__ __forceinline__ float h16(float f) { return h2f(f2h(f)); }
+
 template <class LU>
-__global__ void digital_filter_kernel(uint2* __restrict__ img, int w, int h, int dir) {
+__global__ void digital_filter_kernel(uint16_t* __restrict__ img, int w, int h, int dir) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int lines = dir == 0 ? h : w;
-  if (t >= lines) return;
+  if (t >= lines * 4) return;
+  const int line = t >> 2, ch = t & 3;
   const int nn = dir == 0 ? w : h;
-  auto at = [&](int i, int& x, int& y) {
-    if (dir == 0) { x = i; y = t; } else { x = t; y = i; }
-  };
+  // element i of this lane's line/channel
+  const size_t base = dir == 0 ? (size_t)line * w * 4 + ch : (size_t)line * 4 + ch;
+  const size_t stride = dir == 0 ? 4 : (size_t)w * 4;
+  uint16_t* p = img + base;
   const int m = LU::m;
   const float p_inv = 1.0f;
   const float L_inf = LU::L(m - 1), v_inv = L_inf / (1.f + L_inf);
-  int x, y;
-  // forward pass: f[i] -= L * f[i-1]
-  at(0, x, y);
-  float4 prev = load_px(img, w, x, y);
-  for (int i = 1; i < nn; i++) {
-    at(i, x, y);
-    const float l = i < m ? LU::L(i - 1) : L_inf;
-    const float4 c = load_px(img, w, x, y);
-    float4 r = make_float4(c.x - l * prev.x, c.y - l * prev.y, c.z - l * prev.z, c.w - l * prev.w);
-    store_px(img, w, x, y, r);
-    prev = load_px(img, w, x, y);     // the stored (rounded) value
+  constexpr int B = kDigitalBatch;
+  float cur[B], nxt[B];
+  // forward pass: f[i] -= L * f[i-1], i = 1 .. nn-1
+  float prev = h2f(p[0]);
+#pragma unroll
+  for (int k = 0; k < B; k++)
+    if (1 + k < nn) cur[k] = h2f(p[(size_t)(1 + k) * stride]);
+  for (int i0 = 1; i0 < nn; i0 += B) {
+    const bool more = i0 + B < nn;
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < B; k++)
+        if (i0 + B + k < nn) nxt[k] = h2f(p[(size_t)(i0 + B + k) * stride]);
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      const int i = i0 + k;
+      if (i < nn) {
+        const float l = i < m ? LU::L(i - 1) : L_inf;
+        const float r = cur[k] - l * prev;
+        p[(size_t)i * stride] = f2h(r);
+        prev = h16(r);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) cur[k] = nxt[k];
   }
-  // f[nn-1] *= p_inv * v_inv
-  at(nn - 1, x, y);
+  // f[nn-1] *= p_inv * v_inv  (prev holds the stored f[nn-1])
   {
-    const float4 c = load_px(img, w, x, y);
-    const float s = p_inv * v_inv;
-    store_px(img, w, x, y, make_float4(c.x * s, c.y * s, c.z * s, c.w * s));
-    prev = load_px(img, w, x, y);
+    const float r = prev * (p_inv * v_inv);
+    p[(size_t)(nn - 1) * stride] = f2h(r);
+    prev = h16(r);
   }
-  // reverse pass: f[i] = L * (p_inv * f[i] - f[i+1])
-  for (int i = nn - 2; i >= 0; i--) {
-    at(i, x, y);
-    const float l = i >= m - 1 ? L_inf : LU::L(i);
-    const float4 c = load_px(img, w, x, y);
-    const float4 r = make_float4(l * (p_inv * c.x - prev.x), l * (p_inv * c.y - prev.y),
-                                 l * (p_inv * c.z - prev.z), l * (p_inv * c.w - prev.w));
-    store_px(img, w, x, y, r);
-    prev = load_px(img, w, x, y);
+  // reverse pass: f[i] = L * (p_inv * f[i] - f[i+1]), i = nn-2 .. 0
+#pragma unroll
+  for (int k = 0; k < B; k++)
+    if (nn - 2 - k >= 0) cur[k] = h2f(p[(size_t)(nn - 2 - k) * stride]);
+  for (int i0 = nn - 2; i0 >= 0; i0 -= B) {
+    const bool more = i0 - B >= 0;
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < B; k++)
+        if (i0 - B - k >= 0) nxt[k] = h2f(p[(size_t)(i0 - B - k) * stride]);
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      const int i = i0 - k;
+      if (i >= 0) {
+        const float l = i >= m - 1 ? L_inf : LU::L(i);
+        const float r = l * (p_inv * cur[k] - prev);
+        p[(size_t)i * stride] = f2h(r);
+        prev = h16(r);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) cur[k] = nxt[k];
   }
 }
 
@@ -270,10 +312,11 @@ __global__ void screenshot_kernel(const void* __restrict__ src, int w, int h,
 
 hipError_t launch_digital(int kernel, uint2* img, int w, int h, hipStream_t s) {
   for (int dir = 0; dir < 2; dir++) {
-    const int lines = dir == 0 ? h : w;
-    const dim3 g((lines + 63) / 64), b(64);
-    if (kernel == 4) hipLaunchKernelGGL(digital_filter_kernel<LCbs>, g, b, 0, s, img, w, h, dir);
-    else hipLaunchKernelGGL(digital_filter_kernel<LOmoms>, g, b, 0, s, img, w, h, dir);
+    const int lanes = 4 * (dir == 0 ? h : w);
+    const dim3 g((lanes + 63) / 64), b(64);
+    uint16_t* p = (uint16_t*)img;
+    if (kernel == 4) hipLaunchKernelGGL(digital_filter_kernel<LCbs>, g, b, 0, s, p, w, h, dir);
+    else hipLaunchKernelGGL(digital_filter_kernel<LOmoms>, g, b, 0, s, p, w, h, dir);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -6,6 +6,7 @@
 #include <hip/hip_fp16.h>
 #include <cstdint>
 
+#include "cvr_device.h"
 #include "cvr_internal.h"
 
 namespace cvr {
@@ -62,10 +63,7 @@ __device__ __forceinline__ double norm_sample(const VT* vox, int nx, int ny, int
   return (double)vox[(size_t)x + (size_t)y * nx + (size_t)z * nx * ny] / inv_max;
 }
 
-__device__ __forceinline__ uint32_t f2h_bits(float f) {
-  _Float16 h = (_Float16)f;
-  return (uint32_t)__builtin_bit_cast(uint16_t, h);
-}
+__device__ __forceinline__ uint32_t f2h_bits(float f) { return f32_to_h16(f); }
 
 // GenerateGradientTexture (utils.cpp:146-190) with its defaults, and
 // GenerateSobelFeldmanGradientTexture (utils.cpp:287-333); stored RGB16F.
