@@ -71,6 +71,8 @@ def parse():
                    help="frame format: RGBA16F (the reference's framebuffer) or RGBA32F")
     p.add_argument("--streams", type=int, default=4,
                    help="frames in flight (render streams rotated per frame)")
+    p.add_argument("--exchange-frames", type=int, default=0,
+                   help="frames per gather at N > 1 (default: 4 at >= 8 GPUs, 2 at 4, else 1)")
     p.add_argument("--quad", type=int, default=-1,
                    help="quad (4 lanes per ray) share of the longest tiles, %% "
                         "(default: 10 at >= 8 GPUs, else 0)")
@@ -313,8 +315,12 @@ def main():
     if not shaded:
         N.check(N.lib().cvr_set_option(r.device.handle, b"quad", quad), "quad", r.device.handle)
     try:
+        # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
+        # on rank 0) would otherwise rival a rank's share of the frame (~23 us at N = 8)
+        gx = a.exchange_frames or (4 if world >= 8 else (2 if world >= 4 else 1))
         split = T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev,
-                                  transport=a.transport if world > 1 else None, streams=a.streams)
+                                  transport=a.transport if world > 1 else None, streams=a.streams,
+                                  frames_per_exchange=gx)
     except N.CvrError as e:     # no native communicator: torch's dist.gather instead
         if world == 1 or a.transport != "rccl":
             raise
@@ -489,8 +495,9 @@ def main():
             "roofline": roof,
         }
         if world > 1:
-            res["config"]["gather"] = (f"{a.transport}: packed {a.format} tiles to rank 0 + "
-                                       f"unpack, pipelined one frame deep")
+            res["config"]["gather"] = (f"{a.transport}: packed {a.format} tiles to rank 0 "
+                                       f"({split.G} frame(s) per ncclGather) + unpack of every "
+                                       f"frame, {split.nstreams} render streams")
             res["multi_gpu_bit_exact_vs_1gpu_frame"] = split_exact
         if ebs:
             cells = (n + 2) ** 3

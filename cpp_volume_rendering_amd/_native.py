@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "cvr_set_extinction_volume", "cvr_copy_extinction_level", "cvr_render_dosct",
     "cvr_tf1d_ext_lut", "cvr_set_extinction_sat", "cvr_copy_extinction_sat", "cvr_render_extbsd",
     "cvr_comm_unique_id", "cvr_comm_init", "cvr_comm_destroy", "cvr_gather_tiles",
+    "cvr_gather_tiles_n", "cvr_unpack_tiles_device_n",
     "cvr_gather_sync", "cvr_multiscale_resolution", "cvr_multiscale_filter",
     "cvr_screenshot_rgb8",
 )
@@ -165,6 +166,9 @@ def lib() -> ctypes.CDLL:
         "cvr_comm_destroy": ([P], I),
         "cvr_gather_tiles": ([P, ctypes.POINTER(Frame), P, I, I, P, P], I),
         "cvr_gather_sync": ([P], I),
+        "cvr_unpack_tiles_device_n": ([P, ctypes.POINTER(Frame), P, I, I, I, I, P], I),
+        "cvr_gather_tiles_n": ([P, ctypes.POINTER(Frame), I, P, I, I, P,
+                                ctypes.POINTER(ctypes.c_void_p)], I),
         "cvr_multiscale_resolution": ([I, I, I, IP, IP], I),
         "cvr_multiscale_filter": ([P, I, I, P, I, I, P, I, I], I),
         "cvr_screenshot_rgb8": ([P, P, I, I, I, P], I),

@@ -943,17 +943,28 @@ cvr_status cvr_screenshot_rgb8(cvr_ctx* ctx, const void* d_frame, int format, in
   return CVR_OK;
 }
 
-cvr_status cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* f, const void* d_packed,
-                                   int tpr_max, int format, void* d_rgba) {
+cvr_status cvr_unpack_tiles_device_n(cvr_ctx* ctx, const cvr_frame* f, const void* d_gathered,
+                                     int tpr_max, int nframes, int frame_index, int format,
+                                     void* d_rgba) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
-  if (!f || !d_packed || !d_rgba || f->nranks < 1 || f->tile_size < 16 || tpr_max < 0 ||
+  if (!f || !d_gathered || !d_rgba || f->nranks < 1 || f->tile_size < 16 || tpr_max < 0 ||
+      nframes < 1 || frame_index < 0 || frame_index >= nframes ||
       (format != CVR_FORMAT_RGBA32F && format != CVR_FORMAT_RGBA16F))
     return fail(c, CVR_ERR_ARG, "cvr_unpack_tiles_device: bad arguments");
   HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, cvr::launch_unpack_tiles(d_packed, d_rgba, format == CVR_FORMAT_RGBA16F, f->width, f->height,
-                                      f->tile_size, f->nranks, tpr_max, c->stream));
+  const size_t px = format == CVR_FORMAT_RGBA16F ? 8 : 16;
+  const char* src = static_cast<const char*>(d_gathered) +
+                    (size_t)frame_index * tpr_max * f->tile_size * f->tile_size * px;
+  HIP_TRY(c, cvr::launch_unpack_tiles(src, d_rgba, format == CVR_FORMAT_RGBA16F, f->width,
+                                      f->height, f->tile_size, f->nranks, tpr_max, c->stream,
+                                      (size_t)nframes * tpr_max));
   return CVR_OK;
+}
+
+cvr_status cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* f, const void* d_packed,
+                                   int tpr_max, int format, void* d_rgba) {
+  return cvr_unpack_tiles_device_n(ctx, f, d_packed, tpr_max, 1, 0, format, d_rgba);
 }
 
 

@@ -1,6 +1,6 @@
 // cvr_comm.cpp — the screen-tile split's one exchange step:
-// rank 0 gathers every rank's packed tiles over RCCL (xGMI) and unpacks them
-// into the frame.  Native, so a frame costs two C calls on the host (render +
+// rank 0 gathers every rank's packed tiles with one ncclGather (RCCL over xGMI)
+// and unpacks them into the frame.  Native, so a frame costs two C calls on the host (render +
 // gather) instead of a Python collective: at 8 GPUs a rank's share of a
 // 1024^2 frame renders in tens of microseconds.
 //
@@ -124,57 +124,74 @@ cvr_status cvr_comm_destroy(cvr_ctx* ctx) {
   return CVR_OK;
 }
 
-cvr_status cvr_gather_tiles(cvr_ctx* ctx, const cvr_frame* f, const void* d_packed,
-                            int tpr_max, int format, void* d_gathered, void* d_rgba) {
+cvr_status cvr_gather_tiles_n(cvr_ctx* ctx, const cvr_frame* f, int nframes, const void* d_packed,
+                              int tpr_max, int format, void* d_gathered, void* const* d_images) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
   Comm* m = comm_of(c);
   if (!m) return cfail(c, CVR_ERR_STATE, "cvr_gather_tiles: cvr_comm_init not called");
-  if (!f || !d_packed || tpr_max < 0 || f->tile_size < 16 ||
+  if (!f || !d_packed || nframes < 1 || tpr_max < 0 || (f->nranks > 1 && f->tile_size < 16) ||
       (format != CVR_FORMAT_RGBA32F && format != CVR_FORMAT_RGBA16F))
     return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: bad arguments");
   if (f->nranks != m->nranks || f->rank != m->rank)
     return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: frame rank %d/%d, communicator %d/%d",
                  f->rank, f->nranks, m->rank, m->nranks);
-  if (m->rank == 0 && (!d_gathered || !d_rgba))
-    return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: rank 0 needs the gather buffer and image");
-  if (cvr_tiles_for_rank(f, f->rank) > tpr_max)
+  if (m->rank == 0 && (!d_gathered || !d_images))
+    return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: rank 0 needs the gather buffer and images");
+  if (m->nranks > 1 && cvr_tiles_for_rank(f, f->rank) > tpr_max)
     return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: tiles_per_rank_max too small");
   CHIP(c, hipSetDevice(c->device));
   const size_t px = format == CVR_FORMAT_RGBA16F ? 8 : 16;
-  const size_t bytes = (size_t)tpr_max * f->tile_size * f->tile_size * px;
+  // one rank: the frames were rendered whole (row-major); the "gather" is a copy
+  const size_t fbytes = m->nranks == 1 ? (size_t)f->width * f->height * px
+                                       : (size_t)tpr_max * f->tile_size * f->tile_size * px;
+  const size_t bytes = fbytes * (size_t)nframes;
   hipStream_t s = c->stream;
   CHIP(c, hipEventRecord(m->ev_render, s));
   CHIP(c, hipStreamWaitEvent(m->stream, m->ev_render, 0));
+  // One ncclGather (rccl.h:745) for all nframes frames: block r of the gather
+  // buffer <- rank r's frames.  Rank 0 renders straight into block 0, which makes
+  // its part in place.
   if (m->rank == 0) {
     char* g = static_cast<char*>(d_gathered);
-    // rank 0's own block: skipped when it rendered straight into it
     if (d_packed != d_gathered)
       CHIP(c, hipMemcpyAsync(g, d_packed, bytes, hipMemcpyDeviceToDevice, m->stream));
-    if (m->nranks > 1) {
-      CNCCL(c, ncclGroupStart());
-      for (int r = 1; r < m->nranks; r++)
-        CNCCL(c, ncclRecv(g + (size_t)r * bytes, bytes, ncclChar, r, m->comm, m->stream));
-      CNCCL(c, ncclGroupEnd());
+    CNCCL(c, ncclGather(g, g, bytes, ncclChar, 0, m->comm, m->stream));
+    for (int j = 0; j < nframes; j++) {
+      void* img = d_images[j];
+      if (!img) continue;
+      const char* fj = g + (size_t)j * fbytes;
+      if (m->nranks == 1) {
+        if (img != (const void*)fj)
+          CHIP(c, hipMemcpyAsync(img, fj, fbytes, hipMemcpyDeviceToDevice, m->stream));
+      } else {
+        CHIP(c, cvr::launch_unpack_tiles(fj, img, format == CVR_FORMAT_RGBA16F, f->width,
+                                         f->height, f->tile_size, m->nranks, tpr_max, m->stream,
+                                         (size_t)nframes * tpr_max));
+      }
     }
-    CHIP(c, cvr::launch_unpack_tiles(g, d_rgba, format == CVR_FORMAT_RGBA16F, f->width, f->height,
-                                     f->tile_size, m->nranks, tpr_max, m->stream));
   } else {
-    CNCCL(c, ncclSend(d_packed, bytes, ncclChar, 0, m->comm, m->stream));
+    CNCCL(c, ncclGather(d_packed, nullptr, bytes, ncclChar, 0, m->comm, m->stream));
   }
   const int k = (int)(m->ngather & 1);
   CHIP(c, hipEventRecord(m->ev_gather[k], m->stream));
-  // One render stream and two buffers: the next render reuses the buffers of frame
-  // n-1, so the stream waits for the previous gather (this gather overlaps the next
-  // render).  D >= 2 streams rotated with D buffers: the next render on this stream
-  // is frame n+D in this frame's buffers, so it waits for this gather (the other
-  // streams render the next frames meanwhile, overlapping this frame's tail too).
+  // One render stream and two buffers: the next render reuses the buffers of the
+  // previous exchange, so the stream waits for the previous gather (this gather
+  // overlaps the next render).  D >= 2 streams rotated with D buffer sets: the
+  // next render on this stream reuses this exchange's buffers, so it waits for
+  // this gather (the other streams render the next frames meanwhile).
   if (c->split_streams >= 2)
     CHIP(c, hipStreamWaitEvent(s, m->ev_gather[k], 0));
   else if (m->ngather > 0)
     CHIP(c, hipStreamWaitEvent(s, m->ev_gather[k ^ 1], 0));
   m->ngather++;
   return CVR_OK;
+}
+
+cvr_status cvr_gather_tiles(cvr_ctx* ctx, const cvr_frame* f, const void* d_packed,
+                            int tpr_max, int format, void* d_gathered, void* d_rgba) {
+  void* imgs[1] = {d_rgba};
+  return cvr_gather_tiles_n(ctx, f, 1, d_packed, tpr_max, format, d_gathered, imgs);
 }
 
 cvr_status cvr_gather_sync(cvr_ctx* ctx) {

@@ -264,7 +264,7 @@ hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* sam
                       unsigned long long* shade,
                       unsigned long long* tile_samples, hipStream_t s);
 hipError_t launch_unpack_tiles(const void* packed, void* out, int half, int W, int H, int tile,
-                               int nranks, int tpr_max, hipStream_t s);
+                               int nranks, int tpr_max, hipStream_t s, size_t rank_stride = 0);
 
 inline CellGrid make_cell_grid(const int N[3]) {
   CellGrid g;

@@ -155,10 +155,13 @@ hipError_t launch_gradient(const Ctx& c, int mode, uint2* tmp, hipStream_t s) {
 
 // Scatter packed per-rank tiles (screen-tile split) into the W x H image.
 // PX = float4 (RGBA32F) or uint2 (RGBA16F): pixels are moved, not converted.
+// Rank r's k-th tile sits at tile slot r * rank_stride + k of `packed` (rank_stride
+// = tpr_max for one frame per exchange; nframes * tpr_max when several frames
+// travel together and `packed` points at frame j's first slot).
 template <typename PX>
 __global__ void unpack_tiles_kernel(const PX* __restrict__ packed, PX* __restrict__ out,
-                                    int W, int H, int tile, int nranks, int tpr_max, int ntx,
-                                    size_t n) {
+                                    int W, int H, int tile, int nranks, int tpr_max,
+                                    size_t rank_stride, int ntx, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   size_t tt = (size_t)tile * tile;
@@ -168,22 +171,26 @@ __global__ void unpack_tiles_kernel(const PX* __restrict__ packed, PX* __restric
   int t = r + k * nranks;
   int tx = t % ntx, ty = t / ntx;
   int px = tx * tile + inner % tile, py = ty * tile + inner / tile;
-  if (px < W && py < H && ty * tile < H) out[(size_t)py * W + px] = packed[i];
+  if (px < W && py < H && ty * tile < H)
+    out[(size_t)py * W + px] = packed[((size_t)r * rank_stride + k) * tt + inner];
 }
 
 hipError_t launch_unpack_tiles(const void* packed, void* out, int half, int W, int H, int tile,
-                               int nranks, int tpr_max, hipStream_t s) {
+                               int nranks, int tpr_max, hipStream_t s, size_t rank_stride) {
   int ntx = (W + tile - 1) / tile;
   size_t n = (size_t)nranks * tpr_max * tile * tile;
   int bs = 256;
   size_t nb = (n + bs - 1) / bs;
   if (n == 0) return hipSuccess;
+  if (rank_stride == 0) rank_stride = (size_t)tpr_max;
   if (half)
     hipLaunchKernelGGL(unpack_tiles_kernel<uint2>, dim3((unsigned)nb), dim3(bs), 0, s,
-                       (const uint2*)packed, (uint2*)out, W, H, tile, nranks, tpr_max, ntx, n);
+                       (const uint2*)packed, (uint2*)out, W, H, tile, nranks, tpr_max, rank_stride,
+                       ntx, n);
   else
     hipLaunchKernelGGL(unpack_tiles_kernel<float4>, dim3((unsigned)nb), dim3(bs), 0, s,
-                       (const float4*)packed, (float4*)out, W, H, tile, nranks, tpr_max, ntx, n);
+                       (const float4*)packed, (float4*)out, W, H, tile, nranks, tpr_max,
+                       rank_stride, ntx, n);
   return hipGetLastError();
 }
 

@@ -118,7 +118,7 @@ class ScreenTileSplit:
     def __init__(self, renderer=None, width: int = None, height: int = None, tile: int = 32,
                  fmt: int = N.FORMAT_RGBA16F, group=None, device=None, render_fn=None,
                  unpack_fn=None, count_samples: bool = False, transport: str = None,
-                 streams: int = None):
+                 streams: int = None, frames_per_exchange: int = 1):
         self.r = renderer
         self.width = width if width is not None else renderer.width
         self.height = height if height is not None else renderer.height
@@ -151,14 +151,19 @@ class ScreenTileSplit:
         nimg = streams if not self.split else 1
         self._images = ([torch.zeros((h, w, 4), dtype=dtype, device=self.device)
                          for _ in range(nimg)] if self.rank == 0 else None)
-        # buffer sets: frame n uses set n % nbuf (one per stream; two for one stream)
+        # buffer sets: frame n uses set n % nbuf (one per stream; two for one stream).
+        # With the native transport, G = frames_per_exchange consecutive frames share
+        # one set (one slot each), render on its stream and travel in ONE gather.
         self.nbuf = max(2, streams)
+        self.G = max(1, int(frames_per_exchange)) if (self.transport == "rccl" and
+                                                       self.streams is not None) else 1
         if self.split:
             # padded to tpr_max tiles (gather needs equal sizes); padding stays zero
-            self.packed = [torch.zeros((self.tpr_max, tile, tile, 4), dtype=dtype,
+            self.packed = [torch.zeros((self.G, self.tpr_max, tile, tile, 4), dtype=dtype,
                                        device=self.device) for _ in range(self.nbuf)]
-            self.gathered = ([torch.zeros((self.world, self.tpr_max, tile, tile, 4), dtype=dtype,
-                                          device=self.device) for _ in range(self.nbuf)]
+            self.gathered = ([torch.zeros((self.world, self.G, self.tpr_max, tile, tile, 4),
+                                          dtype=dtype, device=self.device)
+                              for _ in range(self.nbuf)]
                              if self.rank == 0 else None)
         self.total = (torch.zeros((1,), dtype=torch.int64, device=self.device)
                       if count_samples else None)
@@ -179,14 +184,17 @@ class ScreenTileSplit:
             slots = []
             for i in range(self.nbuf):
                 g = self.gathered[i] if self.rank == 0 else None
-                buf = g[0] if self.rank == 0 else self.packed[i]
-                out = N.Output(buf.data_ptr(), None,
-                               self.total.data_ptr() if self.total is not None else None, 1,
-                               fmt)
-                slots.append((self.streams[i % self.nstreams].cuda_stream, out, buf.data_ptr(),
+                blk = g[0] if self.rank == 0 else self.packed[i]     # (G, tpr, T, T, 4)
+                outs = [N.Output(blk[j].data_ptr(), None,
+                                 self.total.data_ptr() if self.total is not None else None, 1,
+                                 fmt) for j in range(self.G)]
+                slots.append((self.streams[i % self.nstreams].cuda_stream, outs, blk.data_ptr(),
                               g.data_ptr() if g is not None else None))
-            self._fast = (L, h, getattr(L, self.r._ENTRY), ctypes.byref(self.r._params),
-                          self._images[0].data_ptr() if self.rank == 0 else None, slots)
+            img = self._images[0].data_ptr() if self.rank == 0 else None
+            imgs = (ctypes.c_void_p * self.G)(*([img] * self.G))
+            self._fast = (L, h, getattr(L, self.r._ENTRY), ctypes.byref(self.r._params), imgs,
+                          slots)
+            self._group = 0      # frames rendered into the open exchange group
 
     @property
     def image(self):
@@ -257,18 +265,20 @@ class ScreenTileSplit:
             return
         slot = n % self.nbuf
         if self._fast is not None:
-            L, h, entry, params, img, slots = self._fast
+            L, h, entry, params, imgs, slots = self._fast
             if self._fresh:
                 self._stream_for(n)
-            sptr, out, buf, g = slots[slot]
+            G = self.G
+            sptr, outs, buf, g = slots[(n // G) % self.nbuf]
+            j = n % G
             L.cvr_set_stream(h, sptr)
             fr = ctypes.byref(frame)
-            st = entry(h, fr, params, ctypes.byref(out))
+            st = entry(h, fr, params, ctypes.byref(outs[j]))
             if st:
                 N.check(st, self.r._ENTRY, h)
-            st = L.cvr_gather_tiles(h, fr, buf, self.tpr_max, self.fmt, g, img)
-            if st:
-                N.check(st, "cvr_gather_tiles", h)
+            self._group = j + 1
+            if self._group == G:
+                self._exchange(G, n)
             self.submitted += 1
             self.completed = n - 1
             return
@@ -276,7 +286,7 @@ class ScreenTileSplit:
             # the library orders this render after the gather of frame n-2 (same slot)
             h = self.r.device.handle
             g = self.gathered[slot] if self.rank == 0 else None
-            buf = g[0] if self.rank == 0 else self.packed[slot]
+            buf = g[0, 0] if self.rank == 0 else self.packed[slot][0]
             self.render_fn(frame, buf, self.total)
             N.check(N.lib().cvr_gather_tiles(h, ctypes.byref(frame), buf.data_ptr(), self.tpr_max,
                                              self.fmt, g.data_ptr() if g is not None else None,
@@ -288,14 +298,27 @@ class ScreenTileSplit:
             return
         # the slot's previous frame (n-2) was completed before frame n-1 was submitted
         # returned, so its gather no longer reads packed[slot]
-        self.render_fn(frame, self.packed[slot], self.total)
-        gl = list(self.gathered[slot].unbind(0)) if self.rank == 0 else None
-        work = dist.gather(self.packed[slot], gather_list=gl, dst=0, group=self.group,
+        self.render_fn(frame, self.packed[slot][0], self.total)
+        gl = [g[0] for g in self.gathered[slot].unbind(0)] if self.rank == 0 else None
+        work = dist.gather(self.packed[slot][0], gather_list=gl, dst=0, group=self.group,
                            async_op=True)
         self._pending.append((n, slot, work, frame))
         self.submitted += 1
         while len(self._pending) > 1:
             self._complete_oldest()
+
+    def _exchange(self, nframes, n_last):
+        """Gather the open group's `nframes` frames, the last of which is frame
+        `n_last`, in one ncclGather on the group's stream."""
+        L, h, entry, params, imgs, slots = self._fast
+        n0 = n_last - nframes + 1                        # first frame of the group
+        sptr, outs, buf, g = slots[(n0 // self.G) % self.nbuf]
+        L.cvr_set_stream(h, sptr)
+        st = L.cvr_gather_tiles_n(h, ctypes.byref(self._frame), nframes, buf, self.tpr_max,
+                                  self.fmt, g, imgs if self.rank == 0 else None)
+        if st:
+            N.check(st, "cvr_gather_tiles_n", h)
+        self._group = 0
 
     def _frame_for(self, camera):
         """This rank's cvr_frame for `camera` (cached while the camera is unchanged)."""
@@ -312,12 +335,14 @@ class ScreenTileSplit:
         n, slot, work, frame = self._pending.pop(0)
         work.wait()       # the current stream waits for the gather (RCCL) / host waits (gloo)
         if self.rank == 0:
-            self.unpack_fn(frame, self.gathered[slot], self._images[0])
+            self.unpack_fn(frame, self.gathered[slot][:, 0], self._images[0])
         self.completed = n
 
     def flush(self):
         """Complete every submitted frame: work queued on the current stream afterwards
         sees the last frame in `image`."""
+        if self._fast is not None and self._group:
+            self._exchange(self._group, self.submitted - 1)   # a partly filled group
         if self.device.type == "cuda":
             cur = torch.cuda.current_stream(self.device)
             if self.streams is not None:
@@ -357,7 +382,7 @@ class TiledRc1pass(ScreenTileSplit):
             if not gather and self.split:
                 frame = make_frame(camera, self.width, self.height, self.tile, self.rank,
                                    self.world)
-                self.render_fn(frame, self.packed[0], self.total)
-                return self.packed[0][:self.k]
+                self.render_fn(frame, self.packed[0][0], self.total)
+                return self.packed[0][0][:self.k]
             img = super().render(camera)
-        return img if self.rank == 0 else self.packed[(self.submitted - 1) % self.nbuf][:self.k]
+        return img if self.rank == 0 else self.packed[(self.submitted - 1) % self.nbuf][0][:self.k]

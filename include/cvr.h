@@ -98,7 +98,8 @@ typedef struct cvr_frame {
  * buffer), in `format`: CVR_FORMAT_RGBA32F (0, 16 B/pixel, the exact
  * composite) or CVR_FORMAT_RGBA16F (1, 8 B/pixel: binary16 rounded to nearest
  * even, the reference's own framebuffer, imageStore into the RGBA16F
- * OutputFrag image, ray_marching_1p.comp:174-176 / renderoutputframe.cpp:64-87).  samples (optional): per-pixel loop-iteration count of
+ * OutputFrag image, ray_marching_1p.comp:174-176 / renderoutputframe.cpp:64-87).
+ * samples (optional): per-pixel loop-iteration count of
  * ray_marching_1p.comp:124-172 (transparent samples included, stopping at the
  * ERT break).  total (optional): the sum of all iteration counts (uint64).
  * on_device = 1: all three are device pointers and the call is asynchronous
@@ -317,6 +318,14 @@ cvr_status  cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* frame,
                                     const void* d_packed, int tiles_per_rank_max,
                                     int format, void* d_rgba);
 
+/* The same for frame `frame_index` of a grouped exchange: `d_gathered` holds
+ * nranks blocks of nframes * tiles_per_rank_max tiles (rank r's frame j at
+ * tile slot (r * nframes + j) * tiles_per_rank_max), as cvr_gather_tiles_n
+ * leaves it. */
+cvr_status  cvr_unpack_tiles_device_n(cvr_ctx* ctx, const cvr_frame* frame,
+                                      const void* d_gathered, int tiles_per_rank_max,
+                                      int nframes, int frame_index, int format, void* d_rgba);
+
 /* ----------------------------------------------------------------------------
  * After the march: pixel multiscaling and the screenshot
  * (libs/vis_utils/renderoutputframe.cpp:89-146, 265-539 and its
@@ -376,7 +385,8 @@ cvr_status  cvr_comm_init(cvr_ctx* ctx, int nranks, int rank,
                           const unsigned char id[CVR_COMM_ID_BYTES]);
 cvr_status  cvr_comm_destroy(cvr_ctx* ctx);
 
-/* Gather one frame's packed tiles on rank 0 and unpack them into the image.
+/* Gather one frame's packed tiles on rank 0 (one ncclGather) and unpack them
+ * into the image.
  * Every rank calls it right after rendering its tiles (frame->rank/nranks
  * must match the communicator) into `d_packed` (tiles_per_rank_max tiles,
  * padding allowed).  Rank 0 also passes `d_gathered` (nranks blocks of
@@ -392,10 +402,22 @@ cvr_status  cvr_comm_destroy(cvr_ctx* ctx);
  * frames overlap on the device as well.
  * Frames on different streams each use their own LPT order state; frames that
  * count samples (cvr_output.total) must not overlap.  Before reading the image
- * on the context stream, call cvr_gather_sync. */
+ * on the context stream, call cvr_gather_sync.  With a one-rank communicator
+ * the frame is rendered whole (nranks 1) and the gather copies it to d_rgba. */
 cvr_status  cvr_gather_tiles(cvr_ctx* ctx, const cvr_frame* frame, const void* d_packed,
                              int tiles_per_rank_max, int format, void* d_gathered,
                              void* d_rgba);
+
+/* The same for `nframes` frames rendered by this rank one after another on the
+ * context stream into consecutive blocks of `d_packed` (frame j at j *
+ * tiles_per_rank_max tiles), exchanged in ONE ncclGather (fewer, larger
+ * collectives: a gather's host and launch cost is shared by nframes frames).
+ * `frame` gives the tile layout (the camera is not used).  Rank 0's
+ * `d_gathered` holds nranks blocks of nframes * tiles_per_rank_max tiles, and
+ * frame j is unpacked into d_images[j] (in frame order; NULL skips it). */
+cvr_status  cvr_gather_tiles_n(cvr_ctx* ctx, const cvr_frame* frame, int nframes,
+                               const void* d_packed, int tiles_per_rank_max, int format,
+                               void* d_gathered, void* const* d_images);
 
 /* The context stream waits for every gather issued so far. */
 cvr_status  cvr_gather_sync(cvr_ctx* ctx);

@@ -204,3 +204,113 @@ def test_rccl_gather_two_ranks_one_gpu():
     assert not alive, "RCCL gather workers hung"
     assert status == "ok"
     assert [p.exitcode for p in procs] == [0, 0]
+
+
+def test_rccl_one_rank_gather_pipeline(dev, bonsai_tf):
+    """A one-rank communicator through cvr_comm_init / cvr_gather_tiles (ncclGather in
+    place + copy), frames rotated over 4 streams with split_streams = 4: after
+    cvr_gather_sync the image holds the last frame, bit-equal to a direct render."""
+    import torch
+    L = N.lib()
+    vol = D.marschner_lobb_u8(64)
+    dev.set_volume(vol, D.voxel_scale(64))
+    dev.set_transfer_function(bonsai_tf)
+    dev.set_gradient(N.GRADIENT_NONE)
+    uid = ctypes.create_string_buffer(N.COMM_ID_BYTES)
+    N.check(L.cvr_comm_unique_id(uid), "uid")
+    N.check(L.cvr_comm_init(dev.handle, 1, 0, uid.raw), "cvr_comm_init", dev.handle)
+    try:
+        N.check(L.cvr_set_option(dev.handle, b"split_streams", 4), "opt", dev.handle)
+        W, H = 160, 120
+        streams = [torch.cuda.Stream() for _ in range(4)]
+        bufs = [torch.zeros((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(4)]
+        img = torch.zeros((H, W, 4), dtype=torch.float16, device="cuda")
+        p = N.Rc1passParams()
+        seq = [0, 1, 2, 0, 1, 2, 1]
+        for n, ci in enumerate(seq):
+            k = n % 4
+            frame = make_frame(Camera(**CAMS[ci]), W, H)
+            dev.set_stream(streams[k].cuda_stream)
+            out = N.Output(bufs[k].data_ptr(), None, None, 1, N.FORMAT_RGBA16F)
+            N.check(L.cvr_render_rc1pass(dev.handle, ctypes.byref(frame), ctypes.byref(p),
+                                         ctypes.byref(out)), "render", dev.handle)
+            N.check(L.cvr_gather_tiles(dev.handle, ctypes.byref(frame), bufs[k].data_ptr(), 0,
+                                       N.FORMAT_RGBA16F, bufs[k].data_ptr(), img.data_ptr()),
+                    "cvr_gather_tiles", dev.handle)
+        dev.set_stream(torch.cuda.current_stream().cuda_stream)
+        N.check(L.cvr_gather_sync(dev.handle), "sync", dev.handle)
+        torch.cuda.synchronize()
+        want = _render(dev, N.FORMAT_RGBA16F, W, H, cam=CAMS[seq[-1]])
+        assert np.array_equal(img.cpu().numpy().view(np.uint16), want.view(np.uint16))
+    finally:
+        N.check(L.cvr_set_option(dev.handle, b"split_streams", 1), "opt", dev.handle)
+        N.check(L.cvr_comm_destroy(dev.handle), "cvr_comm_destroy", dev.handle)
+        dev.set_stream(None)
+
+
+def test_grouped_unpack_matches_full_frames(dev, bonsai_tf):
+    """A grouped exchange's layout (rank r's frame j at slot (r*G + j)*tpr), built on
+    one GPU from per-rank renders of G different cameras, unpacks frame j to the
+    whole frame j bit for bit (cvr_unpack_tiles_device_n)."""
+    import torch
+    vol = D.marschner_lobb_u8(64)
+    dev.set_volume(vol, D.voxel_scale(64))
+    dev.set_transfer_function(bonsai_tf)
+    dev.set_gradient(N.GRADIENT_NONE)
+    W, H, tile, nranks, G = 100, 72, 32, 3, 3
+    tpr = T.max_tiles_per_rank(W, H, tile, nranks)
+    gathered = np.zeros((nranks, G, tpr, tile, tile, 4), np.float16)
+    for r in range(nranks):
+        for j in range(G):
+            p = _render(dev, N.FORMAT_RGBA16F, W, H, tile=tile, rank=r, nranks=nranks, cam=CAMS[j])
+            gathered[r, j, :p.shape[0]] = p
+    d_g = torch.from_numpy(gathered).cuda()
+    frame = make_frame(Camera(**INITIAL), W, H, tile, 0, nranks)
+    dev.set_stream(torch.cuda.current_stream().cuda_stream)
+    for j in range(G):
+        img = torch.zeros((H, W, 4), dtype=torch.float16, device="cuda")
+        N.check(N.lib().cvr_unpack_tiles_device_n(dev.handle, ctypes.byref(frame), d_g.data_ptr(),
+                                                  tpr, G, j, N.FORMAT_RGBA16F, img.data_ptr()),
+                "unpack_n", dev.handle)
+        torch.cuda.synchronize()
+        want = _render(dev, N.FORMAT_RGBA16F, W, H, cam=CAMS[j])
+        assert np.array_equal(img.cpu().numpy().view(np.uint16), want.view(np.uint16)), j
+    dev.set_stream(None)
+
+
+def test_rccl_one_rank_grouped_gather(dev, bonsai_tf):
+    """cvr_gather_tiles_n with a one-rank communicator: G frames rendered into one
+    block, one ncclGather, each frame delivered to its own image."""
+    import torch
+    L = N.lib()
+    vol = D.marschner_lobb_u8(64)
+    dev.set_volume(vol, D.voxel_scale(64))
+    dev.set_transfer_function(bonsai_tf)
+    dev.set_gradient(N.GRADIENT_NONE)
+    uid = ctypes.create_string_buffer(N.COMM_ID_BYTES)
+    N.check(L.cvr_comm_unique_id(uid), "uid")
+    N.check(L.cvr_comm_init(dev.handle, 1, 0, uid.raw), "cvr_comm_init", dev.handle)
+    try:
+        W, H, G = 128, 96, 3
+        blk = torch.zeros((G, H, W, 4), dtype=torch.float16, device="cuda")
+        imgs_t = [torch.zeros((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(G)]
+        imgs = (ctypes.c_void_p * G)(*[t.data_ptr() for t in imgs_t])
+        dev.set_stream(torch.cuda.current_stream().cuda_stream)
+        p = N.Rc1passParams()
+        frame = None
+        for j in range(G):
+            frame = make_frame(Camera(**CAMS[j]), W, H)
+            out = N.Output(blk[j].data_ptr(), None, None, 1, N.FORMAT_RGBA16F)
+            N.check(L.cvr_render_rc1pass(dev.handle, ctypes.byref(frame), ctypes.byref(p),
+                                         ctypes.byref(out)), "render", dev.handle)
+        N.check(L.cvr_gather_tiles_n(dev.handle, ctypes.byref(frame), G, blk.data_ptr(), 0,
+                                     N.FORMAT_RGBA16F, blk.data_ptr(), imgs), "gather_n",
+                dev.handle)
+        N.check(L.cvr_gather_sync(dev.handle), "sync", dev.handle)
+        torch.cuda.synchronize()
+        for j in range(G):
+            want = _render(dev, N.FORMAT_RGBA16F, W, H, cam=CAMS[j])
+            assert np.array_equal(imgs_t[j].cpu().numpy().view(np.uint16), want.view(np.uint16)), j
+    finally:
+        N.check(L.cvr_comm_destroy(dev.handle), "cvr_comm_destroy", dev.handle)
+        dev.set_stream(None)
