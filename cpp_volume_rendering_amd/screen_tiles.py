@@ -118,7 +118,7 @@ class ScreenTileSplit:
     def __init__(self, renderer=None, width: int = None, height: int = None, tile: int = 32,
                  fmt: int = N.FORMAT_RGBA16F, group=None, device=None, render_fn=None,
                  unpack_fn=None, count_samples: bool = False, transport: str = None,
-                 streams: int = None, frames_per_exchange: int = 1):
+                 streams: int = None, frames_per_exchange: int = 1, stream_factory=None):
         self.r = renderer
         self.width = width if width is not None else renderer.width
         self.height = height if height is not None else renderer.height
@@ -144,8 +144,10 @@ class ScreenTileSplit:
         if self.transport == "torch":
             streams = 1
         self.nstreams = streams
-        self.streams = ([torch.cuda.Stream(self.device) for _ in range(streams)]
-                        if streams > 1 else None)
+        # stream_factory: tests drive the native path's control flow with stand-in
+        # streams on CPU
+        mk = stream_factory or (lambda: torch.cuda.Stream(self.device))
+        self.streams = [mk() for _ in range(streams)] if streams > 1 else None
         self.k = tiles_for_rank(w, h, tile, self.rank, self.world) if self.split else 0
         self.tpr_max = max_tiles_per_rank(w, h, tile, self.world) if self.split else 0
         nimg = streams if not self.split else 1

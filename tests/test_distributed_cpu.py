@@ -163,3 +163,128 @@ def test_screen_tile_split_pipeline_gloo(world, W, H, tile):
     codes = [p.exitcode for p in procs]
     assert codes == [0] * world, f"worker exit codes {codes}"
     assert q.get(timeout=10) == "ok"
+
+
+class _FakeStream:
+    _n = 0
+
+    def __init__(self):
+        _FakeStream._n += 1
+        self.cuda_stream = 1000 + _FakeStream._n
+
+    def wait_stream(self, other):
+        pass
+
+
+class _FakeLib:
+    """Records the native split path's C calls (cvr_render_* / cvr_gather_tiles_n)."""
+
+    def __init__(self):
+        self.calls = []
+        self.stream = None
+
+    def cvr_comm_unique_id(self, buf):
+        buf.raw = b"\x07" * len(buf.raw)
+        return 0
+
+    def cvr_comm_init(self, h, world, rank, uid):
+        assert uid == b"\x07" * len(uid)
+        self.calls.append(("init", world, rank))
+        return 0
+
+    def cvr_set_option(self, h, key, val):
+        self.calls.append(("opt", key, val))
+        return 0
+
+    def cvr_set_stream(self, h, s):
+        self.stream = s
+        return 0
+
+    def cvr_render_rc1pass(self, h, fr, params, out):
+        self.calls.append(("render", self.stream, out._obj.rgba))
+        return 0
+
+    def cvr_gather_tiles_n(self, h, fr, nframes, buf, tpr, fmt, g, imgs):
+        self.calls.append(("gather", self.stream, nframes, buf, g is not None))
+        return 0
+
+    def cvr_gather_sync(self, h):
+        self.calls.append(("sync",))
+        return 0
+
+    def cvr_comm_destroy(self, h):
+        self.calls.append(("destroy",))
+        return 0
+
+
+def _native_flow_worker(rank, world, port, q):
+    """ScreenTileSplit's native-RCCL fast path (frames rotated over D streams, G frames
+    per exchange, a partial group at flush) with the library calls recorded: every
+    rank must issue the same gathers, each covering its group's frames in order."""
+    from cpp_volume_rendering_amd import _native as N
+    from cpp_volume_rendering_amd.renderer import Camera
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fake = _FakeLib()
+        N._lib = fake
+
+        class R:
+            _ENTRY = "cvr_render_rc1pass"
+            _params = N.Rc1passParams()
+
+            class device:
+                handle = 1
+
+                @staticmethod
+                def set_stream(s):
+                    fake.stream = s
+
+        D_, G = 3, 4
+        sp = T.ScreenTileSplit(R(), 96, 64, tile=32, fmt=N.FORMAT_RGBA16F, device="cpu",
+                               transport="rccl", streams=D_, frames_per_exchange=G,
+                               stream_factory=_FakeStream)
+        assert sp._fast is not None and sp.G == G and sp.nbuf == D_
+        cam = Camera(**D.INITIAL_STATE_CAMERA)
+        nframes = 10
+        for _ in range(nframes):
+            sp.submit(cam)
+        sp.flush()
+        renders = [c for c in fake.calls if c[0] == "render"]
+        gathers = [c for c in fake.calls if c[0] == "gather"]
+        assert len(renders) == nframes
+        assert [g[2] for g in gathers] == [4, 4, 2]          # two full groups + the rest
+        streams = [s.cuda_stream for s in sp.streams]
+        # group q renders and gathers on stream q % D; frame j of a group -> slot j
+        for n, rc in enumerate(renders):
+            grp, j = divmod(n, G)
+            assert rc[1] == streams[grp % D_]
+            blk = (sp.gathered[grp % D_][0] if rank == 0 else sp.packed[grp % D_])
+            assert rc[2] == blk[j].data_ptr()
+        for grp, g in enumerate(gathers):
+            assert g[1] == streams[grp % D_]
+            assert g[4] == (rank == 0)
+        assert ("opt", b"split_streams", D_) in fake.calls
+        sp.close()
+        assert fake.calls[-1] == ("destroy",)
+        q.put(("ok", rank, len(gathers)))
+    except Exception as e:   # noqa: BLE001  (reported to the parent)
+        q.put(("fail", rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_split_control_flow_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_flow_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    res = [q.get(timeout=10) for _ in range(2)]
+    assert all(r[0] == "ok" for r in res), res
+    assert [p.exitcode for p in procs] == [0, 0]
