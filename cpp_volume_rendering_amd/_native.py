@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = (
     "cvr_set_stream", "cvr_set_option", "cvr_get_option", "cvr_synchronize", "cvr_set_volume", "cvr_set_volume_device",
     "cvr_set_transfer_function", "cvr_set_gradient", "cvr_device_bytes", "cvr_tiles_for_rank",
     "cvr_render_rc1pass", "cvr_unpack_tiles_device", "cvr_copy_tile_stats", "cvr_read_kernel_times", "cvr_read_shade_counters", "cvr_camera_lookat", "cvr_default_step",
-    "cvr_tf1d_build_rgbt", "cvr_read_tf1d", "cvr_read_raw", "cvr_read_syn",
+    "cvr_tf1d_build_rgbt", "cvr_read_tf1d", "cvr_read_raw", "cvr_read_syn", "cvr_read_pvm",
     "cvr_read_camera_state", "cvr_read_light_position", "cvr_read_light", "cvr_build_cone_tables",
     "cvr_set_extinction_volume", "cvr_copy_extinction_level", "cvr_render_dosct",
     "cvr_tf1d_ext_lut", "cvr_set_extinction_sat", "cvr_copy_extinction_sat", "cvr_render_extbsd",
@@ -181,6 +181,7 @@ def lib() -> ctypes.CDLL:
         "cvr_read_tf1d": ([ctypes.c_char_p, FP, IP], I),
         "cvr_read_raw": ([ctypes.c_char_p, P, ctypes.c_size_t, IP, IP, IP, IP], I),
         "cvr_read_syn": ([ctypes.c_char_p, P, ctypes.c_size_t, IP, IP, IP], I),
+        "cvr_read_pvm": ([ctypes.c_char_p, P, ctypes.c_size_t, IP, IP, IP, IP, FP], I),
         "cvr_read_camera_state": ([ctypes.c_char_p, I, ctypes.POINTER(Camera), ctypes.c_char_p,
                                    I, IP], I),
         "cvr_read_light_position": ([ctypes.c_char_p, I, I, FP, IP], I),

@@ -2,6 +2,7 @@
 // reference readers are MSVC-only (fopen_s, sscanf_s, `unsigned char(v)` casts:
 // libs/file_utils/rawloader.cpp:16, libs/volvis_utils/reader.cpp:317,352), so
 // they are re-implemented here with the same grammar and semantics.
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -17,6 +18,168 @@ namespace {
 std::string basename_of(const std::string& p) {
   size_t a = p.find_last_of("/\\");
   return a == std::string::npos ? p : p.substr(a + 1);
+}
+
+// ---------------------------------------------------------------------------
+// PVM / DDS (the V^3 volume format of libs/file_utils/pvm.cpp:191-620).  A .pvm
+// file is either plain or a "Differential Data Stream": an 8-byte id ("DDS v3d\n",
+// or "DDS v3e\n" = interleaved in blocks of 2^24 bytes) and a bit stream of
+// big-endian 32-bit words, MSB first.  The stream holds 2 bits (skip - 1),
+// 16 bits (strip - 1), then runs: 7 bits run length (0 ends the stream), 3 bits
+// code -> bits per delta (code >= 1 ? code + 1 : code), and `run` deltas of
+// that many bits biased by 2^bits / 2.  A delta adds to the running byte value
+// (mod 256), plus, past the first `strip` bytes (strip > 1), the difference of
+// the two bytes one `strip` earlier.  The bytes are then re-interleaved with
+// stride `skip` (DDS_interleave).  The payload is the PVM text header, the
+// voxels and (PVM3) four strings.
+// ---------------------------------------------------------------------------
+struct DdsBits {
+  const unsigned char* data;
+  size_t size, pos = 0;        // size padded to whole words, zeros past the end
+  uint32_t buffer = 0;
+  uint32_t bufsize = 0;
+  static uint32_t shl(uint32_t v, uint32_t b) { return b >= 32 ? 0u : v << b; }
+  static uint32_t shr(uint32_t v, uint32_t b) { return b >= 32 ? 0u : v >> b; }
+  uint32_t read(uint32_t bits) {
+    uint32_t value;
+    if (bits < bufsize) {
+      bufsize -= bits;
+      value = shr(buffer, bufsize);
+    } else {
+      value = shl(buffer, bits - bufsize);
+      if (pos >= size) {
+        buffer = 0;
+      } else {
+        buffer = (uint32_t)data[pos] << 24 | (uint32_t)data[pos + 1] << 16 |
+                 (uint32_t)data[pos + 2] << 8 | (uint32_t)data[pos + 3];
+        pos += 4;
+      }
+      bufsize += 32 - bits;
+      value |= shr(buffer, bufsize);
+    }
+    buffer &= shl(1, bufsize) - 1;
+    return value;
+  }
+};
+
+// DDS_deinterleave(..., restore = true): undo the encoder's stride-`skip` split,
+// whole or per block of skip*block bytes.
+void dds_interleave(std::vector<unsigned char>& d, size_t skip, size_t block) {
+  if (skip <= 1) return;
+  const size_t bytes = d.size();
+  auto run = [&](size_t off, size_t len) {
+    std::vector<unsigned char> t(len);
+    size_t p = off;
+    for (size_t i = 0; i < skip; i++)
+      for (size_t j = i; j < len; j += skip) t[j] = d[p++];
+    std::memcpy(&d[off], t.data(), len);
+  };
+  if (block == 0) {
+    run(0, bytes);
+    return;
+  }
+  size_t k = 0;
+  for (; k < bytes / skip / block; k++) run(k * skip * block, skip * block);
+  if (bytes > k * skip * block) run(k * skip * block, bytes - k * skip * block);
+}
+
+bool dds_decode(std::vector<unsigned char> chunk, size_t block, std::vector<unsigned char>& out) {
+  chunk.resize((chunk.size() + 3) / 4 * 4 + 4, 0);
+  DdsBits b{chunk.data(), chunk.size() - 4};
+  const size_t skip = b.read(2) + 1;
+  const size_t strip = b.read(16) + 1;
+  out.clear();
+  int act = 0;
+  for (;;) {
+    const uint32_t run = b.read(7);                   // DDS_RL
+    if (run == 0) break;
+    const uint32_t code = b.read(3);
+    const uint32_t bits = code >= 1 ? code + 1 : code;
+    for (uint32_t k = 0; k < run; k++) {
+      const size_t cnt = out.size();
+      if (strip == 1 || cnt <= strip)
+        act += (int)b.read(bits) - (int)((1u << bits) / 2);
+      else
+        act += (int)out[cnt - strip] - (int)out[cnt - strip - 1] + (int)b.read(bits) -
+               (int)((1u << bits) / 2);
+      while (act < 0) act += 256;
+      while (act > 255) act -= 256;
+      out.push_back((unsigned char)act);
+      if (out.size() > ((size_t)1 << 36)) return false;   // corrupt stream
+    }
+  }
+  dds_interleave(out, skip, block);
+  return true;
+}
+
+bool read_file(const char* path, std::vector<unsigned char>& buf) {
+  FILE* fp = std::fopen(path, "rb");
+  if (!fp) return false;
+  buf.clear();
+  unsigned char tmp[1 << 16];
+  size_t n;
+  while ((n = std::fread(tmp, 1, sizeof(tmp), fp)) > 0) buf.insert(buf.end(), tmp, tmp + n);
+  std::fclose(fp);
+  return true;
+}
+
+struct Pvm {
+  int w = 0, h = 0, d = 0, comps = 0;
+  float scale[3] = {1.f, 1.f, 1.f};
+  std::vector<unsigned char> payload;
+  size_t data_off = 0;
+};
+
+// DDSV3::readPVMvolume (pvm.cpp:191-308) minus the description strings
+bool read_pvm(const char* path, Pvm& v) {
+  std::vector<unsigned char> file;
+  if (!read_file(path, file) || file.empty()) return false;
+  static const char kV3d[] = "DDS v3d\n", kV3e[] = "DDS v3e\n";
+  if (file.size() >= 8 && (!std::memcmp(file.data(), kV3d, 8) || !std::memcmp(file.data(), kV3e, 8))) {
+    const bool v3e = !std::memcmp(file.data(), kV3e, 8);
+    std::vector<unsigned char> chunk(file.begin() + 8, file.end());
+    if (chunk.empty() || !dds_decode(std::move(chunk), v3e ? ((size_t)1 << 24) : 0, v.payload))
+      return false;
+  } else {
+    v.payload.swap(file);                                // readRAWfile: uncompressed
+  }
+  std::vector<unsigned char>& p = v.payload;
+  if (p.size() < 5) return false;
+  p.push_back(0);                                        // the reader's '\0' guard
+  const char* c = (const char*)p.data();
+  int version = 1;
+  const char* q;
+  if (!std::strncmp(c, "PVM\n", 4)) {
+    q = c + 4;
+    while (*q == '#')
+      while (*q && *q++ != '\n') {}
+    if (std::sscanf(q, "%d %d %d", &v.w, &v.h, &v.d) != 3) return false;
+  } else {
+    if (!std::strncmp(c, "PVM2\n", 5)) version = 2;
+    else if (!std::strncmp(c, "PVM3\n", 5)) version = 3;
+    else return false;
+    q = c + 5;
+    if (std::sscanf(q, "%d %d %d\n%g %g %g", &v.w, &v.h, &v.d, &v.scale[0], &v.scale[1],
+                    &v.scale[2]) != 6)
+      return false;
+    if (!(v.scale[0] > 0.f && v.scale[1] > 0.f && v.scale[2] > 0.f)) return false;
+    q = std::strchr(q, '\n');
+    if (!q) return false;
+    q++;
+  }
+  if (v.w < 1 || v.h < 1 || v.d < 1) return false;
+  q = std::strchr(q, '\n');                               // past the dims (v1) / scale (v2, v3)
+  if (!q) return false;
+  q++;
+  if (std::sscanf(q, "%d", &v.comps) != 1 || v.comps < 1) return false;
+  q = std::strchr(q, '\n');
+  if (!q) return false;
+  q++;
+  v.data_off = (size_t)(q - c);
+  const size_t need = (size_t)v.w * v.h * v.d * v.comps;
+  const size_t have = p.size() - 1 - v.data_off;
+  if (version == 3 ? have < need : have != need) return false;
+  return true;
 }
 
 }  // namespace
@@ -218,6 +381,32 @@ cvr_status cvr_read_light_position(const char* path, int list, int light, float 
   if (st == CVR_OK && out_pos)
     for (int i = 0; i < 3; i++) out_pos[i] = l.position[i];
   return st;
+}
+
+// VolumeReader::readpvm + Pvm::PostProcessData (reader.cpp:100-159,
+// pvm.cpp:23-109): 1 component -> u8, 2 components -> u16 assembled as
+// data[2i] + 256 * data[2i+1] (the reference's byte order); more components are
+// not a scalar volume (CVR_ERR_IO).  scale receives the PVM2/3 voxel spacing
+// (1, 1, 1 for PVM1).  Pass voxels = NULL to query the dimensions.
+cvr_status cvr_read_pvm(const char* path, void* voxels, size_t capacity, int* out_w, int* out_h,
+                        int* out_d, int* out_bpv, float out_scale[3]) {
+  if (!path || !out_w || !out_h || !out_d || !out_bpv) return CVR_ERR_ARG;
+  Pvm v;
+  if (!read_pvm(path, v) || v.comps > 2) return CVR_ERR_IO;
+  *out_w = v.w; *out_h = v.h; *out_d = v.d; *out_bpv = v.comps;
+  if (out_scale)
+    for (int i = 0; i < 3; i++) out_scale[i] = v.scale[i];
+  if (!voxels) return CVR_OK;
+  const size_t n = (size_t)v.w * v.h * v.d;
+  if (capacity < n * v.comps) return CVR_ERR_ARG;
+  const unsigned char* src = v.payload.data() + v.data_off;
+  if (v.comps == 1) {
+    std::memcpy(voxels, src, n);
+  } else {
+    uint16_t* o = static_cast<uint16_t*>(voxels);
+    for (size_t i = 0; i < n; i++) o[i] = (uint16_t)(src[2 * i] + 256u * src[2 * i + 1]);
+  }
+  return CVR_OK;
 }
 
 #pragma GCC visibility pop

@@ -125,7 +125,8 @@ class DataManager:
         self.tf_rgba = rgba
 
     def ReadVolume(self, path: str, scale=None):
-        """.raw (name.<bytes>.<W>x<H>x<D>.raw) or .syn, like VolumeReader::ReadStructuredVolume."""
+        """.raw (name.<bytes>.<W>x<H>x<D>.raw), .syn or .pvm, like
+        VolumeReader::ReadStructuredVolume (reader.cpp:24-60)."""
         L = N.lib()
         w, h, d, b = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         bp = path.encode()
@@ -138,6 +139,15 @@ class DataManager:
             N.check(L.cvr_read_syn(bp, None, 0, w, h, d), "cvr_read_syn")
             vox = np.empty((d.value, h.value, w.value), dtype=np.uint8)
             N.check(L.cvr_read_syn(bp, vox.ctypes.data, vox.nbytes, w, h, d), "cvr_read_syn")
+        elif path.endswith(".pvm"):
+            # VolumeReader::readpvm (reader.cpp:100-159): the PVM2/3 spacing is the scale
+            sc = (ctypes.c_float * 3)()
+            N.check(L.cvr_read_pvm(bp, None, 0, w, h, d, b, sc), "cvr_read_pvm")
+            dt = np.uint8 if b.value == 1 else np.uint16
+            vox = np.empty((d.value, h.value, w.value), dtype=dt)
+            N.check(L.cvr_read_pvm(bp, vox.ctypes.data, vox.nbytes, w, h, d, b, sc),
+                    "cvr_read_pvm")
+            scale = scale or tuple(float(v) for v in sc)
         else:
             raise ValueError(f"unsupported volume format: {path}")
         self.SetVolume(vox, scale or (1.0, 1.0, 1.0), name=path)

@@ -481,6 +481,13 @@ cvr_status  cvr_read_tf1d(const char* path, float* out_rgbt, int* out_n);
 cvr_status  cvr_read_raw(const char* path, void* voxels, size_t capacity,
                          int* out_w, int* out_h, int* out_d, int* out_bytes_per_voxel);
 
+/* .pvm reader (VolumeReader::readpvm, reader.cpp:100-159; DDSV3 decoder,
+ * libs/file_utils/pvm.cpp:191-620): plain or DDS-compressed PVM/PVM2/PVM3,
+ * 1 component -> u8, 2 -> u16 (data[2i] + 256*data[2i+1], as Pvm::PostProcessData).
+ * out_scale (may be NULL) receives the PVM2/3 voxel spacing.  voxels = NULL queries. */
+cvr_status  cvr_read_pvm(const char* path, void* voxels, size_t capacity, int* out_w,
+                         int* out_h, int* out_d, int* out_bytes_per_voxel, float out_scale[3]);
+
 /* .syn reader (VolumeReader::readsyn, reader.cpp:283-371); u8 voxels. */
 cvr_status  cvr_read_syn(const char* path, uint8_t* voxels, size_t capacity,
                          int* out_w, int* out_h, int* out_d);
