@@ -1103,6 +1103,11 @@ cvr_status cvr_set_extinction_volume(cvr_ctx* ctx, const float* tf_rgba, int n, 
   }
   for (int i = 0; i < 3; i++) c->ext_res[i] = res[i];
   c->ext_levels = nl;
+  {   // level values are Gaussian averages of these opacities: all < 1 -> finite tau
+    bool fin = true;
+    for (size_t i = 3; i < q.size(); i += 4) fin = fin && q[i] >= 0.0f && q[i] < 1.0f;
+    c->ext_finite = fin ? 1 : 0;
+  }
   for (int L = 0; L <= nl; L++) c->ext_off[L] = off[L];
   c->ext_sigma0 = sigma0;
   c->cone_valid = 0;
@@ -1209,6 +1214,7 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   }
   // SpotLightMaxAngle: glm::cos(glm::pi<float>() * angle / 180.f) (dosrcrenderer.cpp:158)
   Q.spot_cos = std::cos(3.14159265358979323846f * p->light.spot_angle_deg / 180.0f);
+  Q.zero_skip = c->ext_finite;
   for (int k = 0; k < 2; k++) {
     cvr::DosCone& C = k ? Q.sdw : Q.occ;
     const cvr_cone_tables& T = c->cone_tab[k];

@@ -86,6 +86,7 @@ struct DosArgs {
   float ka, kd, ks;                  // Kambient if occlusion, Kdiffuse/Kspecular if shadow, else 0
   float lfwd[3], lup[3], lright[3];  // light camera vectors (RenderingParameters)
   float spot_cos;                    // SpotLightMaxAngle uniform
+  int zero_skip;                     // every pyramid value finite: taps with a 0 border factor are 0
   DosCone occ, sdw;
 };
 
@@ -209,6 +210,7 @@ struct Ctx {
   int sat_dims[3] = {0, 0, 0};
   int ext_res[3] = {0, 0, 0};
   int ext_levels = 0;
+  int ext_finite = 0;                // every TF opacity < 1: the pyramid's extinctions are finite
   long long ext_off[kMaxExtLevels + 1] = {};
   float ext_sigma0 = 1.0f;
   // cone tables on the device (occlusion, shadow), rebuilt when their params change

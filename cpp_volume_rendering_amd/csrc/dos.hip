@@ -236,22 +236,31 @@ __device__ __forceinline__ ExtTap ext_tap(const ExtLevel& l, f3 p) {
   return t;
 }
 
-__device__ __forceinline__ float ext_value(const DosArgs& Q, uint4 raw, const ExtTap& t, f3 p,
-                                           float mip) {
+// The CONSIDER_BORDERS exponent of a tap outside the box: -(dist) / ((2 sg) sg)
+// with sg = pow(2, mip); the divisor is 2^(2 mip + 1), so the quotient is exactly
+// the product with 2^-(2 mip + 1).  dist = |clamp(p, 0, G) - p|^2.
+__device__ __forceinline__ float border_exponent(const DosArgs& Q, f3 p, float mip) {
+  const float inv = ldexpf(1.0f, -(2 * (int)mip + 1));
+  // clamp(p, 0, G) - p (positions are finite: med3 == min(max()))
+  const float cx = __builtin_amdgcn_fmed3f(p.x, 0.0f, Q.G[0]) - p.x;
+  const float cy = __builtin_amdgcn_fmed3f(p.y, 0.0f, Q.G[1]) - p.y;
+  const float cz = __builtin_amdgcn_fmed3f(p.z, 0.0f, Q.G[2]) - p.z;
+  const float dist = (cx * cx + cy * cy) + cz * cz;
+  return -(dist) * inv;
+}
+
+__device__ __forceinline__ bool outside_box(const DosArgs& Q, f3 p) {
+  return (p.x < 0.0f) | (p.x > Q.G[0]) | (p.y < 0.0f) | (p.y > Q.G[1]) | (p.z < 0.0f) |
+         (p.z > Q.G[2]);
+}
+
+__device__ __forceinline__ float ext_value(const DosArgs& Q, uint4 raw, const ExtTap& t,
+                                           bool outside, float xb) {
   float rg = trilerp_cell(raw, t.ax, t.ay, t.az);
-  const bool outside = (p.x < 0.0f) | (p.x > Q.G[0]) | (p.y < 0.0f) | (p.y > Q.G[1]) |
-                       (p.z < 0.0f) | (p.z > Q.G[2]);
-  if (outside) {
-    // -(dist) / ((2 sg) sg) with sg = pow(2, mip): the divisor is 2^(2 mip + 1),
-    // so the quotient is exactly the product with 2^-(2 mip + 1)
-    const float inv = ldexpf(1.0f, -(2 * (int)mip + 1));
-    // clamp(p, 0, G) - p (positions are finite: med3 == min(max()))
-    const float cx = __builtin_amdgcn_fmed3f(p.x, 0.0f, Q.G[0]) - p.x;
-    const float cy = __builtin_amdgcn_fmed3f(p.y, 0.0f, Q.G[1]) - p.y;
-    const float cz = __builtin_amdgcn_fmed3f(p.z, 0.0f, Q.G[2]) - p.z;
-    const float dist = (cx * cx + cy * cy) + cz * cz;
-    rg = rg * cvr_expf_nonpos(-(dist) * inv);
-  }
+#ifdef CVR_DOS_EXPERIMENT_NO_BORDER   // cost probes only (tools/build_variant.sh): wrong images
+  return rg;
+#endif
+  if (outside) rg = rg * cvr_expf_nonpos(xb);
   return rg;
 }
 
@@ -285,24 +294,35 @@ __device__ __forceinline__ void cone_sections(const DosArgs& Q, const DosCone& C
                                               const uint4* __restrict__ ext, const float4 (&e)[U],
                                               const float (&tr)[U], const f3 (&vk)[J], f3 pos,
                                               float (&rays)[7], float (&last)[7]) {
-  f3 p[U][JN];
   ExtTap tap[U][JN];
   uint4 raw[U][JN];
+  float xb[U][JN];
+  bool out[U][JN], zero[U][JN];
 #pragma unroll
   for (int q = 0; q < U; q++) {
     const ExtLevel l = load_level(Q.levels, level_of(Q, e[q].y));
 #pragma unroll
     for (int j = 0; j < JN; j++) {
-      p[q][j] = vmad(vk[J0 + j], tr[q], pos);
-      tap[q][j] = ext_tap(l, p[q][j]);
-      raw[q][j] = *(const uint4*)((const char*)ext + tap[q][j].off);
+      const f3 p = vmad(vk[J0 + j], tr[q], pos);
+      tap[q][j] = ext_tap(l, p);
+      out[q][j] = outside_box(Q, p);
+      xb[q][j] = out[q][j] ? border_exponent(Q, p, e[q].y) : 0.0f;
+      // Far outside the box the border factor is exactly 0 (exp below -86), and
+      // so is the tap (a finite extinction times 0): no fetch, no filter
+      zero[q][j] = Q.zero_skip && xb[q][j] < -86.0f;
+#ifdef CVR_DOS_EXPERIMENT_NO_FETCH    // cost probes only: wrong images
+      raw[q][j] = make_uint4(tap[q][j].off, tap[q][j].off, tap[q][j].off, tap[q][j].off);
+#else
+      if (!zero[q][j]) raw[q][j] = *(const uint4*)((const char*)ext + tap[q][j].off);
+#endif
     }
   }
 #pragma unroll
   for (int q = 0; q < U; q++)
 #pragma unroll
     for (int j = 0; j < JN; j++) {
-      const float v = ext_value(Q, raw[q][j], tap[q][j], p[q][j], e[q].y) * e[q].w;
+      const float v =
+          zero[q][j] ? 0.0f : ext_value(Q, raw[q][j], tap[q][j], out[q][j], xb[q][j]) * e[q].w;
       rays[J0 + j] += ((last[J0 + j] + v) * e[q].z) * C.ui_weight;
       last[J0 + j] = v;
     }
