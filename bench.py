@@ -46,6 +46,9 @@ sys.path.insert(0, ROOT)
 from cpp_volume_rendering_amd import _native as N  # noqa: E402
 from cpp_volume_rendering_amd import datasets as D  # noqa: E402
 from cpp_volume_rendering_amd import screen_tiles as T  # noqa: E402
+from cpp_volume_rendering_amd.renderer import (CustomRayCasting1PassIsoAdapt,  # noqa: E402
+                                               CustomRayCasting1PassIsodfsAdapt,
+                                               RayCasting1PassIsoAdapt)
 from cpp_volume_rendering_amd.renderer import (Camera, DataManager, RayCasting1Pass,  # noqa: E402
                                                RC1PConeTracingDirOcclusionShading,
                                                RC1PExtinctionBasedShading, RenderingParameters,
@@ -61,7 +64,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=-1, help="default 5 (dos: 1)")
     p.add_argument("--size", type=int, default=0, help="volume N^3 (default 512; ebs 1024)")
     p.add_argument("--res", type=int, default=0, help="viewport (default 1024; dos 2048)")
-    p.add_argument("--renderer", choices=["rc1pass", "dos", "ebs"], default="rc1pass")
+    p.add_argument("--renderer", choices=["rc1pass", "dos", "ebs", "iso", "isodfs", "isoadapt"],
+                   default="rc1pass",
+                   help="iso / isodfs / isoadapt: the isosurface ray-casters (variants 0 / 1 / 2)")
     p.add_argument("--tile", type=int, default=32)
     p.add_argument("--field", choices=["ml", "blobs"], default="ml")
     p.add_argument("--phong", action="store_true")
@@ -85,7 +90,7 @@ def parse():
 
 
 def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgba=None,
-                 phong=None, half=False):
+                 phong=None, half=False, iso=None):
     """The CPU oracle (C++/OpenMP restatement of ray_marching_1p.comp; the reference has
     no CPU ray-caster) on the host cores: whole frames of the same workload, repeated
     until `seconds` of wall time are spent (each frame starts from the centre band of
@@ -101,6 +106,11 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgb
     grad = O.gradient(vol, "fd") if phong is not None else None
 
     def render_rows_full(y0, y1, nthreads):
+        if iso is not None:
+            return O.render_iso(v16, vol, scale, cam, W, H, variant=iso["variant"], grad=grad,
+                                phong=phong is not None,
+                                light=phong["light"] if phong is not None else (0, 0, 0),
+                                rows=(y0, y1), threads=nthreads)
         if dos is not None:
             return O.render_dos(v16, scale, tf, levels, cam, W, H, step, dos["occ"], dos["sdw"],
                                 apply_shadow=True, light=dos["light"], rows=(y0, y1),
@@ -265,6 +275,8 @@ def main():
 
     dos = a.renderer == "dos"
     ebs = a.renderer == "ebs"
+    iso_variant = {"iso": 0, "isodfs": 1, "isoadapt": 2}.get(a.renderer)
+    iso = iso_variant is not None
     shaded = dos or ebs
     a.steps = a.steps or (5 if dos else (2 if ebs else 50))
     a.warmup = a.warmup if a.warmup >= 0 else (1 if shaded else 5)
@@ -290,6 +302,9 @@ def main():
     elif ebs:
         dm.SetExtinctionTable(build_ext_lut(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
         r = RC1PExtinctionBasedShading(local if world > 1 else 0)
+    elif iso:
+        r = (CustomRayCasting1PassIsoAdapt, CustomRayCasting1PassIsodfsAdapt,
+             RayCasting1PassIsoAdapt)[iso_variant](local if world > 1 else 0)
     else:
         r = RayCasting1Pass(local if world > 1 else 0)
     r.m_apply_gradient_shading = a.phong
@@ -312,7 +327,7 @@ def main():
     # the per-GPU share of the frame shrinks with N: at 8 GPUs the longest rays set
     # a rank's frame time, and 4 lanes per ray on the longest 10 % of tiles pay off
     quad = a.quad if a.quad >= 0 else (10 if world >= 8 else 0)
-    if not shaded:
+    if a.renderer == "rc1pass":
         N.check(N.lib().cvr_set_option(r.device.handle, b"quad", quad), "quad", r.device.handle)
     try:
         # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
@@ -346,7 +361,7 @@ def main():
 
     # samples per frame (this rank), counted by the kernel; for the shaded renderer
     # also the shaded / shadow-lit samples (each traces a fixed number of cone fetches)
-    count_shaded = shaded or a.phong
+    count_shaded = shaded or (a.phong and not iso)
     if count_shaded:
         N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 1), "opt", r.device.handle)
     step_once()
@@ -424,7 +439,8 @@ def main():
         # per sample + the output pixel (RGBA16F 8 B, RGBA32F 16 B) (+ 48 B per shaded
         # sample for the Phong gradient: 8 corners x 3 fp16, counted by the kernel)
         px_bytes = 8 if fmt == N.FORMAT_RGBA16F else 16
-        b_alg = 8 * 1 * S_rank + px_bytes * pixels + (48 * int(shade[0]) if a.phong else 0)
+        # (iso: 8 B per volume fetch + the pixel; the <= 1 gradient fetch per hit is left out)
+        b_alg = 8 * 1 * S_rank + px_bytes * pixels + (48 * int(shade[0]) if count_shaded and a.phong else 0)
         fetches = int(shade[2])
         if dos:
             # + 8 fp16 corners (16 B) per trilinear extinction fetch of the cones
@@ -438,6 +454,7 @@ def main():
         wkey = f"{a.renderer}_{a.field}{n}_{W}x{H}{'_phong' if a.phong else ''}"
         kname = ("shaded_march_kernel<DosShader>" if dos else
                  "shaded_march_kernel<EbsShader>" if ebs else
+                 f"iso_tile_kernel<{iso_variant}, {str(a.phong).lower()}>" if iso else
                  f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, *, false, true>")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -445,7 +462,7 @@ def main():
                 "kernel": kname,
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank}
-        if a.phong:
+        if a.phong and count_shaded:
             roof["phong_shaded_samples"] = int(shade[0])
         if dos:
             roof.update({"shaded_samples": shade[0], "shadow_lit_samples": shade[1],
@@ -459,6 +476,8 @@ def main():
                   f"{n}^3 volume at {W}^2" if dos else
                   "Msamples/s (rays x steps), Extinction-Based Shading (SAT AO + SAT shadows), "
                   f"{n}^3 volume at {W}^2" if ebs else
+                  f"Msamples/s (volume fetches), isosurface ray-caster '{r.GetName()}', "
+                  f"{n}^3 volume at {W}^2" if iso else
                   f"Msamples/s (rays x steps), rc1pass ray-march, {n}^3 volume at {W}^2")
         res = {
             "metric": metric,
@@ -478,10 +497,13 @@ def main():
                                     f"shadows (0.5 deg), extinction pyramid 128^3, " if dos else
                                     f"rc1pextbsd SAT AO (15 shells) + point-light SAT box-chain "
                                     f"shadows (1 deg cone), extinction SAT {n + 2}^3, " if ebs else
+                                    f"{r.GetName()} (isovalue 0.5, steps 0.05/1.0/0.1, blocks "
+                                    f"{tuple(r.num_blocks) if iso_variant != 2 else 'none'}), "
+                                    if iso else
                                     f"rc1pass emission-absorption, ")
                                    + f"Marschner-Lobb {n}^3 u8 "
                                    f"({a.field}), {W}x{H}, bonsai_01.tf1d, camera "
-                                   f"'Initial State', step 0.5, ERT 0.99"
+                                   f"'Initial State'" + ("" if iso else ", step 0.5, ERT 0.99")
                                    + (", Blinn-Phong FD gradient" if a.phong else ""),
                        "volume": n, "viewport": [W, H], "samples_per_frame": S_all,
                        "parallelism": f"screen tiles {tile}x{tile} over {world} GPU(s)"
@@ -489,7 +511,7 @@ def main():
                        "storage": "cell8 fp16 (16 B/cell, x-fastest)",
                        "frame_format": a.format,
                        "frames_in_flight": split.nstreams,
-                       "quad_pct": quad if not shaded else 0,
+                       "quad_pct": quad if a.renderer == "rc1pass" else 0,
                        "empty_space_skip": f"macro cells 2^{macro}, auto (on at >= 15 % empty)"
                                            if macro > 0 else "off"},
             "roofline": roof,
@@ -530,7 +552,8 @@ def main():
             phong_cfg = {"light": rp.light_position} if a.phong else None
             res["cpu_baseline"] = cpu_baseline(vol, scale, tf, D.INITIAL_STATE_CAMERA, W, H,
                                                a.cpu_seconds, dos_cfg, ebs_cfg, gpu_img, phong_cfg,
-                                               half=fmt == N.FORMAT_RGBA16F)
+                                               half=fmt == N.FORMAT_RGBA16F,
+                                               iso={"variant": iso_variant} if iso else None)
             if "parity" in res["cpu_baseline"]:
                 res["parity"] = res["cpu_baseline"].pop("parity")
         print(json.dumps(res))

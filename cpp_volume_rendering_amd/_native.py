@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "cvr_comm_unique_id", "cvr_comm_init", "cvr_comm_destroy", "cvr_gather_tiles",
     "cvr_gather_tiles_n", "cvr_unpack_tiles_device_n",
     "cvr_gather_sync", "cvr_multiscale_resolution", "cvr_multiscale_filter",
-    "cvr_screenshot_rgb8",
+    "cvr_screenshot_rgb8", "cvr_iso_params_default", "cvr_render_iso", "cvr_iso_block_ranges",
 )
 SINGLE_RAY_PER_PIXEL, MULTIPLE_RAYS_PER_PIXEL, DOWN_SCALING_RENDER, UP_SCALING_RENDER = range(4)
 (FILTER_BOX, FILTER_HAT, FILTER_CATMULL_ROM, FILTER_MITCHELL_NETRAVALI, FILTER_CARDINAL_BSPLINE_3,
@@ -120,6 +120,16 @@ class EbsParams(ctypes.Structure):
                 ("shadow_ui_weight", ctypes.c_float), ("shadow_max_distance", ctypes.c_float)]
 
 
+class IsoParams(ctypes.Structure):
+    _fields_ = [("variant", ctypes.c_int), ("num_blocks", ctypes.c_int * 3),
+                ("isovalue", ctypes.c_float), ("step_small", ctypes.c_float),
+                ("step_large", ctypes.c_float), ("step_range", ctypes.c_float),
+                ("color", ctypes.c_float * 4), ("apply_gradient_shading", ctypes.c_int),
+                ("ka", ctypes.c_float), ("kd", ctypes.c_float), ("ks", ctypes.c_float),
+                ("shininess", ctypes.c_float), ("ispecular", ctypes.c_float * 3),
+                ("light_pos", ctypes.c_float * 3)]
+
+
 _lib = None
 
 
@@ -196,6 +206,10 @@ def lib() -> ctypes.CDLL:
         "cvr_copy_extinction_sat": ([P, FP, ctypes.c_size_t, IP], I),
         "cvr_render_extbsd": ([P, ctypes.POINTER(Frame), ctypes.POINTER(EbsParams),
                                ctypes.POINTER(Output)], I),
+        "cvr_iso_params_default": ([I, ctypes.POINTER(IsoParams)], None),
+        "cvr_render_iso": ([P, ctypes.POINTER(Frame), ctypes.POINTER(IsoParams),
+                            ctypes.POINTER(Output)], I),
+        "cvr_iso_block_ranges": ([P, IP, FP, FP], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

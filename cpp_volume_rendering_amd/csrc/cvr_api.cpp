@@ -243,6 +243,7 @@ void cvr_destroy(cvr_ctx* ctx) {
   free_dev(c->d_cells);
   void* p = c->d_tf; free_dev(p); c->d_tf = nullptr;
   free_dev(c->d_grad);
+  p = c->d_iso_mm; free_dev(p); c->d_iso_mm = nullptr;
   p = c->d_lut; free_dev(p); c->d_lut = nullptr;
   p = c->d_macro_minmax; free_dev(p); c->d_macro_minmax = nullptr;
   p = c->d_occ; free_dev(p); c->d_occ = nullptr;
@@ -450,6 +451,7 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
   free_dev(c->d_vox); c->vox_bytes = 0;
   free_dev(c->d_cells); c->cells_bytes = 0;
   free_dev(c->d_grad); c->grad_bytes = 0; c->grad_mode = 0;
+  c->iso_valid = 0;
   c->N[0] = w; c->N[1] = h; c->N[2] = d;
   for (int i = 0; i < 3; i++) c->scale[i] = scale[i];
   c->bpv = bpv;
@@ -1388,6 +1390,141 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
   return render_shaded(c, o, ntiles, npix, [&](float4* out, uint32_t* smp, unsigned long long* shade,
                                                 unsigned long long* ts, hipStream_t st) {
     return cvr::launch_ebs(*c, Q, out, smp, shade, ts, st);
+  });
+}
+
+
+
+// ---------------------------------------------------------------------------
+// Isosurface ray-casters with block skipping (rc1pisocustom, rc1pisodfscustom)
+// ---------------------------------------------------------------------------
+
+void cvr_iso_params_default(int variant, cvr_iso_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->variant = variant;
+  const int nb = variant == 1 ? 32 : 4;          // :190 of either renderer
+  for (int i = 0; i < 3; i++) p->num_blocks[i] = nb;
+  p->isovalue = 0.5f;                           // constructor defaults (:119-127)
+  p->step_small = 0.05f;
+  p->step_large = 1.0f;
+  p->step_range = 0.1f;
+  p->color[0] = 0.66f; p->color[1] = 0.6f; p->color[2] = 0.05f; p->color[3] = 1.0f;
+  p->ka = 0.5f; p->kd = 0.5f; p->ks = 0.8f; p->shininess = 30.0f;
+  for (int i = 0; i < 3; i++) p->ispecular[i] = 1.0f;
+}
+
+// The block table for nb: raw extremes on the GPU, normalised here exactly as
+// ComputeBlocksFromVolume stores them (v / 255 or v / 65535 in double, pushed
+// into a float vector; empty blocks keep numeric_limits<float>::max / lowest).
+static cvr_status ensure_iso_blocks(Ctx* c, const int nb[3]) {
+  if (c->iso_valid && c->d_iso_mm && c->iso_nb[0] == nb[0] && c->iso_nb[1] == nb[1] &&
+      c->iso_nb[2] == nb[2])
+    return CVR_OK;
+  const size_t n = (size_t)nb[0] * nb[1] * nb[2];
+  HIP_TRY(c, hipSetDevice(c->device));
+  uint2* d_raw = nullptr;
+  HIP_TRY(c, hipMalloc((void**)&d_raw, n * sizeof(uint2)));
+  std::vector<uint2> raw(n);
+  hipError_t e = cvr::launch_block_minmax(c->d_vox, c->bpv, c->N, nb, d_raw, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(raw.data(), d_raw, n * sizeof(uint2), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_raw);
+  if (e != hipSuccess) return fail(c, CVR_ERR_HIP, "cvr_render_iso: block table: %s", hipGetErrorString(e));
+  const double mx = c->bpv == 1 ? 255.0 : 65535.0;
+  std::vector<float2> mm(n);
+  for (size_t i = 0; i < n; i++) {
+    if (raw[i].x > raw[i].y) {
+      mm[i] = make_float2(3.40282347e38f, -3.40282347e38f);
+    } else {
+      mm[i] = make_float2((float)((double)raw[i].x / mx), (float)((double)raw[i].y / mx));
+    }
+  }
+  if (c->d_iso_mm && (c->iso_nb[0] * c->iso_nb[1] * c->iso_nb[2]) != (int)n) {
+    void* p = c->d_iso_mm; free_dev(p); c->d_iso_mm = nullptr;
+  }
+  if (!c->d_iso_mm) HIP_TRY(c, hipMalloc((void**)&c->d_iso_mm, n * sizeof(float2)));
+  HIP_TRY(c, hipMemcpy(c->d_iso_mm, mm.data(), n * sizeof(float2), hipMemcpyHostToDevice));
+  for (int i = 0; i < 3; i++) c->iso_nb[i] = nb[i];
+  c->iso_valid = 1;
+  return CVR_OK;
+}
+
+static void iso_blocks_of(const cvr_iso_params* p, int nb[3]) {
+  for (int i = 0; i < 3; i++)
+    nb[i] = p->num_blocks[i] > 0 ? p->num_blocks[i] : (p->variant == 1 ? 32 : 4);
+}
+
+cvr_status cvr_iso_block_ranges(cvr_ctx* ctx, const int num_blocks[3], float* out_min, float* out_max) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!num_blocks || !out_min || !out_max) return fail(c, CVR_ERR_ARG, "cvr_iso_block_ranges: null argument");
+  if (!c->d_vox) return fail(c, CVR_ERR_STATE, "cvr_iso_block_ranges: no volume set");
+  for (int i = 0; i < 3; i++)
+    if (num_blocks[i] < 1 || num_blocks[i] > 1024)
+      return fail(c, CVR_ERR_ARG, "cvr_iso_block_ranges: bad block count %d", num_blocks[i]);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  cvr_status st = ensure_iso_blocks(c, num_blocks);
+  if (st != CVR_OK) return st;
+  const size_t n = (size_t)num_blocks[0] * num_blocks[1] * num_blocks[2];
+  std::vector<float2> mm(n);
+  HIP_TRY(c, hipMemcpy(mm.data(), c->d_iso_mm, n * sizeof(float2), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < n; i++) { out_min[i] = mm[i].x; out_max[i] = mm[i].y; }
+  return CVR_OK;
+}
+
+cvr_status cvr_render_iso(cvr_ctx* ctx, const cvr_frame* f, const cvr_iso_params* p,
+                          const cvr_output* o) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_iso: null argument");
+  if (o->format != CVR_FORMAT_RGBA32F && o->format != CVR_FORMAT_RGBA16F)
+    return fail(c, CVR_ERR_ARG, "cvr_render_iso: unknown output format %d", o->format);
+  if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
+    return fail(c, CVR_ERR_ARG, "cvr_render_iso: bad viewport %dx%d", f->width, f->height);
+  if (!c->d_cells || !c->d_vox) return fail(c, CVR_ERR_STATE, "cvr_render_iso: no volume set");
+  if (p->variant < 0 || p->variant > 2) return fail(c, CVR_ERR_ARG, "cvr_render_iso: bad variant %d", p->variant);
+  const bool phong = p->apply_gradient_shading != 0;
+  if (phong && !c->d_grad) return fail(c, CVR_ERR_STATE, "cvr_render_iso: Phong needs cvr_set_gradient");
+  if (f->nranks > 1 && (f->tile_size < 16 || f->tile_size % 16 != 0 || f->rank < 0 || f->rank >= f->nranks))
+    return fail(c, CVR_ERR_ARG, "cvr_render_iso: bad tiling");
+  int nb[3];
+  iso_blocks_of(p, nb);
+  for (int i = 0; i < 3; i++)
+    if (nb[i] > 1024) return fail(c, CVR_ERR_ARG, "cvr_render_iso: bad block count %d", nb[i]);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (p->variant != 2) {   // RayCasting1PassIsoAdapt has no blocks
+    cvr_status st = ensure_iso_blocks(c, nb);
+    if (st != CVR_OK) return st;
+  }
+
+  cvr::IsoArgs Q{};
+  int ntiles = 0;
+  size_t npix = 0;
+  fill_frame_args(c, f, 1.0f, Q.a, ntiles, npix);
+  Q.a.out_half = o->format == CVR_FORMAT_RGBA16F;
+  Q.a.ka = p->ka; Q.a.kd = p->kd; Q.a.ks = p->ks; Q.a.shininess = p->shininess;
+  for (int i = 0; i < 3; i++) { Q.a.ispec[i] = p->ispecular[i]; Q.a.light[i] = p->light_pos[i]; }
+  for (int i = 0; i < 3; i++) {
+    Q.G[i] = (float)c->N[i] * c->scale[i];
+    Q.nb[i] = (float)nb[i];
+    Q.nbi[i] = nb[i];
+  }
+  Q.iso = p->isovalue;
+  Q.step_small = p->step_small;
+  Q.step_large = p->step_large;
+  Q.step_range = p->step_range;
+  {   // length(VolumeGridSize / numBlocks) * 0.5 (rc1pisodfscustom ...iso_adapt.comp:222-223)
+    const float b0 = Q.G[0] / Q.nb[0], b1 = Q.G[1] / Q.nb[1], b2 = Q.G[2] / Q.nb[2];
+    Q.half_block_len = std::sqrt(std::fmaf(b2, b2, std::fmaf(b1, b1, b0 * b0))) * 0.5f;
+  }
+  for (int i = 0; i < 4; i++) Q.color[i] = p->color[i];
+  const float2* mm = p->variant != 2 ? c->d_iso_mm : nullptr;
+  const int variant = p->variant;
+  return render_shaded(c, o, ntiles, npix, [&](float4* out, uint32_t* smp, unsigned long long*,
+                                                unsigned long long* ts, hipStream_t st2) {
+    return cvr::launch_iso(*c, Q, variant, phong, mm, out, smp, ts, st2);
   });
 }
 

@@ -107,6 +107,17 @@ struct EbsArgs {
   float ka, kd, ks;                  // Kambient if occlusion, Kdiffuse/Kspecular if shadow, else 0
 };
 
+// Isosurface ray-casters with block skipping (iso.hip): the shaders' uniforms.
+struct IsoArgs {
+  Rc1passArgs a;                     // ray, volume, Blinn-Phong constants, tiles
+  float G[3];                        // VolumeGridSize
+  float nb[3];                       // numBlocks (vec3 uniform)
+  int nbi[3];                        // the same as int (table addressing, REPEAT wrap)
+  float iso, step_small, step_large, step_range;
+  float half_block_len;              // length(G / numBlocks) * 0.5 (variant 1)
+  float color[4];
+};
+
 // How one frame is cut into work: one 8x8 wave tile per workgroup.
 struct RenderPlan {
   int ntiles;                        // 8x8 wave tiles (one workgroup each)
@@ -220,6 +231,10 @@ struct Ctx {
   cvr_cone_tables* cone_tab = nullptr;   // host copies [2]
   unsigned long long* d_tile_samples = nullptr;   // per-wave-tile sample counts (zeroed)
   int tile_samples_n = 0;
+  // isosurface block table (float2 min/max per block), built for iso_nb
+  float2* d_iso_mm = nullptr;
+  int iso_nb[3] = {0, 0, 0};
+  int iso_valid = 0;               // matches the current volume and iso_nb
   // multi-GPU gather (cvr_comm.cpp): RCCL communicator, its stream and events
   void* comm = nullptr;
   int split_streams = 1;           // option "split_streams": render streams the caller rotates
@@ -265,6 +280,12 @@ hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* sam
 hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade,
                       unsigned long long* tile_samples, hipStream_t s);
+// iso.hip: raw per-block extremes (uint2), and the isosurface march (variant 0/1)
+hipError_t launch_block_minmax(const void* vox, int bpv, const int N[3], const int nb[3], uint2* out,
+                               hipStream_t s);
+hipError_t launch_iso(const Ctx& c, const IsoArgs& q, int variant, bool phong, const float2* mm,
+                      float4* out, uint32_t* samples, unsigned long long* tile_samples,
+                      hipStream_t s);
 hipError_t launch_unpack_tiles(const void* packed, void* out, int half, int W, int H, int tile,
                                int nranks, int tpr_max, hipStream_t s, size_t rank_stride = 0);
 

@@ -167,6 +167,7 @@ struct Ray {
   f3 dir, tpos, o, dt;   // direction, entry point (texture space), texel-space origin/step
   f3 inv_dt;             // 1 / dt (macro-cell exits)
   float D;               // distance to evaluate, |tfar - tnear|
+  float tnear, tfar;     // RayAABBIntersection's rtnear (clamped to >= 0) and rtfar
   bool outside;          // box behind the eye (tfar < 0): the march runs outside the grid
 };
 
@@ -196,6 +197,8 @@ __device__ __forceinline__ bool ray_setup(const Rc1passArgs& A, int px, int py, 
   // must be clamped before addressing cells.
   r.outside = !(tfar >= 0.0f);
   tnear = fmaxf(tnear, 0.0f);
+  r.tnear = tnear;
+  r.tfar = tfar;
   r.dir = dir;
   r.D = fabsf(tfar - tnear);
   r.tpos = f3{fmaf(dir.x, tnear, eye.x) + hg.x, fmaf(dir.y, tnear, eye.y) + hg.y,

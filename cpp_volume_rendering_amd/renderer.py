@@ -699,6 +699,105 @@ class RC1PExtinctionBasedShading(RayCasting1Pass):
     _ENTRY = "cvr_render_extbsd"
 
 
+class RayCasting1PassIsoAdapt(RayCasting1Pass):
+    """HIP implementation of RayCasting1PassIsoAdapt
+    (cppvolrend/structured/rc1pisoadapt/rc1pisoadaptrenderer.cpp): first-hit
+    isosurfaces with adaptive steps (small within StepSizeRange of the isovalue),
+    composited front to back with one colour.  No transfer function."""
+
+    VARIANT = 2
+
+    def __init__(self, device: int = 0):
+        super().__init__(device)
+        self._params = N.IsoParams()
+        N.lib().cvr_iso_params_default(self.VARIANT, ctypes.byref(self._params))
+        d = self._params
+        self.m_u_isovalue = d.isovalue              # rc1pisoadaptrenderer.cpp:15-20
+        self.m_u_step_size_small = d.step_small
+        self.m_u_step_size_large = d.step_large
+        self.m_u_step_size_range = d.step_range
+        self.m_u_color = tuple(d.color)
+        self.num_blocks = tuple(d.num_blocks)
+        self.vr_pixel_multiscaling_support = False  # BaseVolumeRenderer default
+
+    def GetName(self): return "1-Pass - Isosurface Raycaster Adaptive"
+    def GetAbbreviationName(self): return "iso"
+
+    def Init(self, swidth: int, sheight: int) -> bool:
+        if self.IsBuilt():
+            self.Clean()
+        dm = self.m_ext_data_manager
+        if dm is None or dm.volume is None:
+            return False                            # GetCurrentVolumeTexture() == nullptr
+        self._dev = Device(self._device_index)
+        self._dev.set_volume(dm.volume, dm.scale)
+        if dm.gradient_type != N.GRADIENT_NONE:
+            self._dev.set_gradient(dm.gradient_type)
+        self.Reshape(swidth, sheight)
+        self.SetBuilt(True)
+        self.SetOutdated()
+        return True
+
+    def Update(self, camera: Camera) -> bool:
+        rp = self.m_ext_rendering_parameters or RenderingParameters()
+        self._frame = self._camera_frame(camera)
+        p = self._params
+        p.variant = self.VARIANT
+        p.num_blocks[:] = [int(b) for b in self.num_blocks]
+        p.isovalue = float(self.m_u_isovalue)
+        p.step_small = float(self.m_u_step_size_small)
+        p.step_large = float(self.m_u_step_size_large)
+        p.step_range = float(self.m_u_step_size_range)
+        p.color[:] = [float(c) for c in self.m_u_color]
+        p.apply_gradient_shading = int(bool(self.m_apply_gradient_shading) and
+                                       self.m_ext_data_manager.gradient_type != N.GRADIENT_NONE)
+        p.ka, p.kd = rp.blinnphong_ka, rp.blinnphong_kd
+        p.ks, p.shininess = rp.blinnphong_ks, rp.blinnphong_shininess
+        p.ispecular[:] = [float(v) for v in rp.light_specular]
+        p.light_pos[:] = [float(v) for v in rp.light_position]
+        return True
+
+    def FillParameterSpace(self, pspace: dict):
+        pspace.clear()                              # rc1pisoadaptrenderer.cpp:191-197
+        pspace["StepSizeSmall"] = (0.01, 0.25, 0.05)
+        pspace["StepSizeLarge"] = (0.25, 2.0, 0.25)
+        pspace["StepSizeRange"] = (0.05, 0.26, 0.05)
+
+    _ENTRY = "cvr_render_iso"
+
+
+class CustomRayCasting1PassIsoAdapt(RayCasting1PassIsoAdapt):
+    """HIP implementation of CustomRayCasting1PassIsoAdapt
+    (cppvolrend/structured/rc1pisocustom/rc1custompisoadaptrenderer.cpp): the adaptive
+    isosurface march with empty-space skipping over a 4^3 min/max block grid
+    (ComputeBlocksFromVolume, built on the GPU)."""
+
+    VARIANT = 0
+
+    def GetName(self): return "1-Pass - Custom Isosurface Raycaster Adaptive"
+
+    def BlockRanges(self):
+        """The (min, max) block tables the shader reads, float32 (nz, ny, nx)."""
+        nb = (ctypes.c_int * 3)(*[int(b) for b in self.num_blocks])
+        shape = (nb[2], nb[1], nb[0])
+        lo = np.empty(shape, np.float32)
+        hi = np.empty(shape, np.float32)
+        N.check(N.lib().cvr_iso_block_ranges(self.device.handle, nb, N.fptr(lo), N.fptr(hi)),
+                "cvr_iso_block_ranges", self.device.handle)
+        return lo, hi
+
+
+class CustomRayCasting1PassIsodfsAdapt(CustomRayCasting1PassIsoAdapt):
+    """HIP implementation of CustomRayCasting1PassIsodfsAdapt ("Empty Sapce Skipping V2",
+    cppvolrend/structured/rc1pisodfscustom/rc1custompisoadaptdfsrenderer.cpp): 32^3
+    blocks, the block exit distance as the skip, a 0.001 skip tolerance and steps
+    capped at half a block diagonal."""
+
+    VARIANT = 1
+
+    def GetName(self): return "Empty Sapce Skipping V2"
+
+
 def composite_over_white(rgba: np.ndarray) -> np.ndarray:
     """Screen image as RenderFrameToScreen::Draw blends it over the white clear colour
     with SRC_ALPHA / ONE_MINUS_SRC_ALPHA (renderingmanager.cpp:103-112), as RGB8."""

@@ -129,6 +129,30 @@ typedef struct cvr_rc1pass_params {
   float light_pos[3];          /* RenderingParameters::GetBlinnPhongLightingPosition */
 } cvr_rc1pass_params;
 
+/* Isosurface ray-casters with block empty-space skipping:
+ *   variant 0: CustomRayCasting1PassIsoAdapt ("1-Pass - Custom Isosurface
+ *              Raycaster Adaptive", rc1pisocustom/rc1custompisoadaptrenderer.cpp),
+ *              4^3 blocks, the block chord as the skip distance;
+ *   variant 1: CustomRayCasting1PassIsodfsAdapt ("Empty Sapce Skipping V2",
+ *              rc1pisodfscustom/rc1custompisoadaptdfsrenderer.cpp), 32^3 blocks,
+ *              the block exit distance and a tolerance of 0.001;
+ *   variant 2: RayCasting1PassIsoAdapt ("1-Pass - Isosurface Raycaster
+ *              Adaptive", rc1pisoadapt/rc1pisoadaptrenderer.cpp), no blocks.
+ * Defaults (cvr_iso_params_default): rc1custompisoadaptrenderer.cpp:119-127. */
+typedef struct cvr_iso_params {
+  int   variant;               /* 0, 1 or 2                                            */
+  int   num_blocks[3];         /* <= 0: 4^3 (variant 0) / 32^3 (variant 1), :190       */
+  float isovalue;              /* m_u_isovalue 0.5                                     */
+  float step_small;            /* m_u_step_size_small 0.05                             */
+  float step_large;            /* m_u_step_size_large 1.0                              */
+  float step_range;            /* m_u_step_size_range 0.1                              */
+  float color[4];              /* m_u_color (0.66, 0.6, 0.05, 1.0)                     */
+  int   apply_gradient_shading;/* m_apply_gradient_shading (default 0; needs gradient) */
+  float ka, kd, ks, shininess; /* Blinn-Phong constants (renderingparameters.cpp:23-26) */
+  float ispecular[3];          /* BlinnPhongIspecular                                  */
+  float light_pos[3];          /* LightSourcePosition                                  */
+} cvr_iso_params;
+
 /* Directional-occlusion cones (RC1PConeTracingDirOcclusionShading,
  * cppvolrend/structured/rc1pdosct): the parameters of one ConeGaussianSampler
  * (conegaussiansampler.h) and the tables the renderer uploads from it. */
@@ -307,6 +331,19 @@ cvr_status  cvr_copy_extinction_sat(cvr_ctx* ctx, float* out, size_t capacity, i
  * cvr_set_extinction_sat. */
 cvr_status  cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* frame,
                               const cvr_ebs_params* params, const cvr_output* out);
+
+/* The reference renderers' default parameters for `variant`. */
+void        cvr_iso_params_default(int variant, cvr_iso_params* out);
+/* One isosurface frame (first hits composited front to back with Color).  The
+ * block min/max table (ComputeBlocksFromVolume, rc1custompisoadaptrenderer.cpp
+ * :20-117) is built on the GPU when the volume or num_blocks changes. */
+cvr_status  cvr_render_iso(cvr_ctx* ctx, const cvr_frame* frame, const cvr_iso_params* params,
+                           const cvr_output* out);
+/* Copy the current block table back (x-fastest, num_blocks of the last build);
+ * builds it first for `num_blocks` when needed.  Empty blocks hold (FLT_MAX,
+ * -FLT_MAX) as in the reference. */
+cvr_status  cvr_iso_block_ranges(cvr_ctx* ctx, const int num_blocks[3], float* out_min,
+                                 float* out_max);
 
 /* Rank-0 side of the screen-tile split: `d_packed` holds nranks consecutive
  * blocks of `tiles_per_rank_max` packed tiles (rank r's block at offset

@@ -1420,3 +1420,289 @@ ORACLE_API void oracle_screenshot_rgb8(const void* frame, int half, int w, int h
     }
   }
 }
+
+// ===========================================================================
+// Isosurface ray-casters with block empty-space skipping
+// ===========================================================================
+//
+//   variant 0: cppvolrend/structured/rc1pisocustom/custom_ray_marching_1p_iso_adapt.comp
+//              :93-130 (block index / bounds / chord), :155-246 (march), 4^3 blocks
+//   variant 1: cppvolrend/structured/rc1pisodfscustom/custom_ray_marching_1p_iso_adapt.comp
+//              :94-156 (block index / bounds / exit distance), :181-260 (march), 32^3 blocks
+//   variant 2: cppvolrend/structured/rc1pisoadapt/ray_marching_1p_iso_adapt.comp:113-172
+//              (RayCasting1PassIsoAdapt, no blocks)
+//   blocks:    ComputeBlocksFromVolume, rc1custompisoadaptrenderer.cpp:20-117
+//              (R32F textures, NEAREST, default REPEAT wrap)
+// CVR-SPEC: r.Origin + r.Dir * t is fmaf(dir, t, eye) (as in the rc1pass ray
+// entry), the composite is the rc1pass fmaf form, Blinn-Phong the rc1pass one;
+// every other expression in the shader's order, unfused.  `counts` = volume
+// fetches the shader issues (the skip branch's dead re-fetch of variant 1 too).
+struct OracleIso {
+  OracleRc1pass base;                  // volume, gradient, camera, Blinn-Phong (tf unused)
+  int variant;
+  int nb[3];
+  const float* bmin; const float* bmax;   // nb[0]*nb[1]*nb[2] each, x-fastest
+  float iso, step_small, step_large, step_range;
+  float color[4];
+};
+
+ORACLE_API void oracle_iso_blocks(const void* vox, int bpv, int w, int h, int d, const int nb[3],
+                                  float* out_min, float* out_max) {
+  // (N + nb - 1) / nb in float, truncated (:37-39), equals the integer ceiling here
+  const int bs[3] = {(w + nb[0] - 1) / nb[0], (h + nb[1] - 1) / nb[1], (d + nb[2] - 1) / nb[2]};
+  const double mx = bpv == 1 ? 255.0 : 65535.0;
+  size_t k = 0;
+  for (int bz = 0; bz < nb[2]; bz++)
+    for (int by = 0; by < nb[1]; by++)
+      for (int bx = 0; bx < nb[0]; bx++, k++) {
+        const int x0 = bx * bs[0], y0 = by * bs[1], z0 = bz * bs[2];
+        const int x1 = std::min(x0 + bs[0], w), y1 = std::min(y0 + bs[1], h), z1 = std::min(z0 + bs[2], d);
+        double lo = 3.4028234663852886e38, hi = -3.4028234663852886e38;
+        for (int z = z0; z < z1; z++)
+          for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++) {
+              const size_t i = ((size_t)z * h + y) * w + x;
+              const double v = (bpv == 1 ? (double)((const uint8_t*)vox)[i]
+                                         : (double)((const uint16_t*)vox)[i]) / mx;
+              lo = std::min(lo, v);
+              hi = std::max(hi, v);
+            }
+        out_min[k] = (float)lo;
+        out_max[k] = (float)hi;
+      }
+}
+
+namespace {
+
+constexpr uint32_t kIsoMaxIter = 1u << 22;   // the kernel's iteration bound (iso.hip)
+
+inline v3 iso_pos(v3 eye, v3 dir, float t) {
+  return mk(std::fmaf(dir.x, t, eye.x), std::fmaf(dir.y, t, eye.y), std::fmaf(dir.z, t, eye.z));
+}
+
+}  // namespace
+
+ORACLE_API uint64_t oracle_render_iso_rows(const OracleIso* Q, int y0, int y1, float* out,
+                                           uint32_t* counts, int nthreads) {
+  const OracleRc1pass& P = Q->base;
+  float V[16], tanf;
+  oracle_lookat(P.eye, P.center, P.up, P.fovy_deg, V, &tanf);
+  const float aspect = P.aspect > 0 ? P.aspect : (float)P.W / (float)P.H;
+  const v3 eye = mk(P.eye[0], P.eye[1], P.eye[2]);
+  const float G[3] = {(float)P.N[0] * P.scale[0], (float)P.N[1] * P.scale[1], (float)P.N[2] * P.scale[2]};
+  const v3 half = mk(G[0] * 0.5f, G[1] * 0.5f, G[2] * 0.5f);
+  const float NoG[3] = {(float)P.N[0] / G[0], (float)P.N[1] / G[1], (float)P.N[2] / G[2]};
+  const float nbf[3] = {(float)Q->nb[0], (float)Q->nb[1], (float)Q->nb[2]};
+  // length(VolumeGridSize / numBlocks) * 0.5 (variant 1, :222-223)
+  const float bl[3] = {G[0] / nbf[0], G[1] / nbf[1], G[2] / nbf[2]};
+  const float half_block = std::sqrt(std::fmaf(bl[2], bl[2], std::fmaf(bl[1], bl[1], bl[0] * bl[0]))) * 0.5f;
+  const v3 light = mk(P.light[0], P.light[1], P.light[2]);
+  Tex vol{P.vol, {P.N[0], P.N[1], P.N[2]}, 1};
+  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3};
+  const float iso = Q->iso;
+  const int W = P.W, H = P.H;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+  uint64_t total = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
+  for (int py = y0; py < y1; py++) {
+    for (int px = 0; px < W; px++) {
+      const int64_t pix = (int64_t)py * W + px;
+      float dst[4] = {0, 0, 0, 0};
+      uint32_t cnt = 0;
+      float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+      float vx = std::fmaf(fx / (float)W, 2.0f, -1.0f);
+      float vy = std::fmaf(fy / (float)H, 2.0f, -1.0f);
+      v3 c = mk((vx * tanf) * aspect, vy * tanf, -1.0f);
+      v3 dv = mk(dot3(c, mk(V[0], V[1], V[2])), dot3(c, mk(V[4], V[5], V[6])), dot3(c, mk(V[8], V[9], V[10])));
+      v3 dir = normalize3(normalize3(dv));
+      v3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+      v3 ta = mk(inv.x * (-half.x - eye.x), inv.y * (-half.y - eye.y), inv.z * (-half.z - eye.z));
+      v3 tb = mk(inv.x * (half.x - eye.x), inv.y * (half.y - eye.y), inv.z * (half.z - eye.z));
+      float tnear = std::fmax(std::fmax(std::fmin(ta.x, tb.x), std::fmin(ta.y, tb.y)), std::fmin(ta.z, tb.z));
+      const float tfar = std::fmin(std::fmin(std::fmax(ta.x, tb.x), std::fmax(ta.y, tb.y)), std::fmax(ta.z, tb.z));
+      const bool hit = tfar > tnear;
+      tnear = std::fmax(tnear, 0.0f);
+      if (hit) {
+        // texture(TexVolume, (r.Origin + r.Dir * t + G/2) / G).r
+        auto density = [&](float t) {
+          const v3 p = iso_pos(eye, dir, t);
+          float s;
+          vol.sample(std::fmaf(p.x + half.x, NoG[0], -0.5f), std::fmaf(p.y + half.y, NoG[1], -0.5f),
+                     std::fmaf(p.z + half.z, NoG[2], -0.5f), &s);
+          return s;
+        };
+        auto hit_colour_at = [&](v3 st, float rgb[3]) {   // st: s_tex_pos
+          for (int k = 0; k < 3; k++) rgb[k] = Q->color[k];
+          if (!(P.phong && P.grad)) return;
+          float g[3];
+          grd.sample(std::fmaf(st.x, NoG[0], -0.5f), std::fmaf(st.y, NoG[1], -0.5f),
+                     std::fmaf(st.z, NoG[2], -0.5f), g);
+          if (g[0] == 0.0f && g[1] == 0.0f && g[2] == 0.0f) return;
+          const v3 wp = mk(st.x - half.x, st.y - half.y, st.z - half.z);   // ShadeBlinnPhong :58
+          const v3 L = normalize3(mk(light.x - wp.x, light.y - wp.y, light.z - wp.z));
+          const v3 E = normalize3(mk(eye.x - wp.x, eye.y - wp.y, eye.z - wp.z));
+          const v3 Hv = normalize3(mk(E.x + L.x, E.y + L.y, E.z + L.z));
+          const v3 n = normalize3(mk(g[0], g[1], g[2]));
+          const float dd = std::fmax(0.0f, dot3(n, L));
+          const float ds = std::fmax(0.0f, dot3(Hv, n));
+          const float pw = cvr_powf(ds, P.shininess);
+          const float f = std::fmaf(P.kd, dd, P.ka);
+          for (int k = 0; k < 3; k++) rgb[k] = std::fmaf(P.ispec[k] * P.ks, pw, rgb[k] * f);
+        };
+        auto hit_colour = [&](float t, float rgb[3]) {
+          const v3 p = iso_pos(eye, dir, t);
+          hit_colour_at(mk(p.x + half.x, p.y + half.y, p.z + half.z), rgb);
+        };
+        auto composite = [&](const float rgb[3]) {   // src.rgb *= src.a; dst += (1 - dst.a) * src
+          const float a = Q->color[3], om = 1.0f - dst[3];
+          for (int k = 0; k < 3; k++) dst[k] = std::fmaf(om, rgb[k] * a, dst[k]);
+          dst[3] = std::fmaf(om, a, dst[3]);
+        };
+        if (Q->variant == 2) {
+          // rc1pisoadapt/ray_marching_1p_iso_adapt.comp:113-172: s in [0, D) from
+          // tex_pos = r.Origin + r.Dir * tnear + G/2, no blocks
+          const float D = std::fabs(tfar - tnear);
+          const v3 p0 = iso_pos(eye, dir, tnear);
+          const v3 tp = mk(p0.x + half.x, p0.y + half.y, p0.z + half.z);
+          auto dens_at = [&](float s) {
+            float v;
+            vol.sample(std::fmaf(std::fmaf(dir.x, s, tp.x), NoG[0], -0.5f),
+                       std::fmaf(std::fmaf(dir.y, s, tp.y), NoG[1], -0.5f),
+                       std::fmaf(std::fmaf(dir.z, s, tp.z), NoG[2], -0.5f), &v);
+            return v;
+          };
+          float prev = dens_at(0.0f);
+          cnt++;
+          float s = 0.0f;
+          uint32_t iters = 0;
+          while (s < D && iters < kIsoMaxIter) {
+            iters++;
+            const float step = std::fabs(prev - iso) < Q->step_range ? Q->step_small : Q->step_large;
+            const float h = std::fmin(step, D - s);
+            const float dens = dens_at(s + h);
+            cnt++;
+            if ((prev <= iso && iso < dens) || (prev >= iso && iso > dens)) {
+              const float tt = (iso - prev) / (dens - prev);
+              // s_tex_pos = tex_pos + r.Dir * (s + t * h); hit_colour takes t along the
+              // eye ray, so restate the position directly
+              const float st = std::fmaf(tt, h, s);
+              float rgb[3];
+              hit_colour_at(mk(std::fmaf(dir.x, st, tp.x), std::fmaf(dir.y, st, tp.y),
+                               std::fmaf(dir.z, st, tp.z)), rgb);
+              composite(rgb);
+              if (dst[3] > 0.99f) break;
+            }
+            prev = dens;
+            s = s + h;
+          }
+        } else {
+        float t = tnear;
+        float prev = density(t);   // prevDensity (:157-158)
+        cnt++;
+        uint32_t iters = 0;
+        while (t < tfar && iters < kIsoMaxIter) {
+          iters++;
+          // getBlockIndex (:93-96) and the REPEAT-wrapped NEAREST fetch of the tables
+          const v3 p = iso_pos(eye, dir, t);
+          const float pp[3] = {p.x, p.y, p.z}, dd[3] = {dir.x, dir.y, dir.z};
+          int b[3], wr[3];
+          for (int i = 0; i < 3; i++) {
+            b[i] = (int)std::floor(((pp[i] + (G[i] * 0.5f)) / G[i]) * nbf[i]);
+            wr[i] = ((b[i] % Q->nb[i]) + Q->nb[i]) % Q->nb[i];
+          }
+          const size_t bi = ((size_t)wr[2] * Q->nb[1] + wr[1]) * Q->nb[0] + wr[0];
+          const float bmin_v = Q->bmin[bi], bmax_v = Q->bmax[bi];
+          // getBlockBounds (:99-103)
+          float lo[3], hi[3];
+          for (int i = 0; i < 3; i++) {
+            const float bs = G[i] / nbf[i];
+            lo[i] = -G[i] * 0.5f + bs * (float)b[i];
+            hi[i] = lo[i] + bs;
+          }
+          if (Q->variant == 0) {
+            bool tilted = false;
+            if (iso < bmin_v || iso > bmax_v) {
+              float dt;
+              if (std::fabs(dd[0]) < 0.01f || std::fabs(dd[1]) < 0.01f || std::fabs(dd[2]) < 0.01f) {
+                dt = -1.0f;
+              } else {
+                float tmn[3], tmx[3];
+                for (int i = 0; i < 3; i++) {
+                  const float t1 = (lo[i] - pp[i]) / dd[i], t2 = (hi[i] - pp[i]) / dd[i];
+                  tmn[i] = std::fmin(t1, t2);
+                  tmx[i] = std::fmax(t1, t2);
+                }
+                dt = std::fmin(std::fmin(tmx[0], tmx[1]), tmx[2]) -
+                     std::fmax(std::fmax(tmn[0], tmn[1]), tmn[2]);
+              }
+              if (dt == -1.0f) tilted = true;
+              if (dt <= Q->step_small) dt = Q->step_small;
+              t += dt;
+              if (!tilted) continue;
+            }
+            const float step = std::fabs(prev - iso) < Q->step_range ? Q->step_small : Q->step_large;
+            prev = density(t);
+            cnt++;
+            const float h = std::fmin(step, tfar - t);
+            t += h;
+            const float dens = density(t);
+            cnt++;
+            if ((prev <= iso && iso < dens) || (prev >= iso && iso > dens)) {
+              const float tt = (dens - iso) / (dens - prev);
+              t -= tt;
+              float rgb[3];
+              hit_colour(t, rgb);
+              composite(rgb);
+              if (dst[3] > 0.99f) break;
+            }
+          } else {
+            if (iso < bmin_v - 0.001f || iso > bmax_v + 0.001f) {   // isBlockSkippable
+              float tmx[3];
+              for (int i = 0; i < 3; i++) {
+                const float rc = std::fabs(dd[i]) > 1e-6f ? 1.0f / dd[i]
+                                 : (dd[i] > 0.0f ? 1e6f : (dd[i] < 0.0f ? -1e6f : 0.0f));
+                tmx[i] = std::fmax((lo[i] - pp[i]) * rc, (hi[i] - pp[i]) * rc);
+              }
+              float exitT = std::fmin(std::fmin(tmx[0], tmx[1]), tmx[2]);
+              for (int i = 0; i < 3; i++)
+                if (std::fabs(exitT - tmx[i]) < 1e-5f) exitT += 1e-4f;
+              t += std::fmax(Q->step_small, exitT);
+              prev = density(t);   // overwritten before use
+              cnt++;
+              continue;
+            }
+            const float cur = density(t);
+            cnt++;
+            const float step = std::fabs(cur - iso) < Q->step_range ? Q->step_small
+                                                                    : std::fmin(Q->step_large, half_block);
+            const float h = std::fmin(step, tfar - t);
+            prev = cur;
+            t += h;
+            const float dens = density(t);
+            cnt++;
+            if ((prev <= iso && iso < dens) || (prev >= iso && iso > dens)) {
+              const float tt = (iso - prev) / (dens - prev);
+              t = t - h * (1.0f - tt);
+              float rgb[3];
+              hit_colour(t, rgb);
+              composite(rgb);
+              if (dst[3] > 0.99f) break;
+            }
+          }
+        }
+        }   // variants 0, 1
+      }
+      if (out) for (int k = 0; k < 4; k++) out[pix * 4 + k] = dst[k];
+      if (counts) counts[pix] = cnt;
+      total += cnt;
+    }
+  }
+  return total;
+}
+
+ORACLE_API uint64_t oracle_render_iso(const OracleIso* Q, float* out_rgba, uint32_t* out_counts,
+                                      int nthreads) {
+  return oracle_render_iso_rows(Q, 0, Q->base.H, out_rgba, out_counts, nthreads);
+}

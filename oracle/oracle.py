@@ -58,6 +58,13 @@ class OracleEbs(ctypes.Structure):
                 ("light_forward", ctypes.c_float * 3)]
 
 
+class OracleIso(ctypes.Structure):
+    _fields_ = [("base", OracleRc1pass), ("variant", ctypes.c_int), ("nb", ctypes.c_int * 3),
+                ("bmin", ctypes.c_void_p), ("bmax", ctypes.c_void_p), ("iso", ctypes.c_float),
+                ("step_small", ctypes.c_float), ("step_large", ctypes.c_float),
+                ("step_range", ctypes.c_float), ("color", ctypes.c_float * 4)]
+
+
 def build() -> None:
     subprocess.run(["make", "-C", HERE, "-s"], check=True)
 
@@ -102,6 +109,9 @@ def lib():
         L.oracle_multiscale_filter.argtypes = [I, I, P, I, I, P, I, I]
         L.oracle_multiscale_filter.restype = I
         L.oracle_screenshot_rgb8.argtypes = [P, I, I, I, P]
+        L.oracle_iso_blocks.argtypes = [P, I, I, I, I, P, P, P]
+        L.oracle_render_iso_rows.argtypes = [ctypes.POINTER(OracleIso), I, I, P, P, I]
+        L.oracle_render_iso_rows.restype = ctypes.c_uint64
         L.oracle_screenshot_rgb8.restype = None
         _lib = L
     return _lib
@@ -395,3 +405,49 @@ def screenshot_rgb8(frame: np.ndarray) -> np.ndarray:
     out = np.zeros((h, w, 3), np.uint8)
     lib().oracle_screenshot_rgb8(_p(frame), int(frame.dtype == np.float16), w, h, _p(out))
     return out
+
+
+# Block counts of the two isosurface renderers (rc1custompisoadaptrenderer.cpp:190,
+# rc1custompisoadaptdfsrenderer.cpp:190)
+ISO_BLOCKS = {0: (4, 4, 4), 1: (32, 32, 32), 2: (1, 1, 1)}   # variant 2 has none
+
+
+def iso_blocks(vox: np.ndarray, nb) -> tuple[np.ndarray, np.ndarray]:
+    """ComputeBlocksFromVolume: per-block (min, max) of v / (2^bits - 1), float32 (nz, ny, nx)."""
+    vox = np.ascontiguousarray(vox)
+    d, h, w = vox.shape
+    nb = [int(x) for x in nb]
+    bmin = np.empty((nb[2], nb[1], nb[0]), np.float32)
+    bmax = np.empty_like(bmin)
+    nba = (ctypes.c_int * 3)(*nb)
+    lib().oracle_iso_blocks(_p(vox), vox.dtype.itemsize, w, h, d, nba, _p(bmin), _p(bmax))
+    return bmin, bmax
+
+
+def render_iso(vol16: np.ndarray, vox: np.ndarray, scale, camera: dict, W: int, H: int,
+               variant: int = 0, nb=None, isovalue=0.5, step_small=0.05, step_large=1.0,
+               step_range=0.1, color=(0.66, 0.6, 0.05, 1.0), grad: np.ndarray | None = None,
+               phong: bool = False, ka=0.5, kd=0.5, ks=0.8, shininess=30.0,
+               ispec=(1.0, 1.0, 1.0), light=(0.0, 0.0, 0.0), threads: int = 0, rows=None):
+    """One frame of an isosurface ray-caster (variant 0: custom adaptive with 4^3
+    blocks, 1: "Empty Space Skipping V2", 2: RayCasting1PassIsoAdapt, no blocks).  vol16: the R16F volume as float; vox: the raw voxels (block
+    table).  Returns (rgba HxWx4, counts HxW, S, (bmin, bmax))."""
+    vol16 = np.ascontiguousarray(vol16, np.float32)
+    nb = ISO_BLOCKS[variant] if nb is None else tuple(int(x) for x in nb)
+    bmin, bmax = iso_blocks(vox, nb)
+    if grad is not None:
+        grad = np.ascontiguousarray(grad, np.float32)
+    dummy_tf = np.zeros((2, 4), np.float32)
+    Q = OracleIso()
+    Q.base = _params(vol16, scale, dummy_tf, grad, camera, W, H, 1.0, phong, ka, kd, ks,
+                     shininess, ispec, light, aspect=camera.get("aspect", 0.0))
+    Q.variant = int(variant)
+    Q.nb[:] = list(nb)
+    Q.bmin, Q.bmax = _p(bmin), _p(bmax)
+    Q.iso, Q.step_small, Q.step_large, Q.step_range = isovalue, step_small, step_large, step_range
+    Q.color[:] = [float(c) for c in color]
+    rgba = np.zeros((H, W, 4), np.float32)
+    cnt = np.zeros((H, W), np.uint32)
+    y0, y1 = (0, H) if rows is None else (int(rows[0]), int(rows[1]))
+    S = lib().oracle_render_iso_rows(ctypes.byref(Q), y0, y1, _p(rgba), _p(cnt), int(threads))
+    return rgba, cnt, int(S), (bmin, bmax)
