@@ -177,3 +177,40 @@ def test_iso_screen_tiles_match_full_frame(dev):
             S += s
         assert_bitexact(T.unpack(packed, W, H, tile, nranks), full, f"v{variant} tiles")
         assert S == S_full
+
+
+def test_eval_sweep_iso(oracle, tmp_path):
+    """The evaluation sweep (evaluation.run_evaluation) over the 200 points of the
+    custom isosurface renderer: eval.csv as the reference writes it, and the saved
+    screenshots equal to the oracle's frames composited over white."""
+    import csv as _csv
+    import os
+
+    from PIL import Image
+
+    from cpp_volume_rendering_amd import evaluation as E
+    from cpp_volume_rendering_amd.renderer import (CustomRayCasting1PassIsoAdapt, DataManager,
+                                                   RenderingParameters)
+    vol = _ml(64)
+    dm = DataManager()
+    dm.SetVolume(vol, (1.0, 1.0, 1.0))
+    W = H = 64
+    r = CustomRayCasting1PassIsoAdapt()
+    r.SetExternalResources(dm, RenderingParameters(W, H))
+    assert r.Init(W, H)
+    cam = Camera(eye=(70.0, 60.0, 110.0), center=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0))
+    path = E.run_evaluation(r, cam, str(tmp_path), frames_per_sample=2)
+    rows = list(_csv.reader(open(path)))
+    assert rows[0] == ["StepSizeSmall", "StepSizeLarge", "StepSizeRange", "TimePerFrame (ms)",
+                       "FramesPerSecond", "ImageFile"]
+    assert len(rows) == 201 and rows[-1][-1] == "0199.png"
+    v16 = oracle.volume_r16f(vol)
+    for k in (0, 57, 199):
+        small, large, rng = (float(x) for x in rows[k + 1][:3])
+        rgba, _, _, _ = oracle.render_iso(v16, vol, (1.0, 1.0, 1.0), dict(
+            eye=(70.0, 60.0, 110.0), center=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0)), W, H,
+            variant=0, step_small=small, step_large=large, step_range=rng)
+        shot = oracle.screenshot_rgb8(rgba)
+        png = np.asarray(Image.open(os.path.join(str(tmp_path), "img", rows[k + 1][-1])).convert("RGB"))
+        assert np.array_equal(png, shot[::-1]), k
+    r.Clean()
