@@ -1519,6 +1519,11 @@ cvr_status cvr_render_iso(cvr_ctx* ctx, const cvr_frame* f, const cvr_iso_params
     const float b0 = Q.G[0] / Q.nb[0], b1 = Q.G[1] / Q.nb[1], b2 = Q.G[2] / Q.nb[2];
     Q.half_block_len = std::sqrt(std::fmaf(b2, b2, std::fmaf(b1, b1, b0 * b0))) * 0.5f;
   }
+  for (int i = 0; i < 3; i++) {
+    Q.bs[i] = Q.G[i] / Q.nb[i];
+    Q.nhg[i] = -Q.G[i] * 0.5f;
+    Q.inv_g[i] = 1.0f / Q.G[i];
+  }
   for (int i = 0; i < 4; i++) Q.color[i] = p->color[i];
   const float2* mm = p->variant != 2 ? c->d_iso_mm : nullptr;
   const int variant = p->variant;

@@ -115,6 +115,9 @@ struct IsoArgs {
   int nbi[3];                        // the same as int (table addressing, REPEAT wrap)
   float iso, step_small, step_large, step_range;
   float half_block_len;              // length(G / numBlocks) * 0.5 (variant 1)
+  float bs[3];                       // G / numBlocks (getBlockBounds' blockSize)
+  float nhg[3];                      // -G * 0.5
+  float inv_g[3];                    // 1 / G (the block index fast path, verified)
   float color[4];
 };
 

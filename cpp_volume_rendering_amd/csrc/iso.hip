@@ -21,6 +21,7 @@
 // Deviation: a lane stops after kIsoMaxIter iterations (the reference can
 // loop without end when Color.a is 0; the default colour's alpha is 1).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 
 #include "cvr_device.h"
@@ -31,6 +32,10 @@ namespace cvr {
 namespace {
 
 constexpr uint32_t kIsoMaxIter = 1u << 22;
+#ifndef CVR_ISO_SPEC
+#define CVR_ISO_SPEC 4
+#endif
+constexpr int kIsoSpec = CVR_ISO_SPEC;   // speculative steps per round trip (variant 2)
 
 // texture(TexVolume, tex / VolumeGridSize).r: the rc1pass trilinear fetch at the
 // texel coordinate fma(tex, N/G, -0.5), clamped to the grid (CLAMP_TO_EDGE).
@@ -47,11 +52,20 @@ __device__ __forceinline__ f3 iso_tex(f3 eye, f3 dir, float t, f3 hg) {
 }
 
 // getBlockIndex (:86-89): floor((pos + G/2) / G * numBlocks), pos = r.Origin + t * r.Dir
+// Fast path: x * (1/G) * nb is within ~2e-5 of the exact value for the block
+// counts used (<= 1024 blocks), so away from an integer its floor is the
+// exact one; near an integer the correctly rounded division decides.
 __device__ __forceinline__ void iso_block(const IsoArgs& Q, f3 eye, f3 dir, float t, int b[3]) {
   const float p[3] = {fmaf(dir.x, t, eye.x), fmaf(dir.y, t, eye.y), fmaf(dir.z, t, eye.z)};
 #pragma unroll
-  for (int i = 0; i < 3; i++)
-    b[i] = (int)floorf(((p[i] + Q.a.half_grid[i]) / Q.G[i]) * Q.nb[i]);
+  for (int i = 0; i < 3; i++) {
+    const float x = p[i] + Q.a.half_grid[i];
+    const float ya = (x * Q.inv_g[i]) * Q.nb[i];
+    const float fa = floorf(ya);
+    const float margin = fmaxf(1e-3f, fabsf(ya) * 1e-5f);
+    const bool sure = (ya - fa) > margin && (fa + 1.0f - ya) > margin;
+    b[i] = (int)(sure ? fa : floorf((x / Q.G[i]) * Q.nb[i]));
+  }
 }
 
 // texture(TexBlockMin/Max, (idx + 0.5) / numBlocks), NEAREST + REPEAT
@@ -61,7 +75,8 @@ __device__ __forceinline__ float2 iso_block_range(const IsoArgs& Q, const float2
 #pragma unroll
   for (int i = 0; i < 3; i++) {
     const int n = Q.nbi[i];
-    w[i] = ((b[i] % n) + n) % n;
+    const int v = b[i];
+    w[i] = (v >= 0 && v < n) ? v : (v < 0 && v >= -n ? v + n : (v >= n && v < 2 * n ? v - n : ((v % n) + n) % n));
   }
   return mm[((size_t)w[2] * Q.nbi[1] + w[1]) * Q.nbi[0] + w[0]];
 }
@@ -133,29 +148,57 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
   SamplePos sp;
   if (VARIANT == 2) {
     // RayCasting1PassIsoAdapt (rc1pisoadapt/ray_marching_1p_iso_adapt.comp:113-172):
-    // adaptive steps over s in [0, D) from the entry point, no blocks
+    // adaptive steps over s in [0, D) from the entry point, no blocks.  Each step
+    // size depends on the density just fetched, so one lane would have one load
+    // in flight.  Instead kIsoSpec steps are issued at once, all of the size the
+    // current decision gives (s += min(step, D - s) evaluated as the shader
+    // does); they are consumed in order while each new density keeps that
+    // decision, and the rest are dropped.  Results and counts are the shader's.
     const f3 tp = r.tpos;
     const float D = r.D;
     float prev = iso_density(A, cells, tp, sp);
     fetches++;
     float s = 0.0f;
     while (s < D && iters < kIsoMaxIter) {
-      iters++;
-      const float step = fabsf(prev - iso) < Q.step_range ? Q.step_small : Q.step_large;
-      const float h = fminf(step, D - s);
-      const float sh = s + h;
-      const float dens = iso_density(
-          A, cells, f3{fmaf(dir.x, sh, tp.x), fmaf(dir.y, sh, tp.y), fmaf(dir.z, sh, tp.z)}, sp);
-      fetches++;
-      if ((prev <= iso && iso < dens) || (prev >= iso && iso > dens)) {
-        const float tt = (iso - prev) / (dens - prev);
-        const float st = fmaf(tt, h, s);
-        const f3 hp{fmaf(dir.x, st, tp.x), fmaf(dir.y, st, tp.y), fmaf(dir.z, st, tp.z)};
-        iso_composite(Q, iso_hit_colour<PHONG>(Q, grad, hp, hg, eye), dst);
-        if (dst.w > 0.99f) break;
+      const bool near = fabsf(prev - iso) < Q.step_range;
+      const float step = near ? Q.step_small : Q.step_large;
+      uint4 c[kIsoSpec];
+      SamplePos ps[kIsoSpec];
+      float hk[kIsoSpec];
+      bool ok[kIsoSpec];
+      float ss = s;
+#pragma unroll
+      for (int k = 0; k < kIsoSpec; k++) {
+        ok[k] = ss < D;
+        const float h = fminf(step, D - ss);
+        const float sh = ss + h;
+        ps[k] = sample_pos_clamped(fmaf(fmaf(dir.x, sh, tp.x), A.n_over_g[0], -0.5f),
+                                   fmaf(fmaf(dir.y, sh, tp.y), A.n_over_g[1], -0.5f),
+                                   fmaf(fmaf(dir.z, sh, tp.z), A.n_over_g[2], -0.5f), A);
+        c[k] = cells[ps[k].idx];
+        hk[k] = h;
+        ss = sh;
       }
-      prev = dens;
-      s = s + h;
+      bool done = false;
+#pragma unroll
+      for (int k = 0; k < kIsoSpec; k++) {
+        if (k > 0 && (!ok[k] || iters >= kIsoMaxIter || (fabsf(prev - iso) < Q.step_range) != near))
+          break;
+        iters++;
+        const float h = hk[k];
+        const float dens = trilerp_cell(c[k], ps[k].ax, ps[k].ay, ps[k].az);
+        fetches++;
+        if ((prev <= iso && iso < dens) || (prev >= iso && iso > dens)) {
+          const float tt = (iso - prev) / (dens - prev);
+          const float st = fmaf(tt, h, s);
+          const f3 hp{fmaf(dir.x, st, tp.x), fmaf(dir.y, st, tp.y), fmaf(dir.z, st, tp.z)};
+          iso_composite(Q, iso_hit_colour<PHONG>(Q, grad, hp, hg, eye), dst);
+          if (dst.w > 0.99f) { done = true; break; }
+        }
+        prev = dens;
+        s = s + h;
+      }
+      if (done) break;
     }
     return;
   }
@@ -166,6 +209,20 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
   bool have = true;
   while (t < tfar && iters < kIsoMaxIter) {
     iters++;
+    // The in-block path's next fetch depends on t and a density already known
+    // (variant 0: the old prevDensity; variant 1: the density at t when `have`),
+    // not on the block table: issue it before the table lookup so both loads are
+    // in flight together.  It is used only when that path runs at this t.
+    const float known = VARIANT == 0 ? pd : dc;
+    const float sstep = fabsf(known - iso) < Q.step_range
+                            ? Q.step_small
+                            : (VARIANT == 0 ? Q.step_large : fminf(Q.step_large, Q.half_block_len));
+    const float sh = fminf(sstep, tfar - t);
+    const float st2 = t + sh;
+    const SamplePos sp2 = sample_pos_clamped(fmaf(iso_tex(eye, dir, st2, hg).x, A.n_over_g[0], -0.5f),
+                                             fmaf(iso_tex(eye, dir, st2, hg).y, A.n_over_g[1], -0.5f),
+                                             fmaf(iso_tex(eye, dir, st2, hg).z, A.n_over_g[2], -0.5f), A);
+    const uint4 c2 = cells[sp2.idx];
     int b[3];
     iso_block(Q, eye, dir, t, b);
     const float2 m = iso_block_range(Q, mm, b);
@@ -173,9 +230,8 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
     float bmin[3], bmax[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-      const float bs = Q.G[i] / Q.nb[i];
-      bmin[i] = -Q.G[i] * 0.5f + bs * (float)b[i];
-      bmax[i] = bmin[i] + bs;
+      bmin[i] = Q.nhg[i] + Q.bs[i] * (float)b[i];
+      bmax[i] = bmin[i] + Q.bs[i];
     }
     const float d[3] = {dir.x, dir.y, dir.z};
     const float op[3] = {fmaf(dir.x, t, eye.x), fmaf(dir.y, t, eye.y), fmaf(dir.z, t, eye.z)};
@@ -204,11 +260,13 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
       }
       // adaptive step: the size from the OLD prevDensity, then prevDensity at t
       const float step = fabsf(pd - iso) < Q.step_range ? Q.step_small : Q.step_large;
+      const bool fresh = !tilted;   // t and the old prevDensity as at the hoisted fetch
       pd = have ? dc : iso_density(A, cells, iso_tex(eye, dir, t, hg), sp);
       fetches++;
       const float h = fminf(step, tfar - t);
       t += h;
-      const float dens = iso_density(A, cells, iso_tex(eye, dir, t, hg), sp);
+      const float dens = fresh ? trilerp_cell(c2, sp2.ax, sp2.ay, sp2.az)
+                               : iso_density(A, cells, iso_tex(eye, dir, t, hg), sp);
       fetches++;
       dc = dens;
       have = true;
@@ -240,6 +298,7 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
         have = false;
         continue;
       }
+      const bool fresh = have;              // the hoisted fetch used dc = density at t
       const float cur = have ? dc : iso_density(A, cells, iso_tex(eye, dir, t, hg), sp);
       fetches++;
       const float step = fabsf(cur - iso) < Q.step_range ? Q.step_small
@@ -247,7 +306,8 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
       const float h = fminf(step, tfar - t);
       pd = cur;
       t += h;
-      const float dens = iso_density(A, cells, iso_tex(eye, dir, t, hg), sp);
+      const float dens = fresh ? trilerp_cell(c2, sp2.ax, sp2.ay, sp2.az)
+                               : iso_density(A, cells, iso_tex(eye, dir, t, hg), sp);
       fetches++;
       dc = dens;
       have = true;
@@ -292,13 +352,22 @@ iso_tile_kernel(IsoArgs Q, const uint4* __restrict__ cells, const uint4* __restr
 // rc1custompisoadaptrenderer.cpp:20-117): blocks of ceil(N / nb) voxels per
 // axis, [start, min(start + size, N)); raw integer extremes here, normalised by
 // the host (v / 255 or v / 65535 in double, then float, the R32F texture).
+// Workgroup (block, slab): `zc` planes of one block, folded in by atomics, so a
+// 4^3 table still spreads over the whole chip.
+__global__ void block_minmax_init(uint2* __restrict__ out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = make_uint2(0xffffffffu, 0u);
+}
+
 template <typename VT>
-__global__ void block_minmax_kernel(const VT* __restrict__ vox, int nx, int ny, int nz, int nbx,
-                                    int nby, int bsx, int bsy, int bsz, uint2* __restrict__ out) {
-  const int blk = blockIdx.x;
+__global__ void __launch_bounds__(256)
+block_minmax_kernel(const VT* __restrict__ vox, int nx, int ny, int nz, int nbx, int nby, int bsx,
+                    int bsy, int bsz, int zc, int nslab, uint2* __restrict__ out) {
+  const int blk = blockIdx.x / nslab, slab = blockIdx.x % nslab;
   const int bx = blk % nbx, by = (blk / nbx) % nby, bz = blk / (nbx * nby);
-  const int x0 = bx * bsx, y0 = by * bsy, z0 = bz * bsz;
-  const int x1 = min(x0 + bsx, nx), y1 = min(y0 + bsy, ny), z1 = min(z0 + bsz, nz);
+  const int x0 = bx * bsx, y0 = by * bsy, zb = bz * bsz;
+  const int x1 = min(x0 + bsx, nx), y1 = min(y0 + bsy, ny), zb1 = min(zb + bsz, nz);
+  const int z0 = zb + slab * zc, z1 = min(z0 + zc, zb1);
   uint32_t lo = 0xffffffffu, hi = 0;
   const int w = x1 - x0, h = y1 - y0, dpt = z1 - z0;
   const long long n = (w > 0 && h > 0 && dpt > 0) ? (long long)w * h * dpt : 0;
@@ -319,7 +388,10 @@ __global__ void block_minmax_kernel(const VT* __restrict__ vox, int nx, int ny, 
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[blk] = make_uint2(slo[0], shi[0]);
+  if (threadIdx.x == 0 && n > 0) {
+    atomicMin(&out[blk].x, slo[0]);
+    atomicMax(&out[blk].y, shi[0]);
+  }
 }
 
 }  // namespace
@@ -328,13 +400,20 @@ hipError_t launch_block_minmax(const void* vox, int bpv, const int N[3], const i
                                hipStream_t s) {
   const int bs[3] = {(N[0] + nb[0] - 1) / nb[0], (N[1] + nb[1] - 1) / nb[1],
                      (N[2] + nb[2] - 1) / nb[2]};
-  const dim3 g((unsigned)(nb[0] * nb[1] * nb[2])), b(256);
+  const int nblk = nb[0] * nb[1] * nb[2];
+  // slabs of >= 4 planes until the grid has ~4096 workgroups
+  const int want = std::max(1, std::min((4096 + nblk - 1) / nblk, (bs[2] + 3) / 4));
+  const int zc = (bs[2] + want - 1) / want;
+  const int nslab = (bs[2] + zc - 1) / zc;
+  hipLaunchKernelGGL(block_minmax_init, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, out,
+                     nblk);
+  const dim3 g((unsigned)((long long)nblk * nslab)), b(256);
   if (bpv == 1)
     hipLaunchKernelGGL(block_minmax_kernel<uint8_t>, g, b, 0, s, (const uint8_t*)vox, N[0], N[1],
-                       N[2], nb[0], nb[1], bs[0], bs[1], bs[2], out);
+                       N[2], nb[0], nb[1], bs[0], bs[1], bs[2], zc, nslab, out);
   else
     hipLaunchKernelGGL(block_minmax_kernel<uint16_t>, g, b, 0, s, (const uint16_t*)vox, N[0], N[1],
-                       N[2], nb[0], nb[1], bs[0], bs[1], bs[2], out);
+                       N[2], nb[0], nb[1], bs[0], bs[1], bs[2], zc, nslab, out);
   return hipGetLastError();
 }
 
