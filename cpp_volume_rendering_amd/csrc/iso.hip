@@ -202,6 +202,15 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
     }
     return;
   }
+  // rayDirRecip of the V2 file (:107-110), per ray
+  float rdir[3];
+  {
+    const float dd[3] = {dir.x, dir.y, dir.z};
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+      rdir[i] = fabsf(dd[i]) > 1e-6f ? 1.0f / dd[i]
+                                     : (dd[i] > 0.0f ? 1e6f : (dd[i] < 0.0f ? -1e6f : 0.0f));
+  }
   float t = r.tnear;
   float pd = iso_density(A, cells, iso_tex(eye, dir, t, hg), sp);   // prevDensity at tnear
   fetches++;
@@ -283,11 +292,7 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
         // calculateNextBlockIntersection of the V2 file (:105-135): exit distance + offsets
         float tmax[3];
 #pragma unroll
-        for (int i = 0; i < 3; i++) {
-          const float rc = fabsf(d[i]) > 1e-6f ? 1.0f / d[i]
-                                               : (d[i] > 0.0f ? 1e6f : (d[i] < 0.0f ? -1e6f : 0.0f));
-          tmax[i] = fmaxf((bmin[i] - op[i]) * rc, (bmax[i] - op[i]) * rc);
-        }
+        for (int i = 0; i < 3; i++) tmax[i] = fmaxf((bmin[i] - op[i]) * rdir[i], (bmax[i] - op[i]) * rdir[i]);
         float exitT = fminf(fminf(tmax[0], tmax[1]), tmax[2]);
         if (fabsf(exitT - tmax[0]) < 1e-5f) exitT += 1e-4f;
         if (fabsf(exitT - tmax[1]) < 1e-5f) exitT += 1e-4f;
