@@ -217,6 +217,59 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
   float dc = pd;
   bool have = true;
   while (t < tfar && iters < kIsoMaxIter) {
+    if (VARIANT == 1 && have) {
+      // Speculative run of the V2 in-block path: kIsoSpec steps of the size the
+      // density at t gives, their block lookups and volume fetches issued
+      // together, consumed in order while the block is not skippable, the step
+      // decision holds and no surface is hit; anything else falls back to the
+      // one-step path below at the same t.
+      const bool near0 = fabsf(dc - iso) < Q.step_range;
+      const float sstep = near0 ? Q.step_small : fminf(Q.step_large, Q.half_block_len);
+      float tk[kIsoSpec + 1], hk[kIsoSpec];
+      uint4 ck[kIsoSpec];
+      SamplePos pk[kIsoSpec];
+      float2 mk[kIsoSpec];
+      tk[0] = t;
+#pragma unroll
+      for (int k = 0; k < kIsoSpec; k++) {
+        hk[k] = fminf(sstep, tfar - tk[k]);
+        tk[k + 1] = tk[k] + hk[k];
+        const f3 q = iso_tex(eye, dir, tk[k + 1], hg);
+        pk[k] = sample_pos_clamped(fmaf(q.x, A.n_over_g[0], -0.5f), fmaf(q.y, A.n_over_g[1], -0.5f),
+                                   fmaf(q.z, A.n_over_g[2], -0.5f), A);
+        ck[k] = cells[pk[k].idx];
+        int bk[3];
+        iso_block(Q, eye, dir, tk[k], bk);
+        mk[k] = iso_block_range(Q, mm, bk);
+      }
+      int used = 0;
+      bool done = false;
+#pragma unroll
+      for (int k = 0; k < kIsoSpec; k++) {
+        if (!(t < tfar) || iters >= kIsoMaxIter) break;
+        if (iso < mk[k].x - 0.001f || iso > mk[k].y + 0.001f) break;
+        if (k > 0 && (fabsf(dc - iso) < Q.step_range) != near0) break;
+        iters++;
+        used++;
+        fetches++;                       // currentDensity at t (= dc)
+        pd = dc;
+        const float h = hk[k];
+        t = tk[k + 1];                   // t += h
+        const float dens = trilerp_cell(ck[k], pk[k].ax, pk[k].ay, pk[k].az);
+        fetches++;
+        dc = dens;
+        if ((pd <= iso && iso < dens) || (pd >= iso && iso > dens)) {
+          const float tt = (iso - pd) / (dens - pd);
+          t = t - h * (1.0f - tt);
+          have = false;
+          iso_composite(Q, iso_hit_colour<PHONG>(Q, grad, iso_tex(eye, dir, t, hg), hg, eye), dst);
+          if (dst.w > 0.99f) done = true;
+          break;
+        }
+      }
+      if (done) break;
+      if (used > 0) continue;
+    }
     iters++;
     // The in-block path's next fetch depends on t and a density already known
     // (variant 0: the old prevDensity; variant 1: the density at t when `have`),
