@@ -217,14 +217,17 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
   float dc = pd;
   bool have = true;
   while (t < tfar && iters < kIsoMaxIter) {
-    if (VARIANT == 1 && have) {
-      // Speculative run of the V2 in-block path: kIsoSpec steps of the size the
+    if (have) {
+      // Speculative run of the in-block path: kIsoSpec steps of the size the
       // density at t gives, their block lookups and volume fetches issued
       // together, consumed in order while the block is not skippable, the step
       // decision holds and no surface is hit; anything else falls back to the
       // one-step path below at the same t.
-      const bool near0 = fabsf(dc - iso) < Q.step_range;
-      const float sstep = near0 ? Q.step_small : fminf(Q.step_large, Q.half_block_len);
+      // (variant 0 sizes the step from the old prevDensity, variant 1 from the
+      // density at t)
+      const bool near0 = fabsf((VARIANT == 0 ? pd : dc) - iso) < Q.step_range;
+      const float sstep = near0 ? Q.step_small
+                                : (VARIANT == 0 ? Q.step_large : fminf(Q.step_large, Q.half_block_len));
       float tk[kIsoSpec + 1], hk[kIsoSpec];
       uint4 ck[kIsoSpec];
       SamplePos pk[kIsoSpec];
@@ -247,11 +250,13 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
 #pragma unroll
       for (int k = 0; k < kIsoSpec; k++) {
         if (!(t < tfar) || iters >= kIsoMaxIter) break;
-        if (iso < mk[k].x - 0.001f || iso > mk[k].y + 0.001f) break;
-        if (k > 0 && (fabsf(dc - iso) < Q.step_range) != near0) break;
+        if (VARIANT == 0 ? (iso < mk[k].x || iso > mk[k].y)
+                         : (iso < mk[k].x - 0.001f || iso > mk[k].y + 0.001f))
+          break;
+        if (k > 0 && (fabsf((VARIANT == 0 ? pd : dc) - iso) < Q.step_range) != near0) break;
         iters++;
         used++;
-        fetches++;                       // currentDensity at t (= dc)
+        fetches++;                       // prevDensity / currentDensity at t (= dc)
         pd = dc;
         const float h = hk[k];
         t = tk[k + 1];                   // t += h
@@ -259,8 +264,12 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
         fetches++;
         dc = dens;
         if ((pd <= iso && iso < dens) || (pd >= iso && iso > dens)) {
-          const float tt = (iso - pd) / (dens - pd);
-          t = t - h * (1.0f - tt);
+          if (VARIANT == 0) {
+            t -= (dens - iso) / (dens - pd);
+          } else {
+            const float tt = (iso - pd) / (dens - pd);
+            t = t - h * (1.0f - tt);
+          }
           have = false;
           iso_composite(Q, iso_hit_colour<PHONG>(Q, grad, iso_tex(eye, dir, t, hg), hg, eye), dst);
           if (dst.w > 0.99f) done = true;
