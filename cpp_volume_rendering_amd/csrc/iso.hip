@@ -241,9 +241,31 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
         pk[k] = sample_pos_clamped(fmaf(q.x, A.n_over_g[0], -0.5f), fmaf(q.y, A.n_over_g[1], -0.5f),
                                    fmaf(q.z, A.n_over_g[2], -0.5f), A);
         ck[k] = cells[pk[k].idx];
-        int bk[3];
-        iso_block(Q, eye, dir, tk[k], bk);
-        mk[k] = iso_block_range(Q, mm, bk);
+      }
+      // Block of each step start.  The index floor((fma(d, t, e) + G/2) / G * nb)
+      // is a composition of correctly rounded monotone operations, so it is
+      // monotone in t: equal at the first and last start (the starts not
+      // decreasing) means equal at every start in between.
+      {
+        int b0[3], bl[3];
+        iso_block(Q, eye, dir, tk[0], b0);
+        iso_block(Q, eye, dir, tk[kIsoSpec - 1], bl);
+        bool mono = true;                  // every h >= 0: the starts do not decrease
+#pragma unroll
+        for (int k = 0; k + 1 < kIsoSpec; k++) mono = mono && hk[k] >= 0.0f;
+        const bool same = mono && b0[0] == bl[0] && b0[1] == bl[1] && b0[2] == bl[2];
+        mk[0] = iso_block_range(Q, mm, b0);
+        if (same) {
+#pragma unroll
+          for (int k = 1; k < kIsoSpec; k++) mk[k] = mk[0];
+        } else {
+#pragma unroll
+          for (int k = 1; k < kIsoSpec; k++) {
+            int bk[3];
+            iso_block(Q, eye, dir, tk[k], bk);
+            mk[k] = iso_block_range(Q, mm, bk);
+          }
+        }
       }
       int used = 0;
       bool done = false;
