@@ -60,8 +60,10 @@ HBM_PEAK_GBS = 8000.0    # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=0, help="default 50 (dos: 5)")
-    p.add_argument("--warmup", type=int, default=-1, help="default 5 (dos: 1)")
+    p.add_argument("--steps", type=int, default=0,
+                   help="default 200 (iso*: 20, dos: 5, ebs: 2)")
+    p.add_argument("--warmup", type=int, default=-1,
+                   help="default 20 (iso*: 3, dos/ebs: 1)")
     p.add_argument("--size", type=int, default=0, help="volume N^3 (default 512; ebs 1024)")
     p.add_argument("--res", type=int, default=0, help="viewport (default 1024; dos 2048)")
     p.add_argument("--renderer", choices=["rc1pass", "dos", "ebs", "iso", "isodfs", "isoadapt"],
@@ -278,8 +280,10 @@ def main():
     iso_variant = {"iso": 0, "isodfs": 1, "isoadapt": 2}.get(a.renderer)
     iso = iso_variant is not None
     shaded = dos or ebs
-    a.steps = a.steps or (5 if dos else (2 if ebs else 50))
-    a.warmup = a.warmup if a.warmup >= 0 else (1 if shaded else 5)
+    # sub-millisecond frames: enough untimed frames for the clocks to settle
+    # (5 warmup frames measured ~8 % slower than 20) and a timed region of ~25 ms
+    a.steps = a.steps or (5 if dos else (2 if ebs else (20 if iso else 200)))
+    a.warmup = a.warmup if a.warmup >= 0 else (1 if shaded else (3 if iso else 20))
     n, W = a.size or (1024 if ebs else 512), a.res or (2048 if dos else 1024)
     H = W
     vol = D.marschner_lobb_u8(n) if a.field == "ml" else D.blobs_u8(n)
