@@ -311,7 +311,9 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
                             ? Q.step_small
                             : (VARIANT == 0 ? Q.step_large : fminf(Q.step_large, Q.half_block_len));
     const float sh = fminf(sstep, tfar - t);
-    const float st2 = t + sh;
+    // (variant 1 without the density at t: the hoisted fetch is that density,
+    // currentDensity, instead)
+    const float st2 = (VARIANT == 1 && !have) ? t : t + sh;
     const SamplePos sp2 = sample_pos_clamped(fmaf(iso_tex(eye, dir, st2, hg).x, A.n_over_g[0], -0.5f),
                                              fmaf(iso_tex(eye, dir, st2, hg).y, A.n_over_g[1], -0.5f),
                                              fmaf(iso_tex(eye, dir, st2, hg).z, A.n_over_g[2], -0.5f), A);
@@ -388,7 +390,7 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
         continue;
       }
       const bool fresh = have;              // the hoisted fetch used dc = density at t
-      const float cur = have ? dc : iso_density(A, cells, iso_tex(eye, dir, t, hg), sp);
+      const float cur = have ? dc : trilerp_cell(c2, sp2.ax, sp2.ay, sp2.az);
       fetches++;
       const float step = fabsf(cur - iso) < Q.step_range ? Q.step_small
                                                           : fminf(Q.step_large, Q.half_block_len);
