@@ -31,6 +31,36 @@ import time
 
 import numpy as np
 
+
+def _launch_ranks_if_needed():
+    """`bench.py --gpus N` with N > 1 outside a launcher: start N rank processes with
+    torch.distributed.run (127.0.0.1 rendezvous) as a CHILD process, before this process
+    touches HIP, and exit with its status; rank 0's JSON line reaches stdout directly.
+    Under a launcher (WORLD_SIZE set) --gpus must equal WORLD_SIZE."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    known, _ = pre.parse_known_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != known.gpus:
+            sys.exit(f"bench.py: --gpus {known.gpus} but WORLD_SIZE={env_world}")
+        return
+    if known.gpus <= 1:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={known.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    sys.exit(subprocess.call(cmd))
+
+
+if __name__ == "__main__":
+    _launch_ranks_if_needed()
+
 # Frames in flight run on separate HIP streams; HIP maps streams onto at most
 # GPU_MAX_HW_QUEUES hardware queues per process (4 by default), and streams that
 # share a queue serialise.  8 queues keep 4 render streams + RCCL's apart.  Set
@@ -88,7 +118,22 @@ def parse():
     p.add_argument("--postpass", action="store_true",
                    help="also time the multiscaling post-pass filters on this workload's frame")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_rc1pass.json"))
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher rehearsal without a GPU: the ranks join a gloo group and "
+                        "rank 0 prints the world size (tests/test_bench_launch.py)")
     return p.parse_args()
+
+
+def dry_run(world, rank):
+    if world > 1:
+        dist.init_process_group("gloo")
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank)
+        dist.destroy_process_group()
+    else:
+        ranks = [0]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": ranks}))
 
 
 def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgba=None,
@@ -269,6 +314,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry_run:
+        return dry_run(world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

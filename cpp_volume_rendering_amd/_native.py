@@ -57,7 +57,8 @@ class Camera(ctypes.Structure):
 
 class Frame(ctypes.Structure):
     _fields_ = [("camera", Camera), ("width", ctypes.c_int), ("height", ctypes.c_int),
-                ("tile_size", ctypes.c_int), ("rank", ctypes.c_int), ("nranks", ctypes.c_int)]
+                ("tile_size", ctypes.c_int), ("rank", ctypes.c_int), ("nranks", ctypes.c_int),
+                ("use_view", ctypes.c_int), ("view", ctypes.c_float * 16)]
 
 
 FORMAT_RGBA32F = 0

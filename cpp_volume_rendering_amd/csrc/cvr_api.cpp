@@ -266,6 +266,9 @@ void cvr_destroy(cvr_ctx* ctx) {
     if (o.done) (void)hipEventDestroy(o.done);
   }
   if (c->ev_frame) (void)hipEventDestroy(c->ev_frame);
+  if (c->ev_counters) (void)hipEventDestroy(c->ev_counters);
+  c->ev_counters = nullptr;
+  c->counters_stream = nullptr;
   if (c->side) (void)hipStreamDestroy(c->side);
   p = c->d_tile_stats; free_dev(p); c->d_tile_stats = nullptr;
   p = c->d_tile_samples; free_dev(p); c->d_tile_samples = nullptr;
@@ -578,6 +581,23 @@ int cvr_tiles_for_rank(const cvr_frame* f, int rank) {
   return nt > rank ? (nt - rank + f->nranks - 1) / f->nranks : 0;
 }
 
+// The per-tile sample counts and shade counters are shared by every render
+// stream.  A frame that uses them on stream s first waits for the last frame
+// that used them on another stream (frames in flight on rotated streams), and
+// records the event after its own epilogue (counters_release).
+static cvr_status counters_acquire(Ctx* c, hipStream_t s) {
+  if (!c->ev_counters) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_counters, hipEventDisableTiming));
+  if (c->counters_stream && c->counters_stream != s)
+    HIP_TRY(c, hipStreamWaitEvent(s, c->ev_counters, 0));
+  return CVR_OK;
+}
+
+static cvr_status counters_release(Ctx* c, hipStream_t s) {
+  HIP_TRY(c, hipEventRecord(c->ev_counters, s));
+  c->counters_stream = s;
+  return CVR_OK;
+}
+
 static cvr_status ensure_scratch(Ctx* c, size_t bytes) {
   if (c->scratch_bytes >= bytes) return CVR_OK;
   free_dev(c->d_scratch);
@@ -625,6 +645,8 @@ static void fill_frame_args(Ctx* c, const cvr_frame* f, float step, cvr::Rc1pass
                             int& ntiles, size_t& npix) {
   float V[16], tanh;
   cvr_camera_lookat(&f->camera, V, &tanh);
+  if (f->use_view)
+    for (int i = 0; i < 16; i++) V[i] = f->view[i];
   for (int i = 0; i < 3; i++) {
     A.eye[i] = f->camera.eye[i];
     A.col0[i] = V[0 * 4 + i];
@@ -712,6 +734,11 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     A.tile_stats = c->d_tile_stats;
   }
   A.shade_ctr = nullptr;
+  const bool use_counters = (c->shade_counters && phong) || o->total;
+  if (use_counters) {
+    cvr_status st = counters_acquire(c, c->stream);
+    if (st != CVR_OK) return st;
+  }
   if (c->shade_counters && phong) {   // measurement: shaded samples (gradient fetches)
     if (!c->d_shade) HIP_TRY(c, hipMalloc((void**)&c->d_shade, 3 * sizeof(unsigned long long)));
     HIP_TRY(c, hipMemsetAsync(c->d_shade, 0, 3 * sizeof(unsigned long long), c->stream));
@@ -855,6 +882,10 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     os.key = key;
   }
   c->frame_no++;
+  if (use_counters) {
+    cvr_status st = counters_release(c, s);
+    if (st != CVR_OK) return st;
+  }
   if (!o->on_device) {
     HIP_TRY(c, hipMemcpyAsync(o->rgba, d_out, rgba_bytes, hipMemcpyDeviceToHost, s));
     if (o->samples) HIP_TRY(c, hipMemcpyAsync(o->samples, d_samples, smp_bytes, hipMemcpyDeviceToHost, s));
@@ -994,6 +1025,11 @@ static cvr_status render_shaded(Ctx* c, const cvr_output* o, int ntiles, size_t 
     d_samples = o->samples ? (uint32_t*)((char*)c->d_scratch + rgba_bytes) : nullptr;
     d_total = o->total ? c->d_total : nullptr;
   }
+  const bool use_counters = d_total || c->shade_counters;
+  if (use_counters) {
+    cvr_status st = counters_acquire(c, s);
+    if (st != CVR_OK) return st;
+  }
   if (d_total && !o->on_device) HIP_TRY(c, hipMemsetAsync(d_total, 0, sizeof(unsigned long long), s));
   unsigned long long* tile_samples = nullptr;
   if (d_total) {
@@ -1023,6 +1059,10 @@ static cvr_status render_shaded(Ctx* c, const cvr_output* o, int ntiles, size_t 
     cvr::RenderPlan plan{};
     plan.ntiles = ntiles;
     HIP_TRY(c, cvr::launch_tile_epilogue(nullptr, tile_samples, d_total, plan, nullptr, s));
+  }
+  if (use_counters) {
+    cvr_status st = counters_release(c, s);
+    if (st != CVR_OK) return st;
   }
   if (!o->on_device) {
     HIP_TRY(c, hipMemcpyAsync(o->rgba, d_out, rgba_bytes, hipMemcpyDeviceToHost, s));
@@ -1440,6 +1480,8 @@ static cvr_status ensure_iso_blocks(Ctx* c, const int nb[3]) {
       mm[i] = make_float2((float)((double)raw[i].x / mx), (float)((double)raw[i].y / mx));
     }
   }
+  // frames still running on any render stream may read the old table
+  HIP_TRY(c, hipDeviceSynchronize());
   if (c->d_iso_mm && (c->iso_nb[0] * c->iso_nb[1] * c->iso_nb[2]) != (int)n) {
     void* p = c->d_iso_mm; free_dev(p); c->d_iso_mm = nullptr;
   }

@@ -234,6 +234,10 @@ struct Ctx {
   cvr_cone_tables* cone_tab = nullptr;   // host copies [2]
   unsigned long long* d_tile_samples = nullptr;   // per-wave-tile sample counts (zeroed)
   int tile_samples_n = 0;
+  // d_tile_samples and d_shade are one set per context: a frame that uses them on
+  // another stream than the previous user waits for that frame (counters_guard)
+  hipStream_t counters_stream = nullptr;
+  hipEvent_t ev_counters = nullptr;
   // isosurface block table (float2 min/max per block), built for iso_nb
   float2* d_iso_mm = nullptr;
   int iso_nb[3] = {0, 0, 0};

@@ -24,12 +24,12 @@
  *   cvr_render_rc1pass           <- RayCasting1Pass::Update + Redraw
  *                                   cppvolrend/structured/rc1pass/rc1prenderer.cpp:72-151
  *                                   (the dispatch of ray_marching_1p.comp:85-179)
- *   cvr_set_extinction_volume    <- ExtinctionCoefficientVolume::GenerateExtinctionCoefficientVolume
+ *   cvr_set_extinction_volume    <- ExtinctionCoefficientVolume::BuildMipMappedTexture (extcoefvolumegenerator.cpp:20-40)
  *                                   (Gaussian mip pyramid of TF opacity -> extinction)
- *                                   cppvolrend/structured/rc1pdosct/extcoefvolume.cpp
+ *                                   cppvolrend/structured/rc1pdosct/extcoefvolumegenerator.cpp:230-408
  *   cvr_render_dosct             <- RC1PConeTracingDirOcclusionShading::Update + Redraw
  *                                   cppvolrend/structured/rc1pdosct/dosrcrenderer.cpp:134-260
- *                                   (the dispatch of ray_marching_1p_dosct.comp)
+ *                                   (the dispatch of ray_bbox_marching.comp:658-734)
  *   cvr_set_extinction_sat       <- RC1PExtinctionBasedShading::GenerateExtinctionSAT3DTex +
  *                                   SummedAreaTable3D<double>::BuildSAT
  *                                   cppvolrend/structured/rc1pextbsd/ebsrenderer.cpp:624-716,
@@ -92,6 +92,12 @@ typedef struct cvr_frame {
   int tile_size;
   int rank;
   int nranks;
+  /* use_view = 1: `view` is the column-major view matrix the reference uploads
+   * as u_CameraLookAt (vis::Camera::LookAt, camera.cpp:281-284, which keeps the
+   * look-at centre private) and camera.center is ignored; camera.eye is still
+   * CameraEye.  use_view = 0: view = glm::lookAt(eye, center, up).          */
+  int use_view;
+  float view[16];
 } cvr_frame;
 
 /* Output buffers.  rgba: premultiplied RGBA, W*H pixels (or the packed tile
@@ -299,7 +305,7 @@ cvr_status  cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* frame,
                                const cvr_rc1pass_params* params, const cvr_output* out);
 
 /* Extinction-coefficient mip pyramid of the current volume for the DOS
- * renderer (ExtinctionCoefficientVolume, extcoefvolume.cpp): level 0 at
+ * renderer (ExtinctionCoefficientVolume, extcoefvolumegenerator.cpp:230-408): level 0 at
  * res (NULL: 128^3) is a 7^3 Gaussian (sigma0, default 1) of the opacity TF
  * over the volume, level L the sigma 2^L Gaussian of level L-1 at res >> L,
  * each stored R16F and converted to tau = -log(1 - opacity).  tf_rgba is the

@@ -1,0 +1,73 @@
+/**
+ * Reference-side adapters: cppvolrend renderer plugins that forward to libcvr.so
+ * (include/cvr.h).  These files are meant to be dropped into the reference tree
+ * (e.g. cppvolrend/structured/hip/) and registered next to the existing renderers
+ * in cppvolrend/main.cpp:62-79 (see register_hip_renderers.cpp).
+ *
+ * HipRendererBase holds what every adapter shares:
+ *   - the cvr context (one per renderer object, device 0 unless told otherwise);
+ *   - the upload of the current structured volume (DataManager, datamanager.h:82-84;
+ *     StructuredGridVolume::GetArrayData / m_data_storage_size, structuredgridvolume.h:67-76)
+ *     and of the transfer function tables GenerateTexture_1D_RGBt / _RGBA build
+ *     (transferfunction.h:62-63), read back from their GL textures so the library
+ *     samples exactly the table the GLSL renderer samples;
+ *   - the frame: the camera's eye and its LookAt() matrix (camera.cpp:281-284) as
+ *     the reference uploads them (CameraEye, u_CameraLookAt, rc1prenderer.cpp:91-95);
+ *     the viewport as Update chooses it (rc1prenderer.cpp:76-87);
+ *   - Redraw and the three multiscaling redraws: the library renders into a host
+ *     RGBA16F buffer, which is uploaded into RenderFrameToScreen's own RGBA16F
+ *     texture and drawn by the reference's Draw* functions
+ *     (renderoutputframe.h:38-51), as rc1prenderer.cpp:140-189 does after its dispatch.
+ * Errors: a non-OK cvr_status becomes Init() == false (rc1prenderer.cpp:54) or a
+ * printed message; the library never calls exit().
+ */
+#ifndef CVR_HIP_RENDERER_BASE_H
+#define CVR_HIP_RENDERER_BASE_H
+
+#include "../../volrenderbase.h"
+
+#include <cvr.h>
+
+#include <cstdint>
+#include <vector>
+
+class HipRendererBase : public BaseVolumeRenderer
+{
+public:
+  explicit HipRendererBase (int hip_device = 0);
+  virtual ~HipRendererBase ();
+
+  vis::GRID_VOLUME_DATA_TYPE GetDataTypeSupport () override
+  {
+    return vis::GRID_VOLUME_DATA_TYPE::STRUCTURED;
+  }
+
+  void Clean () override;
+  void ReloadShaders () override;       // compiled kernels: only the screen shaders reload
+  void Redraw () override;
+  void MultiSampleRedraw () override;
+  void DownScalingRedraw () override;
+  void UpScalingRedraw () override;
+
+protected:
+  // One frame of this renderer into `out` (host RGBA16F, frame_'s viewport).
+  virtual cvr_status RenderFrame (const cvr_output* out) = 0;
+
+  bool UploadVolume ();                          // cvr_set_volume
+  bool UploadTransferFunction ();                // cvr_set_transfer_function (RGBt)
+  bool ReadTransferFunctionRGBA (std::vector<float>* rgba, int* n);   // opacity TF
+  bool UploadGradient (bool wanted);             // cvr_set_gradient from the DataManager's type
+  float DefaultStep ();                          // rc1prenderer.cpp:62-63
+  void FillFrame (vis::Camera* camera);          // frame_ from the camera + viewport
+  bool Fail (const char* where);
+
+  cvr_ctx* m_cvr;
+  cvr_frame frame_;
+
+private:
+  bool RenderToScreenTexture ();
+  static bool ReadTexture1D (gl::Texture1D* tex, std::vector<float>* rgba, int* n);
+  std::vector<uint16_t> m_rgba16f;
+};
+
+#endif

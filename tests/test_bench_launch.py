@@ -1,0 +1,44 @@
+"""`bench.py --gpus N` starts N ranks itself (torch.distributed.run as a child process,
+127.0.0.1 rendezvous) and rejects a --gpus that disagrees with the launcher's WORLD_SIZE.
+The ranks run bench.py's --dry-run leg (gloo, no GPU), so this runs on the CPU."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env=None):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
+                          capture_output=True, text=True, timeout=300, env=e, cwd=ROOT)
+
+
+def _json_line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_gpus_2_launches_two_ranks():
+    p = _run(["--gpus", "2", "--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _json_line(p.stdout)
+    assert d["n_gpus"] == 2 and sorted(d["ranks"]) == [0, 1]
+
+
+def test_gpus_1_stays_in_process():
+    p = _run(["--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert _json_line(p.stdout)["n_gpus"] == 1
+
+
+def test_gpus_disagreeing_with_world_size_fails():
+    p = _run(["--gpus", "4", "--dry-run"], env={"WORLD_SIZE": "2", "RANK": "0",
+                                                "LOCAL_RANK": "0"})
+    assert p.returncode != 0
+    assert "WORLD_SIZE" in p.stderr
