@@ -989,6 +989,52 @@ ORACLE_API void oracle_sat_build(const void* vox, int bpv, int W, int H, int D, 
       }
 }
 
+// The same recurrence streamed over z with two double planes ((W+2)(H+2) doubles
+// each) instead of the whole (W+2)(H+2)(D+2) grid: every BuildSAT cell is a
+// function of its seven lower neighbours only (summedareatable.h:218-278), so any
+// order that visits a cell after them reproduces the reference's doubles exactly.
+// Emits, as float, the planes listed in zs[0..nz) (ascending), for full-size
+// checks (1026^3 would need 8.6 GB as one double grid).
+ORACLE_API void oracle_sat_planes(const void* vox, int bpv, int W, int H, int D, const float* lut,
+                                  const int* zs, int nz, float* out) {
+  const int w = W + 2, h = H + 2, d = D + 2;
+  const size_t plane = (size_t)w * h;
+  std::vector<double> prev(plane, 0.0), cur(plane, 0.0);
+  auto raw = [&](int x, int y, int z) -> double {
+    if (x == 0 || y == 0 || z == 0 || x == w - 1 || y == h - 1 || z == d - 1) return 0.0f;
+    const int64_t i = (int64_t)(x - 1) + (int64_t)(y - 1) * W + (int64_t)(z - 1) * W * H;
+    const int v = bpv == 1 ? ((const uint8_t*)vox)[i] : ((const uint16_t*)vox)[i];
+    return lut[v];
+  };
+  int k = 0;
+  for (int z = 0; z < d && k < nz; z++) {
+    auto C = [&](int x, int y) -> double& { return cur[(size_t)x + (size_t)w * y]; };
+    auto P = [&](int x, int y) -> double { return prev[(size_t)x + (size_t)w * y]; };
+    if (z == 0) {
+      C(0, 0) = raw(0, 0, 0);
+      for (int x = 1; x < w; x++) C(x, 0) = C(x - 1, 0) + raw(x, 0, 0);
+      for (int y = 1; y < h; y++) C(0, y) = C(0, y - 1) + raw(0, y, 0);
+      for (int x = 1; x < w; x++)
+        for (int y = 1; y < h; y++)
+          C(x, y) = C(x - 1, y) + C(x, y - 1) - C(x - 1, y - 1) + raw(x, y, 0);
+    } else {
+      C(0, 0) = P(0, 0) + raw(0, 0, z);
+      for (int x = 1; x < w; x++) C(x, 0) = C(x - 1, 0) + P(x, 0) - P(x - 1, 0) + raw(x, 0, z);
+      for (int y = 1; y < h; y++) C(0, y) = C(0, y - 1) + P(0, y) - P(0, y - 1) + raw(0, y, z);
+      for (int y = 1; y < h; y++)
+        for (int x = 1; x < w; x++)
+          C(x, y) = raw(x, y, z) + P(x - 1, y - 1) + P(x, y) + C(x, y - 1) + C(x - 1, y)
+                  - C(x - 1, y - 1) - P(x, y - 1) - P(x - 1, y);
+    }
+    if (z == zs[k]) {
+      float* o = out + (size_t)k * plane;
+      for (size_t i = 0; i < plane; i++) o[i] = (float)cur[i];
+      k++;
+    }
+    std::swap(prev, cur);
+  }
+}
+
 struct OracleEbs {
   OracleRc1pass base;
   const float* sat; int sat_dims[3];   // the float SAT (W+2)(H+2)(D+2), x-fastest

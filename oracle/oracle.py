@@ -104,6 +104,8 @@ def lib():
         L.oracle_ext_lut.restype = None
         L.oracle_sat_build.argtypes = [P, I, I, I, I, P, P]
         L.oracle_sat_build.restype = None
+        L.oracle_sat_planes.argtypes = [P, I, I, I, I, P, P, I, P]
+        L.oracle_sat_planes.restype = None
         L.oracle_render_ebs_rows.argtypes = [ctypes.POINTER(OracleEbs), I, I, P, P, I]
         L.oracle_render_ebs_rows.restype = ctypes.c_uint64
         L.oracle_multiscale_filter.argtypes = [I, I, P, I, I, P, I, I]
@@ -341,6 +343,20 @@ def sat_build(vox: np.ndarray, lut: np.ndarray) -> np.ndarray:
     lut = np.ascontiguousarray(lut, np.float32)
     out = np.zeros((d + 2, h + 2, w + 2), np.float64)
     lib().oracle_sat_build(_p(v), v.dtype.itemsize, w, h, d, _p(lut), _p(out))
+    return out
+
+
+def sat_planes(vox: np.ndarray, lut: np.ndarray, zs) -> np.ndarray:
+    """Planes zs of the float SAT of sat_build, by the same recurrence streamed over z
+    (two double planes of memory): for full-size (1024^3) checks."""
+    v = np.ascontiguousarray(vox)
+    d, h, w = v.shape
+    zs = np.ascontiguousarray(sorted(int(z) for z in zs), np.int32)
+    assert zs.size and 0 <= zs[0] and zs[-1] < d + 2
+    lut = np.ascontiguousarray(lut, np.float32)
+    out = np.zeros((zs.size, h + 2, w + 2), np.float32)
+    lib().oracle_sat_planes(_p(v), v.dtype.itemsize, w, h, d, _p(lut), _p(zs), int(zs.size),
+                            _p(out))
     return out
 
 

@@ -74,3 +74,17 @@ def test_sat_recurrence_is_a_prefix_sum(oracle):
 def test_ebs_api_errors():
     L = N.lib()
     assert L.cvr_tf1d_ext_lut(None, 0, None, 0, 255, 0, 3, None) == N.CVR_ERR_ARG
+
+
+@pytest.mark.parametrize("shape,bpv", [((9, 7, 5), 1), ((20, 33, 17), 2), ((48, 40, 36), 1)])
+def test_sat_planes_stream_equals_build(oracle, shape, bpv):
+    """oracle.sat_planes (the recurrence streamed over z, two double planes: the full-size
+    1024^3 check of tests/test_fullsize_gpu.py) == oracle.sat_build plane for plane."""
+    rng = np.random.default_rng(7 + bpv)
+    vox = rng.integers(0, 256 if bpv == 1 else 65536, shape,
+                       dtype=np.uint8 if bpv == 1 else np.uint16)
+    lut = lib_ext_lut(bpv)
+    full = oracle.sat_build(vox, lut).astype(np.float32)
+    zs = sorted({0, 1, 2, shape[0] // 2, shape[0], shape[0] + 1})
+    got = oracle.sat_planes(vox, lut, zs)
+    assert np.array_equal(got.view(np.uint32), full[zs].view(np.uint32))

@@ -158,3 +158,33 @@ def test_ebs_errors(bonsai_tf):
         assert L.cvr_render_extbsd(d.handle, ctypes.byref(fr), ctypes.byref(p), ctypes.byref(out)) == N.CVR_ERR_ARG
     finally:
         d.close()
+
+
+@pytest.mark.parametrize("nranks,tile", [(2, 32), (3, 16), (8, 32)])
+def test_ebs_screen_tiles_match_full_frame(dev, bonsai_tf, nranks, tile):
+    """Multi-GPU split of the EBS renderer (config 5 runs over 8 GPUs): every rank's packed
+    tiles, unpacked, equal the 1-GPU frame bit for bit, and the sample counts add up."""
+    from cpp_volume_rendering_amd import screen_tiles as T
+    n = 40
+    vol = D.marschner_lobb_u8(n)
+    gpu_sat(dev, vol, D.voxel_scale(n))
+    dev.set_transfer_function(bonsai_tf)
+    dev.set_gradient(0)
+    p = ebs_params()
+    W, H = 100, 72
+    full, _, full_total = gpu_ebs(dev, INITIAL, W, H, p)
+    tpr = T.max_tiles_per_rank(W, H, tile, nranks)
+    packed = np.zeros((nranks, tpr, tile, tile, 4), np.float32)
+    tot = 0
+    for r in range(nranks):
+        k = T.tiles_for_rank(W, H, tile, r, nranks)
+        rgba = np.zeros((k, tile, tile, 4), np.float32)
+        total = np.zeros(1, np.uint64)
+        out = N.Output(rgba.ctypes.data, None, total.ctypes.data, 0)
+        fr = make_frame(Camera(**INITIAL), W, H, tile, r, nranks)
+        N.check(N.lib().cvr_render_extbsd(dev.handle, ctypes.byref(fr), ctypes.byref(p),
+                                          ctypes.byref(out)), "extbsd tiles", dev.handle)
+        packed[r, :k] = rgba
+        tot += int(total[0])
+    assert tot == full_total
+    assert_bitexact(T.unpack(packed, W, H, tile, nranks), full, "ebs tiles")
