@@ -82,7 +82,8 @@ from cpp_volume_rendering_amd.renderer import (CustomRayCasting1PassIsoAdapt,  #
 from cpp_volume_rendering_amd.renderer import (Camera, DataManager, RayCasting1Pass,  # noqa: E402
                                                RC1PConeTracingDirOcclusionShading,
                                                RC1PExtinctionBasedShading, RenderingParameters,
-                                               build_ext_lut, build_tf_rgbt, make_frame)
+                                               build_ext_lut, build_tf_rgbt, make_frame,
+                                               read_camera_state)
 
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md (spec)
 
@@ -118,6 +119,13 @@ def parse():
     p.add_argument("--postpass", action="store_true",
                    help="also time the multiscaling post-pass filters on this workload's frame")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_rc1pass.json"))
+    p.add_argument("--orbit", action="store_true",
+                   help="move the camera every frame through the reference's camera states "
+                        "(tests/golden/list_camera_states = data/#list_camera_states), so the "
+                        "LPT/band schedule never replays one view")
+    p.add_argument("--settle-ms", type=float, default=150.0,
+                   help="untimed frames before the warmup until this much wall time has passed "
+                        "(GPU clocks ramp over the first ~100 ms of load)")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher rehearsal without a GPU: the ranks join a gloo group and "
                         "rank 0 prints the world size (tests/test_bench_launch.py)")
@@ -339,6 +347,13 @@ def main():
     # GenerateTexture_1D_RGBA of the same TF (alpha = opacity) for the extinction pyramid
     tf_rgba = build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA, extinction_input=True)
     cam = Camera(**D.INITIAL_STATE_CAMERA)
+    cams = [cam]
+    if a.orbit:
+        path = os.path.join(ROOT, "tests", "golden", "list_camera_states")
+        cnt = ctypes.c_int()
+        N.check(N.lib().cvr_read_camera_state(path.encode(), 0, N.Camera(), None, 0, cnt),
+                "camera list")
+        cams = [read_camera_state(path, i) for i in range(cnt.value)]
 
     dm = DataManager()
     dm.SetVolume(vol, scale)
@@ -395,36 +410,57 @@ def main():
         a.transport = "torch"
         split = T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev, transport="torch")
     if world > 1:
-        frame = make_frame(cam, W, H, tile, rank, world)
+        frames = [make_frame(c, W, H, tile, rank, world) for c in cams]
         k = T.tiles_for_rank(W, H, tile, rank, world)
         pixels = k * tile * tile
         out_buf = split.packed[0]
     else:
-        frame = make_frame(cam, W, H)
+        frames = [make_frame(c, W, H) for c in cams]
         pixels = W * H
         out_buf = split.image
     total = torch.zeros((1,), dtype=torch.int64, device=dev)
     L = N.lib()
     out = N.Output(out_buf.data_ptr(), None, total.data_ptr(), 1, fmt)
 
-    def step_once():
-        r.render_to(frame, out)
+    def step_once(i=0):
+        r.render_to(frames[i % len(frames)], out)
 
-    # samples per frame (this rank), counted by the kernel; for the shaded renderer
-    # also the shaded / shadow-lit samples (each traces a fixed number of cone fetches)
+    # samples per frame (this rank) and camera, counted by the kernel; for the shaded
+    # renderers also the shaded / shadow-lit samples and the secondary fetches
     count_shaded = shaded or (a.phong and not iso)
     if count_shaded:
         N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 1), "opt", r.device.handle)
-    step_once()
-    torch.cuda.synchronize(dev)
-    S_rank = int(total.item())
+    S_cam = []
     shade = (ctypes.c_uint64 * 3)()
+    for i in range(len(frames)):
+        total.zero_()
+        step_once(i)
+        torch.cuda.synchronize(dev)
+        S_cam.append(int(total.item()))
+        if count_shaded:
+            sh = (ctypes.c_uint64 * 3)()
+            N.check(L.cvr_read_shade_counters(r.device.handle, sh), "shade", r.device.handle)
+            for q in range(3):
+                shade[q] += sh[q]
     if count_shaded:
-        N.check(L.cvr_read_shade_counters(r.device.handle, shade), "shade", r.device.handle)
         N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 0), "opt", r.device.handle)
+        for q in range(3):     # per frame, averaged over the camera cycle
+            shade[q] = shade[q] // len(frames)
+    # the timed frames cycle through the cameras: samples of frame i = S_cam[i % ncam]
+    S_rank_steps = sum(S_cam[i % len(S_cam)] for i in range(a.steps))
+    S_rank = int(round(S_rank_steps / a.steps))       # mean samples per frame
 
-    for _ in range(a.warmup):
-        split.submit(cam)
+    # clock settle: untimed frames until the GPU has been busy for settle_ms
+    settle = 0
+    t_settle = time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < a.settle_ms:
+        for _ in range(8):
+            split.submit(cams[settle % len(cams)])
+            settle += 1
+        split.flush()
+        torch.cuda.synchronize(dev)
+    for i in range(a.warmup):
+        split.submit(cams[i % len(cams)])
     split.flush()
     torch.cuda.synchronize(dev)
 
@@ -437,7 +473,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
-        split.submit(cam)
+        split.submit(cams[i % len(cams)])
     split.flush()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -450,7 +486,8 @@ def main():
     split_exact = None
     if world > 1 and rank == 0:
         full = torch.zeros_like(split.image)
-        r.render_to(make_frame(cam, W, H), N.Output(full.data_ptr(), None, None, 1, fmt))
+        last_cam = cams[(a.steps - 1) % len(cams)]
+        r.render_to(make_frame(last_cam, W, H), N.Output(full.data_ptr(), None, None, 1, fmt))
         torch.cuda.synchronize(dev)
         split_exact = bool(torch.equal(full.view(torch.int16 if fmt else torch.int32),
                                        split.image.view(torch.int16 if fmt else torch.int32)))
@@ -461,7 +498,7 @@ def main():
             r.device.handle)
     total.zero_()
     for i in range(a.steps):
-        step_once()
+        step_once(i)
     torch.cuda.synchronize(dev)
     kt = (ctypes.c_float * a.steps)()
     nkt = ctypes.c_int()
@@ -469,7 +506,7 @@ def main():
             "cvr_read_kernel_times", r.device.handle)
     assert nkt.value == a.steps
     kern_ms = float(np.mean(kt[:nkt.value]))
-    assert int(total.item()) == S_rank * a.steps, "sample count changed between frames"
+    assert int(total.item()) == S_rank_steps, "sample count changed between frames"
     batch = L.cvr_get_option(r.device.handle, b"batch")
     macro = L.cvr_get_option(r.device.handle, b"macro")
 
@@ -477,14 +514,15 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        s = torch.tensor([S_rank], dtype=torch.int64, device=dev)
+        s = torch.tensor([S_rank_steps], dtype=torch.int64, device=dev)
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        S_all = int(s.item())
+        S_all_steps = int(s.item())
     else:
-        S_all = S_rank
+        S_all_steps = S_rank_steps
+    S_all = int(round(S_all_steps / a.steps))
 
     if rank == 0:
-        msps = S_all * a.steps / elapsed / 1e6
+        msps = S_all_steps / elapsed / 1e6
         ms_per_step = elapsed / a.steps * 1e3
         # algorithmic bytes per launch: 8 trilinear corners x 1 B (u8 input)
         # per sample + the output pixel (RGBA16F 8 B, RGBA32F 16 B) (+ 48 B per shaded
@@ -494,15 +532,20 @@ def main():
         b_alg = 8 * 1 * S_rank + px_bytes * pixels + (48 * int(shade[0]) if count_shaded and a.phong else 0)
         fetches = int(shade[2])
         if dos:
-            # + 8 fp16 corners (16 B) per trilinear extinction fetch of the cones
+            # + 8 fp16 corners (16 B) per trilinear extinction fetch the kernel issues.
+            # The reference evaluates shade[0]*f_occ + shade[1]*f_sdw taps; those whose
+            # CONSIDER_BORDERS factor is exactly 0 are skipped (not fetched), so they
+            # count in the reference-work rate but not in the roofline's bytes.
             f_occ, f_sdw = cone_fetches(r, n, scale)
-            assert fetches == shade[0] * f_occ + shade[1] * f_sdw
+            ref_taps = shade[0] * f_occ + shade[1] * f_sdw
+            assert 0 < fetches <= ref_taps
             b_alg += 16 * fetches
         elif ebs:
             # + 8 float corners (32 B) per trilinear SAT fetch
             b_alg += 32 * fetches
         achieved = b_alg / (kern_ms * 1e-3) / 1e9
-        wkey = f"{a.renderer}_{a.field}{n}_{W}x{H}{'_phong' if a.phong else ''}"
+        wkey = (f"{a.renderer}_{a.field}{n}_{W}x{H}{'_phong' if a.phong else ''}"
+                f"{'_orbit' if a.orbit else ''}")
         kname = ("shaded_march_kernel<DosShader>" if dos else
                  "shaded_march_kernel<EbsShader>" if ebs else
                  f"iso_tile_kernel<{iso_variant}, {str(a.phong).lower()}>" if iso else
@@ -518,7 +561,10 @@ def main():
         if dos:
             roof.update({"shaded_samples": shade[0], "shadow_lit_samples": shade[1],
                          "cone_fetches_per_shaded": [f_occ, f_sdw],
-                         "secondary_fetches": fetches})
+                         "secondary_fetches": fetches,
+                         "reference_taps": ref_taps,
+                         "skipped_zero_border_taps": ref_taps - fetches,
+                         "reference_taps_per_s": round(ref_taps / (kern_ms * 1e-3), 1)})
         elif ebs:
             roof.update({"shaded_samples": shade[0], "shadow_chains": shade[1],
                          "sat_fetches": fetches,
@@ -553,10 +599,14 @@ def main():
                                     if iso else
                                     f"rc1pass emission-absorption, ")
                                    + f"Marschner-Lobb {n}^3 u8 "
-                                   f"({a.field}), {W}x{H}, bonsai_01.tf1d, camera "
-                                   f"'Initial State'" + ("" if iso else ", step 0.5, ERT 0.99")
+                                   f"({a.field}), {W}x{H}, bonsai_01.tf1d, "
+                                   + (f"camera orbit: the {len(cams)} states of "
+                                      f"data/#list_camera_states, one per frame" if a.orbit
+                                      else "camera 'Initial State'")
+                                   + ("" if iso else ", step 0.5, ERT 0.99")
                                    + (", Blinn-Phong FD gradient" if a.phong else ""),
                        "volume": n, "viewport": [W, H], "samples_per_frame": S_all,
+                       "settle_frames": settle,
                        "parallelism": f"screen tiles {tile}x{tile} over {world} GPU(s)"
                                       if world > 1 else "1 GPU",
                        "storage": "cell8 fp16 (16 B/cell, x-fastest)",

@@ -1257,6 +1257,7 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   // SpotLightMaxAngle: glm::cos(glm::pi<float>() * angle / 180.f) (dosrcrenderer.cpp:158)
   Q.spot_cos = std::cos(3.14159265358979323846f * p->light.spot_angle_deg / 180.0f);
   Q.zero_skip = c->ext_finite;
+  Q.count_taps = c->shade_counters ? 1 : 0;
   for (int k = 0; k < 2; k++) {
     cvr::DosCone& C = k ? Q.sdw : Q.occ;
     const cvr_cone_tables& T = c->cone_tab[k];

@@ -87,6 +87,7 @@ struct DosArgs {
   float lfwd[3], lup[3], lright[3];  // light camera vectors (RenderingParameters)
   float spot_cos;                    // SpotLightMaxAngle uniform
   int zero_skip;                     // every pyramid value finite: taps with a 0 border factor are 0
+  int count_taps;                    // shade_counters: count the taps fetched (measurement)
   DosCone occ, sdw;
 };
 

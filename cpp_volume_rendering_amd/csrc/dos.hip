@@ -293,7 +293,7 @@ template <int J, int U, int J0 = 0, int JN = J>
 __device__ __forceinline__ void cone_sections(const DosArgs& Q, const DosCone& C,
                                               const uint4* __restrict__ ext, const float4 (&e)[U],
                                               const float (&tr)[U], const f3 (&vk)[J], f3 pos,
-                                              float (&rays)[7], float (&last)[7]) {
+                                              float (&rays)[7], float (&last)[7], uint32_t& nf) {
   ExtTap tap[U][JN];
   uint4 raw[U][JN];
   float xb[U][JN];
@@ -317,6 +317,12 @@ __device__ __forceinline__ void cone_sections(const DosArgs& Q, const DosCone& C
 #endif
     }
   }
+  if (Q.count_taps) {   // measurement only: the taps actually fetched (uniform branch)
+#pragma unroll
+    for (int q = 0; q < U; q++)
+#pragma unroll
+      for (int j = 0; j < JN; j++) nf += zero[q][j] ? 0u : 1u;
+  }
 #pragma unroll
   for (int q = 0; q < U; q++)
 #pragma unroll
@@ -334,7 +340,7 @@ template <int J, int U>
 __device__ __forceinline__ void cone_step(const DosArgs& Q, const DosCone& C,
                                           const uint4* __restrict__ ext, ConstSections sec, int s,
                                           float& track, const f3 (&vk)[J], f3 pos,
-                                          float (&rays)[7], float (&last)[7]) {
+                                          float (&rays)[7], float (&last)[7], uint32_t& nf) {
   float4 e[U];
   float tr[U];
 #pragma unroll
@@ -344,10 +350,10 @@ __device__ __forceinline__ void cone_step(const DosArgs& Q, const DosCone& C,
     track += e[q].x;
   }
   if (J == 7) {
-    cone_sections<J, U, 0, 4>(Q, C, ext, e, tr, vk, pos, rays, last);
-    cone_sections<J, U, 4, 3>(Q, C, ext, e, tr, vk, pos, rays, last);
+    cone_sections<J, U, 0, 4>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+    cone_sections<J, U, 4, 3>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
   } else {
-    cone_sections<J, U>(Q, C, ext, e, tr, vk, pos, rays, last);
+    cone_sections<J, U>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
   }
 }
 
@@ -355,19 +361,21 @@ template <int J, int U>
 __device__ __forceinline__ void cone_stage(const DosArgs& Q, const DosCone& C,
                                            const uint4* __restrict__ ext, ConstSections sec, int& s,
                                            int n, float& track, const f3 (&vk)[J], f3 pos,
-                                           float (&rays)[7], float (&last)[7]) {
+                                           float (&rays)[7], float (&last)[7], uint32_t& nf) {
   int i = 0;
   for (; i + U <= n; i += U, s += U)
-    cone_step<J, U>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last);
+    cone_step<J, U>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last,
+                    nf);
   for (; i < n; i++, s++)
-    cone_step<J, 1>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last);
+    cone_step<J, 1>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last,
+                    nf);
 }
 
 // Cone1/3/7 RayOcclusion and Cone1/3/7 RayShadow (the same accumulation): the
 // visibility exp(-sum) of a cone from `pos` along k, split 1 -> 3 -> 7 rays.
 // Every lane walks the same section table (wave-uniform loads and levels).
 __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __restrict__ ext,
-                            f3 pos, f3 k, f3 u, f3 v) {
+                            f3 pos, f3 k, f3 u, f3 v, uint32_t& nf) {
   float rays[7], last[7];
   float track = C.initial_step;
   rays[0] = 0.0f;
@@ -376,7 +384,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
   int s = 0;
   {
     const f3 vk[1] = {k};
-    cone_stage<1, 4>(Q, C, ext, sec, s, C.counts[0], track, vk, pos, rays, last);
+    cone_stage<1, 4>(Q, C, ext, sec, s, C.counts[0], track, vk, pos, rays, last, nf);
   }
   if (C.counts[1] + C.counts[2] == 0) return cvr_expf(-rays[0]);
   rays[2] = rays[0]; rays[1] = rays[0];
@@ -385,7 +393,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
     f3 vk[3];
 #pragma unroll
     for (int j = 0; j < 3; j++) vk[j] = cone_axis(C.axes + 3 * j, k, u, v);
-    cone_stage<3, 2>(Q, C, ext, sec, s, C.counts[1], track, vk, pos, rays, last);
+    cone_stage<3, 2>(Q, C, ext, sec, s, C.counts[1], track, vk, pos, rays, last, nf);
   }
   if (C.counts[2] == 0)
     return ((cvr_expf(-rays[0]) + cvr_expf(-rays[1])) + cvr_expf(-rays[2])) / 3.0f;
@@ -404,7 +412,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
     f3 vk[7];
 #pragma unroll
     for (int j = 0; j < 7; j++) vk[j] = cone_axis(C.axes + 3 * (3 + j), k, u, v);
-    cone_stage<7, 1>(Q, C, ext, sec, s, C.counts[2], track, vk, pos, rays, last);
+    cone_stage<7, 1>(Q, C, ext, sec, s, C.counts[2], track, vk, pos, rays, last, nf);
   }
   float side = cvr_expf(-rays[1]);
 #pragma unroll
@@ -420,7 +428,9 @@ struct DosShader {
   using Args = DosArgs;
   using Data = const uint4*;   // the cell8 extinction pyramid
 
-  // Shaded colour of one job; `lit` counts the shadow cones traced.
+  // Shaded colour of one job; `lit` counts the shadow cones traced, `fetches`
+  // the extinction taps actually fetched (Q.count_taps; taps whose border factor
+  // is exactly 0 are skipped and not counted).
   __device__ static f3 shade(const DosArgs& Q, const uint4* __restrict__ ext, f3 tx, f3 wp,
                              f3 cam, f3 rgb, const f3* g, uint32_t& lit, uint32_t& fetches) {
     const Rc1passArgs& A = Q.a;
@@ -432,8 +442,7 @@ struct DosShader {
       const f3 v_right = normalize3(cross3(cam, f3{0.0f, 1.0f, 0.0f}));
       const f3 v_up = normalize3(cross3(f3{-cam.x, -cam.y, -cam.z}, v_right));
       const f3 k = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
-      iocc = cone_trace(Q, Q.occ, ext, tx, k, v_up, v_right);
-      fetches += Q.occ.counts[0] + 3 * Q.occ.counts[1] + 7 * Q.occ.counts[2];
+      iocc = cone_trace(Q, Q.occ, ext, tx, k, v_up, v_right, fetches);
     }
     if (Q.apply_shadow) {
       f3 k, u, v;
@@ -451,9 +460,8 @@ struct DosShader {
       }
       // Cone1RayShadow(pos, k, v, u) is called as (pos, k, u, v): swapped (:559-561)
       if (on) {
-        isdw = cone_trace(Q, Q.sdw, ext, tx, k, v, u);
+        isdw = cone_trace(Q, Q.sdw, ext, tx, k, v, u, fetches);
         lit++;
-        fetches += Q.sdw.counts[0] + 3 * Q.sdw.counts[1] + 7 * Q.sdw.counts[2];
       }
     }
     const float inv_k = 1.0f / (Q.ka + Q.kd);

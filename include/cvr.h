@@ -480,8 +480,10 @@ cvr_status  cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* 
  * (cvr_render_dosct / cvr_render_extbsd; cvr_render_rc1pass with Blinn-Phong
  * fills out[0] only): out[0] samples that ran the shading
  * (alpha > 0), out[1] those whose shadow was traced (spot cut-off excluded),
- * out[2] the secondary trilinear fetches (extinction pyramid / SAT): the
- * secondary traffic of the roofline. */
+ * out[2] the secondary trilinear fetches actually issued (extinction pyramid /
+ * SAT): the secondary traffic of the roofline.  For DOS the reference's own tap
+ * count is out[0] * (n1 + 3 n3 + 7 n7)_occlusion + out[1] * (...)_shadow; out[2]
+ * leaves out the taps whose CONSIDER_BORDERS factor is exactly 0 (not fetched). */
 cvr_status  cvr_read_shade_counters(cvr_ctx* ctx, uint64_t out[3]);
 
 /* ----------------------------------------------------------------------------
