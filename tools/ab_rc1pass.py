@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--variants", default="b4o1p5q0,b2o1p5q0,b4o1p0q0,b4o0p0q0,b4o1p5q10")
     ap.add_argument("--phong", action="store_true")
+    ap.add_argument("--tf-alpha", type=float, default=1.0, help="scale of the TF alpha points")
     ap.add_argument("--no-total", action="store_true", help="time frames without the sample counter")
     a = ap.parse_args()
     n, W = a.size, a.res
@@ -49,7 +50,8 @@ def main():
     L0 = N.lib()
     dev = Device(0)
     dev.set_volume(vol, D.voxel_scale(n))
-    dev.set_transfer_function(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
+    dev.set_transfer_function(build_tf_rgbt(D.BONSAI_TF_RGB, tuple(
+        (al * a.tf_alpha, iso) for al, iso in D.BONSAI_TF_ALPHA)))
     if a.phong:
         dev.set_gradient(1)
     dev.set_stream(s.cuda_stream)
