@@ -123,6 +123,8 @@ def parse():
                    help="move the camera every frame through the reference's camera states "
                         "(tests/golden/list_camera_states = data/#list_camera_states), so the "
                         "LPT/band schedule never replays one view")
+    p.add_argument("--tf-alpha", type=float, default=1.0,
+                   help="scale of bonsai_01.tf1d's alpha control points (0.02: long rays)")
     p.add_argument("--settle-ms", type=float, default=150.0,
                    help="untimed frames before the warmup until this much wall time has passed "
                         "(GPU clocks ramp over the first ~100 ms of load)")
@@ -267,14 +269,19 @@ def cone_fetches(r, n, scale):
 
 
 def load_traffic(path, workload_key):
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        if d.get("workload_key") != workload_key:
-            return None
-        return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
+    """HBM bytes per launch measured by PMC (tools/pmc_traffic.py) for this exact
+    workload: `path` or any profiles/pmc_<renderer>*.json beside it."""
+    import glob
+    stem = os.path.splitext(path)[0]
+    for f in [path] + sorted(glob.glob(stem + "_*.json")):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload_key") == workload_key:
+            return d.get("hbm_bytes_per_launch")
+    return None
 
 
 def postpass_bench(r, dev, W, H, reps):
@@ -343,9 +350,12 @@ def main():
     H = W
     vol = D.marschner_lobb_u8(n) if a.field == "ml" else D.blobs_u8(n)
     scale = D.voxel_scale(n)
-    tf = build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA)
+    # --tf-alpha scales the TF's alpha control points (0.02: rays rarely reach the ERT
+    # threshold and stream the whole volume -- the long-ray, HBM-bound line)
+    alpha_cp = tuple((a_ * a.tf_alpha, iso_) for a_, iso_ in D.BONSAI_TF_ALPHA)
+    tf = build_tf_rgbt(D.BONSAI_TF_RGB, alpha_cp)
     # GenerateTexture_1D_RGBA of the same TF (alpha = opacity) for the extinction pyramid
-    tf_rgba = build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA, extinction_input=True)
+    tf_rgba = build_tf_rgbt(D.BONSAI_TF_RGB, alpha_cp, extinction_input=True)
     cam = Camera(**D.INITIAL_STATE_CAMERA)
     cams = [cam]
     if a.orbit:
@@ -366,7 +376,7 @@ def main():
         r = RC1PConeTracingDirOcclusionShading(local if world > 1 else 0)
         r.glsl_apply_shadow = True        # config 4: cone AO + cone shadows (point light)
     elif ebs:
-        dm.SetExtinctionTable(build_ext_lut(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
+        dm.SetExtinctionTable(build_ext_lut(D.BONSAI_TF_RGB, alpha_cp))
         r = RC1PExtinctionBasedShading(local if world > 1 else 0)
     elif iso:
         r = (CustomRayCasting1PassIsoAdapt, CustomRayCasting1PassIsodfsAdapt,
@@ -545,7 +555,8 @@ def main():
             b_alg += 32 * fetches
         achieved = b_alg / (kern_ms * 1e-3) / 1e9
         wkey = (f"{a.renderer}_{a.field}{n}_{W}x{H}{'_phong' if a.phong else ''}"
-                f"{'_orbit' if a.orbit else ''}")
+                f"{'_orbit' if a.orbit else ''}"
+                f"{f'_alpha{a.tf_alpha:g}' if a.tf_alpha != 1.0 else ''}")
         kname = ("shaded_march_kernel<DosShader>" if dos else
                  "shaded_march_kernel<EbsShader>" if ebs else
                  f"iso_tile_kernel<{iso_variant}, {str(a.phong).lower()}>" if iso else
@@ -599,7 +610,9 @@ def main():
                                     if iso else
                                     f"rc1pass emission-absorption, ")
                                    + f"Marschner-Lobb {n}^3 u8 "
-                                   f"({a.field}), {W}x{H}, bonsai_01.tf1d, "
+                                   f"({a.field}), {W}x{H}, bonsai_01.tf1d"
+                                   + (f" (alpha x{a.tf_alpha:g})" if a.tf_alpha != 1.0 else "")
+                                   + ", "
                                    + (f"camera orbit: the {len(cams)} states of "
                                       f"data/#list_camera_states, one per frame" if a.orbit
                                       else "camera 'Initial State'")
