@@ -208,6 +208,37 @@ constexpr int kDigitalBatch = 32;
 
 __device__ __forceinline__ float h16(float f) { return h2f(f2h(f)); }
 
+// l * h and c - h for h the binary16 in the low half of `hb`, each one IEEE f32
+// operation on the exactly converted half (v_fma_mix: the product or sum is
+// exact before its single rounding; the -0 addend keeps the sign of a zero
+// product, as a plain multiply does).
+__device__ __forceinline__ float mul_h16(float l, uint32_t hb) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel_hi:[0,1,0]" : "=v"(d) : "v"(l), "v"(hb));
+  return d;
+}
+__device__ __forceinline__ float sub_h16(float c, uint32_t hb) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(hb), "v"(c));
+  return d;
+}
+// (half HI ? x.hi : x.lo) - p, one rounding
+template <bool HI>
+__device__ __forceinline__ float half_minus(uint32_t x, float p) {
+  float d;
+  if (HI) asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(x), "v"(p));
+  else asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(x), "v"(p));
+  return d;
+}
+// (half HI ? x.hi : x.lo) - h for h the binary16 in the low half of hb, one rounding
+template <bool HI>
+__device__ __forceinline__ float half_minus_h16(uint32_t x, uint32_t hb) {
+  float d;
+  if (HI) asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(hb), "v"(x));
+  else asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,1]" : "=v"(d) : "v"(hb), "v"(x));
+  return d;
+}
+
 template <class LU>
 __global__ void digital_filter_kernel(uint16_t* __restrict__ img, int w, int h, int dir) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -281,6 +312,201 @@ __global__ void digital_filter_kernel(uint16_t* __restrict__ img, int w, int h, 
   }
 }
 
+// The same recursion with the lines staged in LDS.  One wave takes `lpw` lines
+// (lpw * 4 chains, one lane per (line, channel)): the lines are read into LDS
+// with coalesced 8-B pixel loads, de-interleaved into one plane of binary16 per
+// chain (chain stride S halves: a multiple of 8, padded so that the 16 lanes of a
+// ds_read_b128 group fall on distinct banks), both passes run on the planes 8
+// elements per LDS access, and the lines are written back once.  Every step
+// still rounds to binary16 and the next step reads the rounded value, as the
+// global-memory kernel above and the reference's imageLoad/imageStore do.
+template <int C> struct Head { static constexpr bool value = true; static constexpr int chunk = C; };
+struct NoHead { static constexpr bool value = false; static constexpr int chunk = 0; };
+
+// Staging: a workgroup of kDigitalThreads moves the lines in and out (memory-level
+// parallelism for the one wave that then runs the sequential recursions).
+constexpr int kDigitalThreads = 256;
+constexpr int kDigitalUnroll = 8;
+
+template <class LU>
+__global__ void __launch_bounds__(kDigitalThreads)
+digital_filter_lds_kernel(uint16_t* __restrict__ img, int w, int h, int dir, int lpw_shift, int S) {
+  extern __shared__ uint4 lds_raw[];
+  uint16_t* plane = reinterpret_cast<uint16_t*>(lds_raw);
+  const int lpw = 1 << lpw_shift;
+  const int lines = dir == 0 ? h : w, nn = dir == 0 ? w : h;
+  const int l0 = blockIdx.x * lpw;
+  const int nl = min(lpw, lines - l0);
+  uint2* px = reinterpret_cast<uint2*>(img);
+  auto put = [&](int l, int i, uint2 v) {
+    uint16_t* q = plane + (size_t)(l * 4) * S + i;
+    q[0] = (uint16_t)(v.x & 0xffffu);
+    q[S] = (uint16_t)(v.x >> 16);
+    q[2 * S] = (uint16_t)(v.y & 0xffffu);
+    q[3 * S] = (uint16_t)(v.y >> 16);
+  };
+  auto get = [&](int l, int i) {
+    const uint16_t* q = plane + (size_t)(l * 4) * S + i;
+    return make_uint2((uint32_t)q[0] | ((uint32_t)q[S] << 16),
+                      (uint32_t)q[2 * S] | ((uint32_t)q[3 * S] << 16));
+  };
+  // ---- stage in: all kDigitalThreads lanes, kDigitalUnroll loads in flight each ----
+  // element e of the wave's nl lines: dir 0 -> (line e / nn, i = e % nn), rows are
+  // contiguous in memory; dir 1 -> (line e % lpw, i = e >> lpw_shift), one image
+  // row of lpw adjacent pixels per lpw elements
+  const int tid = threadIdx.x;
+  const int total = dir == 0 ? nl * nn : (nn << lpw_shift);
+  auto src_of = [&](int e, int& l, int& i) -> size_t {
+    if (dir == 0) {
+      l = e / nn;
+      i = e - l * nn;
+      return (size_t)(l0 + l) * w + i;
+    }
+    i = e >> lpw_shift;
+    l = e & (lpw - 1);
+    return (size_t)i * w + l0 + l;
+  };
+  for (int e0 = 0; e0 < total; e0 += kDigitalThreads * kDigitalUnroll) {
+    uint2 v[kDigitalUnroll];
+#pragma unroll
+    for (int u = 0; u < kDigitalUnroll; u++) {
+      const int e = e0 + u * kDigitalThreads + tid;
+      int l, i;
+      const size_t a = src_of(e, l, i);
+      if (e < total && l < nl) v[u] = px[a];
+    }
+#pragma unroll
+    for (int u = 0; u < kDigitalUnroll; u++) {
+      const int e = e0 + u * kDigitalThreads + tid;
+      int l, i;
+      src_of(e, l, i);
+      if (e < total && l < nl) put(l, i, v[u]);
+    }
+  }
+  __syncthreads();
+  // ---- both passes on this lane's chain ----
+  const int q = tid;   // the first wave runs the recursions (one lane per chain)
+#ifdef CVR_DIGITAL_NO_COMPUTE   // cost probe only (tools/build_variant.sh): wrong images
+  if (false) {
+#else
+  if (q < 64 && (q >> 2) < nl) {
+#endif
+    uint16_t* c = plane + (size_t)q * S;
+    uint4* c4 = reinterpret_cast<uint4*>(c);
+    const int m = LU::m;
+    const float p_inv = 1.0f;
+    const float L_inf = LU::L(m - 1), v_inv = L_inf / (1.f + L_inf);
+    // forward pass: f[i] -= L * f[i-1], i = 1 .. nn-1; reverse pass: f[i] = L * (p_inv
+    // * f[i] - f[i+1]), i = nn-2 .. 0.  8 elements per LDS access.  The first two
+    // chunks (the steps whose coefficient comes from the table: i < m) are peeled
+    // with compile-time coefficients, whole chunks run without bounds checks, and
+    // the chunk holding element nn-1 checks bounds per element.
+    // prev is kept as the stored binary16 bits: the next step reads it straight
+    // from the half (v_fma_mix), one dependent conversion less per step
+    uint32_t prev = 0u;
+    const int nfull = nn >> 3;          // chunks entirely inside [0, nn)
+    auto fwd = [&](uint4 v, int ch, auto head, bool check) {
+      uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = (ch << 3) + k;
+        float l = L_inf;
+        if (decltype(head)::value) {
+          const int ic = (decltype(head)::chunk << 3) + k;   // == i at compile time
+          if (ic == 0) { prev = wd[0] & 0xffffu; continue; }
+          l = ic < m ? LU::L(ic - 1) : L_inf;
+        }
+        if (check && i >= nn) break;
+        const uint32_t x = wd[k >> 1];
+        const float p = mul_h16(l, prev);
+        const uint32_t o = f2h((k & 1) ? half_minus<true>(x, p) : half_minus<false>(x, p));
+        wd[k >> 1] = (k & 1) ? ((x & 0xffffu) | (o << 16)) : ((x & 0xffff0000u) | o);
+        prev = o;
+      }
+      c4[ch] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    };
+    auto rev = [&](uint4 v, int ch, auto head, bool check) {
+      uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 7; k >= 0; k--) {
+        const int i = (ch << 3) + k;
+        float l = L_inf;
+        if (decltype(head)::value) {
+          const int ic = (decltype(head)::chunk << 3) + k;
+          l = ic >= m - 1 ? L_inf : LU::L(ic);
+        }
+        if (check && i > nn - 2) continue;
+        const uint32_t x = wd[k >> 1];
+        // p_inv * f[i] = f[i] exactly (p_inv = 1)
+        const uint32_t o = f2h(l * ((k & 1) ? half_minus_h16<true>(x, prev)
+                                            : half_minus_h16<false>(x, prev)));
+        wd[k >> 1] = (k & 1) ? ((x & 0xffffu) | (o << 16)) : ((x & 0xffff0000u) | o);
+        prev = o;
+      }
+      c4[ch] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    };
+    const int nch = (nn + 7) >> 3;
+    uint4 nxt = c4[0];
+    {
+      const uint4 v = nxt;
+      if (nch > 1) nxt = c4[1];
+      fwd(v, 0, Head<0>{}, nfull < 1);
+    }
+    if (nch > 1) {
+      const uint4 v = nxt;
+      if (nch > 2) nxt = c4[2];
+      fwd(v, 1, Head<1>{}, nfull < 2);
+    }
+    for (int ch = 2; ch < nfull; ch++) {   // the next chunk's read goes out first
+      const uint4 v = nxt;
+      if (ch + 1 < nch) nxt = c4[ch + 1];
+      fwd(v, ch, NoHead{}, false);
+    }
+    if (nch > 2 && nfull < nch) fwd(nxt, nch - 1, NoHead{}, true);
+    // f[nn-1] *= p_inv * v_inv  (prev holds the stored f[nn-1])
+    {
+      const uint32_t o = f2h(h2f((uint16_t)prev) * (p_inv * v_inv));
+      c[nn - 1] = (uint16_t)o;
+      prev = o;
+    }
+    if (nn >= 2) {
+      const int top = (nn - 2) >> 3;            // chunk of element nn-2
+      const bool top_partial = ((top << 3) + 7) > nn - 2;
+      int ch = top;
+      nxt = c4[ch];
+      if (ch >= 2 && top_partial) {
+        const uint4 v = nxt;
+        nxt = c4[ch - 1];
+        rev(v, ch, NoHead{}, true);
+        ch--;
+      }
+      for (; ch >= 2; ch--) {
+        const uint4 v = nxt;
+        nxt = c4[ch - 1];
+        rev(v, ch, NoHead{}, false);
+      }
+      if (ch == 1) {
+        const uint4 v = nxt;
+        nxt = c4[0];
+        rev(v, 1, Head<1>{}, top == 1 && top_partial);
+        ch--;
+      }
+      if (ch == 0) rev(nxt, 0, Head<0>{}, top == 0 && top_partial);
+    }
+  }
+  __syncthreads();
+  // ---- stage out ----
+  for (int e0 = 0; e0 < total; e0 += kDigitalThreads * kDigitalUnroll) {
+#pragma unroll
+    for (int u = 0; u < kDigitalUnroll; u++) {
+      const int e = e0 + u * kDigitalThreads + tid;
+      int l, i;
+      const size_t a = src_of(e, l, i);
+      if (e < total && l < nl) px[a] = get(l, i);
+    }
+  }
+}
+
 // Screenshot: FragColor = texture(frame) blended SRC_ALPHA / ONE_MINUS_SRC_ALPHA over
 // white, stored to an 8-bit unorm back buffer, read as RGB (row 0 = bottom).
 template <bool HALF>
@@ -310,8 +536,38 @@ __global__ void screenshot_kernel(const void* __restrict__ src, int w, int h,
     default: return hipErrorInvalidValue;                                           \
   }
 
+// LDS bytes of one wave of digital_filter_lds_kernel: lpw * 4 chains of S halves.
+constexpr size_t kDigitalLdsMax = 160 * 1024;
+
 hipError_t launch_digital(int kernel, uint2* img, int w, int h, hipStream_t s) {
   for (int dir = 0; dir < 2; dir++) {
+    const int lines = dir == 0 ? h : w, nn = dir == 0 ? w : h;
+    const int S = ((nn + 7) / 8) * 8 + 8;   // chain stride (halves): 16-B chunks + 4-bank pad
+    int shift = 4;                          // 16 lines (64 chains) per wave, fewer for long lines
+    while (shift > 0 && ((size_t)4 << shift) * S * 2 > kDigitalLdsMax) shift--;
+    const size_t lds = ((size_t)4 << shift) * S * 2;
+    if (lds <= kDigitalLdsMax && lines > 0 && nn > 0) {
+      static bool attr = false;   // dynamic LDS beyond 64 KiB must be allowed per kernel
+      if (!attr) {
+        hipError_t e = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&digital_filter_lds_kernel<LCbs>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDigitalLdsMax);
+        if (e == hipSuccess)
+          e = hipFuncSetAttribute(reinterpret_cast<const void*>(&digital_filter_lds_kernel<LOmoms>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDigitalLdsMax);
+        if (e != hipSuccess) return e;
+        attr = true;
+      }
+      const dim3 g((lines + (1 << shift) - 1) >> shift), b(kDigitalThreads);
+      uint16_t* p = (uint16_t*)img;
+      if (kernel == 4)
+        hipLaunchKernelGGL(digital_filter_lds_kernel<LCbs>, g, b, lds, s, p, w, h, dir, shift, S);
+      else
+        hipLaunchKernelGGL(digital_filter_lds_kernel<LOmoms>, g, b, lds, s, p, w, h, dir, shift, S);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      continue;
+    }
     const int lanes = 4 * (dir == 0 ? h : w);
     const dim3 g((lanes + 63) / 64), b(64);
     uint16_t* p = (uint16_t*)img;

@@ -117,3 +117,20 @@ def test_screenshot_rgba32f(dev, oracle):
     torch.cuda.synchronize()
     dev.set_stream(None)
     assert np.array_equal(rgb.cpu().numpy(), oracle.screenshot_rgb8(f))
+
+
+@pytest.mark.parametrize("mode,sw,sh", [(2, 16, 16), (2, 17, 19), (2, 1500, 16), (2, 16, 2700),
+                                        (2, 21000, 16), (3, 1024, 1024), (3, 34, 38)])
+@pytest.mark.parametrize("k", [N.FILTER_CARDINAL_BSPLINE_3, N.FILTER_CARDINAL_OMOMS3])
+def test_digital_filter_shapes(dev, oracle, mode, sw, sh, k):
+    """The cardinal kernels' recursive digital filter (LDS-staged lines, 16/8/4/1 lines per
+    wave by line length, the global-memory kernel past 20472 elements) on ragged, tiny and
+    long lines: bit for bit with the oracle, including the in-place prefilter of mode 3."""
+    rng = np.random.default_rng(sw * 7 + sh + k)
+    fw, fh = (sw * 2, sh * 2) if mode < 3 else (max(1, sw // 2), max(1, sh // 2))
+    frame = (rng.random((fh, fw, 4)) * 1.5 - 0.25).astype(np.float16)
+    got, gframe = gpu_filter(dev, mode, k, frame, sw, sh)
+    oframe = frame.copy()
+    want = oracle.multiscale_filter(mode, k, oframe, sw, sh)
+    assert _eq16(got, want)
+    assert _eq16(gframe, oframe)
