@@ -1405,6 +1405,15 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
   Q.apply_occlusion = p->apply_occlusion != 0;
   Q.occ_shells = p->occlusion_shells;
   Q.occ_radius = p->occlusion_radius;
+  {   // ExtinctionAmbientOcclusion's per-shell weights (:117-144), float as the shader
+    const float R = Q.occ_radius;
+    for (int i = 0; i < cvr::EbsArgs::kMaxAoShells; i++) {
+      const float r1 = i == 0 ? R : R * (float)(i + 1);
+      Q.ao_w[i] = 1.0f / (r1 * r1);
+    }
+    const float rshi = R * (float)Q.occ_shells;
+    Q.ao_wa = 1.0f / (rshi * rshi);
+  }
   Q.apply_shadow = p->apply_shadow != 0;
   Q.shadow_type = p->shadow_type;
   Q.phong = phong;

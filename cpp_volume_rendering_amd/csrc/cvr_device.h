@@ -109,6 +109,18 @@ __device__ __forceinline__ float cvr_powf(float x, float y) {
 }
 
 struct f3 { float x, y, z; };
+// a / b correctly rounded from y = 1.0f / b (itself correctly rounded), for a
+// divisor reused many times: q = RN(a*y), the remainder a - b*q is exact by fma,
+// and RN(q + r*y) = RN(a/b) (Markstein's correction; valid while a/b, a*y and the
+// remainder stay in the normal range -- callers pass finite a >= 0 of moderate
+// size and b in the normal range).  Checked against IEEE division in
+// tests/test_exact_div.py.
+__device__ __forceinline__ float div_by_recip(float a, float b, float y) {
+  const float q = a * y;
+  const float r = fmaf(-b, q, a);
+  return fmaf(r, y, q);
+}
+
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 __device__ __forceinline__ f3 normalize3(f3 v) {
   float inv = 1.0f / sqrtf(dot3(v, v));

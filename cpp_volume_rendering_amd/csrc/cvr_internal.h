@@ -101,6 +101,11 @@ struct EbsArgs {
   float min_sat[3], max_sat[3];      // S / 2, G + 1.5 S
   int apply_occlusion, occ_shells;
   float occ_radius;
+  // 1 / r^2 of shell i (r = R*(i+1)) and W_A = 1 / (R*shells)^2, computed on the host
+  // with the shader's float expressions (the divisions are the same for every sample)
+  static constexpr int kMaxAoShells = 64;
+  float ao_w[kMaxAoShells];
+  float ao_wa;
   int apply_shadow, shadow_type, phong;
   float p_cs, p_sn, n_cs, n_sn;      // cos / sin of +-DirSdwConeAngle
   float interval, initial_step, ui_weight, max_distance;

@@ -56,9 +56,11 @@ __device__ __forceinline__ f3 sat_offset(const EbsArgs& Q, f3 p) {
 }
 
 // EvaluateShadowSAT3D (:148-185, the texture path)
-__device__ __forceinline__ float shadow_box(const EbsArgs& Q, const float4* __restrict__ sat, f3 p1, f3 p2) {
-  const float volquery = ((fabsf(p1.x - p2.x) / Q.S[0])) * ((fabsf(p1.y - p2.y) / Q.S[1])) *
-                         ((fabsf(p1.z - p2.z) / Q.S[2]));
+__device__ __forceinline__ float shadow_box(const EbsArgs& Q, const float4* __restrict__ sat, f3 p1, f3 p2,
+                                           f3 rS) {
+  const float volquery = (div_by_recip(fabsf(p1.x - p2.x), Q.S[0], rS.x)) *
+                         (div_by_recip(fabsf(p1.y - p2.y), Q.S[1], rS.y)) *
+                         (div_by_recip(fabsf(p1.z - p2.z), Q.S[2], rS.z));
   return ((sat_box(Q, sat, sat_offset(Q, p1), sat_offset(Q, p2)) / volquery)) * Q.ui_weight;
 }
 
@@ -68,20 +70,22 @@ __device__ float ebs_occlusion(const EbsArgs& Q, const float4* __restrict__ sat,
   const f3 r0{R * Q.S[0], R * Q.S[1], R * Q.S[2]};
   const float SAT_Sh0 = sat_box(Q, sat, sat_offset(Q, f3{tx.x - r0.x, tx.y - r0.y, tx.z - r0.z}),
                                 sat_offset(Q, f3{tx.x + r0.x, tx.y + r0.y, tx.z + r0.z}));
-  const float rsh0 = R;
-  const float tSh0 = SAT_Sh0 * (1.0f / (rsh0 * rsh0));
+  // the weights 1 / r^2 and W_A are the same for every sample: Q.ao_w / Q.ao_wa,
+  // computed on the host by the same float expressions
+  const bool tab = Q.occ_shells <= EbsArgs::kMaxAoShells;
+  const float tSh0 = SAT_Sh0 * (tab ? Q.ao_w[0] : 1.0f / (R * R));
   float SAT_Shi = SAT_Sh0, tshi = tSh0;
   for (int i = 1; i < Q.occ_shells; i++) {
     const float r1 = R * (float)(i + 1);
     const f3 ri{r1 * Q.S[0], r1 * Q.S[1], r1 * Q.S[2]};
     const float SAT_Shi_1 = sat_box(Q, sat, sat_offset(Q, f3{tx.x - ri.x, tx.y - ri.y, tx.z - ri.z}),
                                     sat_offset(Q, f3{tx.x + ri.x, tx.y + ri.y, tx.z + ri.z}));
-    const float tshi_1 = tshi + (SAT_Shi_1 - SAT_Shi) * (1.0f / (r1 * r1));
+    const float tshi_1 = tshi + (SAT_Shi_1 - SAT_Shi) * (tab ? Q.ao_w[i] : 1.0f / (r1 * r1));
     SAT_Shi = SAT_Shi_1;
     tshi = tshi_1;
   }
   const float rshi = R * (float)Q.occ_shells;
-  const float W_A = 1.0f / (rshi * rshi);
+  const float W_A = tab ? Q.ao_wa : 1.0f / (rshi * rshi);
   const float Stau = W_A * tshi;
   return cvr_expf(-(Stau));
 }
@@ -93,6 +97,7 @@ __device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   float signal = 1.0f;
   if (cv.z < 0) signal = -1.0f;
   const float p_cs = Q.p_cs, p_sn = Q.p_sn, n_cs = Q.n_cs, n_sn = Q.n_sn;
+  const f3 rS{1.0f / Q.S[0], 1.0f / Q.S[1], 1.0f / Q.S[2]};   // loop-invariant divisors
   const f3 proj_y = normalize3(f3{0.0f, cv.y, cv.z});
   const f3 proj_x = normalize3(f3{cv.x, 0.0f, cv.z});
   const f3 pj_x1 = normalize3(f3{proj_x.x * n_cs - proj_x.z * n_sn, 0.0f, proj_x.x * n_sn + proj_x.z * n_cs});
@@ -102,22 +107,26 @@ __device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   const float si = Q.interval * signal * Q.S[2];
   float z_pos = Q.initial_step * signal * Q.S[2];
   const float vmin = Q.S[2] * 0.5f, vmax = Q.G[2] - Q.S[2] * 0.5f;
-  while ((z_pos / cv.z) < Q.max_distance &&
+  const float d_x1 = fabsf(pj_x1.z), d_x2 = fabsf(pj_x2.z), d_y1 = fabsf(pj_y1.z), d_y2 = fabsf(pj_y2.z);
+  const float r_x1 = 1.0f / d_x1, r_x2 = 1.0f / d_x2, r_y1 = 1.0f / d_y1, r_y2 = 1.0f / d_y2;
+  const float rc = 1.0f / cv.z;
+  while (div_by_recip(z_pos, cv.z, rc) < Q.max_distance &&
          (pos.z + (z_pos + si) > vmin && pos.z + (z_pos + si) < vmax)) {
     const float z_mean = fabsf(z_pos + si * 0.5f);
-    const float p_x1 = pj_x1.x * (z_mean / fabsf(pj_x1.z));
-    const float p_x2 = pj_x2.x * (z_mean / fabsf(pj_x2.z));
-    const float p_y1 = pj_y1.y * (z_mean / fabsf(pj_y1.z));
-    const float p_y2 = pj_y2.y * (z_mean / fabsf(pj_y2.z));
+    const float p_x1 = pj_x1.x * div_by_recip(z_mean, d_x1, r_x1);
+    const float p_x2 = pj_x2.x * div_by_recip(z_mean, d_x2, r_x2);
+    const float p_y1 = pj_y1.y * div_by_recip(z_mean, d_y1, r_y1);
+    const float p_y2 = pj_y2.y * div_by_recip(z_mean, d_y2, r_y2);
     float x1 = fminf(p_x1, p_x2), x2 = fmaxf(p_x1, p_x2);
     float y1 = fminf(p_y1, p_y2), y2 = fmaxf(p_y1, p_y2);
     const float xdiff = fabsf(x2 - x1), ydiff = fabsf(y2 - y1);
-    const float xs = (ceilf(xdiff / Q.S[0]) - (xdiff / Q.S[0])) * 0.5f;
-    const float ys = (ceilf(ydiff / Q.S[1]) - (ydiff / Q.S[1])) * 0.5f;
+    const float xq = div_by_recip(xdiff, Q.S[0], rS.x), yq = div_by_recip(ydiff, Q.S[1], rS.y);
+    const float xs = (ceilf(xq) - xq) * 0.5f;
+    const float ys = (ceilf(yq) - yq) * 0.5f;
     x1 = x1 - xs * Q.S[0]; x2 = x2 + xs * Q.S[0];
     y1 = y1 - ys * Q.S[1]; y2 = y2 + ys * Q.S[1];
     const float z1 = fminf(z_pos, z_pos + si), z2 = fmaxf(z_pos, z_pos + si);
-    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2});
+    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2}, rS);
     boxes++;
     z_pos = z_pos + si;
   }
@@ -131,6 +140,7 @@ __device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   float signal = 1.0f;
   if (cv.y < 0) signal = -1.0f;
   const float p_cs = Q.p_cs, p_sn = Q.p_sn, n_cs = Q.n_cs, n_sn = Q.n_sn;
+  const f3 rS{1.0f / Q.S[0], 1.0f / Q.S[1], 1.0f / Q.S[2]};   // loop-invariant divisors
   const f3 proj_x = normalize3(f3{cv.x, cv.y, 0.0f});
   const f3 proj_z = normalize3(f3{0.0f, cv.y, cv.z});
   const f3 pj_x1 = normalize3(f3{proj_x.x * n_cs - proj_x.y * n_sn, proj_x.x * n_sn + proj_x.y * n_cs, 0.0f});
@@ -140,22 +150,26 @@ __device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   const float si = Q.interval * signal * Q.S[1];
   float y_pos = Q.initial_step * signal * Q.S[1];
   const float vmin = Q.S[1] * 0.5f, vmax = Q.G[1] - Q.S[1] * 0.5f;
-  while ((y_pos / cv.y) < Q.max_distance &&
+  const float d_x1 = fabsf(pj_x1.y), d_x2 = fabsf(pj_x2.y), d_z1 = fabsf(pj_z1.y), d_z2 = fabsf(pj_z2.y);
+  const float r_x1 = 1.0f / d_x1, r_x2 = 1.0f / d_x2, r_z1 = 1.0f / d_z1, r_z2 = 1.0f / d_z2;
+  const float rc = 1.0f / cv.y;
+  while (div_by_recip(y_pos, cv.y, rc) < Q.max_distance &&
          (pos.y + (y_pos + si) > vmin && pos.y + (y_pos + si) < vmax)) {
     const float y_mean = fabsf(y_pos + si * 0.5f);
-    const float p_x1 = pj_x1.x * (y_mean / fabsf(pj_x1.y));
-    const float p_x2 = pj_x2.x * (y_mean / fabsf(pj_x2.y));
-    const float p_z1 = pj_z1.z * (y_mean / fabsf(pj_z1.y));
-    const float p_z2 = pj_z2.z * (y_mean / fabsf(pj_z2.y));
+    const float p_x1 = pj_x1.x * div_by_recip(y_mean, d_x1, r_x1);
+    const float p_x2 = pj_x2.x * div_by_recip(y_mean, d_x2, r_x2);
+    const float p_z1 = pj_z1.z * div_by_recip(y_mean, d_z1, r_z1);
+    const float p_z2 = pj_z2.z * div_by_recip(y_mean, d_z2, r_z2);
     float x1 = fminf(p_x1, p_x2), x2 = fmaxf(p_x1, p_x2);
     float z1 = fminf(p_z1, p_z2), z2 = fmaxf(p_z1, p_z2);
     const float xdiff = fabsf(x2 - x1), zdiff = fabsf(z2 - z1);
-    const float xs = (ceilf(xdiff / Q.S[0]) - (xdiff / Q.S[0])) * 0.5f;
-    const float zs = (ceilf(zdiff / Q.S[2]) - (zdiff / Q.S[2])) * 0.5f;
+    const float xq = div_by_recip(xdiff, Q.S[0], rS.x), zq = div_by_recip(zdiff, Q.S[2], rS.z);
+    const float xs = (ceilf(xq) - xq) * 0.5f;
+    const float zs = (ceilf(zq) - zq) * 0.5f;
     x1 = x1 - xs * Q.S[0]; x2 = x2 + xs * Q.S[0];
     z1 = z1 - zs * Q.S[2]; z2 = z2 + zs * Q.S[2];
     const float y1 = fminf(y_pos, y_pos + si), y2 = fmaxf(y_pos, y_pos + si);
-    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2});
+    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2}, rS);
     boxes++;
     y_pos = y_pos + si;
   }
@@ -169,6 +183,7 @@ __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   float signal = 1.0f;
   if (cv.x < 0) signal = -1.0f;
   const float p_cs = Q.p_cs, p_sn = Q.p_sn, n_cs = Q.n_cs, n_sn = Q.n_sn;
+  const f3 rS{1.0f / Q.S[0], 1.0f / Q.S[1], 1.0f / Q.S[2]};   // loop-invariant divisors
   const f3 proj_y = normalize3(f3{cv.x, cv.y, 0.0f});
   const f3 proj_z = normalize3(f3{cv.x, 0.0f, cv.z});
   const f3 pj_y1 = normalize3(f3{proj_y.y * n_sn + proj_y.x * n_cs, proj_y.y * n_cs - proj_y.x * n_sn, 0.0f});
@@ -178,22 +193,26 @@ __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   const float si = Q.interval * signal * Q.S[0];
   float x_pos = Q.initial_step * signal * Q.S[0];
   const float vmin = Q.S[0] * 0.5f, vmax = Q.G[0] - Q.S[0] * 0.5f;
-  while ((x_pos / cv.x) < Q.max_distance &&
+  const float d_y1 = fabsf(pj_y1.x), d_y2 = fabsf(pj_y2.x), d_z1 = fabsf(pj_z1.x), d_z2 = fabsf(pj_z2.x);
+  const float r_y1 = 1.0f / d_y1, r_y2 = 1.0f / d_y2, r_z1 = 1.0f / d_z1, r_z2 = 1.0f / d_z2;
+  const float rc = 1.0f / cv.x;
+  while (div_by_recip(x_pos, cv.x, rc) < Q.max_distance &&
          (pos.x + (x_pos + si) > vmin && pos.x + (x_pos + si) < vmax)) {
     const float x_mean = fabsf(x_pos + si * 0.5f);
-    const float p_y1 = pj_y1.y * (x_mean / fabsf(pj_y1.x));
-    const float p_y2 = pj_y2.y * (x_mean / fabsf(pj_y2.x));
-    const float p_z1 = pj_z1.z * (x_mean / fabsf(pj_z1.x));
-    const float p_z2 = pj_z2.z * (x_mean / fabsf(pj_z2.x));
+    const float p_y1 = pj_y1.y * div_by_recip(x_mean, d_y1, r_y1);
+    const float p_y2 = pj_y2.y * div_by_recip(x_mean, d_y2, r_y2);
+    const float p_z1 = pj_z1.z * div_by_recip(x_mean, d_z1, r_z1);
+    const float p_z2 = pj_z2.z * div_by_recip(x_mean, d_z2, r_z2);
     float y1 = fminf(p_y1, p_y2), y2 = fmaxf(p_y1, p_y2);
     float z1 = fminf(p_z1, p_z2), z2 = fmaxf(p_z1, p_z2);
     const float ydiff = fabsf(y2 - y1), zdiff = fabsf(z2 - z1);
-    const float ys = (ceilf(ydiff / Q.S[1]) - (ydiff / Q.S[1])) * 0.5f;
-    const float zs = (ceilf(zdiff / Q.S[2]) - (zdiff / Q.S[2])) * 0.5f;
+    const float yq = div_by_recip(ydiff, Q.S[1], rS.y), zq = div_by_recip(zdiff, Q.S[2], rS.z);
+    const float ys = (ceilf(yq) - yq) * 0.5f;
+    const float zs = (ceilf(zq) - zq) * 0.5f;
     y1 = y1 - ys * Q.S[1]; y2 = y2 + ys * Q.S[1];
     z1 = z1 - zs * Q.S[2]; z2 = z2 + zs * Q.S[2];
     const float x1 = fminf(x_pos, x_pos + si), x2 = fmaxf(x_pos, x_pos + si);
-    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2});
+    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2}, rS);
     boxes++;
     x_pos = x_pos + si;
   }

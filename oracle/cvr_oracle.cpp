@@ -1752,3 +1752,37 @@ ORACLE_API uint64_t oracle_render_iso(const OracleIso* Q, float* out_rgba, uint3
                                       int nthreads) {
   return oracle_render_iso_rows(Q, 0, Q->base.H, out_rgba, out_counts, nthreads);
 }
+
+// ---------------------------------------------------------------------------
+// Check of the library's division by a precomputed reciprocal (cvr_device.h
+// div_by_recip: q = RN(a*y), r = fma(-b, q, a), RN(q + r*y) with y = RN(1/b))
+// against IEEE division, on n log-uniform random pairs (a in [2^-lo, 2^hi],
+// b in [2^-8, 2^8], both signs).  Returns the number of mismatching quotients.
+// ---------------------------------------------------------------------------
+ORACLE_API uint64_t oracle_check_div_by_recip(uint64_t n, uint64_t seed, int lo, int hi) {
+  uint64_t bad = 0;
+#pragma omp parallel for reduction(+ : bad) schedule(static)
+  for (int64_t t = 0; t < (int64_t)n; t++) {
+    uint64_t x = (seed + (uint64_t)t) * 0x9E3779B97F4A7C15ull;
+    auto next = [&]() {
+      x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 27; x *= 0x94D049BB133111EBull;
+      x ^= x >> 31;
+      return x;
+    };
+    const uint64_t r1 = next(), r2 = next();
+    // exponent uniform, mantissa uniform
+    const int ea = lo + (int)((r1 >> 40) % (uint64_t)(hi - lo + 1));
+    const int eb = -8 + (int)((r2 >> 40) % 17u);
+    float a = std::ldexp(1.0f + (float)(r1 & 0x7fffff) / 8388608.0f, -ea);
+    float b = std::ldexp(1.0f + (float)(r2 & 0x7fffff) / 8388608.0f, eb);
+    if (r1 & (1ull << 63)) a = -a;
+    if (r2 & (1ull << 63)) b = -b;
+    const float y = 1.0f / b;
+    const float q = a * y;
+    const float r = std::fmaf(-b, q, a);
+    const float d = std::fmaf(r, y, q);
+    const float e = a / b;
+    if (f2u(d) != f2u(e)) bad++;
+  }
+  return bad;
+}

@@ -106,6 +106,8 @@ def lib():
         L.oracle_sat_build.restype = None
         L.oracle_sat_planes.argtypes = [P, I, I, I, I, P, P, I, P]
         L.oracle_sat_planes.restype = None
+        L.oracle_check_div_by_recip.argtypes = [ctypes.c_uint64, ctypes.c_uint64, I, I]
+        L.oracle_check_div_by_recip.restype = ctypes.c_uint64
         L.oracle_render_ebs_rows.argtypes = [ctypes.POINTER(OracleEbs), I, I, P, P, I]
         L.oracle_render_ebs_rows.restype = ctypes.c_uint64
         L.oracle_multiscale_filter.argtypes = [I, I, P, I, I, P, I, I]
@@ -467,3 +469,9 @@ def render_iso(vol16: np.ndarray, vox: np.ndarray, scale, camera: dict, W: int, 
     y0, y1 = (0, H) if rows is None else (int(rows[0]), int(rows[1]))
     S = lib().oracle_render_iso_rows(ctypes.byref(Q), y0, y1, _p(rgba), _p(cnt), int(threads))
     return rgba, cnt, int(S), (bmin, bmax)
+
+
+def check_div_by_recip(n: int, seed: int = 1, lo: int = -20, hi: int = 20) -> int:
+    """Mismatches of the reciprocal-corrected division (cvr_device.h div_by_recip) against
+    IEEE a / b over n random pairs (a = +-m * 2^-e, e in [lo, hi]; b = +-m * 2^[-8, 8])."""
+    return int(lib().oracle_check_div_by_recip(n, seed, lo, hi))
