@@ -426,6 +426,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
 
 struct DosShader {
   using Args = DosArgs;
+  static constexpr int kMinWavesPerEU = 1;   // register budget: the compiler's choice
   using Data = const uint4*;   // the cell8 extinction pyramid
 
   // Shaded colour of one job; `lit` counts the shadow cones traced, `fetches`

@@ -221,8 +221,12 @@ __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
 
 }  // namespace
 
+#ifndef CVR_EBS_WAVES
+#define CVR_EBS_WAVES 1
+#endif
 struct EbsShader {
   using Args = EbsArgs;
+  static constexpr int kMinWavesPerEU = CVR_EBS_WAVES;   // register budget (1: compiler's choice)
   using Data = const float4*;   // the float SAT, cell8
 
   // ShadeSample (:498-550); `lit` counts the shadow box chains traced.

@@ -46,7 +46,7 @@ __device__ __forceinline__ f3 cross3(f3 x, f3 y) {   // glm / GLSL cross, no fma
 
 // One wave = one 8x8 tile (XCD b%8 takes a contiguous band of tiles).
 template <class SH, bool PHONG>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH::kMinWavesPerEU)))
 shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
                     typename SH::Data data, float4* __restrict__ out,
