@@ -567,6 +567,12 @@ def main():
                 "kernel": kname,
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank}
+        if roof["traffic"]:
+            # the bytes HBM actually served (PMC) at the kernel's own time: where the
+            # algorithmic figure is mostly served from L1/L2 (frac > 1 for EBS), this
+            # is the quantity the HBM roofline bounds
+            roof["traffic_GBs"] = round(roof["traffic"] / (kern_ms * 1e-3) / 1e9, 1)
+            roof["traffic_frac"] = round(roof["traffic_GBs"] / HBM_PEAK_GBS, 4)
         if a.phong and count_shaded:
             roof["phong_shaded_samples"] = int(shade[0])
         if dos:
