@@ -108,6 +108,12 @@ def lib():
         L.oracle_sat_planes.restype = None
         L.oracle_check_div_by_recip.argtypes = [ctypes.c_uint64, ctypes.c_uint64, I, I]
         L.oracle_check_div_by_recip.restype = ctypes.c_uint64
+        L.oracle_render_rc1pass_literal.argtypes = [ctypes.POINTER(OracleRc1pass), I, I, P, P, I, I]
+        L.oracle_render_rc1pass_literal.restype = ctypes.c_uint64
+        L.oracle_render_dos_literal.argtypes = [ctypes.POINTER(OracleDos), I, I, P, P, I, I]
+        L.oracle_render_dos_literal.restype = ctypes.c_uint64
+        L.oracle_render_ebs_literal.argtypes = [ctypes.POINTER(OracleEbs), I, I, P, P, I, I]
+        L.oracle_render_ebs_literal.restype = ctypes.c_uint64
         L.oracle_render_ebs_rows.argtypes = [ctypes.POINTER(OracleEbs), I, I, P, P, I]
         L.oracle_render_ebs_rows.restype = ctypes.c_uint64
         L.oracle_multiscale_filter.argtypes = [I, I, P, I, I, P, I, I]
@@ -215,8 +221,11 @@ def _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shini
 def render_rc1pass(vol16: np.ndarray, scale, tf: np.ndarray, camera: dict, W: int, H: int,
                    step: float, grad: np.ndarray | None = None, phong: bool = False,
                    ka=0.5, kd=0.5, ks=0.8, shininess=30.0, ispec=(1.0, 1.0, 1.0),
-                   light=(0.0, 0.0, 0.0), threads: int = 0, rows=None):
-    """Full frame (or rows=(y0,y1)) of ray_marching_1p.comp. Returns (rgba HxWx4, counts HxW, S)."""
+                   light=(0.0, 0.0, 0.0), threads: int = 0, rows=None, literal=None):
+    """Full frame (or rows=(y0,y1)) of ray_marching_1p.comp. Returns (rgba HxWx4, counts HxW, S).
+    literal=None: CVR-SPEC (what the HIP kernels reproduce bit for bit); literal=b: the
+    literal GLSL reading (glsl_literal.cpp) with GL filter weights quantised to b fraction
+    bits (0 = exact float weights)."""
     vol16 = np.ascontiguousarray(vol16, np.float32)
     # the TF texture is GL_RGBA16F (GenerateTexture_1D_RGBt): entries round to half (RNE)
     tf = np.ascontiguousarray(np.asarray(tf, np.float32).astype(np.float16), np.float32)
@@ -226,7 +235,11 @@ def render_rc1pass(vol16: np.ndarray, scale, tf: np.ndarray, camera: dict, W: in
                 light, aspect=camera.get("aspect", 0.0))
     rgba = np.zeros((H, W, 4), np.float32)
     cnt = np.zeros((H, W), np.uint32)
-    if rows is None:
+    if literal is not None:
+        y0, y1 = rows if rows is not None else (0, H)
+        S = lib().oracle_render_rc1pass_literal(ctypes.byref(P), int(y0), int(y1), _p(rgba),
+                                                _p(cnt), int(threads), int(literal))
+    elif rows is None:
         S = lib().oracle_render_rc1pass(ctypes.byref(P), _p(rgba), _p(cnt), int(threads))
     else:
         S = lib().oracle_render_rc1pass_rows(ctypes.byref(P), int(rows[0]), int(rows[1]),
@@ -295,9 +308,10 @@ def _cone(tables, keep):
 def render_dos(vol16, scale, tf_rgbt, ext_levels, camera, W, H, step, occ_tables, sdw_tables,
                apply_occlusion=True, apply_shadow=False, shadow_type=0, light=None,
                grad=None, phong=False, ka=0.5, kd=0.5, ks=0.8, shininess=30.0,
-               ispec=(1.0, 1.0, 1.0), threads: int = 0, rows=None):
+               ispec=(1.0, 1.0, 1.0), threads: int = 0, rows=None, literal=None):
     """Directional-occlusion shading frame (ray_bbox_marching.comp), or rows=(y0, y1) of
-    it.  light = dict with position/forward/up/right/spot_angle_deg.
+    it.  light = dict with position/forward/up/right/spot_angle_deg.  literal: as
+    render_rc1pass.
     Returns (rgba, counts, S)."""
     vol16 = np.ascontiguousarray(vol16, np.float32)
     tf = _q16_array(tf_rgbt)
@@ -324,8 +338,12 @@ def render_dos(vol16, scale, tf_rgbt, ext_levels, camera, W, H, step, occ_tables
     rgba = np.zeros((H, W, 4), np.float32)
     cnt = np.zeros((H, W), np.uint32)
     y0, y1 = rows if rows is not None else (0, H)
-    S = lib().oracle_render_dos_rows(ctypes.byref(Q), int(y0), int(y1), _p(rgba), _p(cnt),
-                                     int(threads))
+    if literal is not None:
+        S = lib().oracle_render_dos_literal(ctypes.byref(Q), int(y0), int(y1), _p(rgba), _p(cnt),
+                                            int(threads), int(literal))
+    else:
+        S = lib().oracle_render_dos_rows(ctypes.byref(Q), int(y0), int(y1), _p(rgba), _p(cnt),
+                                         int(threads))
     return rgba, cnt, int(S)
 
 
@@ -375,8 +393,9 @@ def render_ebs(vol16, scale, tf_rgbt, sat_f32, camera, W, H, step, apply_occlusi
                cone_angle_deg=1.0, interval=2.0, initial_step=2.0, ui_weight=1.0,
                max_distance=None, light=(0.0, 0.0, 0.0), light_forward=(0.0, 0.0, -1.0),
                grad=None, phong=False, ka=0.5, kd=0.5, ks=0.8, shininess=30.0,
-               ispec=(1.0, 1.0, 1.0), threads: int = 0, rows=None):
-    """Extinction-based shading frame (ebs_ray_bbox_marching.comp).  Returns (rgba, counts, S)."""
+               ispec=(1.0, 1.0, 1.0), threads: int = 0, rows=None, literal=None):
+    """Extinction-based shading frame (ebs_ray_bbox_marching.comp).  Returns (rgba, counts, S).
+    literal: as render_rc1pass."""
     vol16 = np.ascontiguousarray(vol16, np.float32)
     tf = _q16_array(tf_rgbt)
     sat = np.ascontiguousarray(sat_f32, np.float32)
@@ -398,7 +417,12 @@ def render_ebs(vol16, scale, tf_rgbt, sat_f32, camera, W, H, step, apply_occlusi
     rgba = np.zeros((H, W, 4), np.float32)
     cnt = np.zeros((H, W), np.uint32)
     y0, y1 = rows if rows is not None else (0, H)
-    S = lib().oracle_render_ebs_rows(ctypes.byref(Q), int(y0), int(y1), _p(rgba), _p(cnt), int(threads))
+    if literal is not None:
+        S = lib().oracle_render_ebs_literal(ctypes.byref(Q), int(y0), int(y1), _p(rgba), _p(cnt),
+                                            int(threads), int(literal))
+    else:
+        S = lib().oracle_render_ebs_rows(ctypes.byref(Q), int(y0), int(y1), _p(rgba), _p(cnt),
+                                         int(threads))
     return rgba, cnt, int(S)
 
 
