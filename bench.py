@@ -517,7 +517,7 @@ def main():
     assert nkt.value == a.steps
     kern_ms = float(np.mean(kt[:nkt.value]))
     assert int(total.item()) == S_rank_steps, "sample count changed between frames"
-    batch = L.cvr_get_option(r.device.handle, b"batch")
+    batch = L.cvr_get_option(r.device.handle, b"batch") or (2 if a.phong else 4)   # 0 = auto
     macro = L.cvr_get_option(r.device.handle, b"macro")
 
     if world > 1:

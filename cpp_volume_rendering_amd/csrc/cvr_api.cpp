@@ -294,8 +294,8 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c || !key) return CVR_ERR_ARG;
   if (!std::strcmp(key, "batch")) {
-    if (value != 2 && value != 4)
-      return fail(c, CVR_ERR_ARG, "batch must be 2 or 4");
+    if (value != 0 && value != 2 && value != 4)
+      return fail(c, CVR_ERR_ARG, "batch must be 0 (auto), 2 or 4");
     c->batch = value;
     return CVR_OK;
   }

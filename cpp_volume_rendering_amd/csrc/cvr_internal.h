@@ -173,8 +173,9 @@ struct Ctx {
   void* d_grad = nullptr;          // gradient cell8: 3 uint4 (x, y, z fp16 pairs) per volume cell
   size_t grad_bytes = 0;
   int grad_mode = 0;
-  // march tuning: samples fetched per batch (1, 2, 4, 8), optional block order
-  int batch = 4;
+  // march tuning: samples fetched per batch (2, 4; 0 = auto: 4, or 2 with Phong
+  // shading, whose extra registers make occupancy worth more than a deeper batch)
+  int batch = 0;
   int cost_time = 0;               // option "tile_cost": 0 longest ray, 1 measured time (worse)
   int max_waves_cu = 0;            // experiment (option "max_waves_cu"): cap residency via LDS
   int epi_stop = 0;                // diagnostics (option "debug_epi_stop")

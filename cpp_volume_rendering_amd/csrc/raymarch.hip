@@ -668,7 +668,7 @@ hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
   if (a.ntiles <= 0) return hipSuccess;
   if (a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
-  if (c.batch == 2) return launch_k<2>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
+  if (c.batch == 2 || (c.batch == 0 && phong)) return launch_k<2>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
   return launch_k<4>(c, a, phong, out, samples, tile_samples, order, tile_cost, plan, s);
 }
 
