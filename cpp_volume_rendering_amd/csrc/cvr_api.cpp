@@ -908,6 +908,21 @@ cvr_status cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int* 
   return CVR_OK;
 }
 
+cvr_status cvr_selftest_arith(cvr_ctx* ctx, uint64_t out[3]) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c || !out) return CVR_ERR_ARG;
+  HIP_TRY(c, hipSetDevice(c->device));
+  unsigned long long* d = nullptr;
+  HIP_TRY(c, hipMalloc((void**)&d, 3 * sizeof(unsigned long long)));
+  hipError_t e = hipMemsetAsync(d, 0, 3 * sizeof(unsigned long long), c->stream);
+  if (e == hipSuccess) e = cvr::launch_selftest_arith(-100, 200, -96, 222, d, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d);
+  HIP_TRY(c, e);
+  return CVR_OK;
+}
+
 cvr_status cvr_read_shade_counters(cvr_ctx* ctx, uint64_t out[3]) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c || !out) return CVR_ERR_ARG;

@@ -108,27 +108,6 @@ __device__ __forceinline__ float cvr_powf(float x, float y) {
   return cvr_expf(y * cvr_logf(x));
 }
 
-struct f3 { float x, y, z; };
-// a / b correctly rounded from y = 1.0f / b (itself correctly rounded), for a
-// divisor reused many times: q = RN(a*y), the remainder a - b*q is exact by fma,
-// and RN(q + r*y) = RN(a/b) (Markstein's correction; valid while a/b, a*y and the
-// remainder stay in the normal range -- callers pass finite a >= 0 of moderate
-// size and b in the normal range).  Checked against IEEE division in
-// tests/test_exact_div.py.
-__device__ __forceinline__ float div_by_recip(float a, float b, float y) {
-  const float q = a * y;
-  const float r = fmaf(-b, q, a);
-  return fmaf(r, y, q);
-}
-
-__device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
-__device__ __forceinline__ f3 normalize3(f3 v) {
-  float inv = 1.0f / sqrtf(dot3(v, v));
-  return f3{v.x * inv, v.y * inv, v.z * inv};
-}
-
-
-
 // Branch-free CVR-SPEC exp: same values as cvr_expf (selects instead of the
 // early returns, so a wave never splits on the special cases).
 __device__ __forceinline__ float cvr_expf_nb(float x) {
@@ -148,6 +127,100 @@ __device__ __forceinline__ float cvr_expf_nb(float x) {
   y = x > 88.5f ? __builtin_inff() : y;
   return x != x ? x : y;
 }
+
+// cvr_logf's main path for a positive, normal, finite x (no special cases;
+// the mantissa fold is a select): the same value as cvr_logf there.
+__device__ __forceinline__ float cvr_logf_pos(float x) {
+  const uint32_t bits = __float_as_uint(x);
+  int e = (int)((bits >> 23) & 0xffu) - 126;
+  float m = __uint_as_float((bits & 0x007fffffu) | 0x3f000000u);
+  const bool fold = m < 0.70710678118654752f;
+  m = fold ? m + m : m;
+  e = fold ? e - 1 : e;
+  float f = m - 1.0f;
+  float z = f * f;
+  float p = 7.0376836292e-2f;
+  p = fmaf(p, f, -1.1514610310e-1f);
+  p = fmaf(p, f, 1.1676998740e-1f);
+  p = fmaf(p, f, -1.2420140846e-1f);
+  p = fmaf(p, f, 1.4249322787e-1f);
+  p = fmaf(p, f, -1.6668057665e-1f);
+  p = fmaf(p, f, 2.0000714765e-1f);
+  p = fmaf(p, f, -2.4999993993e-1f);
+  p = fmaf(p, f, 3.3333331174e-1f);
+  float r = (p * f) * z;
+  float fe = (float)e;
+  r = fmaf(fe, -2.12194440e-4f, r);
+  r = fmaf(-0.5f, z, r);
+  float lnx = f + r;
+  return fmaf(fe, 0.693359375f, lnx);
+}
+
+// cvr_powf without branches: the main path on a sanitised argument, then the
+// special cases selected in cvr_powf's order of precedence -- the same value as
+// cvr_powf for every (x, y) (checked on the device by cvr_selftest_arith).
+__device__ __forceinline__ float cvr_powf_nb(float x, float y) {
+  const float inf = __builtin_inff();
+  const bool tiny = !(x > 0.0f) || x < 1.17549435e-38f;     // also NaN (selected below)
+  const float xs = (tiny || x == inf) ? 1.0f : x;
+  float r = cvr_expf_nb(y * cvr_logf_pos(xs));
+  const float r_inf = y > 0.0f ? inf : (y == 0.0f ? 1.0f : 0.0f);
+  const float r_tiny = y > 0.0f ? 0.0f : (y == 0.0f ? 1.0f : inf);
+  r = x == inf ? r_inf : r;
+  r = tiny ? r_tiny : r;
+  return (x != x || y != y) ? x + y : r;
+}
+
+struct f3 { float x, y, z; };
+// a / b correctly rounded from y = 1.0f / b (itself correctly rounded), for a
+// divisor reused many times: q = RN(a*y), the remainder a - b*q is exact by fma,
+// and RN(q + r*y) = RN(a/b) (Markstein's correction; valid while a/b, a*y and the
+// remainder stay in the normal range -- callers pass finite a >= 0 of moderate
+// size and b in the normal range).  Checked against IEEE division in
+// tests/test_exact_div.py.
+__device__ __forceinline__ float div_by_recip(float a, float b, float y) {
+  const float q = a * y;
+  const float r = fmaf(-b, q, a);
+  return fmaf(r, y, q);
+}
+
+// RN(1/b) from the hardware reciprocal (v_rcp_f32, within 1 ulp) and one
+// Newton step with fma (e = 1 - b*y exact, y + e*y rounded once): 3
+// instructions instead of the 11 of the IEEE division sequence.  For b and 1/b
+// in the normal range; equal to 1.0f / b for EVERY such float, checked
+// exhaustively on the device by cvr_selftest_arith (tests/test_selftest_gpu.py).
+__device__ __forceinline__ float rcp_cr(float b) {
+  const float y = __builtin_amdgcn_rcpf(b);
+  const float e = fmaf(-b, y, 1.0f);
+  return fmaf(e, y, y);
+}
+
+// RN(sqrt(x)) for x in [2^-96, 2^126]: the correctly rounded sqrt sequence the
+// compiler emits for sqrtf (v_sqrt_f32, then the neighbours s -/+ 1 ulp tested
+// by exact fma remainders) without its input scaling for tiny x and its
+// zero/inf class fix-up, which are identities in this range.
+__device__ __forceinline__ float sqrt_cr_normal(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+  const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rm = fmaf(-sm, s, x);
+  const float rp = fmaf(-sp, s, x);
+  const float r = rm <= 0.0f ? sm : s;
+  return rp > 0.0f ? sp : r;
+}
+
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+// normalize(v) = v * RN(1 / RN(sqrt(dot(v, v)))) (CVR-SPEC): the short exact
+// sequence when dot(v, v) lies in [2^-96, 2^126), else the IEEE operators.
+__device__ __forceinline__ f3 normalize3(f3 v) {
+  const float d = dot3(v, v);
+  float inv;
+  if (d >= 0x1p-96f && d < 0x1p126f) inv = rcp_cr(sqrt_cr_normal(d));
+  else inv = 1.0f / sqrtf(d);
+  return f3{v.x * inv, v.y * inv, v.z * inv};
+}
+
+
 
 // cvr_expf for x in [-86, 0]: the same value without the range selects (the
 // host enables it only when every sample's -(alpha*h) is known to lie there).

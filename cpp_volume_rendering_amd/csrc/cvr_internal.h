@@ -270,6 +270,8 @@ hipError_t launch_screenshot(const void* frame, int half, int w, int h, uint8_t*
 hipError_t launch_build_cells_impl(const void* vox, int bpv, const uint16_t* lut, const int N[3],
                                    const CellGrid& g, void* cells, hipStream_t s);
 hipError_t launch_gradient(const Ctx& c, int mode, uint2* tmp, hipStream_t s);
+hipError_t launch_selftest_arith(int e_rcp_lo, int e_rcp_n, int e_sqrt_lo, int e_sqrt_n,
+                                 unsigned long long* bad, hipStream_t s);
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
                           uint32_t* samples, unsigned long long* tile_samples, const int* order,
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s);

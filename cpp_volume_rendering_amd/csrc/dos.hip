@@ -475,7 +475,7 @@ struct DosShader {
         const float dd = fmaxf(0.0f, dot3(nrm, L));
         const float ds = fmaxf(0.0f, dot3(Hv, nrm));
         const float diff = inv_k * (iocc * Q.ka + (isdw * Q.kd) * dd);
-        const float spec = (isdw * Q.ks) * cvr_powf(ds, A.shininess);
+        const float spec = (isdw * Q.ks) * cvr_powf_nb(ds, A.shininess);
         return f3{fmaf(A.ispec[0], spec, rgb.x * diff), fmaf(A.ispec[1], spec, rgb.y * diff),
                   fmaf(A.ispec[2], spec, rgb.z * diff)};
       }

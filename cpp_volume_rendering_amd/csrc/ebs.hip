@@ -263,7 +263,7 @@ struct EbsShader {
         const f3 Hv = normalize3(f3{Ve.x + L.x, Ve.y + L.y, Ve.z + L.z});
         const float dd = fmaxf(0.0f, dot3(nrm, L));
         const float ds = fmaxf(0.0f, dot3(Hv, nrm));
-        const float pw = cvr_powf(ds, A.shininess);
+        const float pw = cvr_powf_nb(ds, A.shininess);
         // (1/(ka+kd)) * (L*IOcc*ka + IShadow*(L*kd*dot_diff)) + IShadow*(ks*Ispecular*pow) (:528-530)
         return f3{inv_k * ((rgb.x * iocc) * Q.ka + isdw * ((rgb.x * Q.kd) * dd)) + isdw * ((Q.ks * A.ispec[0]) * pw),
                   inv_k * ((rgb.y * iocc) * Q.ka + isdw * ((rgb.y * Q.kd) * dd)) + isdw * ((Q.ks * A.ispec[1]) * pw),

@@ -94,7 +94,7 @@ __device__ __forceinline__ f3 iso_phong(const Rc1passArgs& A, const uint4* __res
     const f3 n = normalize3(g);
     const float dd = fmaxf(0.0f, dot3(n, L));
     const float ds = fmaxf(0.0f, dot3(H, n));
-    const float pw = cvr_powf(ds, A.shininess);
+    const float pw = cvr_powf_nb(ds, A.shininess);
     const float f = fmaf(A.kd, dd, A.ka);        // the rc1pass Blinn-Phong (CVR-SPEC)
     clr = f3{fmaf(A.ispec[0] * A.ks, pw, clr.x * f), fmaf(A.ispec[1] * A.ks, pw, clr.y * f),
              fmaf(A.ispec[2] * A.ks, pw, clr.z * f)};

@@ -477,6 +477,15 @@ cvr_status  cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int*
  * frames, oldest first.  Waits for those frames; resets the frame count. */
 cvr_status  cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* out_frames);
 
+/* Self-check of the device arithmetic the kernels take shortcuts with
+ * (cvr_device.h), exhaustive over every significand: out[0] = floats b with
+ * |b| in [2^-100, 2^100) whose rcp_cr(b) differs from the IEEE 1.0f / b,
+ * out[1] = floats x in [2^-96, 2^126) whose sqrt_cr_normal(x) differs from the
+ * correctly rounded sqrtf(x), out[2] = (x, y) pairs (every positive normal
+ * x < 4 at five exponents y, and the special arguments) whose branch-free
+ * cvr_powf_nb differs from cvr_powf.  All must be 0; synchronous (~1 s). */
+cvr_status  cvr_selftest_arith(cvr_ctx* ctx, uint64_t out[3]);
+
 /* Measurement (shade_counters option), for the last shaded frame
  * (cvr_render_dosct / cvr_render_extbsd; cvr_render_rc1pass with Blinn-Phong
  * fills out[0] only): out[0] samples that ran the shading
