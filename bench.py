@@ -560,7 +560,7 @@ def main():
         kname = ("shaded_march_kernel<DosShader>" if dos else
                  "shaded_march_kernel<EbsShader>" if ebs else
                  f"iso_tile_kernel<{iso_variant}, {str(a.phong).lower()}>" if iso else
-                 f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, *, false, true>")
+                 f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, *, false, true, *>")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic(a.pmc.replace("rc1pass", a.renderer), wkey),

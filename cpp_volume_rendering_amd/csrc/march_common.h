@@ -53,6 +53,17 @@ __device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lx, 
 // Sampling
 // ---------------------------------------------------------------------------
 
+// Buffer resource word 3 for gfx9-family raw buffers (32-bit data format, no
+// swizzle); with num_records = 0xffffffff a 32-bit byte offset reaches 4 GiB.
+constexpr int kBufferConfigDword = 0x00020000;
+
+// 16-byte buffer load at a 32-bit byte offset from a scalar resource.
+__device__ __forceinline__ uint4 buffer_load_u4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  const u4v v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // floor(x) as int in one instruction (x finite and in int range).
 __device__ __forceinline__ int cvt_flr(float x) {
   int r;

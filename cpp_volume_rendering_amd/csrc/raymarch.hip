@@ -74,7 +74,7 @@ __device__ __forceinline__ bool skip_empty(const Rc1passArgs& A, const Ray& r, f
 // Ray-parallel march (one lane per ray) of ray_marching_1p.comp:124-172.  The
 // arithmetic per sample is exactly the reference's sequential loop (s
 // accumulates h one step at a time); batching only changes when loads issue.
-template <int K, bool PHONG, bool SKIP, bool XF>
+template <int K, bool PHONG, bool SKIP, bool XF, bool BUF>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
                                           const uint4* __restrict__ grad,
                                           const float4* __restrict__ tfp, int px, int py,
@@ -90,6 +90,15 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
   bool done = !(s < D);
   bool probe = true;
   const bool wave_in_box = __ballot(r.outside) == 0;   // the usual case: no clamps
+  // BUF (cell grid < 4 GiB): buffer loads with a 32-bit byte offset from one
+  // scalar resource instead of 64-bit per-lane addresses (two fewer VALU
+  // instructions and VGPRs per load; -3 % on the headline frame)
+  const __amdgpu_buffer_rsrc_t crs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)cells, 0, -1, kBufferConfigDword);
+  auto load_cell = [&](uint32_t i) -> uint4 {
+    if (BUF) return buffer_load_u4(crs, i << 4);
+    return cells[i];
+  };
   while (!done) {
     // Empty-space skipping (bit-exact): if the macro cell holding the next
     // sample is transparent for the current TF (every density its texels can
@@ -146,14 +155,14 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       for (int j = 0; j < K; j++) {
         sp[j] = sample_pos(fmaf(r.dt.x, tj[j], r.o.x), fmaf(r.dt.y, tj[j], r.o.y),
                            fmaf(r.dt.z, tj[j], r.o.z), A);
-        raw[j] = cells[sp[j].idx];
+        raw[j] = load_cell(sp[j].idx);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < K; j++) {
         sp[j] = sample_pos_clamped(fmaf(r.dt.x, tj[j], r.o.x), fmaf(r.dt.y, tj[j], r.o.y),
                                    fmaf(r.dt.z, tj[j], r.o.z), A);
-        raw[j] = cells[sp[j].idx];
+        raw[j] = load_cell(sp[j].idx);
       }
     }
     // stage 2: density and transfer-function classification
@@ -324,7 +333,7 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
 #else
 #define CVR_RC1_OCC
 #endif
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF>
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, bool BUF>
 __global__ void __launch_bounds__(64) CVR_RC1_OCC
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
@@ -359,7 +368,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     const bool inside = px < A.W && py < A.H;
     dst = make_float4(0.f, 0.f, 0.f, 0.f);
     cnt = 0;
-    if (inside) march_ray<K, PHONG, SKIP, XF>(A, cells, grad, tfp, px, py, dst, cnt, nshade);
+    if (inside) march_ray<K, PHONG, SKIP, XF, BUF>(A, cells, grad, tfp, px, py, dst, cnt, nshade);
     writer = inside || A.packed;
   } else {                    // quarter of a tile, four lanes per ray
     const int ray = lane >> 2;
@@ -620,7 +629,7 @@ __global__ void clear_u32_kernel(uint32_t* __restrict__ p, int n) {
 // Kernel variant: K (batch), PHONG, SKIP (empty-space skipping compiled in),
 // QUAD (quad path compiled in), XF (range-free exp).  Paths a frame does not
 // use are compiled out: they would cost the hot loop registers (occupancy).
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF>
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, bool BUF>
 static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                                  unsigned long long* tile_samples, const int* order,
                                  uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
@@ -629,7 +638,7 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
   // cell (1,1,1) <-> texel (0,0,0)
   const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
   int grid = order ? plan.order_slots : plan.ntiles;
-  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF>), dim3(grid), dim3(64), lds, s,
+  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF>), dim3(grid), dim3(64), lds, s,
                      a, cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, out, samples,
                      tile_samples, order, tile_cost, order ? plan.boost : 0);
   return hipGetLastError();
@@ -641,10 +650,14 @@ static hipError_t launch_kps(const Ctx& c, const Rc1passArgs& a, float4* out, ui
                              const RenderPlan& plan, hipStream_t s) {
   const bool quad = order && plan.quad_pct > 0;
   if (quad)
-    return a.exp_fast ? launch_variant<K, PHONG, SKIP, true, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
-                      : launch_variant<K, PHONG, SKIP, true, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
-  return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
-                    : launch_variant<K, PHONG, SKIP, false, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
+    return a.exp_fast ? launch_variant<K, PHONG, SKIP, true, true, false>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                      : launch_variant<K, PHONG, SKIP, true, false, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
+  // buffer loads address the cell grid with 32-bit byte offsets
+  if (c.cells_bytes < (size_t(1) << 32))
+    return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                      : launch_variant<K, PHONG, SKIP, false, false, true>(c, a, out, samples, ts, order, tile_cost, plan, s);
+  return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, false>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                    : launch_variant<K, PHONG, SKIP, false, false, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
 }
 
 template <int K, bool PHONG>
