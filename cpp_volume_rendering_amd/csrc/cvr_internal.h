@@ -46,6 +46,7 @@ struct Rc1passArgs {
   // screen-tile split (cvr_frame)
   int tile, rank, nranks, ntx, my_tiles;
   int packed;
+  int interleave;                    // no launch order: tile t on block t (XCD t % 8) instead of XCD bands
   int out_half;                      // 1: store RGBA16F (uint2 per pixel), 0: float4
   int ntiles;                        // 8x8 wave tiles of this launch
   unsigned long long* tile_stats;    // diagnostics (tile_stats option) or null
@@ -190,7 +191,8 @@ struct Ctx {
   // kernel_timing option: HIP events around every frame's ray-march launch (ring)
   std::vector<hipEvent_t> ev_start, ev_stop;
   long long timed_frames = 0;
-  int use_order = 1;               // 1: longest-first (LPT) from an earlier frame's costs
+  int use_order = 1;               // 1: longest-first (LPT) from an earlier frame's costs;
+                                   // 0: screen order in XCD bands; 2: screen order interleaved over XCDs
   // The LPT order is built off the critical path: frame i's costs are sorted
   // on a side stream while frames i+1, i+2 render, and frame i+3 uses the
   // result (kOrderSlots slots in rotation; frame i uses and refills slot
@@ -208,7 +210,13 @@ struct Ctx {
     hipStream_t stream = nullptr;  // render stream that owns the slot (async_order 0)
     bool owned = false;
     long long frames = 0;          // frames rendered with this slot
+    float view[7] = {0};           // eye, unit forward, tan(fovy/2) of the frame the order came from
+    bool has_view = false;
+    float last_view[7] = {0};      // the previous frame's view on this slot
+    bool has_last = false;
   };
+  int stale_deg = 5;               // option "stale_deg": an order learned on a view more than this
+                                   // far away (degrees / 1/12 of the eye distance) is not used
   static constexpr int kOrderSlots = 8;   // async_order uses the first 3
   int async_order = 0;             // option "async_order": 1 = sort on a side stream (lag 3)
   int order_interval = 8;          // option "order_interval": rebuild the order every n-th frame

@@ -349,7 +349,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     t = e & (kQuadFlag - 1);
     if (QUAD) quarter = (e >> 28) - 1;
     if ((b >> 3) < boost) __builtin_amdgcn_s_setprio(2);
-  } else if ((nt & 7) == 0) {
+  } else if ((nt & 7) == 0 && !A.interleave) {
     t = (b & 7) * (nt >> 3) + (b >> 3);
   } else {
     t = b;

@@ -249,7 +249,13 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                auto: 4, or 2 with gradient shading — measured 8 % faster there)
  *   "tile_order" 1: each XCD takes the tiles of its screen band longest-first (LPT),
  *                using the previous frame's per-tile critical paths (default);
- *                0: screen order
+ *                0: screen order, one contiguous band per XCD; 2: screen order
+ *                interleaved over the XCDs (tile t on XCD t mod 8)
+ *   "stale_deg"  with tile_order 1: an order learned on a view more than this many
+ *                degrees away (view direction; eye moved by that chord of its
+ *                distance to the volume centre; fovy changed by that fraction) is
+ *                not used, the frame runs in interleaved screen order and the
+ *                order is relearned (default 5; 0 = always use it)
  *   "boost"      percent of each band's longest entries launched at raised wave
  *                priority (with tile_order 1; default 5)
  *   "quad"       percent of each band's longest tiles marched sample-parallel, four

@@ -234,6 +234,8 @@ SCHEDULES = [
     # order built on a side stream (lag 3) / rebuilt every frame
     dict(tile_order=1, batch=4, async_order=1, quad=10),
     dict(tile_order=1, batch=2, order_interval=1, boost=0),
+    # screen order interleaved over the XCDs (the fallback of a stale order)
+    dict(tile_order=2, batch=4),
 ]
 
 
@@ -265,6 +267,29 @@ def test_schedules_bitexact(oracle, bonsai_tf, name, sched):
             assert_bitexact(g_cnt, o_cnt, f"{name} frame {frame} counts")
             assert_bitexact(g_rgba, o_rgba, f"{name} frame {frame} rgba")
             assert g_total == o_total
+    finally:
+        d.close()
+
+
+def test_jumping_camera_orders_bitexact(oracle, bonsai_tf):
+    """Frames alternating between distant views (the learned order goes stale and
+    the frame falls back to interleaved screen order), then holding one view (the
+    order is relearned): every frame equals the oracle bit for bit."""
+    vol = _ml(64)
+    scale = (1.0, 1.0, 1.0)
+    cams = [INITIAL, dict(eye=(-80.0, 40.0, -90.0), center=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0)),
+            dict(eye=(10.0, 120.0, 30.0), center=(2.0, 0.0, 0.0), up=(0.0, 0.0, 1.0))]
+    W = H = 96
+    ref = [oracle_render(oracle, vol, scale, bonsai_tf, c, W, H) for c in cams]
+    d = Device(0)
+    try:
+        seq = [0, 1, 2, 0, 1, 1, 1, 2, 2, 2, 2, 0, 0]
+        for k, i in enumerate(seq):
+            g_rgba, g_cnt, g_total = gpu_render(d, vol, scale, bonsai_tf, cams[i], W, H,
+                                                set_data=(k == 0))
+            assert_bitexact(g_cnt, ref[i][1], f"frame {k} (view {i}) counts")
+            assert_bitexact(g_rgba, ref[i][0], f"frame {k} (view {i}) rgba")
+            assert g_total == ref[i][2]
     finally:
         d.close()
 
