@@ -1333,6 +1333,34 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
     for (int i = 0; i < 10; i++)
       for (int j = 0; j < 3; j++) C.axes[3 * i + j] = T.axes[i][j];
     C.sections = c->d_cones + (size_t)k * CVR_MAX_CONE_SECTIONS;
+    // exit tables: the sections' track and border scale, replaying the kernel's
+    // float recurrence (track += interval) on the RGBA16F-rounded table
+    float track = T.initial_step;
+    int s0 = 0;
+    for (int st = 0; st < 3; st++) {
+      cvr::ConeStageExit& X = C.exit[st];
+      X.nruns = 0;
+      bool ok = Q.zero_skip != 0;
+      for (int i = s0; i < s0 + T.counts[st]; i++) {
+        const float mip = half_round(T.sections[i][1]);
+        const float inv = std::ldexp(1.0f, -(2 * (int)mip + 1));
+        if (!(mip >= 0.0f)) ok = false;
+        if (X.nruns == 0 || inv != X.run_inv[X.nruns - 1]) {
+          if (X.nruns == cvr::kMaxConeRuns) ok = false;
+          else {
+            X.run_first[X.nruns] = i;
+            X.run_t[X.nruns] = track;
+            X.run_inv[X.nruns] = inv;
+            X.nruns++;
+          }
+        }
+        track = track + half_round(T.sections[i][0]);
+      }
+      s0 += T.counts[st];
+      X.end_s = s0;
+      X.end_track = track;
+      if (!ok) X.nruns = 0;
+    }
   }
 
   return render_shaded(c, o, ntiles, npix, [&](float4* out, uint32_t* smp, unsigned long long* shade,

@@ -71,11 +71,25 @@ struct ExtLevel {
 };
 
 // Directional-occlusion shading (dos.hip): one cone's tables on the device.
+// Early exit of a cone stage (dos.hip cone_stage): per stage, the sections where
+// the border scale 2^-(2 floor(mip) + 1) changes ("runs": first section, its
+// tap distance `track`, the scale) and the track after the stage's last section,
+// all by the kernel's own float recurrence on the fp16-rounded table.
+constexpr int kMaxConeRuns = 12;
+struct ConeStageExit {
+  int nruns;                         // 0: no exit test for this stage
+  int end_s;                         // first section after the stage
+  float end_track;                   // track after the stage's last section
+  int run_first[kMaxConeRuns];
+  float run_t[kMaxConeRuns], run_inv[kMaxConeRuns];
+};
+
 struct DosCone {
   int counts[3];                     // sections of 1, 3, 7 rays
   float initial_step, ray7w, ui_weight;
   float axes[30];                    // 3-ray then 7-ray axes (x, y, z)
   const float4* sections;            // (interval, mip, d_integral, amplitude), fp16-rounded
+  ConeStageExit exit[3];
 };
 
 struct DosArgs {

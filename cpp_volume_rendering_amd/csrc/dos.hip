@@ -357,15 +357,70 @@ __device__ __forceinline__ void cone_step(const DosArgs& Q, const DosCone& C,
   }
 }
 
+// Early exit, exact: once a ray has left the box and its last tap was 0, every
+// later tap of the stage is 0 too when the border exponent provably stays below
+// -86.  The box is convex and axis-aligned: on an axis where the ray is outside
+// and moving outward, the excess e grows linearly, e(t') = e + |k_a| (t' - t),
+// and the distance to the box is at least e(t').  The border scale
+// 2^-(2 floor(mip) + 1) is constant over each run of sections (ConeStageExit), so
+// the smallest exponent magnitude of a run is at its first section.  The test
+// keeps a margin (1e-2 in distance, 0.1 % in slope, 1 % in the exponent) far
+// beyond the float error of the kernel's own positions and distances.  Such taps
+// add exactly 0 to the ray's sum (last == 0, v == 0), so the stage ends at once:
+// s and track jump to its end, rays/last are final.
+__device__ __forceinline__ bool ray_gone(const DosArgs& Q, const ConeStageExit& X, f3 k, f3 pos,
+                                         float track, int s_next, float inv_next) {
+  const f3 p = vmad(k, track, pos);
+  float e = -1.0f, slope = 0.0f;
+  auto axis = [&](float pa, float ka, float Ga) {
+    const float ea = ka > 0.0f ? pa - Ga : (ka < 0.0f ? -pa : -1.0f);
+    if (ea > e) { e = ea; slope = fabsf(ka); }
+  };
+  axis(p.x, k.x, Q.G[0]);
+  axis(p.y, k.y, Q.G[1]);
+  axis(p.z, k.z, Q.G[2]);
+  e -= 1e-2f;
+  slope *= 0.999f;
+  if (!(e > 0.0f)) return false;
+  constexpr float kLimit = 86.0f * 1.01f;
+  if (!(e * e * inv_next > kLimit)) return false;   // the run holding section s_next
+  for (int r = 0; r < X.nruns; r++) {
+    if (X.run_first[r] <= s_next) continue;
+    const float d = fmaf(slope, X.run_t[r] - track, e);
+    if (!(d * d * X.run_inv[r] > kLimit)) return false;
+  }
+  return true;
+}
+
 template <int J, int U>
 __device__ __forceinline__ void cone_stage(const DosArgs& Q, const DosCone& C,
                                            const uint4* __restrict__ ext, ConstSections sec, int& s,
                                            int n, float& track, const f3 (&vk)[J], f3 pos,
-                                           float (&rays)[7], float (&last)[7], uint32_t& nf) {
+                                           float (&rays)[7], float (&last)[7], uint32_t& nf,
+                                           const ConeStageExit& X) {
   int i = 0;
-  for (; i + U <= n; i += U, s += U)
+  for (; i + U <= n; i += U, s += U) {
     cone_step<J, U>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last,
                     nf);
+    if (X.nruns > 0 && i + U < n) {
+      bool zero = true;
+#pragma unroll
+      for (int j = 0; j < J; j++) zero = zero && last[j] == 0.0f;
+      if (__all(zero)) {   // every lane's rays just took a 0 tap: worth the full test
+        const int sn = __builtin_amdgcn_readfirstlane(s + U);
+        const float mip = load_section(sec, sn).y;
+        const float inv = ldexpf(1.0f, -(2 * (int)mip + 1));
+        bool gone = true;
+#pragma unroll
+        for (int j = 0; j < J; j++) gone = gone && ray_gone(Q, X, vk[j], pos, track, sn, inv);
+        if (__all(gone)) {
+          s = X.end_s;
+          track = X.end_track;
+          return;
+        }
+      }
+    }
+  }
   for (; i < n; i++, s++)
     cone_step<J, 1>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last,
                     nf);
@@ -384,7 +439,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
   int s = 0;
   {
     const f3 vk[1] = {k};
-    cone_stage<1, 4>(Q, C, ext, sec, s, C.counts[0], track, vk, pos, rays, last, nf);
+    cone_stage<1, 4>(Q, C, ext, sec, s, C.counts[0], track, vk, pos, rays, last, nf, C.exit[0]);
   }
   if (C.counts[1] + C.counts[2] == 0) return cvr_expf(-rays[0]);
   rays[2] = rays[0]; rays[1] = rays[0];
@@ -393,7 +448,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
     f3 vk[3];
 #pragma unroll
     for (int j = 0; j < 3; j++) vk[j] = cone_axis(C.axes + 3 * j, k, u, v);
-    cone_stage<3, 2>(Q, C, ext, sec, s, C.counts[1], track, vk, pos, rays, last, nf);
+    cone_stage<3, 2>(Q, C, ext, sec, s, C.counts[1], track, vk, pos, rays, last, nf, C.exit[1]);
   }
   if (C.counts[2] == 0)
     return ((cvr_expf(-rays[0]) + cvr_expf(-rays[1])) + cvr_expf(-rays[2])) / 3.0f;
@@ -412,7 +467,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
     f3 vk[7];
 #pragma unroll
     for (int j = 0; j < 7; j++) vk[j] = cone_axis(C.axes + 3 * (3 + j), k, u, v);
-    cone_stage<7, 1>(Q, C, ext, sec, s, C.counts[2], track, vk, pos, rays, last, nf);
+    cone_stage<7, 1>(Q, C, ext, sec, s, C.counts[2], track, vk, pos, rays, last, nf, C.exit[2]);
   }
   float side = cvr_expf(-rays[1]);
 #pragma unroll
