@@ -103,6 +103,8 @@ def parse():
     p.add_argument("--tile", type=int, default=32)
     p.add_argument("--field", choices=["ml", "blobs"], default="ml")
     p.add_argument("--phong", action="store_true")
+    p.add_argument("--batch", type=int, default=0, choices=[0, 2, 4],
+                   help="rc1pass samples per lane per memory round trip (0 = auto: 4, 2 with Phong)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--format", choices=["rgba16f", "rgba32f"], default="rgba16f",
@@ -405,6 +407,8 @@ def main():
     quad = a.quad if a.quad >= 0 else (10 if world >= 8 else 0)
     if a.renderer == "rc1pass":
         N.check(N.lib().cvr_set_option(r.device.handle, b"quad", quad), "quad", r.device.handle)
+        if a.batch:
+            N.check(N.lib().cvr_set_option(r.device.handle, b"batch", a.batch), "batch", r.device.handle)
     try:
         # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
         # on rank 0) would otherwise rival a rank's share of the frame (~23 us at N = 8)

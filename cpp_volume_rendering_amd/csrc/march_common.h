@@ -148,21 +148,14 @@ __device__ __forceinline__ f3 sample_gradient_cell(const uint4* __restrict__ gce
             trilerp_cell(gz, sp.ax, sp.ay, sp.az)};
 }
 
-// Blinn-Phong (ray_marching_1p.comp:48-81), CVR-SPEC arithmetic.
-__device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint4* __restrict__ grad,
-                                            const SamplePos& sp, f3 dir, float t, f3 tpos, f3 hg,
-                                            f3 eye, float4& src) {
-#ifdef CVR_PROBE_PHONG_NOLOAD   // cost probes (tools/build_variant.sh), images wrong by design
-  f3 g{sp.ax, sp.ay, 1.0f};
-#else
-  f3 g = sample_gradient_cell(grad, sp);
-#endif
+// Blinn-Phong (ray_marching_1p.comp:48-81), CVR-SPEC arithmetic, for gradient g
+// at world position wp (the sample's tex_pos minus half the grid).
+__device__ __forceinline__ void phong_rgb(const Rc1passArgs& A, f3 g, f3 wp, f3 eye, float4& src) {
 #ifdef CVR_PROBE_PHONG_NOMATH
   src.x *= g.x; src.y *= g.y; src.z *= g.z;
   return;
 #endif
   if (g.x != 0.0f || g.y != 0.0f || g.z != 0.0f) {
-    f3 wp{fmaf(dir.x, t, tpos.x) - hg.x, fmaf(dir.y, t, tpos.y) - hg.y, fmaf(dir.z, t, tpos.z) - hg.z};
     f3 n = normalize3(g);
     f3 Ld = normalize3(f3{A.light[0] - wp.x, A.light[1] - wp.y, A.light[2] - wp.z});
     f3 Ve = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
@@ -175,6 +168,26 @@ __device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint4* _
     src.y = fmaf(A.ispec[1] * A.ks, pw, src.y * f);
     src.z = fmaf(A.ispec[2] * A.ks, pw, src.z * f);
   }
+}
+
+__device__ __forceinline__ f3 phong_wpos(f3 dir, float t, f3 tpos, f3 hg) {
+  return f3{fmaf(dir.x, t, tpos.x) - hg.x, fmaf(dir.y, t, tpos.y) - hg.y, fmaf(dir.z, t, tpos.z) - hg.z};
+}
+
+__device__ __forceinline__ f3 phong_gradient(const uint4* __restrict__ grad, const SamplePos& sp) {
+#ifdef CVR_PROBE_PHONG_NOLOAD   // cost probes (tools/build_variant.sh), images wrong by design
+  return f3{sp.ax, sp.ay, 1.0f};
+#else
+  return sample_gradient_cell(grad, sp);
+#endif
+}
+
+// The sample's gradient fetch + Blinn-Phong, in the lane that marches it.
+__device__ __forceinline__ void shade_phong(const Rc1passArgs& A, const uint4* __restrict__ grad,
+                                            const SamplePos& sp, f3 dir, float t, f3 tpos, f3 hg,
+                                            f3 eye, float4& src) {
+  const f3 g = phong_gradient(grad, sp);
+  phong_rgb(A, g, phong_wpos(dir, t, tpos, hg), eye, src);
 }
 
 // ---------------------------------------------------------------------------

@@ -116,6 +116,12 @@ CASES = {
                      tf_alpha_scale=400.0),
     "phong_sobel": dict(vol=lambda: _ml(48), scale=D.voxel_scale(48), W=128, H=128, phong=True,
                         gmode=2, light=D.LIGHT_LIST0_POSITION, shading=(0.3, 0.6, 0.5, 12.5)),
+    # Blinn-Phong with the camera inside the volume (clamped sample positions, shading
+    # jobs rebuilt from the owner's ray on another lane) and a ragged viewport
+    "phong_inside": dict(vol=lambda: _ml(64), scale=D.voxel_scale(64), W=101, H=75, phong=True,
+                         gmode=1, light=D.LIGHT_LIST0_POSITION,
+                         cam=dict(eye=(10.0, -20.0, 30.0), center=(100.0, 50.0, -200.0),
+                                  up=(0.0, 1.0, 0.0))),
 }
 
 
@@ -241,7 +247,7 @@ SCHEDULES = [
 
 @pytest.mark.parametrize("sched", range(len(SCHEDULES)))
 @pytest.mark.parametrize("name", ["ml64_ragged", "ml_aniso", "phong_fd", "camera_inside",
-                                  "blobs_sparse", "dense_tf"])
+                                  "blobs_sparse", "dense_tf", "phong_inside"])
 def test_schedules_bitexact(oracle, bonsai_tf, name, sched):
     """Every scheduling / march variant (LPT order, quad = 4-lanes-per-ray march for the
     longest tiles, batch size, empty-space skipping) reproduces the oracle bit for bit, on the
