@@ -23,6 +23,7 @@
 // served from L2).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "cvr_device.h"
@@ -148,6 +149,73 @@ __global__ void downscale_kernel(const uint2* __restrict__ src, int sw, int sh,
     for (int ic = il_c; ic <= ir_c; ic++) {
       const float wc = K::w((x_c - ((float)ic + 0.5f) / (float)sw) * (float)tw);
       f = madd(f, wr * wc, fetch_px(src, sw, sh, ic, ir));
+    }
+  }
+  const float s = s_r * s_c;
+  store_px(dst, tw, jc, jr, make_float4(f.x * s, f.y * s, f.z * s, f.w * s));
+}
+
+// downscaling_filter.comp with the block's input window staged in LDS.  A 16x16
+// block of screen pixels reads one window of the frame (its first pixel's left /
+// top tap to its last pixel's right / bottom tap: the tap range is monotone in
+// the pixel index), 0 outside the frame as texelFetch's robust access.  Each
+// pixel's column weights are computed once (the same expression as above) and
+// reused for every row; the taps are summed in the same order with the same
+// operations, so the result is bit-identical to downscale_kernel.
+constexpr int kDownMaxTaps = 12;   // taps per axis held in registers
+
+template <class K>
+__global__ void __launch_bounds__(256)
+downscale_lds_kernel(const uint2* __restrict__ src, int sw, int sh, uint2* __restrict__ dst, int tw,
+                     int th) {
+  extern __shared__ uint2 win[];
+  const float kr = 0.5f * K::support;
+  const int bx = blockIdx.x * 16, by = blockIdx.y * 16;
+  auto first_tap = [kr](int j, int t, int s) {
+    const float x = ((float)j + 0.5f) / (float)t;
+    return (int)ceilf((x - kr / (float)t) * (float)s - 0.5f);
+  };
+  auto last_tap = [kr](int j, int t, int s) {
+    const float x = ((float)j + 0.5f) / (float)t;
+    return (int)floorf((x + kr / (float)t) * (float)s - 0.5f);
+  };
+  const int r0 = first_tap(by, th, sh), r1 = last_tap(min(by + 15, th - 1), th, sh);
+  const int c0 = first_tap(bx, tw, sw), c1 = last_tap(min(bx + 15, tw - 1), tw, sw);
+  const int ww = c1 - c0 + 1, wp = ww | 1;   // odd pitch: rows fall on shifted banks
+  const int wh = r1 - r0 + 1;
+  for (int e = threadIdx.x; e < ww * wh; e += 256) {
+    const int rr = e / ww, cc = e - rr * ww;
+    const int r = r0 + rr, c = c0 + cc;
+    win[rr * wp + cc] = (r >= 0 && r < sh && c >= 0 && c < sw) ? src[(size_t)r * sw + c] : make_uint2(0u, 0u);
+  }
+  __syncthreads();
+  const int jc = bx + (threadIdx.x & 15), jr = by + (threadIdx.x >> 4);
+  if (jc >= tw || jr >= th) return;
+  const float s_r = (float)th / (float)sh;
+  const float s_c = (float)tw / (float)sw;
+  const float x_r = ((float)jr + 0.5f) / (float)th;
+  const int il_r = (int)ceilf((x_r - kr / (float)th) * (float)sh - 0.5f);
+  const int ir_r = (int)floorf((x_r + kr / (float)th) * (float)sh - 0.5f);
+  const float x_c = ((float)jc + 0.5f) / (float)tw;
+  const int il_c = (int)ceilf((x_c - kr / (float)tw) * (float)sw - 0.5f);
+  const int ir_c = (int)floorf((x_c + kr / (float)tw) * (float)sw - 0.5f);
+  const int nc = ir_c - il_c + 1;
+  float wc[kDownMaxTaps];
+#pragma unroll
+  for (int q = 0; q < kDownMaxTaps; q++)
+    wc[q] = q < nc ? K::w((x_c - ((float)(il_c + q) + 0.5f) / (float)sw) * (float)tw) : 0.0f;
+  float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int ir = il_r; ir <= ir_r; ir++) {
+    const float wr = K::w((x_r - ((float)ir + 0.5f) / (float)sh) * (float)th);
+    const uint2* row = win + (ir - r0) * wp + (il_c - c0);
+#pragma unroll
+    for (int q = 0; q < kDownMaxTaps; q++) {
+      if (q < nc) {
+        const uint2 p = row[q];
+        const float4 t = make_float4(h2f((uint16_t)(p.x & 0xffffu)), h2f((uint16_t)(p.x >> 16)),
+                                     h2f((uint16_t)(p.y & 0xffffu)), h2f((uint16_t)(p.y >> 16)));
+        f = madd(f, wr * wc[q], t);
+      }
     }
   }
   const float s = s_r * s_c;
@@ -312,49 +380,264 @@ __global__ void digital_filter_kernel(uint16_t* __restrict__ img, int w, int h, 
   }
 }
 
-// The same recursion with the lines staged in LDS.  One wave takes `lpw` lines
-// (lpw * 4 chains, one lane per (line, channel)): the lines are read into LDS
-// with coalesced 8-B pixel loads, de-interleaved into one plane of binary16 per
-// chain (chain stride S halves: a multiple of 8, padded so that the 16 lanes of a
-// ds_read_b128 group fall on distinct banks), both passes run on the planes 8
-// elements per LDS access, and the lines are written back once.  Every step
-// still rounds to binary16 and the next step reads the rounded value, as the
-// global-memory kernel above and the reference's imageLoad/imageStore do.
-template <int C> struct Head { static constexpr bool value = true; static constexpr int chunk = C; };
-struct NoHead { static constexpr bool value = false; static constexpr int chunk = 0; };
+constexpr int kDigitalUnroll = 8;   // staging loads in flight per thread
 
-// Staging: a workgroup of kDigitalThreads moves the lines in and out (memory-level
-// parallelism for the one wave that then runs the sequential recursions).
-constexpr int kDigitalThreads = 256;
-constexpr int kDigitalUnroll = 8;
+// The same recursion, parallel along the line, with the lines staged in LDS.
+//
+// Each step is y_i = round16(x_i - round32(l * y_(i-1))) (forward) or
+// y_i = round16(round32(l * round32(x_i - y_(i+1)))) (reverse), l > 0: for fixed
+// x_i a non-increasing function of the previous value (IEEE rounding is
+// monotone; with -0 ordered below +0 the signed zeros too), so the composition
+// of steps is monotone.  Hence if the previous value of a step lies in [-B, B],
+// its result lies between the results of the two extremes, and once the two
+// extreme trajectories agree bit for bit every value inside gives the same bits.
+// B is a proven bound of every value of the recursion, from the largest |x| of
+// the workgroup's lines M: |y| <= (M + l|y|)(1 + 2^-10) + 2^-25 covers the two
+// f32 roundings and the binary16 one (subnormal: 2^-25 absolute), so
+// B = ((1 + e) M + 2^-25) / (1 - l (1 + e)), e = 2^-9 (slack for the f32
+// evaluation of B itself), rounded up to binary16; the reverse pass takes
+// Br = (l (1 + e) B + 2^-25) / (1 - l (1 + e)).
+//
+// A line is cut into segments of kSeg elements, one lane each.  The lane runs
+// the two extreme trajectories over the W elements before its segment (the
+// warm-up reads only inputs); if they agree the result is the exact value
+// entering the segment, and the lane computes its segment from it.  The
+// recursion contracts by l ~ 0.27 (B-spline) / 0.34 (o-MOMS) per step, so W = 24 /
+// 32 steps bring the extremes together almost always; where they do not (a
+// region whose rounded recursion has a 2-cycle carries its phase from
+// arbitrarily far back) the segment is left unwritten and redone after the
+// parallel phase by one lane per chain, in order, from the exact value its
+// predecessor ends with.  Every stored value is the one the sequential recursion
+// stores.  Lines with a non-finite value, or whose bound leaves binary16, run
+// sequentially (all segments redone).
+constexpr int kSeg = 32;           // elements per segment
+constexpr int kSegChunks = kSeg / 8;
+constexpr int kSegPitch = 40;      // halves per segment in LDS (+16 B: 16 lanes' 16-B reads hit distinct banks)
+constexpr int kSegMaxThreads = 512;
+constexpr size_t kSegLdsMax = 64 * 1024;
+#ifdef CVR_DIGITAL_PROBE   // cost probes only (tools/build_variant.sh), wrong images:
+constexpr int kDigitalProbe = CVR_DIGITAL_PROBE;   // 1 staging only, 2 no redo of segments
+#else
+constexpr int kDigitalProbe = 0;
+#endif
+
+template <class LU> struct SegWarm;
+template <> struct SegWarm<LCbs> { static constexpr int W = 24; };
+template <> struct SegWarm<LOmoms> { static constexpr int W = 32; };
+
+// v_cvt_f16_f32 without masking the upper half (only the low half is read back)
+__device__ __forceinline__ uint32_t h16_raw(float f) {
+  uint32_t r;
+  asm("v_cvt_f16_f32 %0, %1" : "=v"(r) : "v"(f));
+  return r;
+}
+
+// forward coefficient of element i >= 1 (the LU table below m), reverse of i >= 0
+template <class LU>
+__device__ __forceinline__ float fwd_coef(int i) {
+  float c = LU::L(LU::m - 1);
+#pragma unroll
+  for (int j = 1; j < LU::m; j++) c = i == j ? LU::L(j - 1) : c;
+  return c;
+}
+template <class LU>
+__device__ __forceinline__ float rev_coef(int i) {
+  float c = LU::L(LU::m - 1);
+#pragma unroll
+  for (int j = 0; j < LU::m - 1; j++) c = i == j ? LU::L(j) : c;
+  return c;
+}
+
+// 8 forward steps on one 16-B chunk, elements i0 .. i0+7 (element 0 of the line is
+// kept as it is).  CHECK: stop at nn.
+template <class LU, bool CHECK>
+__device__ __forceinline__ uint4 fwd8(uint4 v, uint32_t& prev, int i0, int nn) {
+  float lk[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) lk[k] = LU::L(LU::m - 1);
+  if (i0 < 16) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) lk[k] = fwd_coef<LU>(i0 + k);
+  }
+  uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (CHECK && i0 + k >= nn) break;
+    const uint32_t x = wd[k >> 1];
+    const float p = mul_h16(lk[k], prev);
+    uint32_t o = h16_raw((k & 1) ? half_minus<true>(x, p) : half_minus<false>(x, p));
+    if (k == 0) o = i0 == 0 ? x : o;
+    wd[k >> 1] = (k & 1) ? ((x & 0xffffu) | (o << 16)) : ((x & 0xffff0000u) | (o & 0xffffu));
+    prev = (k & 1) ? (o & 0xffffu) : o;   // the next step reads the low half only
+  }
+  return make_uint4(wd[0], wd[1], wd[2], wd[3]);
+}
+
+// 8 reverse steps, elements i0+7 .. i0 (past nn-2 left alone when CHECK)
+template <class LU, bool CHECK>
+__device__ __forceinline__ uint4 rev8(uint4 v, uint32_t& prev, int i0, int nn) {
+  float lk[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) lk[k] = LU::L(LU::m - 1);
+  if (i0 < 16) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) lk[k] = rev_coef<LU>(i0 + k);
+  }
+  uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 7; k >= 0; k--) {
+    if (CHECK && i0 + k > nn - 2) continue;
+    const uint32_t x = wd[k >> 1];
+    // p_inv * f[i] = f[i] exactly (p_inv = 1)
+    const uint32_t o = h16_raw(lk[k] * ((k & 1) ? half_minus_h16<true>(x, prev) : half_minus_h16<false>(x, prev)));
+    wd[k >> 1] = (k & 1) ? ((x & 0xffffu) | (o << 16)) : ((x & 0xffff0000u) | (o & 0xffffu));
+    prev = o;
+  }
+  return make_uint4(wd[0], wd[1], wd[2], wd[3]);
+}
+
+// chunk ch (elements 8ch .. 8ch+7) of a chain in the segment-padded layout
+__device__ __forceinline__ uint4* seg_chunk(uint4* cb, int ch) {
+  return cb + (ch / kSegChunks) * (kSegPitch / 8) + (ch % kSegChunks);
+}
+__device__ __forceinline__ uint32_t seg_half(const uint16_t* c, int i) {
+  return c[(i / kSeg) * kSegPitch + (i % kSeg)];
+}
+
+// Forward pass over segment k of a chain from the value entering it.  TWO: also
+// from a second candidate value, in lockstep (independent chains: the same
+// latency), its results into `spare` (the segment's chunks).
+template <class LU, bool TWO = false>
+__device__ __forceinline__ void fwd_segment(uint4* cb, int k, uint32_t prev, int nn,
+                                            uint32_t prev2 = 0u, uint4* spare = nullptr) {
+  const int i_beg = k * kSeg, n = min(kSeg, nn - i_beg);
+  const int nfull = n >> 3, nch = (n + 7) >> 3;
+  uint4* base = cb + k * (kSegPitch / 8);
+  uint4 v[kSegChunks], v2[kSegChunks];
+#pragma unroll
+  for (int q = 0; q < kSegChunks; q++) v[q] = v2[q] = base[q];   // inside the padded plane
+#pragma unroll
+  for (int q = 0; q < kSegChunks; q++) {
+    if (q < nfull) {
+      v[q] = fwd8<LU, false>(v[q], prev, i_beg + 8 * q, nn);
+      if (TWO) v2[q] = fwd8<LU, false>(v2[q], prev2, i_beg + 8 * q, nn);
+    } else if (q < nch) {
+      v[q] = fwd8<LU, true>(v[q], prev, i_beg + 8 * q, nn);
+      if (TWO) v2[q] = fwd8<LU, true>(v2[q], prev2, i_beg + 8 * q, nn);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kSegChunks; q++)
+    if (q < nch) {
+      base[q] = v[q];
+      if (TWO && spare) spare[q] = v2[q];
+    }
+}
+
+// Reverse pass over segment k (elements min(top, nn-2) .. k*kSeg) from the value
+// above it (TWO: as fwd_segment).
+template <class LU, bool TWO = false>
+__device__ __forceinline__ void rev_segment(uint4* cb, int k, uint32_t prev, int nn,
+                                            uint32_t prev2 = 0u, uint4* spare = nullptr) {
+  const int i_beg = k * kSeg;
+  const int top = min(i_beg + kSeg - 1, nn - 2);
+  if (top < i_beg) return;
+  const int qtop = (top - i_beg) >> 3;                 // chunk of the top element
+  const bool partial = ((qtop << 3) + 7) > top - i_beg;
+  uint4* base = cb + k * (kSegPitch / 8);
+  uint4 v[kSegChunks], v2[kSegChunks];
+#pragma unroll
+  for (int q = 0; q < kSegChunks; q++) v[q] = v2[q] = base[q];
+#pragma unroll
+  for (int q = kSegChunks - 1; q >= 0; q--) {
+    if (q < qtop || (q == qtop && !partial)) {
+      v[q] = rev8<LU, false>(v[q], prev, i_beg + 8 * q, nn);
+      if (TWO) v2[q] = rev8<LU, false>(v2[q], prev2, i_beg + 8 * q, nn);
+    } else if (q == qtop) {
+      v[q] = rev8<LU, true>(v[q], prev, i_beg + 8 * q, nn);
+      if (TWO) v2[q] = rev8<LU, true>(v2[q], prev2, i_beg + 8 * q, nn);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kSegChunks; q++)
+    if (q <= qtop) {
+      base[q] = v[q];
+      if (TWO && spare) spare[q] = v2[q];
+    }
+}
+
+// The order of binary16 values with -0 below +0, as an integer key.
+__device__ __forceinline__ int h16_key(uint32_t h) {
+  h &= 0xffffu;
+  return (h & 0x8000u) ? (int)(0x7fffu - (h & 0x7fffu)) : (int)(h + 0x8000u);
+}
+
+// Item states.  The value entering a segment is final / the two warm-up values
+// are adjacent binary16 values (the entering value is one of them: both
+// candidate results are computed, the first in place, the second in a spare
+// slot) / unknown (recomputed once its predecessor is final).
+constexpr uint8_t kSegFinal = 1, kSegTwo = 3, kSegRedo = 0, kSegTake2 = 4;
+// second-candidate segments per workgroup and pass: a quarter of the segments
+// (the 1024^2 frames of the bench downscaled with the B-spline kernel, values up
+// to ~36, settle into 2-cycles in ~12 % of the row segments), at most 255
+__host__ __device__ constexpr int spare_slots(int items) {
+  return items / 4 < 16 ? 16 : (items / 4 > 255 ? 255 : items / 4);
+}
+
+// binary16 bits of a value >= b (b >= 0 finite): round to nearest, then up
+__device__ __forceinline__ uint32_t h16_ceil(float b) {
+  uint32_t h = f2h(b);
+  if (h2f((uint16_t)h) < b) h++;
+  return h;
+}
 
 template <class LU>
-__global__ void __launch_bounds__(kDigitalThreads)
-digital_filter_lds_kernel(uint16_t* __restrict__ img, int w, int h, int dir, int lpw_shift, int S) {
+__global__ void __launch_bounds__(kSegMaxThreads)
+digital_filter_seg_kernel(uint16_t* __restrict__ img, int w, int h, int dir, int lpw_shift, int nseg) {
   extern __shared__ uint4 lds_raw[];
+  constexpr int W = SegWarm<LU>::W;
+  const int S = nseg * kSegPitch;   // chain stride (halves)
   uint16_t* plane = reinterpret_cast<uint16_t*>(lds_raw);
   const int lpw = 1 << lpw_shift;
   const int lines = dir == 0 ? h : w, nn = dir == 0 ? w : h;
   const int l0 = blockIdx.x * lpw;
   const int nl = min(lpw, lines - l0);
+  const int nchain = nl * 4, items = nchain * nseg;
+  const int ni = lpw * 4 * nseg;   // item capacity
+  const int nspare = spare_slots(ni);
+  uint4* spare = lds_raw + (size_t)(lpw * 4) * S / 8;   // nspare x kSeg halves
+  uint16_t* start_f = reinterpret_cast<uint16_t*>(spare + nspare * kSegChunks);
+  uint16_t* start_r = start_f + ni;      // per item: value entering the segment (candidate 1)
+  uint16_t* start2_f = start_r + ni;     // candidate 2
+  uint16_t* start2_r = start2_f + ni;
+  uint8_t* ok_f = reinterpret_cast<uint8_t*>(start2_r + ni);
+  uint8_t* ok_r = ok_f + ni;
+  uint8_t* slot_f = ok_r + ni;
+  uint8_t* slot_r = slot_f + ni;
+  const int nwords = (nseg + 63) >> 6;   // per chain: bit mask of unresolved segments
+  unsigned long long* unres_f = reinterpret_cast<unsigned long long*>(
+      (reinterpret_cast<uintptr_t>(slot_r + ni) + 7) & ~(uintptr_t)7);
+  unsigned long long* unres_r = unres_f + lpw * 4 * nwords;
+  for (int i = threadIdx.x; i < 2 * lpw * 4 * nwords; i += blockDim.x) unres_f[i] = 0ull;
+  __shared__ uint32_t max_bits;
+  __shared__ int nfail_f, nfail_r, spare_f, spare_r;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  if (tid == 0) { max_bits = 0u; nfail_f = 0; nfail_r = 0; spare_f = 0; spare_r = 0; }
+  __syncthreads();
   uint2* px = reinterpret_cast<uint2*>(img);
   auto put = [&](int l, int i, uint2 v) {
-    uint16_t* q = plane + (size_t)(l * 4) * S + i;
+    uint16_t* q = plane + (size_t)(l * 4) * S + (i / kSeg) * kSegPitch + (i % kSeg);
     q[0] = (uint16_t)(v.x & 0xffffu);
     q[S] = (uint16_t)(v.x >> 16);
     q[2 * S] = (uint16_t)(v.y & 0xffffu);
     q[3 * S] = (uint16_t)(v.y >> 16);
   };
   auto get = [&](int l, int i) {
-    const uint16_t* q = plane + (size_t)(l * 4) * S + i;
+    const uint16_t* q = plane + (size_t)(l * 4) * S + (i / kSeg) * kSegPitch + (i % kSeg);
     return make_uint2((uint32_t)q[0] | ((uint32_t)q[S] << 16),
                       (uint32_t)q[2 * S] | ((uint32_t)q[3 * S] << 16));
   };
-  // ---- stage in: all kDigitalThreads lanes, kDigitalUnroll loads in flight each ----
-  // element e of the wave's nl lines: dir 0 -> (line e / nn, i = e % nn), rows are
-  // contiguous in memory; dir 1 -> (line e % lpw, i = e >> lpw_shift), one image
-  // row of lpw adjacent pixels per lpw elements
-  const int tid = threadIdx.x;
+  // ---- stage in (coalesced 8-B pixels), with the largest |x| (binary16 bits) ----
   const int total = dir == 0 ? nl * nn : (nn << lpw_shift);
   auto src_of = [&](int e, int& l, int& i) -> size_t {
     if (dir == 0) {
@@ -366,140 +649,248 @@ digital_filter_lds_kernel(uint16_t* __restrict__ img, int w, int h, int dir, int
     l = e & (lpw - 1);
     return (size_t)i * w + l0 + l;
   };
-  for (int e0 = 0; e0 < total; e0 += kDigitalThreads * kDigitalUnroll) {
+  uint32_t mb = 0u;
+  for (int e0 = 0; e0 < total; e0 += nthr * kDigitalUnroll) {
     uint2 v[kDigitalUnroll];
 #pragma unroll
     for (int u = 0; u < kDigitalUnroll; u++) {
-      const int e = e0 + u * kDigitalThreads + tid;
+      const int e = e0 + u * nthr + tid;
       int l, i;
       const size_t a = src_of(e, l, i);
       if (e < total && l < nl) v[u] = px[a];
     }
 #pragma unroll
     for (int u = 0; u < kDigitalUnroll; u++) {
-      const int e = e0 + u * kDigitalThreads + tid;
+      const int e = e0 + u * nthr + tid;
       int l, i;
       src_of(e, l, i);
-      if (e < total && l < nl) put(l, i, v[u]);
+      if (e < total && l < nl) {
+        put(l, i, v[u]);
+        mb = max(mb, max(max(v[u].x & 0x7fffu, (v[u].x >> 16) & 0x7fffu),
+                         max(v[u].y & 0x7fffu, (v[u].y >> 16) & 0x7fffu)));
+      }
+    }
+  }
+  if (mb) atomicMax(&max_bits, mb);
+  __syncthreads();
+  if (kDigitalProbe != 1) {   // (cost probe 1: staging only)
+  // ---- the bounds (every thread the same) ----
+  const float L_inf = LU::L(LU::m - 1);
+  const float lq = L_inf * (1.0f + 0x1p-9f);
+  bool spec = max_bits < 0x7c00u && nseg > 1;   // finite inputs
+  uint32_t bf = 0u, br = 0u;
+  if (spec) {
+    bf = h16_ceil(((1.0f + 0x1p-9f) * h2f((uint16_t)max_bits) + 0x1p-25f) / (1.0f - lq));
+    br = h16_ceil((lq * h2f((uint16_t)bf) + 0x1p-25f) / (1.0f - lq));
+    spec = bf < 0x7c00u && br < 0x7c00u;
+  }
+  // ---- forward: warm-ups (read only), then the segments ----
+  for (int it = tid; it < items; it += nthr) {
+    const int c = it / nseg, k = it - c * nseg;
+    if (k == 0) {   // starts from the line's first element: final
+      ok_f[it] = 1;
+      continue;
+    }
+    uint32_t lo = bf | 0x8000u, hi = bf;
+    bool ok = false;
+    if (spec) {
+      uint4* cb = reinterpret_cast<uint4*>(plane + (size_t)c * S);
+      const int a = max(0, k * kSeg - W);   // from element 0 the warm-up is exact
+      const int ch0 = a >> 3, nq = (k * kSeg - a) >> 3;
+#pragma unroll
+      for (int q = 0; q < W / 8; q++) {
+        if (q < nq) {
+          const uint4 v = *seg_chunk(cb, ch0 + q);
+          fwd8<LU, false>(v, lo, (ch0 + q) * 8, nn);
+          fwd8<LU, false>(v, hi, (ch0 + q) * 8, nn);
+        }
+      }
+      ok = (lo & 0xffffu) == (hi & 0xffffu);
+    }
+    uint8_t st = ok ? kSegFinal : kSegRedo;
+    if (!ok && spec && abs(h16_key(lo) - h16_key(hi)) == 1) {
+      const int sl = atomicAdd(&spare_f, 1);
+      if (sl < nspare) {
+        st = kSegTwo;
+        slot_f[it] = (uint8_t)sl;
+      }
+    }
+    start_f[it] = (uint16_t)lo;
+    start2_f[it] = (uint16_t)hi;
+    ok_f[it] = st;
+    if (!ok) {
+      atomicAdd(&nfail_f, 1);
+      atomicOr(&unres_f[c * nwords + (k >> 6)], 1ull << (k & 63));
     }
   }
   __syncthreads();
-  // ---- both passes on this lane's chain ----
-  const int q = tid;   // the first wave runs the recursions (one lane per chain)
-#ifdef CVR_DIGITAL_NO_COMPUTE   // cost probe only (tools/build_variant.sh): wrong images
-  if (false) {
-#else
-  if (q < 64 && (q >> 2) < nl) {
-#endif
-    uint16_t* c = plane + (size_t)q * S;
-    uint4* c4 = reinterpret_cast<uint4*>(c);
-    const int m = LU::m;
-    const float p_inv = 1.0f;
-    const float L_inf = LU::L(m - 1), v_inv = L_inf / (1.f + L_inf);
-    // forward pass: f[i] -= L * f[i-1], i = 1 .. nn-1; reverse pass: f[i] = L * (p_inv
-    // * f[i] - f[i+1]), i = nn-2 .. 0.  8 elements per LDS access.  The first two
-    // chunks (the steps whose coefficient comes from the table: i < m) are peeled
-    // with compile-time coefficients, whole chunks run without bounds checks, and
-    // the chunk holding element nn-1 checks bounds per element.
-    // prev is kept as the stored binary16 bits: the next step reads it straight
-    // from the half (v_fma_mix), one dependent conversion less per step
-    uint32_t prev = 0u;
-    const int nfull = nn >> 3;          // chunks entirely inside [0, nn)
-    auto fwd = [&](uint4 v, int ch, auto head, bool check) {
-      uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int i = (ch << 3) + k;
-        float l = L_inf;
-        if (decltype(head)::value) {
-          const int ic = (decltype(head)::chunk << 3) + k;   // == i at compile time
-          if (ic == 0) { prev = wd[0] & 0xffffu; continue; }
-          l = ic < m ? LU::L(ic - 1) : L_inf;
-        }
-        if (check && i >= nn) break;
-        const uint32_t x = wd[k >> 1];
-        const float p = mul_h16(l, prev);
-        const uint32_t o = f2h((k & 1) ? half_minus<true>(x, p) : half_minus<false>(x, p));
-        wd[k >> 1] = (k & 1) ? ((x & 0xffffu) | (o << 16)) : ((x & 0xffff0000u) | o);
-        prev = o;
-      }
-      c4[ch] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-    };
-    auto rev = [&](uint4 v, int ch, auto head, bool check) {
-      uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 7; k >= 0; k--) {
-        const int i = (ch << 3) + k;
-        float l = L_inf;
-        if (decltype(head)::value) {
-          const int ic = (decltype(head)::chunk << 3) + k;
-          l = ic >= m - 1 ? L_inf : LU::L(ic);
-        }
-        if (check && i > nn - 2) continue;
-        const uint32_t x = wd[k >> 1];
-        // p_inv * f[i] = f[i] exactly (p_inv = 1)
-        const uint32_t o = f2h(l * ((k & 1) ? half_minus_h16<true>(x, prev)
-                                            : half_minus_h16<false>(x, prev)));
-        wd[k >> 1] = (k & 1) ? ((x & 0xffffu) | (o << 16)) : ((x & 0xffff0000u) | o);
-        prev = o;
-      }
-      c4[ch] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-    };
-    const int nch = (nn + 7) >> 3;
-    uint4 nxt = c4[0];
-    {
-      const uint4 v = nxt;
-      if (nch > 1) nxt = c4[1];
-      fwd(v, 0, Head<0>{}, nfull < 1);
-    }
-    if (nch > 1) {
-      const uint4 v = nxt;
-      if (nch > 2) nxt = c4[2];
-      fwd(v, 1, Head<1>{}, nfull < 2);
-    }
-    for (int ch = 2; ch < nfull; ch++) {   // the next chunk's read goes out first
-      const uint4 v = nxt;
-      if (ch + 1 < nch) nxt = c4[ch + 1];
-      fwd(v, ch, NoHead{}, false);
-    }
-    if (nch > 2 && nfull < nch) fwd(nxt, nch - 1, NoHead{}, true);
-    // f[nn-1] *= p_inv * v_inv  (prev holds the stored f[nn-1])
-    {
-      const uint32_t o = f2h(h2f((uint16_t)prev) * (p_inv * v_inv));
-      c[nn - 1] = (uint16_t)o;
-      prev = o;
-    }
-    if (nn >= 2) {
-      const int top = (nn - 2) >> 3;            // chunk of element nn-2
-      const bool top_partial = ((top << 3) + 7) > nn - 2;
-      int ch = top;
-      nxt = c4[ch];
-      if (ch >= 2 && top_partial) {
-        const uint4 v = nxt;
-        nxt = c4[ch - 1];
-        rev(v, ch, NoHead{}, true);
-        ch--;
-      }
-      for (; ch >= 2; ch--) {
-        const uint4 v = nxt;
-        nxt = c4[ch - 1];
-        rev(v, ch, NoHead{}, false);
-      }
-      if (ch == 1) {
-        const uint4 v = nxt;
-        nxt = c4[0];
-        rev(v, 1, Head<1>{}, top == 1 && top_partial);
-        ch--;
-      }
-      if (ch == 0) rev(nxt, 0, Head<0>{}, top == 0 && top_partial);
+  for (int it = tid; it < items; it += nthr) {
+    const int c = it / nseg, k = it - c * nseg;
+    // every item runs both trajectories (a final one twice from the same value):
+    // one code path for the wave, the second chain costs no latency
+    uint4* cb = reinterpret_cast<uint4*>(plane + (size_t)c * S);
+    const uint8_t st = k == 0 ? kSegFinal : ok_f[it];
+    if (st != kSegRedo) {
+      const uint32_t s1 = k ? start_f[it] : 0u;
+      const bool two = st == kSegTwo;
+      fwd_segment<LU, true>(cb, k, s1, nn, two ? start2_f[it] : s1,
+                            two ? spare + slot_f[it] * kSegChunks : nullptr);
     }
   }
   __syncthreads();
+  // resolve the segments whose warm-up did not settle, in order along each chain
+  // (one lane per chain, over the chain's bit mask of such segments).  The value
+  // entering one is then final: a two-candidate segment keeps the first candidate
+  // or takes the second (its end value goes on to the next; the copies are made
+  // afterwards, in parallel), any other is recomputed from it.
+  if (nfail_f && kDigitalProbe != 2) {
+    for (int c = tid; c < nchain; c += nthr) {
+      uint16_t* ch = plane + (size_t)c * S;
+      int kp = -2;          // the last segment resolved, and the value it ends with
+      uint32_t ep = 0u;
+      for (int wd = 0; wd < nwords; wd++) {
+        unsigned long long m = unres_f[c * nwords + wd];
+        while (m) {
+          const int k = wd * 64 + __builtin_ctzll(m);
+          m &= m - 1ull;
+          const int it = c * nseg + k;
+          const uint32_t t = kp == k - 1 ? ep : seg_half(ch, k * kSeg - 1);   // entering value
+          const int last = min(nn, (k + 1) * kSeg) - 1;
+          if (ok_f[it] == kSegRedo) {
+            fwd_segment<LU>(reinterpret_cast<uint4*>(ch), k, t, nn);
+            ep = seg_half(ch, last);
+          } else if (t == start2_f[it]) {
+            ok_f[it] = kSegTake2;
+            ep = reinterpret_cast<const uint16_t*>(spare + slot_f[it] * kSegChunks)[last - k * kSeg];
+          } else {
+            ep = seg_half(ch, last);
+          }
+          kp = k;
+        }
+      }
+    }
+    __syncthreads();
+    for (int it = tid; it < items; it += nthr) {
+      if (ok_f[it] != kSegTake2) continue;
+      const int c = it / nseg, k = it - c * nseg;
+      uint4* base = reinterpret_cast<uint4*>(plane + (size_t)c * S) + k * (kSegPitch / 8);
+      const uint4* sp = spare + slot_f[it] * kSegChunks;
+      const int nch = (min(kSeg, nn - k * kSeg) + 7) >> 3;
+#pragma unroll
+      for (int q = 0; q < kSegChunks; q++)
+        if (q < nch) base[q] = sp[q];
+    }
+    __syncthreads();
+  }
+  // f[nn-1] *= p_inv * v_inv
+  const float v_inv = L_inf / (1.f + L_inf);
+  for (int c = tid; c < nchain; c += nthr) {
+    uint16_t* ch = plane + (size_t)c * S;
+    uint16_t* last = ch + ((nn - 1) / kSeg) * kSegPitch + ((nn - 1) % kSeg);
+    *last = (uint16_t)f2h(h2f(*last) * (1.0f * v_inv));
+  }
+  __syncthreads();
+  // ---- reverse: warm-ups, then the segments ----
+  for (int it = tid; it < items; it += nthr) {
+    const int c = it / nseg, k = it - c * nseg;
+    if (k == nseg - 1) {   // starts from the exact f[nn-1]
+      ok_r[it] = 1;
+      continue;
+    }
+    uint4* cb = reinterpret_cast<uint4*>(plane + (size_t)c * S);
+    const int b0 = (k + 1) * kSeg;          // first element above the segment
+    uint32_t lo = br | 0x8000u, hi = br;
+    bool ok = false;
+    if (b0 + W - 1 >= nn - 2) {
+      // the warm-up would reach the line's end: start from the exact f[nn-1]
+      lo = seg_half(reinterpret_cast<const uint16_t*>(cb), nn - 1);
+      for (int ch = (nn - 2) >> 3; ch >= (b0 >> 3); ch--)
+        rev8<LU, true>(*seg_chunk(cb, ch), lo, ch * 8, nn);
+      ok = true;
+    } else if (spec) {
+#pragma unroll
+      for (int q = W / 8 - 1; q >= 0; q--) {
+        const uint4 v = *seg_chunk(cb, (b0 >> 3) + q);
+        rev8<LU, false>(v, lo, b0 + 8 * q, nn);
+        rev8<LU, false>(v, hi, b0 + 8 * q, nn);
+      }
+      ok = (lo & 0xffffu) == (hi & 0xffffu);
+    }
+    uint8_t st = ok ? kSegFinal : kSegRedo;
+    if (!ok && spec && abs(h16_key(lo) - h16_key(hi)) == 1) {
+      const int sl = atomicAdd(&spare_r, 1);
+      if (sl < nspare) {
+        st = kSegTwo;
+        slot_r[it] = (uint8_t)sl;
+      }
+    }
+    start_r[it] = (uint16_t)lo;
+    start2_r[it] = (uint16_t)hi;
+    ok_r[it] = st;
+    if (!ok) {
+      atomicAdd(&nfail_r, 1);
+      atomicOr(&unres_r[c * nwords + (k >> 6)], 1ull << (k & 63));
+    }
+  }
+  __syncthreads();
+  for (int it = tid; it < items; it += nthr) {
+    const int c = it / nseg, k = it - c * nseg;
+    uint16_t* ch = plane + (size_t)c * S;
+    uint4* cb = reinterpret_cast<uint4*>(ch);
+    const uint8_t st = k == nseg - 1 ? kSegFinal : ok_r[it];
+    if (st != kSegRedo) {
+      const uint32_t s1 = k == nseg - 1 ? seg_half(ch, nn - 1) : start_r[it];
+      const bool two = st == kSegTwo;
+      rev_segment<LU, true>(cb, k, s1, nn, two ? start2_r[it] : s1,
+                            two ? spare + slot_r[it] * kSegChunks : nullptr);
+    }
+  }
+  __syncthreads();
+  if (nfail_r && kDigitalProbe != 2) {
+    for (int c = tid; c < nchain; c += nthr) {
+      uint16_t* ch = plane + (size_t)c * S;
+      int kp = -2;
+      uint32_t ep = 0u;
+      for (int wd = nwords - 1; wd >= 0; wd--) {
+        unsigned long long m = unres_r[c * nwords + wd];
+        while (m) {
+          const int bit = 63 - __builtin_clzll(m);
+          m &= ~(1ull << bit);
+          const int k = wd * 64 + bit;
+          const int it = c * nseg + k;
+          const uint32_t t = kp == k + 1 ? ep : seg_half(ch, (k + 1) * kSeg);
+          if (ok_r[it] == kSegRedo) {
+            rev_segment<LU>(reinterpret_cast<uint4*>(ch), k, t, nn);
+            ep = seg_half(ch, k * kSeg);
+          } else if (t == start2_r[it]) {
+            ok_r[it] = kSegTake2;
+            ep = reinterpret_cast<const uint16_t*>(spare + slot_r[it] * kSegChunks)[0];
+          } else {
+            ep = seg_half(ch, k * kSeg);
+          }
+          kp = k;
+        }
+      }
+    }
+    __syncthreads();
+    for (int it = tid; it < items; it += nthr) {
+      if (ok_r[it] != kSegTake2) continue;
+      const int c = it / nseg, k = it - c * nseg;
+      uint4* base = reinterpret_cast<uint4*>(plane + (size_t)c * S) + k * (kSegPitch / 8);
+      const uint4* sp = spare + slot_r[it] * kSegChunks;
+      const int qtop = (min(k * kSeg + kSeg - 1, nn - 2) - k * kSeg) >> 3;
+#pragma unroll
+      for (int q = 0; q < kSegChunks; q++)
+        if (q <= qtop) base[q] = sp[q];
+    }
+    __syncthreads();
+  }
+  }
   // ---- stage out ----
-  for (int e0 = 0; e0 < total; e0 += kDigitalThreads * kDigitalUnroll) {
+  for (int e0 = 0; e0 < total; e0 += nthr * kDigitalUnroll) {
 #pragma unroll
     for (int u = 0; u < kDigitalUnroll; u++) {
-      const int e = e0 + u * kDigitalThreads + tid;
+      const int e = e0 + u * nthr + tid;
       int l, i;
       const size_t a = src_of(e, l, i);
       if (e < total && l < nl) px[a] = get(l, i);
@@ -536,39 +927,60 @@ __global__ void screenshot_kernel(const void* __restrict__ src, int w, int h,
     default: return hipErrorInvalidValue;                                           \
   }
 
-// LDS bytes of one wave of digital_filter_lds_kernel: lpw * 4 chains of S halves.
-constexpr size_t kDigitalLdsMax = 160 * 1024;
+#define CVR_KERNEL_SWITCH_LDS(KFN, kernel, g, b, lds, s, ...)                          \
+  switch (kernel) {                                                                  \
+    case 0: hipLaunchKernelGGL(KFN<KBox>, g, b, lds, s, __VA_ARGS__); break;         \
+    case 1: hipLaunchKernelGGL(KFN<KHat>, g, b, lds, s, __VA_ARGS__); break;         \
+    case 2: hipLaunchKernelGGL(KFN<KCatmullRom>, g, b, lds, s, __VA_ARGS__); break;  \
+    case 3: hipLaunchKernelGGL(KFN<KMitchell>, g, b, lds, s, __VA_ARGS__); break;    \
+    case 4: hipLaunchKernelGGL(KFN<KCardinalBSpline3>, g, b, lds, s, __VA_ARGS__); break; \
+    case 5: hipLaunchKernelGGL(KFN<KCardinalOmoms3>, g, b, lds, s, __VA_ARGS__); break;   \
+    default: return hipErrorInvalidValue;                                            \
+  }
+
+// LDS bytes of digital_filter_seg_kernel for 2^shift lines of nn elements.
+static size_t seg_lds_bytes(int shift, int nseg) {
+  const size_t chains = (size_t)4 << shift;
+  return chains * nseg * kSegPitch * 2 + (size_t)spare_slots((int)(chains * nseg)) * kSeg * 2 + chains * nseg * 12 + 8 +
+         chains * ((nseg + 63) / 64) * 16;
+}
 
 hipError_t launch_digital(int kernel, uint2* img, int w, int h, hipStream_t s) {
   for (int dir = 0; dir < 2; dir++) {
     const int lines = dir == 0 ? h : w, nn = dir == 0 ? w : h;
-    const int S = ((nn + 7) / 8) * 8 + 8;   // chain stride (halves): 16-B chunks + 4-bank pad
-    int shift = 4;                          // 16 lines (64 chains) per wave, fewer for long lines
-    while (shift > 0 && ((size_t)4 << shift) * S * 2 > kDigitalLdsMax) shift--;
-    const size_t lds = ((size_t)4 << shift) * S * 2;
-    if (lds <= kDigitalLdsMax && lines > 0 && nn > 0) {
+    if (lines <= 0 || nn <= 0) continue;
+    const int nseg = (nn + kSeg - 1) / kSeg;
+    // lines per workgroup: enough workgroups for every CU (>= 256), at most 16 lines
+    int shift = 0;
+    while (shift < 4 && (lines >> (shift + 1)) >= 256) shift++;
+    while (shift > 0 && seg_lds_bytes(shift, nseg) > kSegLdsMax) shift--;
+    const size_t lds = seg_lds_bytes(shift, nseg);
+    const int items = (4 << shift) * nseg;
+    if (lds <= kSegLdsMax && items <= 8 * kSegMaxThreads) {
       static bool attr = false;   // dynamic LDS beyond 64 KiB must be allowed per kernel
       if (!attr) {
         hipError_t e = hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&digital_filter_lds_kernel<LCbs>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDigitalLdsMax);
+            reinterpret_cast<const void*>(&digital_filter_seg_kernel<LCbs>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLdsMax);
         if (e == hipSuccess)
-          e = hipFuncSetAttribute(reinterpret_cast<const void*>(&digital_filter_lds_kernel<LOmoms>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDigitalLdsMax);
+          e = hipFuncSetAttribute(reinterpret_cast<const void*>(&digital_filter_seg_kernel<LOmoms>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLdsMax);
         if (e != hipSuccess) return e;
         attr = true;
       }
-      const dim3 g((lines + (1 << shift) - 1) >> shift), b(kDigitalThreads);
+      const int thr = std::min(kSegMaxThreads, (items + 63) / 64 * 64);
+      const dim3 g((lines + (1 << shift) - 1) >> shift), b(thr);
       uint16_t* p = (uint16_t*)img;
       if (kernel == 4)
-        hipLaunchKernelGGL(digital_filter_lds_kernel<LCbs>, g, b, lds, s, p, w, h, dir, shift, S);
+        hipLaunchKernelGGL(digital_filter_seg_kernel<LCbs>, g, b, lds, s, p, w, h, dir, shift, nseg);
       else
-        hipLaunchKernelGGL(digital_filter_lds_kernel<LOmoms>, g, b, lds, s, p, w, h, dir, shift, S);
+        hipLaunchKernelGGL(digital_filter_seg_kernel<LOmoms>, g, b, lds, s, p, w, h, dir, shift, nseg);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       continue;
     }
-    const int lanes = 4 * (dir == 0 ? h : w);
+    // lines too long for LDS: one lane per chain in global memory
+    const int lanes = 4 * lines;
     const dim3 g((lanes + 63) / 64), b(64);
     uint16_t* p = (uint16_t*)img;
     if (kernel == 4) hipLaunchKernelGGL(digital_filter_kernel<LCbs>, g, b, 0, s, p, w, h, dir);
@@ -592,7 +1004,18 @@ hipError_t launch_multiscale(int mode, int kernel, void* frame, int fw, int fh, 
   }
   const bool cardinal = kernel == 4 || kernel == 5;
   if (mode == 2) {
-    CVR_KERNEL_SWITCH(downscale_kernel, kernel, g, b, s, src, fw, fh, dst, sw, sh);
+    // taps per axis <= support * frame / screen + 2; the window of a 16x16 block
+    // <= (16 + support) * frame / screen + 3 a side
+    static const float support[6] = {1.0f, 2.0f, 4.0f, 4.0f, 4.0f, 4.0f};
+    const float fr = std::max((float)fw / (float)sw, (float)fh / (float)sh);
+    const float sup = support[kernel];
+    const size_t side = (size_t)((16.0f + sup) * fr) + 4;
+    const size_t lds = (side | 1) * side * sizeof(uint2);
+    if (sup * fr + 2.0f <= (float)kDownMaxTaps && lds <= 64 * 1024) {
+      CVR_KERNEL_SWITCH_LDS(downscale_lds_kernel, kernel, g, b, lds, s, src, fw, fh, dst, sw, sh);
+    } else {
+      CVR_KERNEL_SWITCH(downscale_kernel, kernel, g, b, s, src, fw, fh, dst, sw, sh);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !cardinal) return e;
     return launch_digital(kernel, dst, sw, sh, s);        // over the filtered screen

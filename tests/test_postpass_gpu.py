@@ -43,6 +43,12 @@ def _eq16(a, b):
     return np.array_equal(a.view(np.uint16), b.view(np.uint16))
 
 
+def _eq16_nan(a, b):
+    """Bit-equal, except that any NaN equals any NaN."""
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(a.view(np.uint16)[~na], b.view(np.uint16)[~nb])
+
+
 @pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("k", KERNELS)
 def test_filters_match_oracle_random(dev, oracle, mode, k):
@@ -120,12 +126,14 @@ def test_screenshot_rgba32f(dev, oracle):
 
 
 @pytest.mark.parametrize("mode,sw,sh", [(2, 16, 16), (2, 17, 19), (2, 1500, 16), (2, 16, 2700),
-                                        (2, 21000, 16), (3, 1024, 1024), (3, 34, 38)])
+                                        (2, 21000, 16), (3, 1024, 1024), (3, 34, 38),
+                                        (2, 65, 129), (2, 8000, 16), (3, 34, 130), (2, 16, 88)])
 @pytest.mark.parametrize("k", [N.FILTER_CARDINAL_BSPLINE_3, N.FILTER_CARDINAL_OMOMS3])
 def test_digital_filter_shapes(dev, oracle, mode, sw, sh, k):
-    """The cardinal kernels' recursive digital filter (LDS-staged lines, 16/8/4/1 lines per
-    wave by line length, the global-memory kernel past 20472 elements) on ragged, tiny and
-    long lines: bit for bit with the oracle, including the in-place prefilter of mode 3."""
+    """The cardinal kernels' recursive digital filter (LDS-staged lines cut into 64-element
+    segments, 16/8/4/2/1 lines per workgroup by line length, the global-memory kernel past
+    ~8900 elements) on ragged, tiny and long lines: bit for bit with the oracle, including
+    the in-place prefilter of mode 3."""
     rng = np.random.default_rng(sw * 7 + sh + k)
     fw, fh = (sw * 2, sh * 2) if mode < 3 else (max(1, sw // 2), max(1, sh // 2))
     frame = (rng.random((fh, fw, 4)) * 1.5 - 0.25).astype(np.float16)
@@ -134,3 +142,61 @@ def test_digital_filter_shapes(dev, oracle, mode, sw, sh, k):
     want = oracle.multiscale_filter(mode, k, oframe, sw, sh)
     assert _eq16(got, want)
     assert _eq16(gframe, oframe)
+
+
+def _spec_frames():
+    """Frames aimed at the segment-parallel digital filter: constant lines (their rounded
+    recursion can settle into a 2-cycle, so warm-ups do not agree and segments are redone
+    in order), signed zeros, non-finite values and values whose bound leaves binary16
+    (whole workgroups sequential), and plain random data."""
+    rng = np.random.default_rng(77)
+    fh, fw = 260, 300
+    out = {}
+    out["const_rows"] = np.repeat(rng.random((fh, 1, 4)), fw, axis=1).astype(np.float16)
+    out["const_cols"] = np.repeat(rng.random((1, fw, 4)), fh, axis=0).astype(np.float16)
+    z = np.zeros((fh, fw, 4), np.float16)
+    z[:, ::3] = np.float16(-0.0)
+    z[::7, ::5] = np.float16(1e-7)
+    out["signed_zeros"] = z
+    f = (rng.random((fh, fw, 4)) * 2 - 1).astype(np.float16)
+    f[100, 17, 2] = np.float16(np.inf)
+    f[3, 250, 0] = np.float16(np.nan)
+    out["nonfinite"] = f
+    out["huge"] = (rng.random((fh, fw, 4)) * 60000 - 30000).astype(np.float16)
+    out["near_max"] = np.where(rng.random((fh, fw, 4)) < 0.01, 65000.0,
+                               rng.random((fh, fw, 4))).astype(np.float16)
+    b = (rng.random((fh, fw, 4)) < 0.5).astype(np.float16)
+    b[:, 130:170] = np.float16(0.5)
+    out["blocks"] = b
+    return out
+
+
+@pytest.mark.parametrize("name", sorted(_spec_frames()))
+@pytest.mark.parametrize("k", [N.FILTER_CARDINAL_BSPLINE_3, N.FILTER_CARDINAL_OMOMS3])
+def test_digital_filter_speculation_cases(dev, oracle, name, k):
+    """The in-place prefilter (mode 3) on frames that drive the segment-parallel filter
+    through its redo and sequential paths: bit for bit with the sequential oracle."""
+    frame = _spec_frames()[name]
+    fh, fw = frame.shape[:2]
+    got, gframe = gpu_filter(dev, 3, k, frame, fw * 2, fh * 2)
+    oframe = frame.copy()
+    want = oracle.multiscale_filter(3, k, oframe, fw * 2, fh * 2)
+    # a recursion that overflows makes inf - inf: the sign of that fresh NaN is the
+    # hardware's (x86: negative default NaN, gfx950: positive), not part of CVR-SPEC
+    assert _eq16_nan(gframe, oframe)
+    assert _eq16_nan(got, want)
+    if name in ("const_rows", "const_cols", "blocks", "signed_zeros"):
+        assert _eq16(gframe, oframe) and _eq16(got, want)
+
+
+@pytest.mark.parametrize("ratio", [3, 5])
+@pytest.mark.parametrize("k", KERNELS)
+def test_downscale_ratios(dev, oracle, ratio, k):
+    """Kernel decimation at other frame/screen ratios: the LDS-window kernel where its taps
+    and window fit (ratio 3: box, hat), the global-memory kernel otherwise; bit for bit."""
+    rng = np.random.default_rng(100 * ratio + k)
+    sw, sh = 40, 33
+    frame = (rng.random((sh * ratio, sw * ratio, 4)) * 1.5 - 0.25).astype(np.float16)
+    got, _ = gpu_filter(dev, 2, k, frame, sw, sh)
+    want = oracle.multiscale_filter(2, k, frame.copy(), sw, sh)
+    assert _eq16(got, want)
