@@ -162,7 +162,16 @@ __global__ void downscale_kernel(const uint2* __restrict__ src, int sw, int sh,
 // pixel's column weights are computed once (the same expression as above) and
 // reused for every row; the taps are summed in the same order with the same
 // operations, so the result is bit-identical to downscale_kernel.
+// wgt * (half HI ? w.hi : w.lo), one rounding (= the f32 multiply of the converted half)
+template <bool HI>
+__device__ __forceinline__ float mul_half(float wgt, uint32_t w) {
+  float d;
+  if (HI) asm("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(wgt), "v"(w));
+  else asm("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel_hi:[0,1,0]" : "=v"(d) : "v"(wgt), "v"(w));
+  return d;
+}
 constexpr int kDownMaxTaps = 12;   // taps per axis held in registers
+constexpr int kUpMaxTaps = 8;
 
 template <class K>
 __global__ void __launch_bounds__(256)
@@ -211,10 +220,14 @@ downscale_lds_kernel(const uint2* __restrict__ src, int sw, int sh, uint2* __res
 #pragma unroll
     for (int q = 0; q < kDownMaxTaps; q++) {
       if (q < nc) {
+        // f += wgt * t per channel: the product of the exactly converted half in one
+        // v_fma_mix (-0 addend: the rounded product, sign of zero kept), then the add
         const uint2 p = row[q];
-        const float4 t = make_float4(h2f((uint16_t)(p.x & 0xffffu)), h2f((uint16_t)(p.x >> 16)),
-                                     h2f((uint16_t)(p.y & 0xffffu)), h2f((uint16_t)(p.y >> 16)));
-        f = madd(f, wr * wc[q], t);
+        const float wgt = wr * wc[q];
+        f.x += mul_half<false>(wgt, p.x);
+        f.y += mul_half<true>(wgt, p.x);
+        f.z += mul_half<false>(wgt, p.y);
+        f.w += mul_half<true>(wgt, p.y);
       }
     }
   }
@@ -235,11 +248,36 @@ __global__ void upscale_kernel(const uint2* __restrict__ src, int sw, int sh,
   const float x_c = ((float)jc + 0.5f) / (float)tw;
   const float xi_c = x_c * (float)sw - 0.5f;
   const int il_c = (int)ceilf(xi_c - kr), ir_c = (int)floorf(xi_c + kr);
+  // the column weights once per pixel (the same expression for every row), the
+  // taps in the same order with the same operations (products through v_fma_mix)
+  const int nc = ir_c - il_c + 1;
   float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int ir = il_r; ir <= ir_r; ir++) {
-    const float wr = K::w(xi_r - (float)ir);
-    for (int ic = il_c; ic <= ir_c; ic++)
-      f = madd(f, wr * K::w(xi_c - (float)ic), fetch_px(src, sw, sh, ic, ir));
+  if (nc > kUpMaxTaps) {
+    for (int ir = il_r; ir <= ir_r; ir++) {
+      const float wr = K::w(xi_r - (float)ir);
+      for (int ic = il_c; ic <= ir_c; ic++)
+        f = madd(f, wr * K::w(xi_c - (float)ic), fetch_px(src, sw, sh, ic, ir));
+    }
+  } else {
+    float wc[kUpMaxTaps];
+#pragma unroll
+    for (int q = 0; q < kUpMaxTaps; q++) wc[q] = q < nc ? K::w(xi_c - (float)(il_c + q)) : 0.0f;
+    for (int ir = il_r; ir <= ir_r; ir++) {
+      const float wr = K::w(xi_r - (float)ir);
+      const bool row_in = ir >= 0 && ir < sh;
+#pragma unroll
+      for (int q = 0; q < kUpMaxTaps; q++) {
+        if (q < nc) {
+          const int ic = il_c + q;
+          const uint2 p = (row_in && ic >= 0 && ic < sw) ? src[(size_t)ir * sw + ic] : make_uint2(0u, 0u);
+          const float wgt = wr * wc[q];
+          f.x += mul_half<false>(wgt, p.x);
+          f.y += mul_half<true>(wgt, p.x);
+          f.z += mul_half<false>(wgt, p.y);
+          f.w += mul_half<true>(wgt, p.y);
+        }
+      }
+    }
   }
   store_px(dst, tw, jc, jr, f);
 }
