@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdint>
 
 #include "cvr_device.h"
@@ -170,6 +171,7 @@ __device__ __forceinline__ float mul_half(float wgt, uint32_t w) {
   else asm("v_fma_mix_f32 %0, %1, %2, neg(0) op_sel_hi:[0,1,0]" : "=v"(d) : "v"(wgt), "v"(w));
   return d;
 }
+typedef float float2v __attribute__((ext_vector_type(2)));
 constexpr int kDownMaxTaps = 12;   // taps per axis held in registers
 constexpr int kUpMaxTaps = 8;
 
@@ -213,24 +215,34 @@ downscale_lds_kernel(const uint2* __restrict__ src, int sw, int sh, uint2* __res
 #pragma unroll
   for (int q = 0; q < kDownMaxTaps; q++)
     wc[q] = q < nc ? K::w((x_c - ((float)(il_c + q) + 0.5f) / (float)sw) * (float)tw) : 0.0f;
-  float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int ir = il_r; ir <= ir_r; ir++) {
-    const float wr = K::w((x_r - ((float)ir + 0.5f) / (float)sh) * (float)th);
-    const uint2* row = win + (ir - r0) * wp + (il_c - c0);
+  // rows of taps; a tap count of 8 or 9 (every pixel at ratio 2) runs unrolled
+  // without per-tap conditions; the channel sums go pairwise through v_pk_add_f32
+  float2v f01 = {0.0f, 0.0f}, f23 = {0.0f, 0.0f};
+  auto rows = [&](auto nct) {
+    constexpr int NC = decltype(nct)::value;
+    for (int ir = il_r; ir <= ir_r; ir++) {
+      const float wr = K::w((x_r - ((float)ir + 0.5f) / (float)sh) * (float)th);
+      const uint2* row = win + (ir - r0) * wp + (il_c - c0);
 #pragma unroll
-    for (int q = 0; q < kDownMaxTaps; q++) {
-      if (q < nc) {
-        // f += wgt * t per channel: the product of the exactly converted half in one
-        // v_fma_mix (-0 addend: the rounded product, sign of zero kept), then the add
-        const uint2 p = row[q];
-        const float wgt = wr * wc[q];
-        f.x += mul_half<false>(wgt, p.x);
-        f.y += mul_half<true>(wgt, p.x);
-        f.z += mul_half<false>(wgt, p.y);
-        f.w += mul_half<true>(wgt, p.y);
+      for (int q = 0; q < (NC > 0 ? NC : kDownMaxTaps); q++) {
+        if (NC > 0 || q < nc) {
+          // f += wgt * t per channel: the product of the exactly converted half in
+          // one v_fma_mix (-0 addend: the rounded product, sign of zero kept), then
+          // the add
+          const uint2 p = row[q];
+          const float wgt = wr * wc[q];
+          const float2v a = {mul_half<false>(wgt, p.x), mul_half<true>(wgt, p.x)};
+          const float2v b = {mul_half<false>(wgt, p.y), mul_half<true>(wgt, p.y)};
+          f01 += a;
+          f23 += b;
+        }
       }
     }
-  }
+  };
+  if (nc == 8) rows(std::integral_constant<int, 8>{});
+  else if (nc == 9) rows(std::integral_constant<int, 9>{});
+  else rows(std::integral_constant<int, 0>{});
+  const float4 f = make_float4(f01.x, f01.y, f23.x, f23.y);
   const float s = s_r * s_c;
   store_px(dst, tw, jc, jr, make_float4(f.x * s, f.y * s, f.z * s, f.w * s));
 }
@@ -687,8 +699,44 @@ digital_filter_seg_kernel(uint16_t* __restrict__ img, int w, int h, int dir, int
     l = e & (lpw - 1);
     return (size_t)i * w + l0 + l;
   };
+  // rows of even length from a 16-B aligned image: two pixels per 16-B load, one
+  // 4-B LDS store per channel
+  const bool pairs = dir == 0 && (nn & 1) == 0 && (reinterpret_cast<uintptr_t>(img) & 15) == 0;
+  const int half = nn >> 1, tp = nl * half;
+  uint4* p4 = reinterpret_cast<uint4*>(img);
+  auto plane_word = [&](int l, int c, int i) {   // i even: channel c halves i, i+1
+    return reinterpret_cast<uint32_t*>(plane + (size_t)(l * 4 + c) * S + (i / kSeg) * kSegPitch + (i % kSeg));
+  };
   uint32_t mb = 0u;
-  for (int e0 = 0; e0 < total; e0 += nthr * kDigitalUnroll) {
+  if (pairs) {
+    for (int e0 = 0; e0 < tp; e0 += nthr * kDigitalUnroll) {
+      uint4 v[kDigitalUnroll];
+#pragma unroll
+      for (int u = 0; u < kDigitalUnroll; u++) {
+        const int e = e0 + u * nthr + tid;
+        if (e < tp) {
+          const int l = e / half, i = (e - l * half) * 2;
+          v[u] = p4[((size_t)(l0 + l) * w + i) >> 1];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kDigitalUnroll; u++) {
+        const int e = e0 + u * nthr + tid;
+        if (e < tp) {
+          const int l = e / half, i = (e - l * half) * 2;
+          const uint4 q = v[u];
+          *plane_word(l, 0, i) = (q.x & 0xffffu) | (q.z << 16);
+          *plane_word(l, 1, i) = (q.x >> 16) | (q.z & 0xffff0000u);
+          *plane_word(l, 2, i) = (q.y & 0xffffu) | (q.w << 16);
+          *plane_word(l, 3, i) = (q.y >> 16) | (q.w & 0xffff0000u);
+          const uint32_t m0 = max(max(q.x & 0x7fffu, (q.x >> 16) & 0x7fffu), max(q.y & 0x7fffu, (q.y >> 16) & 0x7fffu));
+          const uint32_t m1 = max(max(q.z & 0x7fffu, (q.z >> 16) & 0x7fffu), max(q.w & 0x7fffu, (q.w >> 16) & 0x7fffu));
+          mb = max(mb, max(m0, m1));
+        }
+      }
+    }
+  }
+  for (int e0 = 0; e0 < (pairs ? 0 : total); e0 += nthr * kDigitalUnroll) {
     uint2 v[kDigitalUnroll];
 #pragma unroll
     for (int u = 0; u < kDigitalUnroll; u++) {
@@ -925,6 +973,17 @@ digital_filter_seg_kernel(uint16_t* __restrict__ img, int w, int h, int dir, int
   }
   }
   // ---- stage out ----
+  if (pairs) {
+    for (int e = tid; e < tp; e += nthr) {
+      const int l = e / half, i = (e - l * half) * 2;
+      const uint32_t c0 = *plane_word(l, 0, i), c1 = *plane_word(l, 1, i);
+      const uint32_t c2 = *plane_word(l, 2, i), c3 = *plane_word(l, 3, i);
+      p4[((size_t)(l0 + l) * w + i) >> 1] =
+          make_uint4((c0 & 0xffffu) | (c1 << 16), (c2 & 0xffffu) | (c3 << 16), (c0 >> 16) | (c1 & 0xffff0000u),
+                     (c2 >> 16) | (c3 & 0xffff0000u));
+    }
+    return;
+  }
   for (int e0 = 0; e0 < total; e0 += nthr * kDigitalUnroll) {
 #pragma unroll
     for (int u = 0; u < kDigitalUnroll; u++) {

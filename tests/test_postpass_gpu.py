@@ -200,3 +200,25 @@ def test_downscale_ratios(dev, oracle, ratio, k):
     got, _ = gpu_filter(dev, 2, k, frame, sw, sh)
     want = oracle.multiscale_filter(2, k, frame.copy(), sw, sh)
     assert _eq16(got, want)
+
+
+@pytest.mark.parametrize("k", [N.FILTER_CARDINAL_BSPLINE_3, N.FILTER_CARDINAL_OMOMS3])
+def test_digital_filter_unaligned_frame(dev, oracle, k):
+    """A frame that starts 8 B past a 16-B boundary: the row pass stages single pixels
+    instead of pixel pairs; same bits."""
+    import torch
+    rng = np.random.default_rng(31 + k)
+    fh, fw = 40, 52
+    frame = (rng.random((fh, fw, 4)) * 1.5 - 0.25).astype(np.float16)
+    buf = torch.zeros(fh * fw * 4 + 4, dtype=torch.float16, device="cuda")
+    buf[4:] = torch.from_numpy(frame.reshape(-1)).cuda()
+    out = torch.zeros((2 * fh, 2 * fw, 4), dtype=torch.float16, device="cuda")
+    dev.set_stream(torch.cuda.current_stream().cuda_stream)
+    N.check(N.lib().cvr_multiscale_filter(dev.handle, 3, k, buf.data_ptr() + 8, fw, fh,
+                                          out.data_ptr(), 2 * fw, 2 * fh), "filter", dev.handle)
+    torch.cuda.synchronize()
+    dev.set_stream(None)
+    oframe = frame.copy()
+    want = oracle.multiscale_filter(3, k, oframe, 2 * fw, 2 * fh)
+    assert _eq16(buf[4:].cpu().numpy().reshape(fh, fw, 4), oframe)
+    assert _eq16(out.cpu().numpy(), want)
