@@ -199,6 +199,20 @@ downscale_lds_kernel(const uint2* __restrict__ src, int sw, int sh, uint2* __res
     const int r = r0 + rr, c = c0 + cc;
     win[rr * wp + cc] = (r >= 0 && r < sh && c >= 0 && c < sw) ? src[(size_t)r * sw + c] : make_uint2(0u, 0u);
   }
+  // The block's 16 column and 16 row weight sets, once per block (every pixel of
+  // a block column shares its column weights): the same expressions per tap.
+  __shared__ float wcol[16][kDownMaxTaps], wrow[16][kDownMaxTaps];
+  for (int e = threadIdx.x; e < 2 * 16 * kDownMaxTaps; e += 256) {
+    const bool col = e < 16 * kDownMaxTaps;
+    const int i = (col ? e : e - 16 * kDownMaxTaps) / kDownMaxTaps, q = e % kDownMaxTaps;
+    const int j = (col ? bx : by) + i, t = col ? tw : th, sz = col ? sw : sh;
+    const float x = ((float)j + 0.5f) / (float)t;
+    const int il = (int)ceilf((x - kr / (float)t) * (float)sz - 0.5f);
+    const int ir = (int)floorf((x + kr / (float)t) * (float)sz - 0.5f);
+    const float wv = q <= ir - il ? K::w((x - ((float)(il + q) + 0.5f) / (float)sz) * (float)t) : 0.0f;
+    if (col) wcol[i][q] = wv;
+    else wrow[i][q] = wv;
+  }
   __syncthreads();
   const int jc = bx + (threadIdx.x & 15), jr = by + (threadIdx.x >> 4);
   if (jc >= tw || jr >= th) return;
@@ -213,15 +227,15 @@ downscale_lds_kernel(const uint2* __restrict__ src, int sw, int sh, uint2* __res
   const int nc = ir_c - il_c + 1;
   float wc[kDownMaxTaps];
 #pragma unroll
-  for (int q = 0; q < kDownMaxTaps; q++)
-    wc[q] = q < nc ? K::w((x_c - ((float)(il_c + q) + 0.5f) / (float)sw) * (float)tw) : 0.0f;
+  for (int q = 0; q < kDownMaxTaps; q++) wc[q] = wcol[threadIdx.x & 15][q];
+  const float* wrj = wrow[threadIdx.x >> 4];
   // rows of taps; a tap count of 8 or 9 (every pixel at ratio 2) runs unrolled
   // without per-tap conditions; the channel sums go pairwise through v_pk_add_f32
   float2v f01 = {0.0f, 0.0f}, f23 = {0.0f, 0.0f};
   auto rows = [&](auto nct) {
     constexpr int NC = decltype(nct)::value;
     for (int ir = il_r; ir <= ir_r; ir++) {
-      const float wr = K::w((x_r - ((float)ir + 0.5f) / (float)sh) * (float)th);
+      const float wr = wrj[ir - il_r];
       const uint2* row = win + (ir - r0) * wp + (il_c - c0);
 #pragma unroll
       for (int q = 0; q < (NC > 0 ? NC : kDownMaxTaps); q++) {
