@@ -103,6 +103,9 @@ def parse():
     p.add_argument("--tile", type=int, default=32)
     p.add_argument("--field", choices=["ml", "blobs"], default="ml")
     p.add_argument("--phong", action="store_true")
+    p.add_argument("--skip-min-pct", type=int, default=-1,
+                   help="empty-space skipping when >= this %% of macro cells are empty (101: off; "
+                        "-1: the library default)")
     p.add_argument("--batch", type=int, default=0, choices=[0, 2, 4],
                    help="rc1pass samples per lane per memory round trip (0 = auto: 4, 2 with Phong)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -409,6 +412,9 @@ def main():
         N.check(N.lib().cvr_set_option(r.device.handle, b"quad", quad), "quad", r.device.handle)
         if a.batch:
             N.check(N.lib().cvr_set_option(r.device.handle, b"batch", a.batch), "batch", r.device.handle)
+        if a.skip_min_pct >= 0:
+            N.check(N.lib().cvr_set_option(r.device.handle, b"skip_min_pct", a.skip_min_pct),
+                    "skip_min_pct", r.device.handle)
     try:
         # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
         # on rank 0) would otherwise rival a rank's share of the frame (~23 us at N = 8)

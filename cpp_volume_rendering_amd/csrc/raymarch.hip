@@ -155,7 +155,15 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       for (int j = 0; j < K; j++) {
         sp[j] = sample_pos(fmaf(r.dt.x, tj[j], r.o.x), fmaf(r.dt.y, tj[j], r.o.y),
                            fmaf(r.dt.z, tj[j], r.o.z), A);
+#ifdef CVR_PROBE_LDS_CELLS   // cost probe only: every sample from a 4 KiB LDS table (wrong images)
+        {
+          const uint4 v = reinterpret_cast<const uint4*>(tfp)[(sp[j].idx * 7u) & 255u];
+          raw[j] = make_uint4((v.x & 0x01ff01ffu) | 0x00000000u, (v.y & 0x01ff01ffu) | 0x00000000u,
+                              (v.z & 0x01ff01ffu) | 0x00000000u, (v.w & 0x01ff01ffu) | 0x00000000u);
+        }
+#else
         raw[j] = load_cell(sp[j].idx);
+#endif
       }
     } else {
 #pragma unroll
