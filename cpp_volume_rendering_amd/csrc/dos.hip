@@ -305,8 +305,11 @@ __device__ __forceinline__ void cone_sections(const DosArgs& Q, const DosCone& C
     for (int j = 0; j < JN; j++) {
       const f3 p = vmad(vk[J0 + j], tr[q], pos);
       tap[q][j] = ext_tap(l, p);
-      out[q][j] = outside_box(Q, p);
-      xb[q][j] = out[q][j] ? border_exponent(Q, p, e[q].y) : 0.0f;
+      // The border exponent is -0 inside the box, so "outside" is xb < 0: a tap
+      // outside whose exponent is still -0 (a distance that underflows) gets the
+      // factor exp(-0) = 1 exactly, the inside value (no 6-compare box test)
+      xb[q][j] = border_exponent(Q, p, e[q].y);
+      out[q][j] = xb[q][j] < 0.0f;
       // Far outside the box the border factor is exactly 0 (exp below -86), and
       // so is the tap (a finite extinction times 0): no fetch, no filter
       zero[q][j] = Q.zero_skip && xb[q][j] < -86.0f;
