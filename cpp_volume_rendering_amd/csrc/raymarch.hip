@@ -175,6 +175,20 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
     }
     // stage 2: density and transfer-function classification
     float4 src[K];
+    // Emission-absorption: alpha first (two 4-B LDS reads); the rgb lerps (two
+    // 16-B reads) only for visible samples, ~1 in 5 on the headline frame
+    int tfi[K];
+    float tfa[K];
+    if (!PHONG) {
+#pragma unroll
+      for (int j = 0; j < K; j++) {
+        const float xd = fmaf(trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az), fn, -0.5f);
+        const float fl = floorf(xd);
+        tfa[j] = xd - fl;
+        tfi[j] = (int)fl + 1;
+        src[j].w = lerpf(tfp[tfi[j]].w, tfp[tfi[j] + 1].w, tfa[j]);
+      }
+    } else
 #pragma unroll
     for (int j = 0; j < K; j++)
       src[j] = classify(tfp, fn, trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az));
@@ -193,6 +207,12 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
           float4 sc = src[j];
           if (sc.w > 0.0f) {
             visible = true;
+            if (!PHONG) {   // classify's rgb, same lerps
+              const float4 t0 = tfp[tfi[j]], t1 = tfp[tfi[j] + 1];
+              sc.x = lerpf(t0.x, t1.x, tfa[j]);
+              sc.y = lerpf(t0.y, t1.y, tfa[j]);
+              sc.z = lerpf(t0.z, t1.z, tfa[j]);
+            }
             if (PHONG) {
               shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
               nshade++;
