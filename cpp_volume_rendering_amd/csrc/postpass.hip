@@ -516,13 +516,12 @@ __device__ __forceinline__ float rev_coef(int i) {
 // kept as it is).  CHECK: stop at nn.
 template <class LU, bool CHECK>
 __device__ __forceinline__ uint4 fwd8(uint4 v, uint32_t& prev, int i0, int nn) {
+  // the table coefficients sit in chunks 0 and 1 of a line (i0 = 0, 8); with
+  // compile-time k both candidates are constants: two selects per element
   float lk[8];
+  const bool c0 = i0 == 0, c1 = i0 == 8;
 #pragma unroll
-  for (int k = 0; k < 8; k++) lk[k] = LU::L(LU::m - 1);
-  if (i0 < 16) {
-#pragma unroll
-    for (int k = 0; k < 8; k++) lk[k] = fwd_coef<LU>(i0 + k);
-  }
+  for (int k = 0; k < 8; k++) lk[k] = c0 ? fwd_coef<LU>(k) : (c1 ? fwd_coef<LU>(8 + k) : LU::L(LU::m - 1));
   uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int k = 0; k < 8; k++) {
@@ -541,12 +540,9 @@ __device__ __forceinline__ uint4 fwd8(uint4 v, uint32_t& prev, int i0, int nn) {
 template <class LU, bool CHECK>
 __device__ __forceinline__ uint4 rev8(uint4 v, uint32_t& prev, int i0, int nn) {
   float lk[8];
+  const bool c0 = i0 == 0, c1 = i0 == 8;
 #pragma unroll
-  for (int k = 0; k < 8; k++) lk[k] = LU::L(LU::m - 1);
-  if (i0 < 16) {
-#pragma unroll
-    for (int k = 0; k < 8; k++) lk[k] = rev_coef<LU>(i0 + k);
-  }
+  for (int k = 0; k < 8; k++) lk[k] = c0 ? rev_coef<LU>(k) : (c1 ? rev_coef<LU>(8 + k) : LU::L(LU::m - 1));
   uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int k = 7; k >= 0; k--) {
