@@ -108,6 +108,16 @@ __device__ __forceinline__ float4 madd(float4 acc, float wgt, float4 t) {
   return make_float4(acc.x + wgt * t.x, acc.y + wgt * t.y, acc.z + wgt * t.z, acc.w + wgt * t.w);
 }
 
+// XCD-aware 2D block: the dispatcher deals workgroups to the 8 XCDs round-robin
+// in linear order; remapped so that each XCD takes a contiguous run of blocks
+// (row-major), whose overlapping input windows then share its L2.
+__device__ __forceinline__ void xcd_block(int& bx, int& by) {
+  const int nb = (int)(gridDim.x * gridDim.y), b = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+  const int l = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
+  by = l / (int)gridDim.x;
+  bx = l - by * (int)gridDim.x;
+}
+
 // multisample_filter.comp: texture(TexGeneratedFrame, (p + 0.5) / size), bilinear,
 // clamp to edge, texel centres at (i + 0.5) / n
 __global__ void multisample_kernel(const uint2* __restrict__ src, int sw, int sh,
@@ -181,7 +191,10 @@ downscale_lds_kernel(const uint2* __restrict__ src, int sw, int sh, uint2* __res
                      int th) {
   extern __shared__ uint2 win[];
   const float kr = 0.5f * K::support;
-  const int bx = blockIdx.x * 16, by = blockIdx.y * 16;
+  int bx, by;
+  xcd_block(bx, by);
+  bx *= 16;
+  by *= 16;
   auto first_tap = [kr](int j, int t, int s) {
     const float x = ((float)j + 0.5f) / (float)t;
     return (int)ceilf((x - kr / (float)t) * (float)s - 0.5f);
@@ -265,7 +278,9 @@ downscale_lds_kernel(const uint2* __restrict__ src, int sw, int sh, uint2* __res
 template <class K>
 __global__ void upscale_kernel(const uint2* __restrict__ src, int sw, int sh,
                                uint2* __restrict__ dst, int tw, int th) {
-  const int jc = blockIdx.x * 16 + (threadIdx.x & 15), jr = blockIdx.y * 16 + (threadIdx.x >> 4);
+  int ubx, uby;
+  xcd_block(ubx, uby);
+  const int jc = ubx * 16 + (threadIdx.x & 15), jr = uby * 16 + (threadIdx.x >> 4);
   if (jc >= tw || jr >= th) return;
   const float kr = 0.5f * K::support;
   const float x_r = ((float)jr + 0.5f) / (float)th;
@@ -660,7 +675,12 @@ digital_filter_seg_kernel(uint16_t* __restrict__ img, int w, int h, int dir, int
   uint16_t* plane = reinterpret_cast<uint16_t*>(lds_raw);
   const int lpw = 1 << lpw_shift;
   const int lines = dir == 0 ? h : w, nn = dir == 0 ? w : h;
-  const int l0 = blockIdx.x * lpw;
+  // XCD-aware: workgroup b runs on XCD b % 8, so consecutive line groups go to the
+  // same XCD (column groups of the column pass share 128-B lines in its L2)
+  const int nblk = gridDim.x;
+  const int blk = (nblk & 7) == 0 ? (int)(blockIdx.x & 7) * (nblk >> 3) + (int)(blockIdx.x >> 3)
+                                  : (int)blockIdx.x;
+  const int l0 = blk * lpw;
   const int nl = min(lpw, lines - l0);
   const int nchain = nl * 4, items = nchain * nseg;
   const int ni = lpw * 4 * nseg;   // item capacity
