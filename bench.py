@@ -103,6 +103,8 @@ def parse():
     p.add_argument("--tile", type=int, default=32)
     p.add_argument("--field", choices=["ml", "blobs"], default="ml")
     p.add_argument("--phong", action="store_true")
+    p.add_argument("--tile-order", type=int, default=-1, choices=[-1, 0, 1, 2],
+                   help="rc1pass launch order: 0 XCD bands, 1 learned LPT (default), 2 interleaved")
     p.add_argument("--skip-min-pct", type=int, default=-1,
                    help="empty-space skipping when >= this %% of macro cells are empty (101: off; "
                         "-1: the library default)")
@@ -412,6 +414,9 @@ def main():
         N.check(N.lib().cvr_set_option(r.device.handle, b"quad", quad), "quad", r.device.handle)
         if a.batch:
             N.check(N.lib().cvr_set_option(r.device.handle, b"batch", a.batch), "batch", r.device.handle)
+        if a.tile_order >= 0:
+            N.check(N.lib().cvr_set_option(r.device.handle, b"tile_order", a.tile_order), "tile_order",
+                    r.device.handle)
         if a.skip_min_pct >= 0:
             N.check(N.lib().cvr_set_option(r.device.handle, b"skip_min_pct", a.skip_min_pct),
                     "skip_min_pct", r.device.handle)
