@@ -482,9 +482,14 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
 // ShadeSample (ray_bbox_marching.comp:607-656) for the deferred march
 // ---------------------------------------------------------------------------
 
+#ifndef CVR_DOS_WAVES
+#define CVR_DOS_WAVES 3
+#endif
 struct DosShader {
   using Args = DosArgs;
-  static constexpr int kMinWavesPerEU = 1;   // register budget: the compiler's choice
+  // register budget: 3 waves/SIMD (168 VGPRs; the compiler alone takes 172 -> 2 waves):
+  // kernel 21.1 -> 18.0 ms, 4 waves 18.8 ms (spills)
+  static constexpr int kMinWavesPerEU = CVR_DOS_WAVES;
   using Data = const uint4*;   // the cell8 extinction pyramid
 
   // Shaded colour of one job; `lit` counts the shadow cones traced, `fetches`
