@@ -354,15 +354,22 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
 // (four lanes per ray).  Without an order, block b -> tile in XCD bands
 // (blocks b and b+8 share an XCD, so XCD b%8 gets one contiguous band).
 // Waves of the `boost` longest tiles of each band raise their priority.
-// (CVR_RC1_WAVES_PER_EU: residency experiments only, tools/build_variant.sh; the
-// default leaves register allocation to the compiler per variant)
+// Register budget: the plain emission-absorption march at K = 4 (the headline
+// kernel, 69 VGPRs by itself -> 7 waves/SIMD) is held to 64 VGPRs for 8
+// waves/SIMD (2 spilled): one kernel takes the same time (0.1207 vs 0.1217 ms)
+// but frames in flight overlap better, 0.1070 -> 0.1018 ms per frame on the
+// driver's command.  Every other variant is left to the compiler.
+// (CVR_RC1_WAVES_PER_EU: residency experiments, tools/build_variant.sh)
+template <int K, bool PHONG, bool SKIP, bool QUAD>
+constexpr int rc1_waves_per_eu() {
 #ifdef CVR_RC1_WAVES_PER_EU
-#define CVR_RC1_OCC __attribute__((amdgpu_waves_per_eu(CVR_RC1_WAVES_PER_EU)))
+  return CVR_RC1_WAVES_PER_EU;
 #else
-#define CVR_RC1_OCC
+  return (K == 4 && !PHONG && !SKIP && !QUAD) ? 8 : 1;
 #endif
+}
 template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, bool BUF>
-__global__ void __launch_bounds__(64) CVR_RC1_OCC
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rc1_waves_per_eu<K, PHONG, SKIP, QUAD>())))
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
                     float4* __restrict__ out, uint32_t* __restrict__ samples,
