@@ -413,8 +413,25 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
   }
 }
 
+// Register budget per variant (waves/SIMD; 1 = the compiler's choice): 6 / 6 / 8
+// (80 / 80 / 63 VGPRs; the compiler alone: 84 / 88 / 67 -> 5 / 5 / 7 waves).  One
+// kernel takes the same time, frames in flight overlap better: frame 2.20 ->
+// 2.11, 1.59 -> 1.53, 1.54 -> 1.50 ms.
+#ifndef CVR_ISO_WAVES0
+#define CVR_ISO_WAVES0 6
+#endif
+#ifndef CVR_ISO_WAVES1
+#define CVR_ISO_WAVES1 6
+#endif
+#ifndef CVR_ISO_WAVES2
+#define CVR_ISO_WAVES2 8
+#endif
 template <int VARIANT, bool PHONG>
-__global__ void __launch_bounds__(64)
+constexpr int iso_waves_per_eu() {
+  return PHONG ? 1 : (VARIANT == 0 ? CVR_ISO_WAVES0 : (VARIANT == 1 ? CVR_ISO_WAVES1 : CVR_ISO_WAVES2));
+}
+template <int VARIANT, bool PHONG>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(iso_waves_per_eu<VARIANT, PHONG>())))
 iso_tile_kernel(IsoArgs Q, const uint4* __restrict__ cells, const uint4* __restrict__ grad,
                 const float2* __restrict__ mm, float4* __restrict__ out,
                 uint32_t* __restrict__ samples, unsigned long long* __restrict__ tile_samples) {
