@@ -358,13 +358,22 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
 // kernel, 69 VGPRs by itself -> 7 waves/SIMD) is held to 64 VGPRs for 8
 // waves/SIMD (2 spilled): one kernel takes the same time (0.1207 vs 0.1217 ms)
 // but frames in flight overlap better, 0.1070 -> 0.1018 ms per frame on the
-// driver's command.  Every other variant is left to the compiler.
+// driver's command.  Blinn-Phong at K = 2 is held to 80 VGPRs, 6 waves/SIMD (the
+// compiler's 93 give 5): kernel 0.3094 -> 0.3148 ms, frame 0.2723 -> 0.2608 ms.
+// Every other variant is left to the compiler (Phong K = 4 at 4 waves: neutral).
 // (CVR_RC1_WAVES_PER_EU: residency experiments, tools/build_variant.sh)
 template <int K, bool PHONG, bool SKIP, bool QUAD>
 constexpr int rc1_waves_per_eu() {
 #ifdef CVR_RC1_WAVES_PER_EU
   return CVR_RC1_WAVES_PER_EU;
 #else
+#ifndef CVR_RC1_PHONG_WAVES2
+#define CVR_RC1_PHONG_WAVES2 6
+#endif
+#ifndef CVR_RC1_PHONG_WAVES4
+#define CVR_RC1_PHONG_WAVES4 1
+#endif
+  if (PHONG && !SKIP && !QUAD) return K == 2 ? CVR_RC1_PHONG_WAVES2 : CVR_RC1_PHONG_WAVES4;
   return (K == 4 && !PHONG && !SKIP && !QUAD) ? 8 : 1;
 #endif
 }
