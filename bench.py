@@ -581,7 +581,10 @@ def main():
                 "traffic": load_traffic(a.pmc.replace("rc1pass", a.renderer), wkey),
                 "kernel": kname,
                 "kernel_ms": round(kern_ms, 4),
-                "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank}
+                "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank,
+                # the same bytes over the frame time of the timed region (frames in
+                # flight overlap, so a frame takes less than one launch's duration)
+                "frac_frame": round(b_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         if roof["traffic"]:
             # the bytes HBM actually served (PMC) at the kernel's own time: where the
             # algorithmic figure is mostly served from L1/L2 (frac > 1 for EBS), this
