@@ -64,6 +64,125 @@ __device__ __forceinline__ float shadow_box(const EbsArgs& Q, const float4* __re
   return ((sat_box(Q, sat, sat_offset(Q, p1), sat_offset(Q, p2)) / volquery)) * Q.ui_weight;
 }
 
+// The same shadow box as a software pipeline, half a box deep.  A box's eight
+// SAT fetches fall in two halves, V1..V4 (at p2.y) and V5..V8 (at p1.y).  The
+// chain issues the second half of box i, finishes the first half, issues the
+// first half of box i+1 and finishes the second half of box i, so eight cell
+// loads are always in flight behind the lerps while only two half-boxes (64
+// VGPRs, as many as one whole box) are held.  The operations and their order
+// are shadow_box's, so the bits are too.  The loads of a box past the end of a
+// chain are in bounds (its coordinates are clamped as for any box) and unused.
+// (A generic NP-part version, 2 / 4 / 8 parts with NP-1 in flight and the next
+// box's coordinates computed at the top, measured slower at every depth: EBS
+// 512^3 kernel 37.6 ms at 4 parts, 36.0 at 2, 36.3 at 8, vs 36.1 unpipelined and
+// 32.9 for this one; profiles/r02_ebs_pipe_ab.txt.)
+struct SatBoxCoord {
+  float tx[2], ty[2], tz[2];         // texel coordinates of p1 / p2 (after sat_offset)
+  float vq;                          // volquery
+};
+
+__device__ __forceinline__ float sat_texel(float x, float inv_vs, float n, float n_m1) {
+  return __builtin_amdgcn_fmed3f(fmaf(x * inv_vs, n, -0.5f), 0.0f, n_m1);
+}
+
+__device__ __forceinline__ SatBoxCoord shadow_box_coord(const EbsArgs& Q, f3 p1, f3 p2, f3 rS) {
+  SatBoxCoord C;
+  C.vq = (div_by_recip(fabsf(p1.x - p2.x), Q.S[0], rS.x)) *
+         (div_by_recip(fabsf(p1.y - p2.y), Q.S[1], rS.y)) *
+         (div_by_recip(fabsf(p1.z - p2.z), Q.S[2], rS.z));
+  const f3 q1 = sat_offset(Q, p1), q2 = sat_offset(Q, p2);
+  C.tx[0] = sat_texel(q1.x, Q.inv_vs[0], Q.nsat[0], Q.nsat_m1[0]);
+  C.tx[1] = sat_texel(q2.x, Q.inv_vs[0], Q.nsat[0], Q.nsat_m1[0]);
+  C.ty[0] = sat_texel(q1.y, Q.inv_vs[1], Q.nsat[1], Q.nsat_m1[1]);
+  C.ty[1] = sat_texel(q2.y, Q.inv_vs[1], Q.nsat[1], Q.nsat_m1[1]);
+  C.tz[0] = sat_texel(q1.z, Q.inv_vs[2], Q.nsat[2], Q.nsat_m1[2]);
+  C.tz[1] = sat_texel(q2.z, Q.inv_vs[2], Q.nsat[2], Q.nsat_m1[2]);
+  return C;
+}
+
+// V_k (k = 0..7 for V1..V8) is the fetch at p1.x if k & 1, p1.z if k & 2,
+// p1.y if k & 4 (else p2): half H holds k = 4H .. 4H+3.
+template <int H>
+__device__ __forceinline__ void shadow_half_issue(const EbsArgs& Q, const float4* __restrict__ sat,
+                                                  const SatBoxCoord& C, float4 (&c)[8]) {
+  const uint32_t ty = (uint32_t)C.ty[H ? 0 : 1];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int k = 4 * H + j;
+    const int xi = (k & 1) ? 0 : 1, zi = (k & 2) ? 0 : 1;
+    const uint32_t row = __umul24((uint32_t)C.tz[zi], (uint32_t)Q.sat_dims[1]) + ty;
+    const uint32_t idx = __umul24(row, (uint32_t)Q.sat_dims[0]) + (uint32_t)C.tx[xi];
+    const float4* cell = sat + 2 * (size_t)idx;
+    c[2 * j] = cell[0];
+    c[2 * j + 1] = cell[1];
+  }
+}
+
+template <int H>
+__device__ __forceinline__ void shadow_half_finish(const SatBoxCoord& C, const float4 (&c)[8], float (&V)[4]) {
+  const float ay = __builtin_amdgcn_fractf(C.ty[H ? 0 : 1]);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int k = 4 * H + j;
+    const int xi = (k & 1) ? 0 : 1, zi = (k & 2) ? 0 : 1;
+    const float ax = __builtin_amdgcn_fractf(C.tx[xi]), az = __builtin_amdgcn_fractf(C.tz[zi]);
+    const float4 lo = c[2 * j], hi = c[2 * j + 1];
+    const float c00 = lerpf(lo.x, lo.y, ax), c10 = lerpf(lo.z, lo.w, ax);
+    const float c01 = lerpf(hi.x, hi.y, ax), c11 = lerpf(hi.z, hi.w, ax);
+    V[j] = lerpf(lerpf(c00, c10, ay), lerpf(c01, c11, ay), az);
+  }
+}
+
+#ifndef CVR_EBS_PIPE
+#define CVR_EBS_PIPE 1
+#endif
+
+// The box chain of a cone: while cond(w) { Stau += box(w); w += si }, with
+// box_at(w, p1, p2) giving the box corners at axis position w (ConeZAxis
+// :240-272 and its Y / X twins).  Pipelined half a box deep (CVR_EBS_PIPE).
+template <class Cond, class BoxAt>
+__device__ __forceinline__ float shadow_chain(const EbsArgs& Q, const float4* __restrict__ sat, f3 rS,
+                                              float w, float si, Cond cond, BoxAt box_at,
+                                              uint32_t& boxes) {
+  float Stau = 0.0f;
+  f3 p1, p2;
+  if (!CVR_EBS_PIPE) {
+    while (cond(w)) {
+      box_at(w, p1, p2);
+      Stau += shadow_box(Q, sat, p1, p2, rS);
+      boxes++;
+      w = w + si;
+    }
+    return Stau;
+  }
+  if (!cond(w)) return Stau;
+  box_at(w, p1, p2);
+  SatBoxCoord C = shadow_box_coord(Q, p1, p2, rS);
+  float4 F[8], S[8];
+  float V[4];
+  shadow_half_issue<0>(Q, sat, C, F);
+  for (;;) {
+    shadow_half_issue<1>(Q, sat, C, S);
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the lerps
+    shadow_half_finish<0>(C, F, V);
+    float sum = V[0] - V[1] - V[2] + V[3];
+    const float wn = w + si;
+    const bool more = cond(wn);
+    box_at(wn, p1, p2);
+    const SatBoxCoord Cn = shadow_box_coord(Q, p1, p2, rS);
+    shadow_half_issue<0>(Q, sat, Cn, F);
+    __builtin_amdgcn_sched_barrier(0);
+    shadow_half_finish<1>(C, S, V);
+    sum = sum - V[0] + V[1] + V[2] - V[3];
+    Stau += (sum / C.vq) * Q.ui_weight;
+    boxes++;
+    if (!more) break;
+    w = wn;
+    C = Cn;
+  }
+  return Stau;
+}
+
 // ExtinctionAmbientOcclusion (:109-146)
 __device__ float ebs_occlusion(const EbsArgs& Q, const float4* __restrict__ sat, f3 tx) {
   const float R = Q.occ_radius;
@@ -93,7 +212,6 @@ __device__ float ebs_occlusion(const EbsArgs& Q, const float4* __restrict__ sat,
 // ConeZAxis (:187-275)
 __device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
-  float Stau = 0.0f;
   float signal = 1.0f;
   if (cv.z < 0) signal = -1.0f;
   const float p_cs = Q.p_cs, p_sn = Q.p_sn, n_cs = Q.n_cs, n_sn = Q.n_sn;
@@ -110,8 +228,11 @@ __device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   const float d_x1 = fabsf(pj_x1.z), d_x2 = fabsf(pj_x2.z), d_y1 = fabsf(pj_y1.z), d_y2 = fabsf(pj_y2.z);
   const float r_x1 = 1.0f / d_x1, r_x2 = 1.0f / d_x2, r_y1 = 1.0f / d_y1, r_y2 = 1.0f / d_y2;
   const float rc = 1.0f / cv.z;
-  while (div_by_recip(z_pos, cv.z, rc) < Q.max_distance &&
-         (pos.z + (z_pos + si) > vmin && pos.z + (z_pos + si) < vmax)) {
+  auto cond = [&](float z_pos) {
+    return div_by_recip(z_pos, cv.z, rc) < Q.max_distance &&
+           (pos.z + (z_pos + si) > vmin && pos.z + (z_pos + si) < vmax);
+  };
+  auto box_at = [&](float z_pos, f3& p1, f3& p2) {
     const float z_mean = fabsf(z_pos + si * 0.5f);
     const float p_x1 = pj_x1.x * div_by_recip(z_mean, d_x1, r_x1);
     const float p_x2 = pj_x2.x * div_by_recip(z_mean, d_x2, r_x2);
@@ -126,17 +247,15 @@ __device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
     x1 = x1 - xs * Q.S[0]; x2 = x2 + xs * Q.S[0];
     y1 = y1 - ys * Q.S[1]; y2 = y2 + ys * Q.S[1];
     const float z1 = fminf(z_pos, z_pos + si), z2 = fmaxf(z_pos, z_pos + si);
-    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2}, rS);
-    boxes++;
-    z_pos = z_pos + si;
-  }
-  return Stau;
+    p1 = f3{pos.x + x1, pos.y + y1, pos.z + z1};
+    p2 = f3{pos.x + x2, pos.y + y2, pos.z + z2};
+  };
+  return shadow_chain(Q, sat, rS, z_pos, si, cond, box_at, boxes);
 }
 
 // ConeYAxis (:277-364)
 __device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
-  float Stau = 0.0f;
   float signal = 1.0f;
   if (cv.y < 0) signal = -1.0f;
   const float p_cs = Q.p_cs, p_sn = Q.p_sn, n_cs = Q.n_cs, n_sn = Q.n_sn;
@@ -153,8 +272,11 @@ __device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   const float d_x1 = fabsf(pj_x1.y), d_x2 = fabsf(pj_x2.y), d_z1 = fabsf(pj_z1.y), d_z2 = fabsf(pj_z2.y);
   const float r_x1 = 1.0f / d_x1, r_x2 = 1.0f / d_x2, r_z1 = 1.0f / d_z1, r_z2 = 1.0f / d_z2;
   const float rc = 1.0f / cv.y;
-  while (div_by_recip(y_pos, cv.y, rc) < Q.max_distance &&
-         (pos.y + (y_pos + si) > vmin && pos.y + (y_pos + si) < vmax)) {
+  auto cond = [&](float y_pos) {
+    return div_by_recip(y_pos, cv.y, rc) < Q.max_distance &&
+           (pos.y + (y_pos + si) > vmin && pos.y + (y_pos + si) < vmax);
+  };
+  auto box_at = [&](float y_pos, f3& p1, f3& p2) {
     const float y_mean = fabsf(y_pos + si * 0.5f);
     const float p_x1 = pj_x1.x * div_by_recip(y_mean, d_x1, r_x1);
     const float p_x2 = pj_x2.x * div_by_recip(y_mean, d_x2, r_x2);
@@ -169,17 +291,15 @@ __device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
     x1 = x1 - xs * Q.S[0]; x2 = x2 + xs * Q.S[0];
     z1 = z1 - zs * Q.S[2]; z2 = z2 + zs * Q.S[2];
     const float y1 = fminf(y_pos, y_pos + si), y2 = fmaxf(y_pos, y_pos + si);
-    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2}, rS);
-    boxes++;
-    y_pos = y_pos + si;
-  }
-  return Stau;
+    p1 = f3{pos.x + x1, pos.y + y1, pos.z + z1};
+    p2 = f3{pos.x + x2, pos.y + y2, pos.z + z2};
+  };
+  return shadow_chain(Q, sat, rS, y_pos, si, cond, box_at, boxes);
 }
 
 // ConeXAxis (:366-453)
 __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
-  float Stau = 0.0f;
   float signal = 1.0f;
   if (cv.x < 0) signal = -1.0f;
   const float p_cs = Q.p_cs, p_sn = Q.p_sn, n_cs = Q.n_cs, n_sn = Q.n_sn;
@@ -196,8 +316,11 @@ __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   const float d_y1 = fabsf(pj_y1.x), d_y2 = fabsf(pj_y2.x), d_z1 = fabsf(pj_z1.x), d_z2 = fabsf(pj_z2.x);
   const float r_y1 = 1.0f / d_y1, r_y2 = 1.0f / d_y2, r_z1 = 1.0f / d_z1, r_z2 = 1.0f / d_z2;
   const float rc = 1.0f / cv.x;
-  while (div_by_recip(x_pos, cv.x, rc) < Q.max_distance &&
-         (pos.x + (x_pos + si) > vmin && pos.x + (x_pos + si) < vmax)) {
+  auto cond = [&](float x_pos) {
+    return div_by_recip(x_pos, cv.x, rc) < Q.max_distance &&
+           (pos.x + (x_pos + si) > vmin && pos.x + (x_pos + si) < vmax);
+  };
+  auto box_at = [&](float x_pos, f3& p1, f3& p2) {
     const float x_mean = fabsf(x_pos + si * 0.5f);
     const float p_y1 = pj_y1.y * div_by_recip(x_mean, d_y1, r_y1);
     const float p_y2 = pj_y2.y * div_by_recip(x_mean, d_y2, r_y2);
@@ -212,11 +335,10 @@ __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
     y1 = y1 - ys * Q.S[1]; y2 = y2 + ys * Q.S[1];
     z1 = z1 - zs * Q.S[2]; z2 = z2 + zs * Q.S[2];
     const float x1 = fminf(x_pos, x_pos + si), x2 = fmaxf(x_pos, x_pos + si);
-    Stau += shadow_box(Q, sat, f3{pos.x + x1, pos.y + y1, pos.z + z1}, f3{pos.x + x2, pos.y + y2, pos.z + z2}, rS);
-    boxes++;
-    x_pos = x_pos + si;
-  }
-  return Stau;
+    p1 = f3{pos.x + x1, pos.y + y1, pos.z + z1};
+    p2 = f3{pos.x + x2, pos.y + y2, pos.z + z2};
+  };
+  return shadow_chain(Q, sat, rS, x_pos, si, cond, box_at, boxes);
 }
 
 }  // namespace

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Session 49: EBS chain pipeline depth (2 / 4 / 8 parts per box): parity of the default, A/B.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_ebs_gpu.py tests/test_fullsize_gpu.py -k "ebs or c5" -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r02_s49_tests.log 2>&1 || { tail -30 gpurun_out/r02_s49_tests.log; exit 1; }
+tail -1 gpurun_out/r02_s49_tests.log
+for A in prev np2 np8; do
+  bash tools/ab_bench.sh $A ebs512$A "--renderer ebs --size 512 --steps 5 --warmup 1" 2 || exit 1
+done
+bash tools/ab_bench.sh np2 ebs1024 "--renderer ebs --steps 2 --warmup 1" 1 || exit 1
