@@ -426,6 +426,9 @@ __device__ void iso_march(const IsoArgs& Q, const uint4* __restrict__ cells,
 #ifndef CVR_ISO_WAVES2
 #define CVR_ISO_WAVES2 8
 #endif
+#ifndef CVR_ISO_COLGROUP
+#define CVR_ISO_COLGROUP 4   // iso 2.11 -> 2.09 ms, isoadapt 1.494 -> 1.483, isodfs neutral (tools/r02_s56.sh)
+#endif
 template <int VARIANT, bool PHONG>
 constexpr int iso_waves_per_eu() {
   return PHONG ? 1 : (VARIANT == 0 ? CVR_ISO_WAVES0 : (VARIANT == 1 ? CVR_ISO_WAVES1 : CVR_ISO_WAVES2));
@@ -437,11 +440,10 @@ iso_tile_kernel(IsoArgs Q, const uint4* __restrict__ cells, const uint4* __restr
                 uint32_t* __restrict__ samples, unsigned long long* __restrict__ tile_samples) {
   const Rc1passArgs& A = Q.a;
   const int b = blockIdx.x, nt = A.ntiles;
-  // tile t on XCD t % 8 (interleaved screen order): every XCD gets a share of
-  // every screen region, so the long iso rays spread evenly (contiguous XCD
-  // bands measured 4-8 % slower)
-  const int t = b;
-  (void)nt;
+  // groups of 4 tile columns dealt round-robin over the XCDs: every XCD gets a
+  // share of every screen region, so the long iso rays spread evenly (contiguous
+  // XCD bands measured 4-8 % slower), and neighbouring tiles share an L2
+  const int t = screen_tile_of_block<CVR_ISO_COLGROUP>(A, b, nt);
   const int lane = threadIdx.x;
   int px, py;
   long long oidx;

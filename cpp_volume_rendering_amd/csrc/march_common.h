@@ -49,6 +49,26 @@ __device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lx, 
   }
 }
 
+// Workgroup b runs on XCD b % 8.  With t = b, tile column tx lands on XCD
+// tx % 8 (every tile row has a multiple of 8 tiles at the bench sizes), so a
+// tile's vertical neighbours share its XCD's L2 but its horizontal ones never
+// do.  With column groups of G, columns [G c, G c + G)
+// share an XCD instead, still dealt round-robin over the XCDs (balance), when
+// the row has a multiple of 8 G tiles; otherwise t = b.  The shaded marches
+// use G = 4 (CVR_SHADED_COLGROUP, tools/r02_s54.sh, frame ms, G = 1 -> 2 / 4 /
+// 8): EBS 512^3 28.5 -> 27.2 / 27.0 / 30.0, DOS 15.56 -> 15.31 / 14.81 / 14.99.
+template <int G>
+__device__ __forceinline__ int screen_tile_of_block(const Rc1passArgs& A, int b, int nt) {
+  if (G <= 1 || A.packed) return b;
+  const int ntx8 = (A.W + 7) >> 3;
+  if (ntx8 % (8 * G) != 0 || nt % ntx8 != 0) return b;
+  const int per_row = ntx8 >> 3;               // tiles of one XCD in one row
+  const int x = b & 7, j = b >> 3;
+  const int ty = j / per_row, rem = j - ty * per_row;
+  const int c = rem / G, r = rem - c * G;
+  return ty * ntx8 + (c * 8 + x) * G + r;
+}
+
 // ---------------------------------------------------------------------------
 // Sampling
 // ---------------------------------------------------------------------------

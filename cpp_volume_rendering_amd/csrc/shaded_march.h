@@ -48,26 +48,6 @@ __device__ __forceinline__ f3 cross3(f3 x, f3 y) {   // glm / GLSL cross, no fma
 #define CVR_SHADED_COLGROUP 4
 #endif
 
-// Workgroup b runs on XCD b % 8.  With t = b, tile column tx lands on XCD
-// tx % 8 (every tile row has a multiple of 8 tiles at the bench sizes), so a
-// tile's vertical neighbours share its XCD's L2 but its horizontal ones never
-// do.  With column groups of G (CVR_SHADED_COLGROUP), columns [G c, G c + G)
-// share an XCD instead, still dealt round-robin over the XCDs (balance), when
-// the row has a multiple of 8 G tiles; otherwise t = b.  G = 4 measured best
-// (tools/r02_s54.sh, frame ms, G = 1 -> 2 / 4 / 8): EBS 512^3 28.5 -> 27.2 /
-// 27.0 / 30.0, DOS 15.56 -> 15.31 / 14.81 / 14.99; EBS 1024^3 123.4 -> 122.9 at 4.
-__device__ __forceinline__ int screen_tile_of_block(const Rc1passArgs& A, int b, int nt) {
-  constexpr int G = CVR_SHADED_COLGROUP;
-  if (G <= 1 || A.packed) return b;
-  const int ntx8 = (A.W + 7) >> 3;
-  if (ntx8 % (8 * G) != 0 || nt % ntx8 != 0) return b;
-  const int per_row = ntx8 >> 3;               // tiles of one XCD in one row
-  const int x = b & 7, j = b >> 3;
-  const int ty = j / per_row, rem = j - ty * per_row;
-  const int c = rem / G, r = rem - c * G;
-  return ty * ntx8 + (c * 8 + x) * G + r;
-}
-
 // One wave = one 8x8 tile.
 template <class SH, bool PHONG>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH::kMinWavesPerEU)))
@@ -90,7 +70,7 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
   // column groups dealt round-robin over the XCDs: each XCD gets a share of
   // every screen region, so the costly shading regions spread over all XCDs
   // (contiguous XCD bands: DOS kernel 23.5 vs 21.1 ms, EBS 512^3 42.0 vs 35.1 ms)
-  const int t = screen_tile_of_block(A, b, nt);
+  const int t = screen_tile_of_block<CVR_SHADED_COLGROUP>(A, b, nt);
   const int lane = threadIdx.x;
   int px, py;
   long long oidx;
