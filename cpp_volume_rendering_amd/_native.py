@@ -19,6 +19,9 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libc
 # tools/ab_builds.sh: A/B timing of two builds of the library in one GPU session
 LIB_PATH = os.environ.get("CVR_LIB_OVERRIDE", LIB_PATH)
 
+# include/cvr.h CVR_ABI_VERSION: the struct layouts declared below
+ABI_VERSION = 2
+
 CVR_OK, CVR_ERR_ARG, CVR_ERR_HIP, CVR_ERR_OOM, CVR_ERR_STATE, CVR_ERR_IO = range(6)
 GRADIENT_NONE, GRADIENT_FINITE_DIFFERENCES, GRADIENT_SOBEL_FELDMAN = 0, 1, 2
 
@@ -219,6 +222,10 @@ def lib() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    got = L.cvr_abi_version()
+    if got != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI version {got}, this binding declares {ABI_VERSION} "
+                          "(struct layouts differ; rebuild the library)")
     _lib = L
     return L
 

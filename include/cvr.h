@@ -54,7 +54,11 @@
 extern "C" {
 #endif
 
-#define CVR_ABI_VERSION 1
+/* Bumped whenever a public struct's layout or an entry point's meaning changes
+ * (2: cvr_frame gained use_view/view).  Callers compare cvr_abi_version() with
+ * the CVR_ABI_VERSION they were compiled against before the first call that
+ * passes a struct. */
+#define CVR_ABI_VERSION 2
 
 typedef enum cvr_status {
   CVR_OK = 0,

@@ -15,6 +15,29 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+# Run order of the GPU suites under `-x`: the headline parity first, the 1024^3 /
+# 2048^2 full-size cases last, so one full-size failure (or OOM) never hides the
+# faster parity rows. Files not listed keep their collection order in between.
+_SUITE_ORDER = ("test_rc1pass_gpu.py", "test_postpass_gpu.py", "test_split_gpu.py",
+                "test_dos_gpu.py", "test_ebs_gpu.py", "test_iso_gpu.py",
+                "test_selftest_gpu.py")
+_SUITE_LAST = ("test_fullsize_gpu.py",)
+
+
+def _suite_rank(item):
+    name = os.path.basename(str(item.fspath))
+    if name in _SUITE_ORDER:
+        return _SUITE_ORDER.index(name)
+    if name in _SUITE_LAST:
+        return len(_SUITE_ORDER) + 1 + _SUITE_LAST.index(name)
+    return len(_SUITE_ORDER)
+
+
+def pytest_collection_modifyitems(session, config, items):
+    # sorted() is stable: tests inside one file keep their own order.
+    items[:] = sorted(items, key=_suite_rank)
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     assert sorted(N.EXPORTED_SYMBOLS) == declared
     for name in declared:
         assert hasattr(L, name), name
-    assert L.cvr_abi_version() == 1
+    assert L.cvr_abi_version() == N.ABI_VERSION == 2
 
 
 def test_status_strings():
