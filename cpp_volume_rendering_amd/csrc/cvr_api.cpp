@@ -316,6 +316,13 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     for (auto& o : c->oslot) o.valid = 0;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "filter_bits")) {
+    if (value != 0 && value != 8)
+      return fail(c, CVR_ERR_ARG, "filter_bits must be 0 (exact weights) or 8 (texture-unit weights)");
+    c->filter_bits = value;
+    for (auto& o : c->oslot) o.valid = 0;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "sat_chunk")) {
     if (value < 1 || value > 64) return fail(c, CVR_ERR_ARG, "sat_chunk must be 1..64");
     c->sat_chunk = value;
@@ -426,6 +433,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "shade_counters")) return c->shade_counters;
   if (!std::strcmp(key, "sat_chunk")) return c->sat_chunk;
   if (!std::strcmp(key, "quad")) return c->quad_pct;
+  if (!std::strcmp(key, "filter_bits")) return c->filter_bits;
   if (!std::strcmp(key, "kernel_timing")) return (int)c->ev_start.size();
   return -1;
 }
@@ -742,6 +750,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   fill_frame_args(c, f, p->step, A, plan.ntiles, npix);
   A.ka = p->ka; A.kd = p->kd; A.ks = p->ks; A.shininess = p->shininess;
   for (int i = 0; i < 3; i++) { A.ispec[i] = p->ispecular[i]; A.light[i] = p->light_pos[i]; }
+  A.filter_bits = c->filter_bits;
   A.tile_stats = nullptr;
   A.cost_time = c->cost_time;
   A.occ = nullptr;
@@ -775,7 +784,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     HIP_TRY(c, hipMemsetAsync(c->d_shade, 0, 3 * sizeof(unsigned long long), c->stream));
     A.shade_ctr = c->d_shade;
   }
-  plan.quad_pct = c->quad_pct;
+  plan.quad_pct = c->filter_bits ? 0 : c->quad_pct;   // the quad march has no filter_bits variant
   {
     // Bands are cut by predicted work, so one may hold more than 1/8 of the
     // tiles: up to 2x the even share (the epilogue falls back to even bands
@@ -1250,6 +1259,8 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_dosct: null argument");
+  if (c->filter_bits)
+    return fail(c, CVR_ERR_ARG, "cvr_render_dosct: filter_bits %d is implemented for cvr_render_rc1pass only", c->filter_bits);
   if (o->format != CVR_FORMAT_RGBA32F && o->format != CVR_FORMAT_RGBA16F)
     return fail(c, CVR_ERR_ARG, "cvr_render_dosct: unknown output format %d", o->format);
   if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
@@ -1459,6 +1470,8 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: null argument");
+  if (c->filter_bits)
+    return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: filter_bits %d is implemented for cvr_render_rc1pass only", c->filter_bits);
   if (o->format != CVR_FORMAT_RGBA32F && o->format != CVR_FORMAT_RGBA16F)
     return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: unknown output format %d", o->format);
   if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
@@ -1514,6 +1527,7 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
   const float ang = (float)(p->shadow_cone_angle_deg * 3.14159265358979323846 / 180.0);
   Q.p_cs = std::cos(ang); Q.p_sn = std::sin(ang);
   Q.n_cs = std::cos(-ang); Q.n_sn = std::sin(-ang);
+  Q.recip_cone = std::fabs(p->shadow_cone_angle_deg) <= 44.0f;
   Q.interval = p->shadow_sample_interval;
   Q.initial_step = p->shadow_initial_step;
   Q.ui_weight = p->shadow_ui_weight;
@@ -1624,6 +1638,8 @@ cvr_status cvr_render_iso(cvr_ctx* ctx, const cvr_frame* f, const cvr_iso_params
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_iso: null argument");
+  if (c->filter_bits)
+    return fail(c, CVR_ERR_ARG, "cvr_render_iso: filter_bits %d is implemented for cvr_render_rc1pass only", c->filter_bits);
   if (o->format != CVR_FORMAT_RGBA32F && o->format != CVR_FORMAT_RGBA16F)
     return fail(c, CVR_ERR_ARG, "cvr_render_iso: unknown output format %d", o->format);
   if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)

@@ -175,8 +175,10 @@ struct f3 { float x, y, z; };
 // a / b correctly rounded from y = 1.0f / b (itself correctly rounded), for a
 // divisor reused many times: q = RN(a*y), the remainder a - b*q is exact by fma,
 // and RN(q + r*y) = RN(a/b) (Markstein's correction; valid while a/b, a*y and the
-// remainder stay in the normal range -- callers pass finite a >= 0 of moderate
-// size and b in the normal range).  Checked against IEEE division in
+// remainder stay in the normal range -- callers pass finite a of moderate size,
+// either sign (RN is symmetric, so a / b and -a / b round alike), and b, 1/b in
+// the normal range; a divisor that may approach 0 needs the IEEE division, see
+// ebs.hip cone_div).  Checked against IEEE division in
 // tests/test_exact_div.py.
 __device__ __forceinline__ float div_by_recip(float a, float b, float y) {
   const float q = a * y;

@@ -56,6 +56,10 @@ struct Rc1passArgs {
   const uint8_t* occ;
   int mdim[3];                       // macro cells per axis
   int mshift;                        // macro cell = 2^mshift texels a side
+  // GL texture-unit filter mode (option "filter_bits"): 0 = exact float weights
+  // (CVR-SPEC), 8 = every GL_LINEAR weight (volume, gradient, TF) rounded to 8
+  // fraction bits, as GPU texture units filter (CVR-SPEC-8)
+  int filter_bits;
 };
 
 constexpr int kMaxTfLds = 4096;          // TF entries a kernel stages into LDS
@@ -123,6 +127,7 @@ struct EbsArgs {
   float ao_wa;
   int apply_shadow, shadow_type, phong;
   float p_cs, p_sn, n_cs, n_sn;      // cos / sin of +-DirSdwConeAngle
+  int recip_cone;                    // cone angle <= 44 deg: cone-edge divisions by reciprocal (ebs.hip cone_div)
   float interval, initial_step, ui_weight, max_distance;
   float lfwd[3];
   float ka, kd, ks;                  // Kambient if occlusion, Kdiffuse/Kspecular if shadow, else 0
@@ -196,6 +201,7 @@ struct Ctx {
   int epi_stop = 0;                // diagnostics (option "debug_epi_stop")
   int debug_keep = 0;              // diagnostics (option "debug_keep"): render only the longest entries
   int boost_pct = 5;               // % of every band's longest entries run at raised priority
+  int filter_bits = 0;             // GL_LINEAR weights at this many fraction bits (0 = exact; rc1pass)
   int quad_pct = 0;                // % of every band's longest tiles marched 4 lanes per ray
   int shade_counters = 0;          // DOS/EBS: count shaded and shadow-lit samples
   unsigned long long* d_shade = nullptr;   // [3]: shaded, lit, secondary fetches (last frame)

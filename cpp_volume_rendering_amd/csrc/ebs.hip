@@ -55,6 +55,17 @@ __device__ __forceinline__ f3 sat_offset(const EbsArgs& Q, f3 p) {
             fminf(fmaxf(p.z + Q.S[2], Q.min_sat[2]), Q.max_sat[2])};
 }
 
+// z_mean / d of a cone edge: by the reciprocal (div_by_recip, exact for a normal
+// d and 1/d) when the host has proven d >= cos(89 deg) for every sample (cone
+// angle <= 44 deg: the dominant-axis projection is within 45 deg of its axis and
+// the cone turns it by at most the cone angle), else the IEEE division (d -> 0
+// as the cone angle nears 90 deg: z_mean / 0 = inf, where the reciprocal path
+// would give NaN).
+template <bool R>
+__device__ __forceinline__ float cone_div(float a, float d, float rd) {
+  return R ? div_by_recip(a, d, rd) : a / d;
+}
+
 // EvaluateShadowSAT3D (:148-185, the texture path)
 __device__ __forceinline__ float shadow_box(const EbsArgs& Q, const float4* __restrict__ sat, f3 p1, f3 p2,
                                            f3 rS) {
@@ -210,6 +221,7 @@ __device__ float ebs_occlusion(const EbsArgs& Q, const float4* __restrict__ sat,
 }
 
 // ConeZAxis (:187-275)
+template <bool R>
 __device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
   float signal = 1.0f;
@@ -234,10 +246,10 @@ __device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   };
   auto box_at = [&](float z_pos, f3& p1, f3& p2) {
     const float z_mean = fabsf(z_pos + si * 0.5f);
-    const float p_x1 = pj_x1.x * div_by_recip(z_mean, d_x1, r_x1);
-    const float p_x2 = pj_x2.x * div_by_recip(z_mean, d_x2, r_x2);
-    const float p_y1 = pj_y1.y * div_by_recip(z_mean, d_y1, r_y1);
-    const float p_y2 = pj_y2.y * div_by_recip(z_mean, d_y2, r_y2);
+    const float p_x1 = pj_x1.x * cone_div<R>(z_mean, d_x1, r_x1);
+    const float p_x2 = pj_x2.x * cone_div<R>(z_mean, d_x2, r_x2);
+    const float p_y1 = pj_y1.y * cone_div<R>(z_mean, d_y1, r_y1);
+    const float p_y2 = pj_y2.y * cone_div<R>(z_mean, d_y2, r_y2);
     float x1 = fminf(p_x1, p_x2), x2 = fmaxf(p_x1, p_x2);
     float y1 = fminf(p_y1, p_y2), y2 = fmaxf(p_y1, p_y2);
     const float xdiff = fabsf(x2 - x1), ydiff = fabsf(y2 - y1);
@@ -254,6 +266,7 @@ __device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
 }
 
 // ConeYAxis (:277-364)
+template <bool R>
 __device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
   float signal = 1.0f;
@@ -278,10 +291,10 @@ __device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   };
   auto box_at = [&](float y_pos, f3& p1, f3& p2) {
     const float y_mean = fabsf(y_pos + si * 0.5f);
-    const float p_x1 = pj_x1.x * div_by_recip(y_mean, d_x1, r_x1);
-    const float p_x2 = pj_x2.x * div_by_recip(y_mean, d_x2, r_x2);
-    const float p_z1 = pj_z1.z * div_by_recip(y_mean, d_z1, r_z1);
-    const float p_z2 = pj_z2.z * div_by_recip(y_mean, d_z2, r_z2);
+    const float p_x1 = pj_x1.x * cone_div<R>(y_mean, d_x1, r_x1);
+    const float p_x2 = pj_x2.x * cone_div<R>(y_mean, d_x2, r_x2);
+    const float p_z1 = pj_z1.z * cone_div<R>(y_mean, d_z1, r_z1);
+    const float p_z2 = pj_z2.z * cone_div<R>(y_mean, d_z2, r_z2);
     float x1 = fminf(p_x1, p_x2), x2 = fmaxf(p_x1, p_x2);
     float z1 = fminf(p_z1, p_z2), z2 = fmaxf(p_z1, p_z2);
     const float xdiff = fabsf(x2 - x1), zdiff = fabsf(z2 - z1);
@@ -298,6 +311,7 @@ __device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
 }
 
 // ConeXAxis (:366-453)
+template <bool R>
 __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
   float signal = 1.0f;
@@ -322,10 +336,10 @@ __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
   };
   auto box_at = [&](float x_pos, f3& p1, f3& p2) {
     const float x_mean = fabsf(x_pos + si * 0.5f);
-    const float p_y1 = pj_y1.y * div_by_recip(x_mean, d_y1, r_y1);
-    const float p_y2 = pj_y2.y * div_by_recip(x_mean, d_y2, r_y2);
-    const float p_z1 = pj_z1.z * div_by_recip(x_mean, d_z1, r_z1);
-    const float p_z2 = pj_z2.z * div_by_recip(x_mean, d_z2, r_z2);
+    const float p_y1 = pj_y1.y * cone_div<R>(x_mean, d_y1, r_y1);
+    const float p_y2 = pj_y2.y * cone_div<R>(x_mean, d_y2, r_y2);
+    const float p_z1 = pj_z1.z * cone_div<R>(x_mean, d_z1, r_z1);
+    const float p_z2 = pj_z2.z * cone_div<R>(x_mean, d_z2, r_z2);
     float y1 = fminf(p_y1, p_y2), y2 = fmaxf(p_y1, p_y2);
     float z1 = fminf(p_z1, p_z2), z2 = fmaxf(p_z1, p_z2);
     const float ydiff = fabsf(y2 - y1), zdiff = fabsf(z2 - z1);
@@ -346,7 +360,8 @@ __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
 #ifndef CVR_EBS_WAVES
 #define CVR_EBS_WAVES 1
 #endif
-struct EbsShader {
+template <bool RECIP_CONE>
+struct EbsShaderT {
   using Args = EbsArgs;
   static constexpr int kMinWavesPerEU = CVR_EBS_WAVES;   // register budget (1: compiler's choice)
   using Data = const float4*;   // the float SAT, cell8
@@ -369,9 +384,9 @@ struct EbsShader {
       const f3 ac{fabsf(cv.x), fabsf(cv.y), fabsf(cv.z)};
       float Stau;
       uint32_t boxes = 0;
-      if (ac.z > ac.x && ac.z > ac.y) Stau = cone_z(Q, sat, tx, cv, boxes);
-      else if (ac.y > ac.x) Stau = cone_y(Q, sat, tx, cv, boxes);
-      else Stau = cone_x(Q, sat, tx, cv, boxes);
+      if (ac.z > ac.x && ac.z > ac.y) Stau = cone_z<RECIP_CONE>(Q, sat, tx, cv, boxes);
+      else if (ac.y > ac.x) Stau = cone_y<RECIP_CONE>(Q, sat, tx, cv, boxes);
+      else Stau = cone_x<RECIP_CONE>(Q, sat, tx, cv, boxes);
       fetches += 8 * boxes;
       isdw = cvr_expf(-Stau);
       lit++;
@@ -401,8 +416,11 @@ struct EbsShader {
 
 hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
-  return launch_shaded_march<EbsShader>(c, q, q.phong != 0, c.d_sat_cells, out, samples, shade,
-                                        tile_samples, s);
+  if (q.recip_cone)
+    return launch_shaded_march<EbsShaderT<true>>(c, q, q.phong != 0, c.d_sat_cells, out, samples, shade,
+                                                 tile_samples, s);
+  return launch_shaded_march<EbsShaderT<false>>(c, q, q.phong != 0, c.d_sat_cells, out, samples, shade,
+                                                tile_samples, s);
 }
 
 }  // namespace cvr

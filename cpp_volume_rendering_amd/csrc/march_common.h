@@ -144,13 +144,30 @@ __device__ __forceinline__ float trilerp_cell(uint4 raw, float ax, float ay, flo
   return lerpf(c0, c1, az);
 }
 
+// A GL_LINEAR weight at FB fraction bits (FB = 0: the exact float weight).
+// rint(a * 2^FB) * 2^-FB: both scalings are exact, rint rounds half to even
+// (the literal reading's nearbyint, oracle/glsl_literal.cpp weight()).
+template <int FB>
+__device__ __forceinline__ float filter_weight(float a) {
+  if (FB == 0) return a;
+  return __builtin_rintf(a * (float)(1 << FB)) * (1.0f / (float)(1 << FB));
+}
+
+template <int FB>
+__device__ __forceinline__ void quantise_weights(SamplePos& p) {
+  p.ax = filter_weight<FB>(p.ax);
+  p.ay = filter_weight<FB>(p.ay);
+  p.az = filter_weight<FB>(p.az);
+}
+
 // texture(TexTransferFunc, density) from the padded LDS table: x = d*n - 0.5
 // reads the adjacent entries tfp[floor(x)+1], tfp[floor(x)+2]; d in [0,1]
 // (a lerp of [0,1] values) keeps floor(x)+1 in [0, n].
+template <int FB = 0>
 __device__ __forceinline__ float4 classify(const float4* __restrict__ tfp, float fn, float dens) {
   float x = fmaf(dens, fn, -0.5f);
   float fl = floorf(x);
-  float a = x - fl;
+  float a = filter_weight<FB>(x - fl);
   int i = (int)fl + 1;
   float4 t0 = tfp[i], t1 = tfp[i + 1];
   return make_float4(lerpf(t0.x, t1.x, a), lerpf(t0.y, t1.y, a), lerpf(t0.z, t1.z, a),

@@ -22,6 +22,7 @@
 // small HBM-bound passes (8 B per pixel in, 8 B out, x the kernel's footprint
 // served from L2).
 #include <hip/hip_runtime.h>
+#include <atomic>
 
 #include <algorithm>
 #include <type_traits>
@@ -1084,8 +1085,13 @@ hipError_t launch_digital(int kernel, uint2* img, int w, int h, hipStream_t s) {
     const size_t lds = seg_lds_bytes(shift, nseg);
     const int items = (4 << shift) * nseg;
     if (lds <= kSegLdsMax && items <= 8 * kSegMaxThreads) {
-      static bool attr = false;   // dynamic LDS beyond 64 KiB must be allowed per kernel
-      if (!attr) {
+      // the dynamic-LDS limit is a per-device kernel attribute: set it once per
+      // device (a bit per device id; two threads setting it together is harmless)
+      static std::atomic<uint64_t> attr_devices{0};
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+      const uint64_t bit = 1ull << (dev & 63);
+      if (!(attr_devices.load(std::memory_order_acquire) & bit)) {
         hipError_t e = hipFuncSetAttribute(
             reinterpret_cast<const void*>(&digital_filter_seg_kernel<LCbs>),
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLdsMax);
@@ -1093,7 +1099,7 @@ hipError_t launch_digital(int kernel, uint2* img, int w, int h, hipStream_t s) {
           e = hipFuncSetAttribute(reinterpret_cast<const void*>(&digital_filter_seg_kernel<LOmoms>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSegLdsMax);
         if (e != hipSuccess) return e;
-        attr = true;
+        attr_devices.fetch_or(bit, std::memory_order_acq_rel);
       }
       const int thr = std::min(kSegMaxThreads, (items + 63) / 64 * 64);
       const dim3 g((lines + (1 << shift) - 1) >> shift), b(thr);
@@ -1138,7 +1144,9 @@ hipError_t launch_multiscale(int mode, int kernel, void* frame, int fw, int fh, 
     const float sup = support[kernel];
     const size_t side = (size_t)((16.0f + sup) * fr) + 4;
     const size_t lds = (side | 1) * side * sizeof(uint2);
-    if (sup * fr + 2.0f <= (float)kDownMaxTaps && lds <= 64 * 1024) {
+    // the kernel's static weight tables (wcol, wrow) share the 64 KiB with the window
+    constexpr size_t kDownStaticLds = sizeof(float) * 2 * 16 * kDownMaxTaps;
+    if (sup * fr + 2.0f <= (float)kDownMaxTaps && lds + kDownStaticLds <= 64 * 1024) {
       CVR_KERNEL_SWITCH_LDS(downscale_lds_kernel, kernel, g, b, lds, s, src, fw, fh, dst, sw, sh);
     } else {
       CVR_KERNEL_SWITCH(downscale_kernel, kernel, g, b, s, src, fw, fh, dst, sw, sh);

@@ -74,7 +74,7 @@ __device__ __forceinline__ bool skip_empty(const Rc1passArgs& A, const Ray& r, f
 // Ray-parallel march (one lane per ray) of ray_marching_1p.comp:124-172.  The
 // arithmetic per sample is exactly the reference's sequential loop (s
 // accumulates h one step at a time); batching only changes when loads issue.
-template <int K, bool PHONG, bool SKIP, bool XF, bool BUF>
+template <int K, bool PHONG, bool SKIP, bool XF, bool BUF, int FB>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
                                           const uint4* __restrict__ grad,
                                           const float4* __restrict__ tfp, int px, int py,
@@ -173,6 +173,10 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
         raw[j] = load_cell(sp[j].idx);
       }
     }
+    if (FB) {   // GL texture-unit weights (filter_bits): volume and gradient fetches
+#pragma unroll
+      for (int j = 0; j < K; j++) quantise_weights<FB>(sp[j]);
+    }
     // stage 2: density and transfer-function classification
     float4 src[K];
     // Emission-absorption: alpha first (two 4-B LDS reads); the rgb lerps (two
@@ -184,14 +188,14 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       for (int j = 0; j < K; j++) {
         const float xd = fmaf(trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az), fn, -0.5f);
         const float fl = floorf(xd);
-        tfa[j] = xd - fl;
+        tfa[j] = filter_weight<FB>(xd - fl);
         tfi[j] = (int)fl + 1;
         src[j].w = lerpf(tfp[tfi[j]].w, tfp[tfi[j] + 1].w, tfa[j]);
       }
     } else
 #pragma unroll
     for (int j = 0; j < K; j++)
-      src[j] = classify(tfp, fn, trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az));
+      src[j] = classify<FB>(tfp, fn, trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az));
     bool visible = false;
     // stage 3: front-to-back composite + ERT, in sample order.  The branches
     // matter: a wave whose samples are all transparent (empty space) skips
@@ -377,7 +381,7 @@ constexpr int rc1_waves_per_eu() {
   return (K == 4 && !PHONG && !SKIP && !QUAD) ? 8 : 1;
 #endif
 }
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, bool BUF>
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, bool BUF, int FB>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rc1_waves_per_eu<K, PHONG, SKIP, QUAD>())))
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
@@ -412,7 +416,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     const bool inside = px < A.W && py < A.H;
     dst = make_float4(0.f, 0.f, 0.f, 0.f);
     cnt = 0;
-    if (inside) march_ray<K, PHONG, SKIP, XF, BUF>(A, cells, grad, tfp, px, py, dst, cnt, nshade);
+    if (inside) march_ray<K, PHONG, SKIP, XF, BUF, FB>(A, cells, grad, tfp, px, py, dst, cnt, nshade);
     writer = inside || A.packed;
   } else {                    // quarter of a tile, four lanes per ray
     const int ray = lane >> 2;
@@ -673,7 +677,7 @@ __global__ void clear_u32_kernel(uint32_t* __restrict__ p, int n) {
 // Kernel variant: K (batch), PHONG, SKIP (empty-space skipping compiled in),
 // QUAD (quad path compiled in), XF (range-free exp).  Paths a frame does not
 // use are compiled out: they would cost the hot loop registers (occupancy).
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, bool BUF>
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, bool BUF, int FB = 0>
 static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                                  unsigned long long* tile_samples, const int* order,
                                  uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
@@ -682,7 +686,7 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
   // cell (1,1,1) <-> texel (0,0,0)
   const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
   int grid = order ? plan.order_slots : plan.ntiles;
-  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF>), dim3(grid), dim3(64), lds, s,
+  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF, FB>), dim3(grid), dim3(64), lds, s,
                      a, cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, out, samples,
                      tile_samples, order, tile_cost, order ? plan.boost : 0);
   return hipGetLastError();
@@ -692,6 +696,13 @@ template <int K, bool PHONG, bool SKIP>
 static hipError_t launch_kps(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                              unsigned long long* ts, const int* order, uint32_t* tile_cost,
                              const RenderPlan& plan, hipStream_t s) {
+  if (a.filter_bits == 8) {   // GL texture-unit weights: the ray-parallel march only
+    if (c.cells_bytes < (size_t(1) << 32))
+      return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, true, 8>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                        : launch_variant<K, PHONG, SKIP, false, false, true, 8>(c, a, out, samples, ts, order, tile_cost, plan, s);
+    return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, false, 8>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                      : launch_variant<K, PHONG, SKIP, false, false, false, 8>(c, a, out, samples, ts, order, tile_cost, plan, s);
+  }
   const bool quad = order && plan.quad_pct > 0;
   if (quad)
     return a.exp_fast ? launch_variant<K, PHONG, SKIP, true, true, false>(c, a, out, samples, ts, order, tile_cost, plan, s)

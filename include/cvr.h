@@ -276,7 +276,13 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                (cvr_read_kernel_times); 0 off (default)
  *   "sat_chunk"  z planes per work item of the EBS SAT build (1..64, default 32)
  *   "shade_counters" 1: count shaded / shadow-lit samples of cvr_render_dosct
- *                and cvr_render_extbsd (cvr_read_shade_counters; one atomic per wave) */
+ *                and cvr_render_extbsd (cvr_read_shade_counters; one atomic per wave)
+ * One option changes the arithmetic (and so the image) rather than the speed:
+ *   "filter_bits" 0: exact float GL_LINEAR weights (CVR-SPEC, the default);
+ *                8: every GL_LINEAR weight of cvr_render_rc1pass (volume, gradient,
+ *                TF; ray_marching_1p.comp:133, :138) rounded to 8 fraction bits, the
+ *                fixed-point weights of GPU texture units (CVR-SPEC-8).  The other
+ *                renderers return CVR_ERR_ARG while it is set. */
 cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
 int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);

@@ -364,15 +364,26 @@ ORACLE_API void oracle_gradient_sobel(const void* vox, int bpv, int w, int h, in
 
 namespace {
 
+// A GL_LINEAR weight at `bits` fraction bits (0: exact): the fixed-point filter
+// weights of GPU texture units, rounded to nearest even (CVR-SPEC-8, the
+// library's filter_bits option; glsl_literal.cpp weight() rounds the same way).
+inline float filter_weight(float a, int bits) {
+  if (bits <= 0) return a;
+  const float s = std::ldexp(1.0f, bits);
+  return std::nearbyint(a * s) * (1.0f / s);
+}
+
 struct Tex {
   const float* v; int N[3]; int comps;
+  int wbits = 0;   // filter_weight fraction bits
   // trilinear, clamp-to-edge, texel-centre convention; x,y,z already in texel space
   inline void sample(float x, float y, float z, float* out) const {
     float cx = std::fmin(std::fmax(x, -1.0f), (float)(N[0] - 1));
     float cy = std::fmin(std::fmax(y, -1.0f), (float)(N[1] - 1));
     float cz = std::fmin(std::fmax(z, -1.0f), (float)(N[2] - 1));
     float flx = std::floor(cx), fly = std::floor(cy), flz = std::floor(cz);
-    float ax = cx - flx, ay = cy - fly, az = cz - flz;
+    float ax = filter_weight(cx - flx, wbits), ay = filter_weight(cy - fly, wbits),
+          az = filter_weight(cz - flz, wbits);
     int ix = (int)flx, iy = (int)fly, iz = (int)flz;
     int x0 = std::max(ix, 0), x1 = std::min(ix + 1, N[0] - 1);
     int y0 = std::max(iy, 0), y1 = std::min(iy + 1, N[1] - 1);
@@ -393,11 +404,11 @@ struct Tex {
 };
 
 // texture(TexTransferFunc, density): 1D linear, clamp-to-edge, x = u*n - 0.5
-inline void tf_lookup(const float* tf, int n, float density, float out[4]) {
+inline void tf_lookup(const float* tf, int n, float density, float out[4], int wbits = 0) {
   float x = std::fmaf(density, (float)n, -0.5f);
   x = std::fmin(std::fmax(x, -1.0f), (float)(n - 1));
   float fl = std::floor(x);
-  float a = x - fl;
+  float a = filter_weight(x - fl, wbits);
   int i = (int)fl;
   int i0 = std::max(i, 0), i1 = std::min(i + 1, n - 1);
   for (int c = 0; c < 4; c++) out[c] = lerpf(tf[i0 * 4 + c], tf[i1 * 4 + c], a);
@@ -417,8 +428,8 @@ static void rc1pass_rows(const OracleRc1pass& P, int y0, int y1, float* out, uin
   const v3 half = mk(G.x * 0.5f, G.y * 0.5f, G.z * 0.5f);
   const v3 NoG = mk((float)P.N[0] / G.x, (float)P.N[1] / G.y, (float)P.N[2] / G.z);
   const v3 light = mk(P.light[0], P.light[1], P.light[2]);
-  Tex vol{P.vol, {P.N[0], P.N[1], P.N[2]}, 1};
-  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3};
+  Tex vol{P.vol, {P.N[0], P.N[1], P.N[2]}, 1, P.filter_bits};
+  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3, P.filter_bits};
   const float step = P.step;
   const int W = P.W, H = P.H;
 #ifdef _OPENMP
@@ -463,7 +474,7 @@ static void rc1pass_rows(const OracleRc1pass& P, int y0, int y1, float* out, uin
           float dens;
           vol.sample(x, y, z, &dens);
           float src[4];
-          tf_lookup(P.tf, P.tf_n, dens, src);
+          tf_lookup(P.tf, P.tf_n, dens, src, P.filter_bits);
           cnt++;
           if (src[3] > 0.0f) {
             if (P.phong && P.grad) {

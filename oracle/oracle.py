@@ -24,7 +24,8 @@ class OracleRc1pass(ctypes.Structure):
                 ("aspect", ctypes.c_float), ("W", ctypes.c_int), ("H", ctypes.c_int),
                 ("step", ctypes.c_float), ("phong", ctypes.c_int), ("ka", ctypes.c_float),
                 ("kd", ctypes.c_float), ("ks", ctypes.c_float), ("shininess", ctypes.c_float),
-                ("ispec", ctypes.c_float * 3), ("light", ctypes.c_float * 3)]
+                ("ispec", ctypes.c_float * 3), ("light", ctypes.c_float * 3),
+                ("filter_bits", ctypes.c_int)]
 
 
 class OracleExtVol(ctypes.Structure):
@@ -221,11 +222,13 @@ def _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shini
 def render_rc1pass(vol16: np.ndarray, scale, tf: np.ndarray, camera: dict, W: int, H: int,
                    step: float, grad: np.ndarray | None = None, phong: bool = False,
                    ka=0.5, kd=0.5, ks=0.8, shininess=30.0, ispec=(1.0, 1.0, 1.0),
-                   light=(0.0, 0.0, 0.0), threads: int = 0, rows=None, literal=None):
+                   light=(0.0, 0.0, 0.0), threads: int = 0, rows=None, literal=None,
+                   filter_bits: int = 0):
     """Full frame (or rows=(y0,y1)) of ray_marching_1p.comp. Returns (rgba HxWx4, counts HxW, S).
-    literal=None: CVR-SPEC (what the HIP kernels reproduce bit for bit); literal=b: the
-    literal GLSL reading (glsl_literal.cpp) with GL filter weights quantised to b fraction
-    bits (0 = exact float weights)."""
+    literal=None: CVR-SPEC (what the HIP kernels reproduce bit for bit), with every GL_LINEAR
+    weight rounded to `filter_bits` fraction bits (0 = exact: CVR-SPEC; 8 = CVR-SPEC-8, the
+    library's filter_bits option); literal=b: the literal GLSL reading (glsl_literal.cpp)
+    with GL filter weights quantised to b fraction bits (0 = exact float weights)."""
     vol16 = np.ascontiguousarray(vol16, np.float32)
     # the TF texture is GL_RGBA16F (GenerateTexture_1D_RGBt): entries round to half (RNE)
     tf = np.ascontiguousarray(np.asarray(tf, np.float32).astype(np.float16), np.float32)
@@ -233,6 +236,7 @@ def render_rc1pass(vol16: np.ndarray, scale, tf: np.ndarray, camera: dict, W: in
         grad = np.ascontiguousarray(grad, np.float32)
     P = _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shininess, ispec,
                 light, aspect=camera.get("aspect", 0.0))
+    P.filter_bits = int(filter_bits)
     rgba = np.zeros((H, W, 4), np.float32)
     cnt = np.zeros((H, W), np.uint32)
     if literal is not None:
@@ -499,3 +503,26 @@ def check_div_by_recip(n: int, seed: int = 1, lo: int = -20, hi: int = 20) -> in
     """Mismatches of the reciprocal-corrected division (cvr_device.h div_by_recip) against
     IEEE a / b over n random pairs (a = +-m * 2^-e, e in [lo, hi]; b = +-m * 2^[-8, 8])."""
     return int(lib().oracle_check_div_by_recip(n, seed, lo, hi))
+
+
+def finite_shaded_bands(rgba: np.ndarray, band: int, need: int, max_bands: int = 4):
+    """Row bands of a frame where the parity check compares real shading: up to
+    `max_bands` non-overlapping `band`-row windows, richest first in pixels that are
+    shaded (alpha > 0) and finite in every channel, until `need` such pixels are covered.
+    (The EBS frame at 1024^3 is mostly inf/NaN -- the float-SAT cancellation of
+    ebsrenderer.cpp:700-716 -- so a centre band would compare NaN with NaN.)
+    Returns [(y0, y1), ...] and the count of finite shaded pixels they hold."""
+    ok = np.isfinite(rgba).all(-1) & (rgba[..., 3] > 0)
+    per_row = ok.sum(1).astype(np.int64)
+    win = np.convolve(per_row, np.ones(band, np.int64), mode="valid")   # win[y] = rows y..y+band-1
+    taken = np.zeros(per_row.shape[0], bool)
+    bands, got = [], 0
+    for y in np.argsort(-win, kind="stable"):
+        if len(bands) == max_bands or got >= need or win[y] == 0:
+            break
+        if taken[y:y + band].any():
+            continue
+        taken[y:y + band] = True
+        bands.append((int(y), int(y) + band))
+        got += int(win[y])
+    return sorted(bands), got

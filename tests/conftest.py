@@ -18,7 +18,7 @@ def pytest_configure(config):
 # Run order of the GPU suites under `-x`: the headline parity first, the 1024^3 /
 # 2048^2 full-size cases last, so one full-size failure (or OOM) never hides the
 # faster parity rows. Files not listed keep their collection order in between.
-_SUITE_ORDER = ("test_rc1pass_gpu.py", "test_postpass_gpu.py", "test_split_gpu.py",
+_SUITE_ORDER = ("test_rc1pass_gpu.py", "test_filter8_gpu.py", "test_postpass_gpu.py", "test_split_gpu.py",
                 "test_dos_gpu.py", "test_ebs_gpu.py", "test_iso_gpu.py",
                 "test_selftest_gpu.py")
 _SUITE_LAST = ("test_fullsize_gpu.py",)

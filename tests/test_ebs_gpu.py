@@ -103,6 +103,10 @@ EBS_CASES = {
     "phong": dict(phong=True),
     "wide_cone": dict(angle=12.0, interval=3.0, initial=1.0, weight=0.7, shells=6, radius=1.5,
                       max_distance=150.0),
+    # cone angles past 44 deg take the IEEE division for the cone edges (ebs.hip
+    # cone_div): the edge's axis component d can reach 0 near 90 deg
+    "cone_60": dict(angle=60.0, max_distance=60.0),
+    "cone_89": dict(angle=89.0, max_distance=40.0, apply_occlusion=False),
     "ragged_inside": dict(W=57, H=43, cam=dict(eye=(10.0, -20.0, 30.0), center=(100.0, 50.0, -200.0),
                                             up=(0.0, 1.0, 0.0))),
 }

@@ -1,0 +1,103 @@
+"""GPU parity of the texture-unit filter mode (option filter_bits = 8, CVR-SPEC-8): every
+GL_LINEAR weight of the rc1pass march (volume, gradient, TF; ray_marching_1p.comp:133,
+:138) rounded to 8 fraction bits, as GPU texture units filter.  The HIP kernel against the
+oracle with the same weights (oracle.render_rc1pass(filter_bits=8)), bit for bit, over the
+rc1pass cases and schedules; the shaded renderers refuse the mode.  (That CVR-SPEC-8 sits
+inside BASELINE's image gate against the literal 8-bit reading: tests/test_literal.py.)"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from cpp_volume_rendering_amd import _native as N
+from cpp_volume_rendering_amd import datasets as D
+from cpp_volume_rendering_amd.renderer import Camera, Device, make_frame
+
+from test_rc1pass_gpu import CASES, INITIAL, assert_bitexact, case_tf, gpu_render
+
+pytestmark = pytest.mark.gpu
+
+SCHED8 = [dict(tile_order=1, batch=4), dict(tile_order=0, batch=2),
+          dict(tile_order=1, batch=4, macro=3, skip_min_pct=0, quad=10),
+          dict(tile_order=2, batch=4)]
+
+
+def oracle8(oracle, vol, scale, tf, cam, W, H, step=0.0, phong=False, gmode=0, light=(0, 0, 0),
+            shading=(0.5, 0.5, 0.8, 30.0), rows=None):
+    v16 = oracle.volume_r16f(vol)
+    grad = oracle.gradient(vol, "fd" if gmode == 1 else "sobel") if gmode else None
+    st = step if step > 0 else oracle.default_step(scale)
+    ka, kd, ks, sh = shading
+    return oracle.render_rc1pass(v16, scale, tf, cam, W, H, st, grad=grad, phong=phong, ka=ka,
+                                 kd=kd, ks=ks, shininess=sh, light=light, rows=rows, filter_bits=8)
+
+
+@pytest.mark.parametrize("sched", range(len(SCHED8)))
+@pytest.mark.parametrize("name", ["c1_sphere64", "ml64_ragged", "ml_aniso", "u16", "camera_inside",
+                                  "phong_fd", "phong_sobel", "dense_tf", "blobs_sparse"])
+def test_filter8_bitexact_vs_oracle(oracle, bonsai_tf, name, sched):
+    c = CASES[name]
+    vol = c["vol"]()
+    tf = case_tf(c, bonsai_tf)
+    cam = c.get("cam", INITIAL)
+    kw = dict(step=c.get("step", 0.0), phong=c.get("phong", False), gmode=c.get("gmode", 0),
+              light=c.get("light", (0, 0, 0)), shading=c.get("shading", (0.5, 0.5, 0.8, 30.0)))
+    o_rgba, o_cnt, o_total = oracle8(oracle, vol, c["scale"], tf, cam, c["W"], c["H"], **kw)
+    d = Device(0)
+    try:
+        L = N.lib()
+        N.check(L.cvr_set_option(d.handle, b"filter_bits", 8), "filter_bits", d.handle)
+        assert L.cvr_get_option(d.handle, b"filter_bits") == 8
+        for k, v in SCHED8[sched].items():
+            N.check(L.cvr_set_option(d.handle, k.encode(), v), k, d.handle)
+        for frame in range(3):      # screen order, then the learned order
+            g_rgba, g_cnt, g_total = gpu_render(d, vol, c["scale"], tf, cam, c["W"], c["H"],
+                                                set_data=(frame == 0), **kw)
+            assert_bitexact(g_cnt, o_cnt, f"{name} frame {frame} counts")
+            assert_bitexact(g_rgba, o_rgba, f"{name} frame {frame} rgba")
+            assert g_total == o_total
+    finally:
+        d.close()
+
+
+def test_filter8_differs_from_exact_and_headline_band(oracle, bonsai_tf):
+    """At 512^3 / 1024^2 (the headline workload) a band of rows matches the oracle's 8-bit
+    mode bit for bit, and the mode does change the image (it is not a no-op)."""
+    vol = D.marschner_lobb_u8(512)
+    sc = D.voxel_scale(512)
+    d = Device(0)
+    try:
+        g0, _, _ = gpu_render(d, vol, sc, bonsai_tf, INITIAL, 1024, 1024)
+        N.check(N.lib().cvr_set_option(d.handle, b"filter_bits", 8), "filter_bits", d.handle)
+        g8, c8, _ = gpu_render(d, vol, sc, bonsai_tf, INITIAL, 1024, 1024, set_data=False)
+    finally:
+        d.close()
+    rows = (496, 528)
+    o8, oc8, _ = oracle8(oracle, vol, sc, bonsai_tf, INITIAL, 1024, 1024, rows=rows)
+    assert_bitexact(g8[rows[0]:rows[1]], o8[rows[0]:rows[1]], "band rgba (8-bit weights)")
+    assert_bitexact(c8[rows[0]:rows[1]], oc8[rows[0]:rows[1]], "band counts (8-bit weights)")
+    assert (g8.view(np.uint32) != g0.view(np.uint32)).mean() > 0.1
+
+
+def test_filter_bits_option_errors(bonsai_tf):
+    d = Device(0)
+    try:
+        L = N.lib()
+        assert L.cvr_set_option(d.handle, b"filter_bits", 7) == N.CVR_ERR_ARG
+        assert L.cvr_get_option(d.handle, b"filter_bits") == 0
+        N.check(L.cvr_set_option(d.handle, b"filter_bits", 8), "filter_bits", d.handle)
+        d.set_volume(D.marschner_lobb_u8(32), D.voxel_scale(32))
+        d.set_transfer_function(bonsai_tf)
+        rgba = np.zeros((16, 16, 4), np.float32)
+        out = N.Output(rgba.ctypes.data, None, None, 0)
+        f = make_frame(Camera(**INITIAL), 16, 16)
+        p = N.EbsParams()
+        assert L.cvr_render_extbsd(d.handle, ctypes.byref(f), ctypes.byref(p),
+                                   ctypes.byref(out)) == N.CVR_ERR_ARG
+        assert b"filter_bits" in L.cvr_last_error(d.handle)
+        ip = N.IsoParams()
+        L.cvr_iso_params_default(2, ctypes.byref(ip))
+        assert L.cvr_render_iso(d.handle, ctypes.byref(f), ctypes.byref(ip),
+                                ctypes.byref(out)) == N.CVR_ERR_ARG
+    finally:
+        d.close()

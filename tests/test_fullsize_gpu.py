@@ -16,7 +16,9 @@ launches and a 34.6 GiB cell8 copy) no toy case reaches:
     sample count against the oracle's count over the same march.
   * C5: 1024^3 extinction SAT (ebsrenderer.cpp:624-723) + EBS frame at 1024^2: every
     plane of the 1026^3 float SAT against the reference recurrence (streamed over z,
-    oracle.sat_planes), and a 64-row band of the frame bit for bit.
+    oracle.sat_planes), and bands of the frame bit for bit: the centre band and the
+    bands richest in finite shaded pixels (at least 5,000 of them; most of the frame
+    is inf/NaN through the reference's float-SAT cancellation).
 Tolerance 0 throughout (CVR-SPEC).
 """
 import ctypes
@@ -140,12 +142,23 @@ def test_c5_sat_and_ebs_1024(fresh_dev, oracle, bonsai_tf):
     step = oracle.default_step(sc)
     p = ebs_params(step=step)
     g_rgba, g_cnt, g_S = gpu_ebs(fresh_dev, INITIAL, W, W, p)
-    rows = (W // 2 - 32, W // 2 + 32)
-    o_rgba, o_cnt, _ = oracle.render_ebs(v16, sc, bonsai_tf, sat, INITIAL, W,
-                                         W, step, light=LIGHT_POS, light_forward=LIGHT_FWD,
-                                         rows=rows)
-    assert_bitexact(g_cnt[rows[0]:rows[1]], o_cnt[rows[0]:rows[1]], "C5 band counts")
-    assert_bitexact(g_rgba[rows[0]:rows[1]], o_rgba[rows[0]:rows[1]], "C5 band rgba")
+    # At 1024^3 most shaded pixels are inf/NaN (the reference's float-SAT cancellation,
+    # DESIGN §5c), so the centre band compares mostly NaN with NaN.  Compare the centre
+    # band AND the bands richest in finite shaded pixels, and require thousands of
+    # those to match bit for bit.
+    bands, n_fin = oracle.finite_shaded_bands(g_rgba, 32, need=8000, max_bands=4)
+    bands = sorted(set(bands) | {(W // 2 - 32, W // 2 + 32)})
+    compared = 0
+    for rows in bands:
+        o_rgba, o_cnt, _ = oracle.render_ebs(v16, sc, bonsai_tf, sat, INITIAL, W,
+                                             W, step, light=LIGHT_POS, light_forward=LIGHT_FWD,
+                                             rows=rows)
+        assert_bitexact(g_cnt[rows[0]:rows[1]], o_cnt[rows[0]:rows[1]], f"C5 band {rows} counts")
+        assert_bitexact(g_rgba[rows[0]:rows[1]], o_rgba[rows[0]:rows[1]], f"C5 band {rows} rgba")
+        ob = o_rgba[rows[0]:rows[1]]
+        compared += int((np.isfinite(ob).all(-1) & (ob[..., 3] > 0)).sum())
+    print(f"C5: bands {bands}, {compared} finite shaded pixels compared bit for bit")
+    assert compared >= 5000, f"only {compared} finite shaded pixels in the compared bands"
     _, e_cnt, e_S = oracle.render_rc1pass(v16, sc, bonsai_tf, INITIAL, W, W, step)
     assert_bitexact(g_cnt, e_cnt, "C5 full-frame counts")
     assert g_S == e_S

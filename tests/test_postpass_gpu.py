@@ -222,3 +222,17 @@ def test_digital_filter_unaligned_frame(dev, oracle, k):
     want = oracle.multiscale_filter(3, k, oframe, 2 * fw, 2 * fh)
     assert _eq16(buf[4:].cpu().numpy().reshape(fh, fw, 4), oframe)
     assert _eq16(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("k", [N.FILTER_BOX, N.FILTER_HAT])
+def test_downscale_lds_budget_boundary(dev, oracle, k):
+    """Frame/screen ratio 4.8: the hat kernel's LDS window (90 x 91 pixels, 65,520 B) plus
+    the kernel's static weight tables no longer fit 64 KiB, so the launch takes the
+    global-memory kernel instead of failing; the box kernel's window still fits.  Bit for
+    bit either way."""
+    rng = np.random.default_rng(4800 + k)
+    sw, sh, fw, fh = 40, 33, 192, 158
+    frame = (rng.random((fh, fw, 4)) * 1.5 - 0.25).astype(np.float16)
+    got, _ = gpu_filter(dev, 2, k, frame, sw, sh)
+    want = oracle.multiscale_filter(2, k, frame.copy(), sw, sh)
+    assert _eq16(got, want)
