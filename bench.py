@@ -64,8 +64,11 @@ if __name__ == "__main__":
 # Frames in flight run on separate HIP streams; HIP maps streams onto at most
 # GPU_MAX_HW_QUEUES hardware queues per process (4 by default), and streams that
 # share a queue serialise.  8 queues keep 4 render streams + RCCL's apart.  Set
-# before torch initialises HIP.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# unconditionally (not setdefault), before torch initialises HIP, so the bench runs
+# the configuration DESIGN §7 measured whatever the box's environment holds; the
+# value is reported in config.hw_queues.
+HW_QUEUES = 8
+os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -669,6 +672,7 @@ def main():
                        "storage": "cell8 fp16 (16 B/cell, x-fastest)",
                        "frame_format": a.format,
                        "frames_in_flight": split.nstreams,
+                       "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
                        "quad_pct": quad if a.renderer == "rc1pass" else 0,
                        "empty_space_skip": f"macro cells 2^{macro}, auto (on at >= 15 % empty)"
                                            if macro > 0 else "off"},

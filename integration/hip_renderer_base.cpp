@@ -13,6 +13,13 @@
 HipRendererBase::HipRendererBase (int hip_device)
   : m_cvr(nullptr)
   , frame_()
+  , m_gl_interop(true)
+  , m_stream(nullptr)
+  , m_gl_res(nullptr)
+  , m_gl_tex(0)
+  , m_gl_w(0)
+  , m_gl_h(0)
+  , m_dev_rgba16f(nullptr)
 {
   if (cvr_create(hip_device, &m_cvr) != CVR_OK) m_cvr = nullptr;
 #ifdef MULTISAMPLE_AVAILABLE
@@ -25,10 +32,13 @@ HipRendererBase::~HipRendererBase ()
   Clean();
   if (m_cvr) cvr_destroy(m_cvr);
   m_cvr = nullptr;
+  if (m_stream) (void)hipStreamDestroy(m_stream);
+  m_stream = nullptr;
 }
 
 void HipRendererBase::Clean ()
 {
+  DetachScreenTexture();
   m_rgba16f.clear();
   m_rgba16f.shrink_to_fit();
   BaseVolumeRenderer::Clean();
@@ -160,11 +170,95 @@ void HipRendererBase::FillFrame (vis::Camera* camera)
   frame_.nranks = 1;
 }
 
-// Render into the host RGBA16F buffer and upload it into RenderFrameToScreen's
-// output texture (the image the compute shader's imageStore fills; row 0 = bottom).
+// (Re)registers RenderFrameToScreen's RGBA16F output texture with HIP when its
+// GL name or size changed (Update re-creates it on a viewport change).  Any
+// failure switches the interop path off for the rest of this object's life.
+bool HipRendererBase::AttachScreenTexture (gl::Texture2D* t)
+{
+  if (!m_gl_interop || t == nullptr) return false;
+  const GLuint id = t->GetTextureID();
+  if (m_gl_res != nullptr && id == m_gl_tex && frame_.width == m_gl_w && frame_.height == m_gl_h)
+    return true;
+  DetachScreenTexture();
+  hipGraphicsResource_t res = nullptr;
+  if (hipGraphicsGLRegisterImage(&res, id, GL_TEXTURE_2D, hipGraphicsRegisterFlagsWriteDiscard) != hipSuccess) {
+    m_gl_interop = false;
+    return false;
+  }
+  const size_t bytes = (size_t)frame_.width * frame_.height * 8;
+  if (hipMalloc(&m_dev_rgba16f, bytes) != hipSuccess) {
+    (void)hipGraphicsUnregisterResource(res);
+    m_dev_rgba16f = nullptr;
+    m_gl_interop = false;
+    return false;
+  }
+  m_gl_res = res;
+  m_gl_tex = id;
+  m_gl_w = frame_.width;
+  m_gl_h = frame_.height;
+  return true;
+}
+
+void HipRendererBase::DetachScreenTexture ()
+{
+  if (m_stream) (void)hipStreamSynchronize(m_stream);
+  if (m_gl_res) (void)hipGraphicsUnregisterResource(m_gl_res);
+  if (m_dev_rgba16f) (void)hipFree(m_dev_rgba16f);
+  m_gl_res = nullptr;
+  m_dev_rgba16f = nullptr;
+  m_gl_tex = 0;
+  m_gl_w = m_gl_h = 0;
+}
+
+// Device-resident handoff, the counterpart of the compute shader's imageStore into
+// the RGBA16F screen texture (renderoutputframe.cpp:197-202): map the registered
+// texture, render into a device RGBA16F buffer on the context stream, copy it into
+// the texture's array (device to device, 8 B per pixel), unmap.  Map and unmap
+// order the HIP work against GL's use of the texture; nothing crosses PCIe.
+bool HipRendererBase::RenderToMappedTexture (gl::Texture2D* t)
+{
+  if (!AttachScreenTexture(t)) return false;
+  if (hipGraphicsMapResources(1, &m_gl_res, m_stream) != hipSuccess) {
+    DetachScreenTexture();
+    m_gl_interop = false;
+    return false;
+  }
+  bool ok = false;
+  hipArray_t arr = nullptr;
+  if (hipGraphicsSubResourceGetMappedArray(&arr, m_gl_res, 0, 0) == hipSuccess) {
+    cvr_output out;
+    out.rgba = m_dev_rgba16f;
+    out.samples = nullptr;
+    out.total = nullptr;
+    out.on_device = 1;
+    out.format = CVR_FORMAT_RGBA16F;
+    const size_t row = (size_t)frame_.width * 8;
+    if (RenderFrame(&out) == CVR_OK)
+      ok = hipMemcpy2DToArrayAsync(arr, 0, 0, m_dev_rgba16f, row, row, frame_.height,
+                                   hipMemcpyDeviceToDevice, m_stream) == hipSuccess;
+    else
+      Fail(GetName());
+  }
+  if (hipGraphicsUnmapResources(1, &m_gl_res, m_stream) != hipSuccess) ok = false;
+  return ok;
+}
+
+// One frame into RenderFrameToScreen's output texture (the image the compute
+// shader's imageStore fills; row 0 = bottom): through HIP-GL interop when the
+// texture registers, else rendered into a host RGBA16F buffer and uploaded with
+// glTexSubImage2D (one PCIe copy of 8 B per pixel).
 bool HipRendererBase::RenderToScreenTexture ()
 {
   if (!m_cvr || frame_.width <= 0 || frame_.height <= 0) return false;
+  gl::Texture2D* screen = m_rdr_frame_to_screen.GetScreenOutputTexture();
+  if (m_gl_interop) {
+    if (m_stream == nullptr) {
+      if (hipStreamCreateWithFlags(&m_stream, hipStreamNonBlocking) != hipSuccess ||
+          cvr_set_stream(m_cvr, m_stream) != CVR_OK)
+        m_gl_interop = false;
+    }
+    if (m_gl_interop && RenderToMappedTexture(screen)) return true;
+  }
   m_rgba16f.resize((size_t)frame_.width * frame_.height * 4);
   cvr_output out;
   out.rgba = m_rgba16f.data();
@@ -173,8 +267,7 @@ bool HipRendererBase::RenderToScreenTexture ()
   out.on_device = 0;
   out.format = CVR_FORMAT_RGBA16F;
   if (RenderFrame(&out) != CVR_OK) return Fail(GetName());
-  gl::Texture2D* t = m_rdr_frame_to_screen.GetScreenOutputTexture();
-  glBindTexture(GL_TEXTURE_2D, t->GetTextureID());
+  glBindTexture(GL_TEXTURE_2D, screen->GetTextureID());
   glTexSubImage2D(GL_TEXTURE_2D, 0, 0, 0, frame_.width, frame_.height, GL_RGBA, GL_HALF_FLOAT,
                   m_rgba16f.data());
   glBindTexture(GL_TEXTURE_2D, 0);

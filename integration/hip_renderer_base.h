@@ -14,10 +14,14 @@
  *   - the frame: the camera's eye and its LookAt() matrix (camera.cpp:281-284) as
  *     the reference uploads them (CameraEye, u_CameraLookAt, rc1prenderer.cpp:91-95);
  *     the viewport as Update chooses it (rc1prenderer.cpp:76-87);
- *   - Redraw and the three multiscaling redraws: the library renders into a host
- *     RGBA16F buffer, which is uploaded into RenderFrameToScreen's own RGBA16F
- *     texture and drawn by the reference's Draw* functions
- *     (renderoutputframe.h:38-51), as rc1prenderer.cpp:140-189 does after its dispatch.
+ *   - Redraw and the three multiscaling redraws: RenderFrameToScreen's own RGBA16F
+ *     texture is registered with HIP-GL interop (hipGraphicsGLRegisterImage), the
+ *     library renders into a device RGBA16F buffer and a device-to-device copy
+ *     fills the mapped texture, as the compute shader's imageStore does
+ *     (renderoutputframe.cpp:197-202); if the texture does not register, the frame
+ *     comes back to a host buffer and glTexSubImage2D uploads it.  The reference's
+ *     Draw* functions then draw it (renderoutputframe.h:38-51), as
+ *     rc1prenderer.cpp:140-189 does after its dispatch.
  * Errors: a non-OK cvr_status becomes Init() == false (rc1prenderer.cpp:54) or a
  * printed message; the library never calls exit().
  */
@@ -27,6 +31,9 @@
 #include "../../volrenderbase.h"
 
 #include <cvr.h>
+
+#include <hip/hip_runtime_api.h>
+#include <hip/hip_gl_interop.h>
 
 #include <cstdint>
 #include <vector>
@@ -66,8 +73,18 @@ protected:
 
 private:
   bool RenderToScreenTexture ();
+  bool AttachScreenTexture (gl::Texture2D* t);    // hipGraphicsGLRegisterImage
+  void DetachScreenTexture ();
+  bool RenderToMappedTexture (gl::Texture2D* t);  // map, render, D2D copy, unmap
   static bool ReadTexture1D (gl::Texture1D* tex, std::vector<float>* rgba, int* n);
-  std::vector<uint16_t> m_rgba16f;
+  std::vector<uint16_t> m_rgba16f;               // host fallback frame
+
+  bool m_gl_interop;                              // off after the first interop failure
+  hipStream_t m_stream;                           // the context stream (interop path)
+  hipGraphicsResource_t m_gl_res;                 // the registered screen texture
+  GLuint m_gl_tex;
+  int m_gl_w, m_gl_h;
+  void* m_dev_rgba16f;                            // device frame, 8 B per pixel
 };
 
 #endif
