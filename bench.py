@@ -107,7 +107,8 @@ def parse():
     p.add_argument("--renderer", choices=["rc1pass", "dos", "ebs", "iso", "isodfs", "isoadapt"],
                    default="rc1pass",
                    help="iso / isodfs / isoadapt: the isosurface ray-casters (variants 0 / 1 / 2)")
-    p.add_argument("--tile", type=int, default=32)
+    p.add_argument("--tile", type=int, default=16,
+                   help="screen-tile side of the N > 1 split (16: diagonal lattice, DESIGN §7)")
     p.add_argument("--field", choices=["ml", "blobs"], default="ml")
     p.add_argument("--phong", action="store_true")
     p.add_argument("--tile-order", type=int, default=-1, choices=[-1, 0, 1, 2],
@@ -130,6 +131,10 @@ def parse():
                         "(default: 10 at >= 8 GPUs, else 0)")
     p.add_argument("--transport", choices=["rccl", "torch"], default="rccl",
                    help="N > 1 gather: the library's RCCL communicator or dist.gather")
+    p.add_argument("--shade-flat", type=int, default=-1, choices=[-1, 0, 1],
+                   help="dos/ebs: 1 flat job list (library default), 0 per-wave shading batches")
+    p.add_argument("--flat-group", type=int, default=0,
+                   help="dos/ebs flat shading: 64-job chunks per XCD turn (0: library default)")
     p.add_argument("--postpass", action="store_true",
                    help="also time the multiscaling post-pass filters on this workload's frame")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_rc1pass.json"))
@@ -148,16 +153,30 @@ def parse():
     return p.parse_args()
 
 
-def dry_run(world, rank):
+def dry_run(world, rank, a):
+    """The N-rank control flow without a GPU (gloo): every rank packs its tiles of the
+    workload's viewport (a pixel-id image, through screen_tiles' host mirror of the
+    device packing), rank 0 gathers and unpacks them, and checks that every pixel
+    arrived exactly once (tests/test_bench_launch.py)."""
+    n, W = a.size or (1024 if a.renderer == "ebs" else 512), a.res or (2048 if a.renderer == "dos" else 1024)
+    ids = np.arange(1, W * W + 1, dtype=np.int32).reshape(W, W, 1)
+    tiles = [T.tiles_for_rank(W, W, a.tile, r, world) for r in range(world)]
+    exact = True
     if world > 1:
         dist.init_process_group("gloo")
         ranks = [None] * world
         dist.all_gather_object(ranks, rank)
+        mine = torch.from_numpy(T.pack_rank(ids, a.tile, rank, world))
+        allp = T.gather_to_root(mine, T.max_tiles_per_rank(W, W, a.tile, world))
+        if rank == 0:
+            exact = bool(np.array_equal(T.unpack(allp.numpy(), W, W, a.tile, world), ids))
         dist.destroy_process_group()
     else:
         ranks = [0]
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": ranks}))
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": ranks,
+                          "renderer": a.renderer, "volume": n, "viewport": [W, W],
+                          "tile": a.tile, "tiles_per_rank": tiles, "gather_exact": exact}))
 
 
 def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgba=None,
@@ -352,7 +371,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.dry_run:
-        return dry_run(world, rank)
+        return dry_run(world, rank, a)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -435,6 +454,12 @@ def main():
         if a.skip_min_pct >= 0:
             N.check(N.lib().cvr_set_option(r.device.handle, b"skip_min_pct", a.skip_min_pct),
                     "skip_min_pct", r.device.handle)
+    if shaded and a.shade_flat >= 0:
+        N.check(N.lib().cvr_set_option(r.device.handle, b"shade_flat", a.shade_flat), "shade_flat",
+                r.device.handle)
+    if shaded and a.flat_group > 0:
+        N.check(N.lib().cvr_set_option(r.device.handle, b"flat_group", a.flat_group), "flat_group",
+                r.device.handle)
     try:
         # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
         # on rank 0) would otherwise rival a rank's share of the frame (~23 us at N = 8)
@@ -674,6 +699,8 @@ def main():
                        "frames_in_flight": split.nstreams,
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
                        "quad_pct": quad if a.renderer == "rc1pass" else 0,
+                       "shading": ("flat job list" if N.lib().cvr_get_option(r.device.handle, b"shade_flat")
+                                   else "per-wave batches") if shaded else None,
                        "empty_space_skip": f"macro cells 2^{macro}, auto (on at >= 15 % empty)"
                                            if macro > 0 else "off"},
             "roofline": roof,

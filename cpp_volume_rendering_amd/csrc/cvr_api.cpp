@@ -255,6 +255,7 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr;
   p = c->d_sat_scratch; free_dev(p); c->d_sat_scratch = nullptr;
   p = c->d_shade; free_dev(p); c->d_shade = nullptr;
+  cvr::flat_release(c->flat);
   p = c->d_cones; free_dev(p); c->d_cones = nullptr;
   delete[] c->cone_tab;
   p = c->d_total; free_dev(p); c->d_total = nullptr;
@@ -326,6 +327,16 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
   if (!std::strcmp(key, "sat_chunk")) {
     if (value < 1 || value > 64) return fail(c, CVR_ERR_ARG, "sat_chunk must be 1..64");
     c->sat_chunk = value;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "shade_flat")) {
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "shade_flat must be 0 or 1");
+    c->shade_flat = value;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "flat_group")) {
+    if (value < 1 || value > 4096) return fail(c, CVR_ERR_ARG, "flat_group must be in [1, 4096]");
+    c->flat_group = value;
     return CVR_OK;
   }
   if (!std::strcmp(key, "shade_counters")) {
@@ -431,6 +442,8 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
     return c->occ_valid ? (int)(c->occ_empty * 1000.0f + 0.5f) : -1;
   if (!std::strcmp(key, "tile_stats")) return c->tile_stats;
   if (!std::strcmp(key, "shade_counters")) return c->shade_counters;
+  if (!std::strcmp(key, "shade_flat")) return c->shade_flat;
+  if (!std::strcmp(key, "flat_group")) return c->flat_group;
   if (!std::strcmp(key, "sat_chunk")) return c->sat_chunk;
   if (!std::strcmp(key, "quad")) return c->quad_pct;
   if (!std::strcmp(key, "filter_bits")) return c->filter_bits;
@@ -1099,7 +1112,9 @@ static cvr_status render_shaded(Ctx* c, const cvr_output* o, int ntiles, size_t 
     d_samples = o->samples ? (uint32_t*)((char*)c->d_scratch + rgba_bytes) : nullptr;
     d_total = o->total ? c->d_total : nullptr;
   }
-  const bool use_counters = d_total || c->shade_counters;
+  // flat shading (c->shade_flat) keeps one job list per context: frames on other
+  // streams wait for it like for the counters
+  const bool use_counters = d_total || c->shade_counters || c->shade_flat;
   if (use_counters) {
     cvr_status st = counters_acquire(c, s);
     if (st != CVR_OK) return st;

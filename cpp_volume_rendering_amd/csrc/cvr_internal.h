@@ -22,6 +22,23 @@ struct CellGrid {
   long long linear_origin;  // index of cell (1,1,1) = texel (0,0,0)
 };
 
+// Screen-tile split: which TxT tile is rank r's k-th.  Tiles
+// are numbered in a virtual row-major order in which tile row ty is rotated by
+// s*ty tiles, and virtual tile v belongs to rank v mod N.  When N divides the
+// tiles per row, rank(tx, ty) = (tx + s*ty) mod N: a diagonal lattice instead
+// of the columns plain t mod N gives (tools/split_balance.py, samples max/mean
+// over ranks on four reference camera views at 1024^2, 16^2 tiles, N = 8:
+// columns up to 1.21, s = 3 at most 1.014).  Any s keeps the per-rank counts of
+// t mod N (cvr_tiles_for_rank).
+__host__ __device__ inline int split_shift(int nranks) { return nranks >= 4 ? 3 : 1; }
+__host__ __device__ inline void split_tile(int rank, int nranks, int k, int ntx, int& tx, int& ty) {
+  const int v = rank + k * nranks;
+  ty = v / ntx;
+  const int xv = v - ty * ntx;
+  tx = xv - (int)(((long long)split_shift(nranks) * ty) % ntx);
+  if (tx < 0) tx += ntx;
+}
+
 // Per-frame constants of the rc1pass kernel (passed by value).
 struct Rc1passArgs {
   // ray generation (ray_marching_1p.comp:87-99)
@@ -158,7 +175,22 @@ struct RenderPlan {
   int epi_stop;                      // diagnostics: the epilogue stops after phase k (0 = full)
 };
 
-constexpr int kMaxBandTiles = 8192;    // the epilogue sorts a band in LDS (32 KiB + group prefixes)
+constexpr int kMaxBandTiles = 8192;
+
+// Flat shading of the DOS/EBS renderers (option "shade_flat", shaded_march.h):
+// one frame's shading jobs in a single global list, shaded by a grid of their own
+// and folded into the pixels afterwards.  Buffers grow on demand, one set per context.
+struct FlatJobs {
+  uint32_t* lane_jobs = nullptr;            // jobs per pixel slot (tile * 64 + lane)
+  uint32_t* tile_off = nullptr;             // jobs per 8x8 tile, scanned in place to offsets
+  unsigned long long* total = nullptr;      // the frame's job count (device)
+  unsigned long long* h_total = nullptr;    // pinned host copy
+  float4* cam = nullptr;                    // the ray's camera direction per pixel slot
+  float4* jobs = nullptr;                   // 2 float4 per job (+1 with Phong)
+  float4* res = nullptr;                    // shaded rgb * alpha, alpha, per job
+  int tiles = 0;                            // allocated 8x8 tiles
+  size_t cap = 0;                           // allocated jobs (float4 units: cap * 3)
+};    // the epilogue sorts a band in LDS (32 KiB + group prefixes)
 
 struct Ctx {
   int device = 0;
@@ -204,6 +236,9 @@ struct Ctx {
   int filter_bits = 0;             // GL_LINEAR weights at this many fraction bits (0 = exact; rc1pass)
   int quad_pct = 0;                // % of every band's longest tiles marched 4 lanes per ray
   int shade_counters = 0;          // DOS/EBS: count shaded and shadow-lit samples
+  int shade_flat = 1;              // DOS/EBS: 1 = flat job list (FlatJobs), 0 = per-wave batches
+  int flat_group = 8;              // flat shading: 64-job chunks per XCD turn (XCD-aware order)
+  mutable FlatJobs flat;
   unsigned long long* d_shade = nullptr;   // [3]: shaded, lit, secondary fetches (last frame)
   int tile_stats = 0;              // record per-tile timing (diagnostics)
   unsigned long long* d_tile_stats = nullptr;
@@ -287,6 +322,7 @@ struct Ctx {
 };
 
 void comm_release(Ctx* c);   // cvr_comm.cpp
+void flat_release(FlatJobs& J);   // flat.hip
 
 // postpass.hip: multiscaling filters (mode 1-3, kernel 0-5) and the screenshot
 hipError_t launch_multiscale(int mode, int kernel, void* frame, int fw, int fh, void* screen, int sw,

@@ -552,6 +552,9 @@ struct DosShader {
 
 hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
+  if (c.shade_flat)
+    return launch_shaded_flat<DosShader>(c, q, q.phong != 0, c.d_ext_cells, out, samples, shade,
+                                         tile_samples, s);
   return launch_shaded_march<DosShader>(c, q, q.phong != 0, c.d_ext_cells, out, samples, shade,
                                         tile_samples, s);
 }

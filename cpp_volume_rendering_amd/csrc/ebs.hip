@@ -416,10 +416,17 @@ struct EbsShaderT {
 
 hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
+  const bool ph = q.phong != 0;
+  if (c.shade_flat)
+    return q.recip_cone
+               ? launch_shaded_flat<EbsShaderT<true>>(c, q, ph, c.d_sat_cells, out, samples, shade,
+                                                      tile_samples, s)
+               : launch_shaded_flat<EbsShaderT<false>>(c, q, ph, c.d_sat_cells, out, samples, shade,
+                                                       tile_samples, s);
   if (q.recip_cone)
-    return launch_shaded_march<EbsShaderT<true>>(c, q, q.phong != 0, c.d_sat_cells, out, samples, shade,
+    return launch_shaded_march<EbsShaderT<true>>(c, q, ph, c.d_sat_cells, out, samples, shade,
                                                  tile_samples, s);
-  return launch_shaded_march<EbsShaderT<false>>(c, q, q.phong != 0, c.d_sat_cells, out, samples, shade,
+  return launch_shaded_march<EbsShaderT<false>>(c, q, ph, c.d_sat_cells, out, samples, shade,
                                                 tile_samples, s);
 }
 

@@ -28,7 +28,8 @@ __device__ __forceinline__ void store_rgba(float4* out, long long i, float4 v, i
 
 // Tile `t` (8x8 pixels), local pixel (lx, ly) -> pixel and output index.
 // Unpacked: tiles are row-major over the (W/8)x(H/8) grid.  Packed (screen
-// split): tile t = k*(T/8)^2 + j is sub-tile j of this rank's k-th TxT tile.
+// split): tile t = k*(T/8)^2 + j is sub-tile j of this rank's k-th TxT tile
+// (split_tile, cvr_internal.h).
 __device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lx, int ly, int& px,
                                            int& py, long long& out_idx) {
   if (!A.packed) {
@@ -40,8 +41,8 @@ __device__ __forceinline__ void tile_pixel(const Rc1passArgs& A, int t, int lx, 
   } else {
     const int s = A.tile >> 3;               // 8x8 sub-tiles per tile row
     const int k = t / (s * s), j = t - k * s * s;
-    const int g = A.rank + k * A.nranks;     // global tile index
-    const int gy = g / A.ntx, gx = g - gy * A.ntx;
+    int gx, gy;                              // this rank's k-th TxT tile
+    split_tile(A.rank, A.nranks, k, A.ntx, gx, gy);
     const int ox = ((j % s) << 3) | lx, oy = ((j / s) << 3) | ly;
     px = gx * A.tile + ox;
     py = gy * A.tile + oy;

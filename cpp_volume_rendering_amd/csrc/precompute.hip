@@ -168,8 +168,8 @@ __global__ void unpack_tiles_kernel(const PX* __restrict__ packed, PX* __restric
   size_t slot = i / tt;                     // rank * tpr_max + k
   int inner = (int)(i - slot * tt);
   int r = (int)(slot / (size_t)tpr_max), k = (int)(slot % (size_t)tpr_max);
-  int t = r + k * nranks;
-  int tx = t % ntx, ty = t / ntx;
+  int tx, ty;
+  split_tile(r, nranks, k, ntx, tx, ty);
   int px = tx * tile + inner % tile, py = ty * tile + inner / tile;
   if (px < W && py < H && ty * tile < H)
     out[(size_t)py * W + px] = packed[((size_t)r * rank_stride + k) * tt + inner];

@@ -195,6 +195,198 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Flat shading (option "shade_flat", the default).  The per-wave batches above
+// tie a tile's shading to its wave, so a frame lasts as long as its longest
+// tile: with fewer tiles per GPU (the screen split) the longest waves set the
+// frame time (one 1024^3 EBS wave runs for ~45 ms; 8 ranks: 2.1x, not 8x).
+// Flat shading cuts the frame at the job instead:
+//   1. shaded_jobs_kernel<count>: the march, counting each pixel's jobs
+//      (samples with alpha > 0 before the ERT break; opacity does not depend on
+//      shading, so the march is exact without it) and the tile sums;
+//   2. flat_scan_kernel: the tiles' exclusive offsets and the frame total,
+//      which the host reads to size the grid (one stream sync per frame);
+//   3. shaded_jobs_kernel<emit>: the same march, writing every job (position,
+//      alpha, TF rgb, pixel slot; + gradient with Phong) at its pixel's offset;
+//   4. flat_shade_kernel: one job per lane over the whole list, 64-job chunks
+//      dealt to the XCDs in groups of flat_group consecutive chunks (one XCD's
+//      L2 sees neighbouring rays' neighbouring samples);
+//   5. flat_fold_kernel: per pixel, its results folded front to back with the
+//      sequential loop's fma order (dst.a replayed from the alphas), so the
+//      image is bit-identical to the per-wave kernel and to the oracle.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x - v;
+}
+
+template <class SH, bool PHONG, bool EMIT>
+__global__ void __launch_bounds__(64)
+shaded_jobs_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
+                   const uint4* __restrict__ grad, const float4* __restrict__ tf_g, FlatJobs J,
+                   uint32_t* __restrict__ samples, unsigned long long* __restrict__ shade_ctr,
+                   unsigned long long* __restrict__ tile_samples) {
+  extern __shared__ float4 tfp[];
+  load_tf_lds(tfp, tf_g, Q.a.tf_n);
+  const Rc1passArgs& A = Q.a;
+  const int t = screen_tile_of_block<CVR_SHADED_COLGROUP>(A, blockIdx.x, A.ntiles);
+  const int lane = threadIdx.x;
+  const int slot = t * 64 + lane;
+  int px, py;
+  long long oidx;
+  tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
+  const bool inside = px < A.W && py < A.H;
+  Ray r;
+  bool active = inside && ray_setup(A, px, py, r);
+  active = active && 0.0f < r.D;
+  const bool wave_in_box = __ballot(active && r.outside) == 0;   // else clamp positions
+  size_t next = 0;                                                // EMIT: this lane's next job
+  if (EMIT) next = (size_t)J.tile_off[t] + wave_excl_scan(J.lane_jobs[slot], lane);
+  const float step = A.step, fn = (float)A.tf_n;
+  float s = 0.0f, dst_a = 0.0f;
+  uint32_t cnt = 0, n = 0;
+  while (active) {
+    const float h = fminf(step, r.D - s);
+    const float tt = fmaf(h, 0.5f, s);
+    const float x = fmaf(r.dt.x, tt, r.o.x), y = fmaf(r.dt.y, tt, r.o.y), z = fmaf(r.dt.z, tt, r.o.z);
+    const SamplePos sp = wave_in_box ? sample_pos(x, y, z, A) : sample_pos_clamped(x, y, z, A);
+    const float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
+    cnt++;
+    if (sc.w > 0.0f) {
+      const float a = 1.0f - cvr_expf(-(sc.w * h));
+      if (EMIT) {
+        const f3 tx = vmad(r.dir, tt, r.tpos);        // tx_pos, box at [0, G]
+        float4* jp = J.jobs + next * (PHONG ? 3 : 2);
+        jp[0] = make_float4(tx.x, tx.y, tx.z, a);
+        jp[1] = make_float4(sc.x, sc.y, sc.z, __int_as_float(slot));
+        if (PHONG) {
+          const f3 g = sample_gradient_cell(grad, sp);
+          jp[2] = make_float4(g.x, g.y, g.z, 0.0f);
+        }
+        next++;
+      }
+      dst_a = fmaf(1.0f - dst_a, a, dst_a);
+      n++;
+      if (dst_a > 0.99f) break;
+    }
+    s = s + h;
+    active = s < r.D;
+  }
+  if (EMIT) return;
+  J.lane_jobs[slot] = n;
+  J.cam[slot] = (inside && n) ? make_float4(r.cam.x, r.cam.y, r.cam.z, 0.0f)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+  const unsigned long long tj = wave_sum((unsigned long long)n);
+  if (lane == 0) J.tile_off[t] = (uint32_t)tj;
+  if ((inside || A.packed) && samples) samples[oidx] = cnt;
+  if (tile_samples) {
+    const unsigned long long v = wave_sum(cnt);
+    if (lane == 0) tile_samples[t] = v;
+  }
+  if (shade_ctr && lane == 0) atomicAdd(&shade_ctr[0], tj);
+}
+
+template <class SH, bool PHONG>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH::kMinWavesPerEU)))
+flat_shade_kernel(typename SH::Args Q, typename SH::Data data, FlatJobs J, unsigned long long total,
+                  int nchunks, int group, unsigned long long* __restrict__ shade_ctr) {
+  // block b runs on XCD b % 8; XCD x takes chunk groups x, x + 8, ... in order
+  const int b = blockIdx.x, x = b & 7, k = b >> 3;
+  const int chunk = ((k / group) * 8 + x) * group + (k % group);
+  if (chunk >= nchunks) return;
+  const int lane = threadIdx.x;
+  const unsigned long long i = (unsigned long long)chunk * 64 + lane;
+  uint32_t nlit = 0, nfetch = 0;
+  if (i < total) {
+    const float4* jp = J.jobs + i * (PHONG ? 3 : 2);
+    const float4 q0 = jp[0], q1 = jp[1];
+    const f3 tx{q0.x, q0.y, q0.z};
+    const f3 hg{Q.a.half_grid[0], Q.a.half_grid[1], Q.a.half_grid[2]};
+    const f3 wp{tx.x - hg.x, tx.y - hg.y, tx.z - hg.z};
+    const float4 cm = J.cam[__float_as_int(q1.w)];
+    const f3 cam{cm.x, cm.y, cm.z};
+    const f3 rgb{q1.x, q1.y, q1.z};
+    f3 g;
+    if (PHONG) {
+      const float4 q2 = jp[2];
+      g = f3{q2.x, q2.y, q2.z};
+    }
+    const f3 c = SH::shade(Q, data, tx, wp, cam, rgb, PHONG ? &g : nullptr, nlit, nfetch);
+    const float a = q0.w;
+    J.res[i] = make_float4(c.x * a, c.y * a, c.z * a, a);
+  }
+  if (shade_ctr) {   // measurement only (secondary-fetch count of the roofline)
+    const unsigned long long sl = wave_sum(nlit), sf = wave_sum(nfetch);
+    if (lane == 0) {
+      atomicAdd(&shade_ctr[1], sl);
+      atomicAdd(&shade_ctr[2], sf);
+    }
+  }
+}
+
+hipError_t launch_flat_scan(FlatJobs& J, int ntiles, hipStream_t s);
+hipError_t launch_flat_fold(const Rc1passArgs& a, FlatJobs& J, float4* out, hipStream_t s);
+hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, int phong);
+
+template <class SH>
+hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool phong,
+                              typename SH::Data data, float4* out, uint32_t* samples,
+                              unsigned long long* shade_ctr, unsigned long long* tile_samples,
+                              hipStream_t s) {
+  const int nt = q.a.ntiles;
+  if (nt <= 0) return hipSuccess;
+  if (q.a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
+  FlatJobs& J = c.flat;
+  hipError_t e = flat_reserve(J, nt, 0, phong);
+  if (e != hipSuccess) return e;
+  const size_t lds = (size_t)(q.a.tf_n + 2) * sizeof(float4);
+  const uint4* cells = (const uint4*)c.d_cells;
+  const uint4* grad = (const uint4*)c.d_grad;
+  const float4* tf = (const float4*)c.d_tf;
+  if (phong)
+    hipLaunchKernelGGL((shaded_jobs_kernel<SH, true, false>), dim3(nt), dim3(64), lds, s, q, cells,
+                       grad, tf, J, samples, shade_ctr, tile_samples);
+  else
+    hipLaunchKernelGGL((shaded_jobs_kernel<SH, false, false>), dim3(nt), dim3(64), lds, s, q, cells,
+                       grad, tf, J, samples, shade_ctr, tile_samples);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = launch_flat_scan(J, nt, s)) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(J.h_total, J.total, sizeof(unsigned long long), hipMemcpyDeviceToHost, s)) !=
+      hipSuccess)
+    return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  const unsigned long long total = *J.h_total;
+  if (total > 0) {
+    if ((e = flat_reserve(J, nt, (size_t)total, phong)) != hipSuccess) return e;
+    if (phong)
+      hipLaunchKernelGGL((shaded_jobs_kernel<SH, true, true>), dim3(nt), dim3(64), lds, s, q, cells,
+                         grad, tf, J, nullptr, nullptr, nullptr);
+    else
+      hipLaunchKernelGGL((shaded_jobs_kernel<SH, false, true>), dim3(nt), dim3(64), lds, s, q, cells,
+                         grad, tf, J, nullptr, nullptr, nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const unsigned long long nch = (total + 63) / 64;
+    if (nch > (1ull << 30)) return hipErrorInvalidValue;
+    const int nchunks = (int)nch, group = c.flat_group;
+    const long long span = 8LL * group;                           // chunks per round of the XCDs
+    const long long nb = (nchunks + span - 1) / span * span;      // every XCD gets whole groups
+    if (phong)
+      hipLaunchKernelGGL((flat_shade_kernel<SH, true>), dim3((unsigned)nb), dim3(64), 0, s, q, data, J,
+                         total, nchunks, group, shade_ctr);
+    else
+      hipLaunchKernelGGL((flat_shade_kernel<SH, false>), dim3((unsigned)nb), dim3(64), 0, s, q, data, J,
+                         total, nchunks, group, shade_ctr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return launch_flat_fold(q.a, J, out, s);
+}
+
 template <class SH>
 hipError_t launch_shaded_march(const Ctx& c, const typename SH::Args& q, bool phong,
                                typename SH::Data data, float4* out, uint32_t* samples,

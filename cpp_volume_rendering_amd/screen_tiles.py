@@ -1,8 +1,9 @@
 """Screen-tile split of one frame over the GPUs of a node.
 
 The reference renders on one GPU; pixels are independent, so the framebuffer
-is cut into ``tile`` x ``tile`` tiles, tile t (row-major over the tile grid)
-belongs to rank ``t % nranks`` (interleaved for load balance: ERT and empty
+is cut into ``tile`` x ``tile`` tiles (16 by default) dealt over the ranks on a
+diagonal lattice (``split_tile``: rank (tx + s*ty) mod N when N divides the tiles
+per row, s = 3 at N >= 4; interleaved for load balance, since ERT and empty
 space skew per-tile cost), every rank keeps a full replica of the volume and
 renders its tiles packed contiguously, and rank 0 gathers the packed buffers
 over RCCL (xGMI) and scatters them into the image with one small kernel
@@ -33,6 +34,20 @@ def tiles_for_rank(width: int, height: int, tile: int, rank: int, nranks: int) -
     return (nt - rank + nranks - 1) // nranks if nt > rank else 0
 
 
+def split_shift(nranks: int) -> int:
+    return 3 if nranks >= 4 else 1
+
+
+def split_tile(rank: int, nranks: int, k: int, ntx: int) -> tuple[int, int]:
+    """(tx, ty) of rank's k-th tile: virtual row-major tile v = rank + k*nranks, whose
+    row ty is rotated by split_shift*ty tiles (mirror of cvr::split_tile, cvr_internal.h;
+    tools/split_balance.py measures the balance)."""
+    v = rank + k * nranks
+    ty = v // ntx
+    tx = (v - ty * ntx - split_shift(nranks) * ty) % ntx
+    return tx, ty
+
+
 def max_tiles_per_rank(width: int, height: int, tile: int, nranks: int) -> int:
     return tiles_for_rank(width, height, tile, 0, nranks)
 
@@ -44,8 +59,7 @@ def pack_rank(image: np.ndarray, tile: int, rank: int, nranks: int) -> np.ndarra
     k = tiles_for_rank(w, h, tile, rank, nranks)
     out = np.zeros((k, tile, tile) + image.shape[2:], image.dtype)
     for i in range(k):
-        t = rank + i * nranks
-        tx, ty = t % ntx, t // ntx
+        tx, ty = split_tile(rank, nranks, i, ntx)
         blk = image[ty * tile:(ty + 1) * tile, tx * tile:(tx + 1) * tile]
         out[i, :blk.shape[0], :blk.shape[1]] = blk
     return out
@@ -57,8 +71,7 @@ def unpack(packed_all: np.ndarray, width: int, height: int, tile: int, nranks: i
     out = np.zeros((height, width) + packed_all.shape[4:], packed_all.dtype)
     for r in range(nranks):
         for i in range(tiles_for_rank(width, height, tile, r, nranks)):
-            t = r + i * nranks
-            tx, ty = t % ntx, t // ntx
+            tx, ty = split_tile(r, nranks, i, ntx)
             blk = out[ty * tile:(ty + 1) * tile, tx * tile:(tx + 1) * tile]
             blk[...] = packed_all[r, i, :blk.shape[0], :blk.shape[1]]
     return out
@@ -115,7 +128,7 @@ class ScreenTileSplit:
     the library (renderer.render_to, cvr_unpack_tiles_device); the CPU tests pass
     host mirrors."""
 
-    def __init__(self, renderer=None, width: int = None, height: int = None, tile: int = 32,
+    def __init__(self, renderer=None, width: int = None, height: int = None, tile: int = 16,
                  fmt: int = N.FORMAT_RGBA16F, group=None, device=None, render_fn=None,
                  unpack_fn=None, count_samples: bool = False, transport: str = None,
                  streams: int = None, frames_per_exchange: int = 1, stream_factory=None):
@@ -371,7 +384,7 @@ class TiledRc1pass(ScreenTileSplit):
     and a per-frame sample total; ``render(camera)`` returns the image on rank 0 and
     this rank's packed tiles elsewhere."""
 
-    def __init__(self, renderer, tile: int = 32):
+    def __init__(self, renderer, tile: int = 16):
         super().__init__(renderer, tile=tile, fmt=N.FORMAT_RGBA32F, count_samples=True,
                          streams=1)
 

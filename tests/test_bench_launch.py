@@ -6,6 +6,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -29,6 +31,18 @@ def test_gpus_2_launches_two_ranks():
     assert p.returncode == 0, p.stderr[-2000:]
     d = _json_line(p.stdout)
     assert d["n_gpus"] == 2 and sorted(d["ranks"]) == [0, 1]
+
+
+@pytest.mark.parametrize("renderer,res", [("dos", 2048), ("ebs", 1024)])
+def test_gpus_2_dry_run_shaded_configs(renderer, res):
+    """Configs 4 and 5 over two gloo ranks: every pixel of the 2048^2 / 1024^2 viewport
+    travels through pack -> gather -> unpack exactly once."""
+    p = _run(["--gpus", "2", "--dry-run", "--renderer", renderer])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _json_line(p.stdout)
+    assert d["viewport"] == [res, res] and d["renderer"] == renderer
+    assert d["gather_exact"] is True
+    assert sum(d["tiles_per_rank"]) == (res // d["tile"]) ** 2
 
 
 def test_gpus_1_stays_in_process():

@@ -61,7 +61,8 @@ def _worker(rank, world, port, W, H, tile, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,W,H,tile", [(2, 96, 80, 32), (3, 70, 45, 16), (2, 16, 16, 32)])
+@pytest.mark.parametrize("world,W,H,tile", [(2, 96, 80, 32), (3, 70, 45, 16), (2, 16, 16, 32),
+                                            (4, 128, 96, 16)])
 def test_gather_unpack_gloo(world, W, H, tile):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -288,3 +289,22 @@ def test_native_split_control_flow_gloo():
     res = [q.get(timeout=10) for _ in range(2)]
     assert all(r[0] == "ok" for r in res), res
     assert [p.exitcode for p in procs] == [0, 0]
+
+
+@pytest.mark.parametrize("W,H,tile,world", [(1024, 1024, 16, 8), (1024, 1024, 32, 4),
+                                            (2048, 2048, 16, 8), (100, 72, 16, 3), (70, 45, 16, 2)])
+def test_split_tile_is_a_partition(W, H, tile, world):
+    """split_tile deals every tile to exactly one rank, with tiles_for_rank tiles each;
+    when N divides the tiles per row it is the diagonal lattice (tx + s*ty) mod N."""
+    ntx, nty = T.tile_grid(W, H, tile)
+    seen = np.zeros((nty, ntx), np.int32)
+    owner = np.full((nty, ntx), -1, np.int32)
+    for r in range(world):
+        for k in range(T.tiles_for_rank(W, H, tile, r, world)):
+            tx, ty = T.split_tile(r, world, k, ntx)
+            seen[ty, tx] += 1
+            owner[ty, tx] = r
+    assert (seen == 1).all()
+    if ntx % world == 0:
+        tx, ty = np.meshgrid(np.arange(ntx), np.arange(nty))
+        assert np.array_equal(owner, (tx + T.split_shift(world) * ty) % world)

@@ -1,58 +1,98 @@
 #!/usr/bin/env python3
-"""Do consecutive frames on two streams overlap on the device?  Renders rank 0 of
-an N-way screen split (the per-GPU work at N GPUs) alternating two streams; run it
-under `rocprofv3 --kernel-trace` and read the kernels' start/end stamps.
-Usage: python tools/overlap_probe.py [--nranks 8] [--quad 0] [--frames 16]"""
-import argparse
-import ctypes
+"""Per-rank cost of the N-way screen split, measured on one GPU: renders rank r's
+share of the headline frame (512^3 ML, 1024^2) F times over D rotated streams, for
+every rank r, and prints ms per frame per rank and the max over ranks (the bench
+takes the max over ranks).  --renderer dos|ebs: configs 4/5 instead (512^3 at 2048^2,
+1024^3 at 1024^2).  Gathers are not included.
+Usage: python tools/overlap_probe.py [--nranks 1,2,4,8] [--tile 16] [--streams 4]
+       [--quad 0] [--frames 32] [--renderer rc1pass]"""
 import os
-import sys
-import time
+os.environ["GPU_MAX_HW_QUEUES"] = "8"          # as bench.py, before HIP initialises
+import argparse  # noqa: E402
+import ctypes  # noqa: E402
+import json  # noqa: E402
+import sys  # noqa: E402
+import time  # noqa: E402
 
-import torch
+import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cpp_volume_rendering_amd import _native as N  # noqa: E402
 from cpp_volume_rendering_amd import datasets as D  # noqa: E402
 from cpp_volume_rendering_amd import screen_tiles as T  # noqa: E402
-from cpp_volume_rendering_amd.renderer import Camera, Device, build_tf_rgbt, make_frame  # noqa: E402
+from cpp_volume_rendering_amd.renderer import (Camera, DataManager, RayCasting1Pass,  # noqa: E402
+                                               RC1PConeTracingDirOcclusionShading,
+                                               RC1PExtinctionBasedShading, RenderingParameters,
+                                               build_ext_lut, build_tf_rgbt, make_frame)
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--nranks", type=int, default=8)
-ap.add_argument("--quad", type=int, default=0)
-ap.add_argument("--frames", type=int, default=16)
-ap.add_argument("--order", type=int, default=1)
-ap.add_argument("--streams", default="1,2,3,4")
-ap.add_argument("--quads", default="")
+ap.add_argument("--nranks", default="1,2,4,8")
+ap.add_argument("--tile", default="16")
+ap.add_argument("--quad", default="0")
+ap.add_argument("--frames", type=int, default=32)
+ap.add_argument("--streams", default="4")
+ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks")
+ap.add_argument("--renderer", choices=["rc1pass", "dos", "ebs"], default="rc1pass")
+ap.add_argument("--out", default="")
 a = ap.parse_args()
-W = 1024
-dev = Device(0)
-dev.set_volume(D.marschner_lobb_u8(512), D.voxel_scale(512))
-dev.set_transfer_function(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
+
+n, W = (1024, 1024) if a.renderer == "ebs" else ((512, 2048) if a.renderer == "dos" else (512, 1024))
+vol = D.marschner_lobb_u8(n)
+dm = DataManager()
+dm.SetVolume(vol, D.voxel_scale(n))
+dm.SetTransferFunction(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA),
+                       build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA, extinction_input=True))
+if a.renderer == "dos":                      # bench.py --renderer dos (config 4)
+    r = RC1PConeTracingDirOcclusionShading(0)
+    r.glsl_apply_shadow = True
+elif a.renderer == "ebs":                    # bench.py --renderer ebs (config 5)
+    dm.SetExtinctionTable(build_ext_lut(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
+    r = RC1PExtinctionBasedShading(0)
+else:
+    r = RayCasting1Pass(0)
+r.SetExternalResources(dm, RenderingParameters(W, W, light_position=D.LIGHT_LIST0_POSITION))
+assert r.Init(W, W)
+r.PrepareRender(Camera(**D.INITIAL_STATE_CAMERA))
 L = N.lib()
-L.cvr_set_option(dev.handle, b"quad", a.quad)
-L.cvr_set_option(dev.handle, b"tile_order", a.order)
-frame = make_frame(Camera(**D.INITIAL_STATE_CAMERA), W, W, 32, 0, a.nranks) if a.nranks > 1 \
-    else make_frame(Camera(**D.INITIAL_STATE_CAMERA), W, W)
-npx = (T.tiles_for_rank(W, W, 32, 0, a.nranks) * 1024) if a.nranks > 1 else W * W
-p = N.Rc1passParams()
-p.step = 0.5
-quads = [int(q) for q in a.quads.split(",")] if a.quads else [a.quad]
-pool = [torch.cuda.Stream() for _ in range(8)]
-for q in quads:
-    L.cvr_set_option(dev.handle, b"quad", q)
-    for ns in [int(x) for x in a.streams.split(",")]:
-        st = pool[:ns]
-        bufs = [torch.zeros((npx, 4), dtype=torch.float16, device="cuda") for _ in range(ns)]
-        outs = [N.Output(b.data_ptr(), None, None, 1, 1) for b in bufs]
-        best = 1e9
-        for rep in range(3):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for i in range(a.frames):
-                dev.set_stream(st[i % ns].cuda_stream)
-                N.check(L.cvr_render_rc1pass(dev.handle, ctypes.byref(frame), ctypes.byref(p),
-                                             ctypes.byref(outs[i % ns])), "render", dev.handle)
-            torch.cuda.synchronize()
-            best = min(best, (time.perf_counter() - t0) / a.frames * 1e3)
-        print(f"nranks {a.nranks} quad {q} streams {ns}: {best:.4f} ms/frame", flush=True)
+handle = r.device.handle
+
+
+def render(frame, out):
+    r.render_to(frame, out)
+
+
+res = []
+for q in [int(x) for x in a.quad.split(",")]:
+    if a.renderer == "rc1pass":
+        L.cvr_set_option(handle, b"quad", q)
+    for nr in [int(x) for x in a.nranks.split(",")]:
+        for tile in [int(x) for x in a.tile.split(",")]:
+            ranks = range(nr) if a.ranks == "all" else [int(x) for x in a.ranks.split(",") if int(x) < nr]
+            for ns in [int(x) for x in a.streams.split(",")]:
+                pool = [torch.cuda.Stream() for _ in range(ns)]
+                per = []
+                for rk in ranks:
+                    frame = make_frame(Camera(**D.INITIAL_STATE_CAMERA), W, W, tile, rk, nr) \
+                        if nr > 1 else make_frame(Camera(**D.INITIAL_STATE_CAMERA), W, W)
+                    npx = T.tiles_for_rank(W, W, tile, rk, nr) * tile * tile if nr > 1 else W * W
+                    bufs = [torch.zeros((npx, 4), dtype=torch.float16, device="cuda") for _ in range(ns)]
+                    outs = [N.Output(b.data_ptr(), None, None, 1, 1) for b in bufs]
+                    best = 1e9
+                    for rep in range(3):
+                        torch.cuda.synchronize()
+                        t0 = time.perf_counter()
+                        for i in range(a.frames):
+                            L.cvr_set_stream(handle, ctypes.c_void_p(pool[i % ns].cuda_stream))
+                            render(frame, outs[i % ns])
+                        torch.cuda.synchronize()
+                        best = min(best, (time.perf_counter() - t0) / a.frames * 1e3)
+                    per.append(best)
+                line = dict(renderer=a.renderer, nranks=nr, tile=tile, quad=q, streams=ns,
+                            ms_per_rank=[round(x, 5) for x in per], max_ms=round(max(per), 5),
+                            mean_ms=round(sum(per) / len(per), 5),
+                            max_over_mean=round(max(per) / (sum(per) / len(per)), 4))
+                print(json.dumps(line), flush=True)
+                res.append(line)
+if a.out:
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
