@@ -482,6 +482,9 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
 // ShadeSample (ray_bbox_marching.comp:607-656) for the deferred march
 // ---------------------------------------------------------------------------
 
+#ifndef CVR_DOS_FLAT_WAVES
+#define CVR_DOS_FLAT_WAVES 4   // flat shading: 128 VGPRs (the compiler's choice is 129, 3 waves)
+#endif
 #ifndef CVR_DOS_WAVES
 #define CVR_DOS_WAVES 3
 #endif
@@ -490,6 +493,7 @@ struct DosShader {
   // register budget: 3 waves/SIMD (168 VGPRs; the compiler alone takes 172 -> 2 waves):
   // kernel 21.1 -> 18.0 ms, 4 waves 18.8 ms (spills)
   static constexpr int kMinWavesPerEU = CVR_DOS_WAVES;
+  static constexpr int kFlatWavesPerEU = CVR_DOS_FLAT_WAVES;   // flat_shade_kernel
   using Data = const uint4*;   // the cell8 extinction pyramid
 
   // Shaded colour of one job; `lit` counts the shadow cones traced, `fetches`

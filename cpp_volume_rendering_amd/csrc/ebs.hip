@@ -357,6 +357,9 @@ __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
 
 }  // namespace
 
+#ifndef CVR_EBS_FLAT_WAVES
+#define CVR_EBS_FLAT_WAVES 1   // flat shading: the compiler's 128 VGPRs, 4 waves/SIMD
+#endif
 #ifndef CVR_EBS_WAVES
 #define CVR_EBS_WAVES 1
 #endif
@@ -364,6 +367,7 @@ template <bool RECIP_CONE>
 struct EbsShaderT {
   using Args = EbsArgs;
   static constexpr int kMinWavesPerEU = CVR_EBS_WAVES;   // register budget (1: compiler's choice)
+  static constexpr int kFlatWavesPerEU = CVR_EBS_FLAT_WAVES;   // flat_shade_kernel
   using Data = const float4*;   // the float SAT, cell8
 
   // ShadeSample (:498-550); `lit` counts the shadow box chains traced.

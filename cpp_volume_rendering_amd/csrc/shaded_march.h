@@ -293,7 +293,7 @@ shaded_jobs_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
 }
 
 template <class SH, bool PHONG>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH::kMinWavesPerEU)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH::kFlatWavesPerEU)))
 flat_shade_kernel(typename SH::Args Q, typename SH::Data data, FlatJobs J, unsigned long long total,
                   int nchunks, int group, unsigned long long* __restrict__ shade_ctr) {
   // block b runs on XCD b % 8; XCD x takes chunk groups x, x + 8, ... in order

@@ -7,11 +7,13 @@ takes the max over ranks).  --renderer dos|ebs: configs 4/5 instead (512^3 at 20
 Usage: python tools/overlap_probe.py [--nranks 1,2,4,8] [--tile 16] [--streams 4]
        [--quad 0] [--frames 32] [--renderer rc1pass]"""
 import os
-os.environ["GPU_MAX_HW_QUEUES"] = "8"          # as bench.py, before HIP initialises
+import sys
+# hardware queues: 8 as bench.py (--hwq N overrides), set before HIP initialises
+os.environ["GPU_MAX_HW_QUEUES"] = (sys.argv[sys.argv.index("--hwq") + 1]
+                                   if "--hwq" in sys.argv else "8")
 import argparse  # noqa: E402
 import ctypes  # noqa: E402
 import json  # noqa: E402
-import sys  # noqa: E402
 import time  # noqa: E402
 
 import torch  # noqa: E402
@@ -34,6 +36,7 @@ ap.add_argument("--streams", default="4")
 ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks")
 ap.add_argument("--renderer", choices=["rc1pass", "dos", "ebs"], default="rc1pass")
 ap.add_argument("--out", default="")
+ap.add_argument("--hwq", default="8")
 a = ap.parse_args()
 
 n, W = (1024, 1024) if a.renderer == "ebs" else ((512, 2048) if a.renderer == "dos" else (512, 1024))
@@ -87,7 +90,7 @@ for q in [int(x) for x in a.quad.split(",")]:
                         torch.cuda.synchronize()
                         best = min(best, (time.perf_counter() - t0) / a.frames * 1e3)
                     per.append(best)
-                line = dict(renderer=a.renderer, nranks=nr, tile=tile, quad=q, streams=ns,
+                line = dict(renderer=a.renderer, nranks=nr, tile=tile, quad=q, streams=ns, hwq=int(a.hwq),
                             ms_per_rank=[round(x, 5) for x in per], max_ms=round(max(per), 5),
                             mean_ms=round(sum(per) / len(per), 5),
                             max_over_mean=round(max(per) / (sum(per) / len(per)), 4))
