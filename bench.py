@@ -309,9 +309,9 @@ def cone_fetches(r, n, scale):
     return out
 
 
-def load_traffic(path, workload_key):
-    """HBM bytes per launch measured by PMC (tools/pmc_traffic.py) for this exact
-    workload: `path` or any profiles/pmc_<renderer>*.json beside it."""
+def load_pmc(path, workload_key):
+    """The PMC record (tools/pmc_traffic.py, tools/pmc_bench.sh) of this exact workload:
+    `path` or any profiles/pmc_<renderer>*.json beside it; {} if none."""
     import glob
     stem = os.path.splitext(path)[0]
     for f in [path] + sorted(glob.glob(stem + "_*.json")):
@@ -321,8 +321,13 @@ def load_traffic(path, workload_key):
         except (OSError, ValueError):
             continue
         if d.get("workload_key") == workload_key:
-            return d.get("hbm_bytes_per_launch")
-    return None
+            return d
+    return {}
+
+
+def load_traffic(path, workload_key):
+    """HBM bytes per launch measured by PMC for this exact workload (or None)."""
+    return load_pmc(path, workload_key).get("hbm_bytes_per_launch")
 
 
 def postpass_bench(r, dev, W, H, reps):
@@ -612,7 +617,10 @@ def main():
         wkey = (f"{a.renderer}_{a.field}{n}_{W}x{H}{'_phong' if a.phong else ''}"
                 f"{'_orbit' if a.orbit else ''}"
                 f"{f'_alpha{a.tf_alpha:g}' if a.tf_alpha != 1.0 else ''}")
-        kname = ("shaded_march_kernel<DosShader>" if dos else
+        flat = shaded and N.lib().cvr_get_option(r.device.handle, b"shade_flat") == 1
+        kname = ("flat_shade_kernel<DosShader> (+ shaded_jobs_kernel x2, flat_fold_kernel)" if dos and flat else
+                 "flat_shade_kernel<EbsShaderT> (+ shaded_jobs_kernel x2, flat_fold_kernel)" if ebs and flat else
+                 "shaded_march_kernel<DosShader>" if dos else
                  "shaded_march_kernel<EbsShader>" if ebs else
                  f"iso_tile_kernel<{iso_variant}, {str(a.phong).lower()}>" if iso else
                  f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, *, false, true, *>")
@@ -630,8 +638,18 @@ def main():
                 # flight overlap, so a frame takes less than one launch's duration)
                 "frac_frame": round(b_alg / (ms_per_step * 1e-3) / 1e9 / peak, 4)}
         if ebs:
-            # the vector-memory pipe: 2 dwordx4 wave-loads (2 x 1 KiB) per 64 SAT fetches
-            roof["vmem_dwordx4_per_s"] = round(2 * fetches / 64 / (kern_ms * 1e-3), 1)
+            # the vector-memory pipe: 2 dwordx4 wave-loads (2 x 1 KiB) per 64 SAT fetches,
+            # against 256 CUs x one 1-KiB wave-load per 16 clocks (64 B/clk per CU L1) at
+            # 2.4 GHz; PMC: the texture-data unit's busy share per CU (pmc_ebs.json)
+            vm = 2 * fetches / 64 / (kern_ms * 1e-3)
+            vm_peak = 256 * 2.4e9 / 16
+            roof["vmem_dwordx4_per_s"] = round(vm, 1)
+            roof["vmem_peak_dwordx4_per_s"] = vm_peak
+            roof["vmem_frac"] = round(vm / vm_peak, 4)
+            pmc = load_pmc(a.pmc.replace("rc1pass", a.renderer), wkey)
+            if pmc.get("td_busy_frac_per_cu") is not None:
+                roof["pmc_td_busy_per_cu"] = round(pmc["td_busy_frac_per_cu"], 3)
+                roof["pmc_l2_hit_rate"] = round(pmc["tcc_hit_rate"], 3)
             roof["alg_over_hbm_peak"] = round(achieved / HBM_PEAK_GBS, 4)
         if roof["traffic"]:
             # the bytes HBM actually served (PMC) at the kernel's own time: where the

@@ -181,15 +181,17 @@ constexpr int kMaxBandTiles = 8192;
 // one frame's shading jobs in a single global list, shaded by a grid of their own
 // and folded into the pixels afterwards.  Buffers grow on demand, one set per context.
 struct FlatJobs {
-  uint32_t* lane_jobs = nullptr;            // jobs per pixel slot (tile * 64 + lane)
-  uint32_t* tile_off = nullptr;             // jobs per 8x8 tile, scanned in place to offsets
-  unsigned long long* total = nullptr;      // the frame's job count (device)
+  uint32_t* tile_off = nullptr;             // jobs per 8x8 tile, scanned in place to offsets [tiles + 1]
+  uint32_t* tile_roff = nullptr;            // march rounds with a job per tile, scanned likewise
+  unsigned long long* masks = nullptr;      // per such round: the lanes that made a job (ballot)
+  unsigned long long* total = nullptr;      // [2]: the frame's jobs and rounds (device)
   unsigned long long* h_total = nullptr;    // pinned host copy
   float4* cam = nullptr;                    // the ray's camera direction per pixel slot
   float4* jobs = nullptr;                   // 2 float4 per job (+1 with Phong)
   float4* res = nullptr;                    // shaded rgb * alpha, alpha, per job
   int tiles = 0;                            // allocated 8x8 tiles
   size_t cap = 0;                           // allocated jobs (float4 units: cap * 3)
+  size_t rcap = 0;                          // allocated round masks
 };    // the epilogue sorts a band in LDS (32 KiB + group prefixes)
 
 struct Ctx {

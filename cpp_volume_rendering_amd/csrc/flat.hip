@@ -10,58 +10,84 @@
 
 namespace cvr {
 
-// Exclusive scan of the per-tile job counts (in place) and the frame total.
-// One workgroup: a contiguous run of tiles per thread, then a scan of the runs.
-__global__ void __launch_bounds__(1024) flat_scan_kernel(uint32_t* __restrict__ tile_off, int n,
+// Exclusive scans (in place) of the per-tile job and round counts, each with
+// its total at index n and in total[0] / total[1].  One workgroup walks the
+// array in coalesced blocks of 4096 counts (a uint4 per thread), scanning each
+// block through LDS and carrying its sum into the next.
+__device__ void flat_scan_one(uint32_t* __restrict__ a, int n, unsigned long long* __restrict__ total,
+                              unsigned long long* part) {
+  const int t = threadIdx.x;
+  unsigned long long carry = 0;
+  for (int base = 0; base < n; base += 4096) {
+    const int i0 = base + 4 * t;
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = i0 + k < n ? a[i0 + k] : 0u;
+    const unsigned long long sum = (unsigned long long)v[0] + v[1] + v[2] + v[3];
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {          // Hillis-Steele inclusive scan
+      const unsigned long long x = t >= d ? part[t - d] : 0ull;
+      __syncthreads();
+      part[t] += x;
+      __syncthreads();
+    }
+    unsigned long long run = carry + part[t] - sum;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (i0 + k < n) a[i0 + k] = (uint32_t)run;
+      run += v[k];
+    }
+    carry += part[1023];
+    __syncthreads();
+  }
+  if (t == 0) {
+    *total = carry;
+    a[n] = (uint32_t)carry;
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(1024) flat_scan_kernel(uint32_t* __restrict__ tile_off,
+                                                         uint32_t* __restrict__ tile_roff, int n,
                                                          unsigned long long* __restrict__ total) {
   __shared__ unsigned long long part[1024];
-  const int t = threadIdx.x;
-  const int per = (n + 1023) / 1024;
-  const int lo = min(n, t * per), hi = min(n, lo + per);
-  unsigned long long sum = 0;
-  for (int i = lo; i < hi; i++) sum += tile_off[i];
-  part[t] = sum;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {          // Hillis-Steele inclusive scan of the runs
-    const unsigned long long v = t >= d ? part[t - d] : 0ull;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  unsigned long long run = part[t] - sum;       // exclusive start of this thread's run
-  for (int i = lo; i < hi; i++) {
-    const uint32_t v = tile_off[i];
-    tile_off[i] = (uint32_t)run;
-    run += v;
-  }
-  if (t == 1023) *total = part[1023];
+  flat_scan_one(tile_off, n, total + 0, part);
+  flat_scan_one(tile_roff, n, total + 1, part);
 }
 
 // Per pixel: its jobs' results folded in sample order, dst.a replayed from the
 // alphas (the sequential loop: om = 1 - dst.a; dst.a = fma(om, a, dst.a);
-// dst.rgb = fma(om, rgb * a, dst.rgb)).
+// dst.rgb = fma(om, rgb * a, dst.rgb)).  The tile's march rounds are replayed
+// from their ballot masks: round r's results sit contiguously in lane order.
 __global__ void __launch_bounds__(64) flat_fold_kernel(Rc1passArgs A, FlatJobs J,
                                                        float4* __restrict__ out) {
-  const int t = blockIdx.x, lane = threadIdx.x, slot = t * 64 + lane;
+  const int t = blockIdx.x, lane = threadIdx.x;
+  const unsigned long long lt = (1ull << lane) - 1ull;
   int px, py;
   long long oidx;
   tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
-  const uint32_t n = J.lane_jobs[slot];
-  size_t i = (size_t)J.tile_off[t] + wave_excl_scan(n, lane);
+  size_t j = J.tile_off[t];
+  const uint32_t r0 = J.tile_roff[t], r1 = J.tile_roff[t + 1];
   float4 dst = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (uint32_t j = 0; j < n; j++, i++) {
-    const float4 r = J.res[i];
-    const float om = 1.0f - dst.w;
-    dst.w = fmaf(om, r.w, dst.w);
-    dst.x = fmaf(om, r.x, dst.x);
-    dst.y = fmaf(om, r.y, dst.y);
-    dst.z = fmaf(om, r.z, dst.z);
+  for (uint32_t r = r0; r < r1; r++) {
+    const unsigned long long m = J.masks[r];
+    if ((m >> lane) & 1ull) {
+      const float4 v = J.res[j + __popcll(m & lt)];
+      const float om = 1.0f - dst.w;
+      dst.w = fmaf(om, v.w, dst.w);
+      dst.x = fmaf(om, v.x, dst.x);
+      dst.y = fmaf(om, v.y, dst.y);
+      dst.z = fmaf(om, v.z, dst.z);
+    }
+    j += __popcll(m);
   }
   if ((px < A.W && py < A.H) || A.packed) store_rgba(out, oidx, dst, A.out_half);
 }
 
 hipError_t launch_flat_scan(FlatJobs& J, int ntiles, hipStream_t s) {
-  hipLaunchKernelGGL(flat_scan_kernel, dim3(1), dim3(1024), 0, s, J.tile_off, ntiles, J.total);
+  hipLaunchKernelGGL(flat_scan_kernel, dim3(1), dim3(1024), 0, s, J.tile_off, J.tile_roff, ntiles,
+                     J.total);
   return hipGetLastError();
 }
 
@@ -76,26 +102,27 @@ static void free_ptr(void*& p) {
   p = nullptr;
 }
 
-// Buffers for `ntiles` 8x8 tiles and `jobs` jobs (0: the per-pixel part only).
-// Grows, never shrinks; the job list gets 1/4 headroom so a slowly moving camera
-// does not re-allocate every frame.  Blocks the calling thread only when it allocates.
-hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, int /*phong*/) {
+// Buffers for `ntiles` 8x8 tiles, `jobs` jobs and `rounds` round masks (0: the
+// per-tile part only).  Grows, never shrinks; the job list and the masks get
+// 1/4 headroom so a slowly moving camera does not re-allocate every frame.
+// Blocks the calling thread only when it allocates.
+hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds) {
   hipError_t e = hipSuccess;
   if (J.tiles < ntiles) {
-    void* p = J.lane_jobs; free_ptr(p); J.lane_jobs = nullptr;
-    p = J.tile_off; free_ptr(p); J.tile_off = nullptr;
+    void* p = J.tile_off; free_ptr(p); J.tile_off = nullptr;
+    p = J.tile_roff; free_ptr(p); J.tile_roff = nullptr;
     p = J.cam; free_ptr(p); J.cam = nullptr;
     J.tiles = 0;
     const size_t slots = (size_t)ntiles * 64;
-    if ((e = hipMalloc((void**)&J.lane_jobs, slots * sizeof(uint32_t))) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&J.tile_off, ((size_t)ntiles + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+    if ((e = hipMalloc((void**)&J.tile_roff, ((size_t)ntiles + 1) * sizeof(uint32_t))) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&J.cam, slots * sizeof(float4))) != hipSuccess) return e;
     J.tiles = ntiles;
   }
-  if (!J.total && (e = hipMalloc((void**)&J.total, sizeof(unsigned long long))) != hipSuccess) return e;
-  if (!J.h_total && (e = hipHostMalloc((void**)&J.h_total, sizeof(unsigned long long))) != hipSuccess)
+  if (!J.total && (e = hipMalloc((void**)&J.total, 2 * sizeof(unsigned long long))) != hipSuccess) return e;
+  if (!J.h_total && (e = hipHostMalloc((void**)&J.h_total, 2 * sizeof(unsigned long long))) != hipSuccess)
     return e;
-  if (jobs >= (1ull << 32)) return hipErrorInvalidValue;   // 32-bit tile offsets
+  if (jobs >= (1ull << 32) || rounds >= (1ull << 32)) return hipErrorInvalidValue;   // 32-bit offsets
   if (jobs > J.cap) {
     void* p = J.jobs; free_ptr(p); J.jobs = nullptr;
     p = J.res; free_ptr(p); J.res = nullptr;
@@ -105,12 +132,20 @@ hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, int /*phong*/) {
     if ((e = hipMalloc((void**)&J.res, cap * sizeof(float4))) != hipSuccess) return e;
     J.cap = cap;
   }
+  if (rounds > J.rcap) {
+    void* p = J.masks; free_ptr(p); J.masks = nullptr;
+    J.rcap = 0;
+    const size_t cap = rounds + rounds / 4 + 1024;
+    if ((e = hipMalloc((void**)&J.masks, cap * sizeof(unsigned long long))) != hipSuccess) return e;
+    J.rcap = cap;
+  }
   return hipSuccess;
 }
 
 void flat_release(FlatJobs& J) {
-  void* p = J.lane_jobs; free_ptr(p);
-  p = J.tile_off; free_ptr(p);
+  void* p = J.tile_off; free_ptr(p);
+  p = J.tile_roff; free_ptr(p);
+  p = J.masks; free_ptr(p);
   p = J.cam; free_ptr(p);
   p = J.total; free_ptr(p);
   p = J.jobs; free_ptr(p);

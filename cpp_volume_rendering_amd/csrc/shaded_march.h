@@ -201,30 +201,23 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
 // tile: with fewer tiles per GPU (the screen split) the longest waves set the
 // frame time (one 1024^3 EBS wave runs for ~45 ms; 8 ranks: 2.1x, not 8x).
 // Flat shading cuts the frame at the job instead:
-//   1. shaded_jobs_kernel<count>: the march, counting each pixel's jobs
+//   1. shaded_jobs_kernel<count>: the march, counting per tile the jobs
 //      (samples with alpha > 0 before the ERT break; opacity does not depend on
-//      shading, so the march is exact without it) and the tile sums;
-//   2. flat_scan_kernel: the tiles' exclusive offsets and the frame total,
+//      shading, so the march is exact without it) and the march rounds in which
+//      at least one lane made a job;
+//   2. flat_scan_kernel: both counts to exclusive offsets and frame totals,
 //      which the host reads to size the grid (one stream sync per frame);
-//   3. shaded_jobs_kernel<emit>: the same march, writing every job (position,
-//      alpha, TF rgb, pixel slot; + gradient with Phong) at its pixel's offset;
+//   3. shaded_jobs_kernel<emit>: the same march; each round's jobs are written
+//      contiguously (lane order, so the stores coalesce: position, alpha, TF
+//      rgb, pixel slot; + gradient with Phong) and the round's ballot mask kept;
 //   4. flat_shade_kernel: one job per lane over the whole list, 64-job chunks
 //      dealt to the XCDs in groups of flat_group consecutive chunks (one XCD's
 //      L2 sees neighbouring rays' neighbouring samples);
-//   5. flat_fold_kernel: per pixel, its results folded front to back with the
-//      sequential loop's fma order (dst.a replayed from the alphas), so the
-//      image is bit-identical to the per-wave kernel and to the oracle.
+//   5. flat_fold_kernel: the tile's rounds replayed from their masks, each
+//      lane folding its results front to back with the sequential loop's fma
+//      order (dst.a from the alphas), so the image is bit-identical to the
+//      per-wave kernel and to the oracle.
 // ---------------------------------------------------------------------------
-
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  return x - v;
-}
 
 template <class SH, bool PHONG, bool EMIT>
 __global__ void __launch_bounds__(64)
@@ -238,6 +231,7 @@ shaded_jobs_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
   const int t = screen_tile_of_block<CVR_SHADED_COLGROUP>(A, blockIdx.x, A.ntiles);
   const int lane = threadIdx.x;
   const int slot = t * 64 + lane;
+  const unsigned long long lt = (1ull << lane) - 1ull;
   int px, py;
   long long oidx;
   tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
@@ -246,50 +240,75 @@ shaded_jobs_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
   bool active = inside && ray_setup(A, px, py, r);
   active = active && 0.0f < r.D;
   const bool wave_in_box = __ballot(active && r.outside) == 0;   // else clamp positions
-  size_t next = 0;                                                // EMIT: this lane's next job
-  if (EMIT) next = (size_t)J.tile_off[t] + wave_excl_scan(J.lane_jobs[slot], lane);
+  size_t jbase = 0, rbase = 0;                                    // EMIT: the tile's next job / round
+  if (EMIT) {
+    jbase = J.tile_off[t];
+    rbase = J.tile_roff[t];
+  }
   const float step = A.step, fn = (float)A.tf_n;
   float s = 0.0f, dst_a = 0.0f;
-  uint32_t cnt = 0, n = 0;
-  while (active) {
-    const float h = fminf(step, r.D - s);
-    const float tt = fmaf(h, 0.5f, s);
-    const float x = fmaf(r.dt.x, tt, r.o.x), y = fmaf(r.dt.y, tt, r.o.y), z = fmaf(r.dt.z, tt, r.o.z);
-    const SamplePos sp = wave_in_box ? sample_pos(x, y, z, A) : sample_pos_clamped(x, y, z, A);
-    const float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
-    cnt++;
-    if (sc.w > 0.0f) {
-      const float a = 1.0f - cvr_expf(-(sc.w * h));
-      if (EMIT) {
-        const f3 tx = vmad(r.dir, tt, r.tpos);        // tx_pos, box at [0, G]
-        float4* jp = J.jobs + next * (PHONG ? 3 : 2);
-        jp[0] = make_float4(tx.x, tx.y, tx.z, a);
-        jp[1] = make_float4(sc.x, sc.y, sc.z, __int_as_float(slot));
-        if (PHONG) {
-          const f3 g = sample_gradient_cell(grad, sp);
-          jp[2] = make_float4(g.x, g.y, g.z, 0.0f);
+  uint32_t cnt = 0, rounds = 0, tjobs = 0;   // rounds, tjobs: wave-uniform
+  bool any_job = false;
+  for (;;) {   // one sample per live lane per round (wave-uniform loop)
+    if (__ballot(active) == 0) break;
+    bool pushed = false;
+    float4 q0, q1, q2;
+    if (active) {
+      const float h = fminf(step, r.D - s);
+      const float tt = fmaf(h, 0.5f, s);
+      const float x = fmaf(r.dt.x, tt, r.o.x), y = fmaf(r.dt.y, tt, r.o.y), z = fmaf(r.dt.z, tt, r.o.z);
+      const SamplePos sp = wave_in_box ? sample_pos(x, y, z, A) : sample_pos_clamped(x, y, z, A);
+      const float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
+      cnt++;
+      if (sc.w > 0.0f) {
+        const float a = 1.0f - cvr_expf(-(sc.w * h));
+        if (EMIT) {
+          const f3 tx = vmad(r.dir, tt, r.tpos);        // tx_pos, box at [0, G]
+          q0 = make_float4(tx.x, tx.y, tx.z, a);
+          q1 = make_float4(sc.x, sc.y, sc.z, __int_as_float(slot));
+          if (PHONG) {
+            const f3 g = sample_gradient_cell(grad, sp);
+            q2 = make_float4(g.x, g.y, g.z, 0.0f);
+          }
         }
-        next++;
+        dst_a = fmaf(1.0f - dst_a, a, dst_a);
+        pushed = true;
+        any_job = true;
+        if (dst_a > 0.99f) active = false;
       }
-      dst_a = fmaf(1.0f - dst_a, a, dst_a);
-      n++;
-      if (dst_a > 0.99f) break;
+      if (active) {
+        s = s + h;
+        active = s < r.D;
+      }
     }
-    s = s + h;
-    active = s < r.D;
+    const unsigned long long m = __ballot(pushed);
+    if (m) {
+      if (EMIT) {
+        if (pushed) {
+          float4* jp = J.jobs + (jbase + __popcll(m & lt)) * (PHONG ? 3 : 2);
+          jp[0] = q0;
+          jp[1] = q1;
+          if (PHONG) jp[2] = q2;
+        }
+        if (lane == 0) J.masks[rbase + rounds] = m;
+        jbase += __popcll(m);
+      }
+      tjobs += __popcll(m);
+      rounds++;
+    }
   }
   if (EMIT) return;
-  J.lane_jobs[slot] = n;
-  J.cam[slot] = (inside && n) ? make_float4(r.cam.x, r.cam.y, r.cam.z, 0.0f)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-  const unsigned long long tj = wave_sum((unsigned long long)n);
-  if (lane == 0) J.tile_off[t] = (uint32_t)tj;
+  J.cam[slot] = any_job ? make_float4(r.cam.x, r.cam.y, r.cam.z, 0.0f) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (lane == 0) {
+    J.tile_off[t] = tjobs;
+    J.tile_roff[t] = rounds;
+  }
   if ((inside || A.packed) && samples) samples[oidx] = cnt;
   if (tile_samples) {
     const unsigned long long v = wave_sum(cnt);
     if (lane == 0) tile_samples[t] = v;
   }
-  if (shade_ctr && lane == 0) atomicAdd(&shade_ctr[0], tj);
+  if (shade_ctr && lane == 0) atomicAdd(&shade_ctr[0], (unsigned long long)tjobs);
 }
 
 template <class SH, bool PHONG>
@@ -332,7 +351,7 @@ flat_shade_kernel(typename SH::Args Q, typename SH::Data data, FlatJobs J, unsig
 
 hipError_t launch_flat_scan(FlatJobs& J, int ntiles, hipStream_t s);
 hipError_t launch_flat_fold(const Rc1passArgs& a, FlatJobs& J, float4* out, hipStream_t s);
-hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, int phong);
+hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds);
 
 template <class SH>
 hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool phong,
@@ -343,7 +362,7 @@ hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool pho
   if (nt <= 0) return hipSuccess;
   if (q.a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
   FlatJobs& J = c.flat;
-  hipError_t e = flat_reserve(J, nt, 0, phong);
+  hipError_t e = flat_reserve(J, nt, 0, 0);
   if (e != hipSuccess) return e;
   const size_t lds = (size_t)(q.a.tf_n + 2) * sizeof(float4);
   const uint4* cells = (const uint4*)c.d_cells;
@@ -357,13 +376,13 @@ hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool pho
                        grad, tf, J, samples, shade_ctr, tile_samples);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = launch_flat_scan(J, nt, s)) != hipSuccess) return e;
-  if ((e = hipMemcpyAsync(J.h_total, J.total, sizeof(unsigned long long), hipMemcpyDeviceToHost, s)) !=
-      hipSuccess)
+  if ((e = hipMemcpyAsync(J.h_total, J.total, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                          s)) != hipSuccess)
     return e;
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-  const unsigned long long total = *J.h_total;
+  const unsigned long long total = J.h_total[0], rounds = J.h_total[1];
   if (total > 0) {
-    if ((e = flat_reserve(J, nt, (size_t)total, phong)) != hipSuccess) return e;
+    if ((e = flat_reserve(J, nt, (size_t)total, (size_t)rounds)) != hipSuccess) return e;
     if (phong)
       hipLaunchKernelGGL((shaded_jobs_kernel<SH, true, true>), dim3(nt), dim3(64), lds, s, q, cells,
                          grad, tf, J, nullptr, nullptr, nullptr);

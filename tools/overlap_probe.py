@@ -37,6 +37,7 @@ ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks")
 ap.add_argument("--renderer", choices=["rc1pass", "dos", "ebs"], default="rc1pass")
 ap.add_argument("--out", default="")
 ap.add_argument("--hwq", default="8")
+ap.add_argument("--boost", default="-1", help="rc1pass: comma list of boost percentages (-1: library default)")
 a = ap.parse_args()
 
 n, W = (1024, 1024) if a.renderer == "ebs" else ((512, 2048) if a.renderer == "dos" else (512, 1024))
@@ -65,9 +66,12 @@ def render(frame, out):
 
 
 res = []
-for q in [int(x) for x in a.quad.split(",")]:
+import itertools  # noqa: E402
+for q, bst in itertools.product([int(x) for x in a.quad.split(",")], [int(x) for x in a.boost.split(",")]):
     if a.renderer == "rc1pass":
         L.cvr_set_option(handle, b"quad", q)
+        if bst >= 0:
+            L.cvr_set_option(handle, b"boost", bst)
     for nr in [int(x) for x in a.nranks.split(",")]:
         for tile in [int(x) for x in a.tile.split(",")]:
             ranks = range(nr) if a.ranks == "all" else [int(x) for x in a.ranks.split(",") if int(x) < nr]
@@ -90,7 +94,7 @@ for q in [int(x) for x in a.quad.split(",")]:
                         torch.cuda.synchronize()
                         best = min(best, (time.perf_counter() - t0) / a.frames * 1e3)
                     per.append(best)
-                line = dict(renderer=a.renderer, nranks=nr, tile=tile, quad=q, streams=ns, hwq=int(a.hwq),
+                line = dict(renderer=a.renderer, nranks=nr, tile=tile, quad=q, boost=bst, streams=ns, hwq=int(a.hwq),
                             ms_per_rank=[round(x, 5) for x in per], max_ms=round(max(per), 5),
                             mean_ms=round(sum(per) / len(per), 5),
                             max_over_mean=round(max(per) / (sum(per) / len(per)), 4))
