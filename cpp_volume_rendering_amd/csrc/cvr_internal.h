@@ -20,6 +20,8 @@ struct CellGrid {
   int cx, cy, cz;           // cells per axis = N + 1
   int pitch_y, pitch_z;     // cx, cx*cy
   long long linear_origin;  // index of cell (1,1,1) = texel (0,0,0)
+  int bpitch_y, bpitch_z;   // the pitches in bytes (16 B per cell)
+  uint32_t borigin;         // linear_origin * 16, mod 2^32 (byte offsets of buffer loads)
 };
 
 // Screen-tile split: which TxT tile is rank r's k-th.  Tiles
@@ -377,6 +379,9 @@ inline CellGrid make_cell_grid(const int N[3]) {
   g.pitch_y = g.cx;
   g.pitch_z = g.cx * g.cy;
   g.linear_origin = 1 + (long long)g.pitch_y + (long long)g.pitch_z;
+  g.bpitch_y = (int)((long long)g.pitch_y * 16 < (1ll << 31) ? g.pitch_y * 16 : 0);
+  g.bpitch_z = (int)((long long)g.pitch_z * 16 < (1ll << 31) ? (long long)g.pitch_z * 16 : 0);
+  g.borigin = (uint32_t)((unsigned long long)g.linear_origin * 16ull);
   return g;
 }
 

@@ -74,7 +74,7 @@ __device__ __forceinline__ bool skip_empty(const Rc1passArgs& A, const Ray& r, f
 // Ray-parallel march (one lane per ray) of ray_marching_1p.comp:124-172.  The
 // arithmetic per sample is exactly the reference's sequential loop (s
 // accumulates h one step at a time); batching only changes when loads issue.
-template <int K, bool PHONG, bool SKIP, bool XF, bool BUF, int FB>
+template <int K, bool PHONG, bool SKIP, bool XF, int BUF, int FB>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
                                           const uint4* __restrict__ grad,
                                           const float4* __restrict__ tfp, int px, int py,
@@ -95,9 +95,15 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
   // instructions and VGPRs per load; -3 % on the headline frame)
   const __amdgpu_buffer_rsrc_t crs =
       __builtin_amdgcn_make_buffer_rsrc((void*)cells, 0, -1, kBufferConfigDword);
-  auto load_cell = [&](uint32_t i) -> uint4 {
-    if (BUF) return buffer_load_u4(crs, i << 4);
-    return cells[i];
+  // BUF 2 (16 * pitch_z fits a signed 24-bit operand): the byte offset in three
+  // instructions, two v_mad_i32_i24 whose sums wrap mod 2^32 to the exact
+  // offset (< 4 GiB); BUF 1: the cell index times 16
+  auto load_cell = [&](const SamplePos& p) -> uint4 {
+    if (BUF == 2)
+      return buffer_load_u4(crs, mad_i24(p.iz, A.cells.bpitch_z,
+                                         mad_i24(p.iy, A.cells.bpitch_y, ((uint32_t)p.ix << 4) + A.cells.borigin)));
+    if (BUF == 1) return buffer_load_u4(crs, p.idx << 4);
+    return cells[p.idx];
   };
   while (!done) {
     // Empty-space skipping (bit-exact): if the macro cell holding the next
@@ -162,7 +168,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
                               (v.z & 0x01ff01ffu) | 0x00000000u, (v.w & 0x01ff01ffu) | 0x00000000u);
         }
 #else
-        raw[j] = load_cell(sp[j].idx);
+        raw[j] = load_cell(sp[j]);
 #endif
       }
     } else {
@@ -170,7 +176,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       for (int j = 0; j < K; j++) {
         sp[j] = sample_pos_clamped(fmaf(r.dt.x, tj[j], r.o.x), fmaf(r.dt.y, tj[j], r.o.y),
                                    fmaf(r.dt.z, tj[j], r.o.z), A);
-        raw[j] = load_cell(sp[j].idx);
+        raw[j] = load_cell(sp[j]);
       }
     }
     if (FB) {   // GL texture-unit weights (filter_bits): volume and gradient fetches
@@ -187,9 +193,8 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
 #pragma unroll
       for (int j = 0; j < K; j++) {
         const float xd = fmaf(trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az), fn, -0.5f);
-        const float fl = floorf(xd);
-        tfa[j] = filter_weight<FB>(xd - fl);
-        tfi[j] = (int)fl + 1;
+        tfa[j] = filter_weight<FB>(__builtin_amdgcn_fractf(xd));   // see classify
+        tfi[j] = cvt_flr(xd) + 1;
         src[j].w = lerpf(tfp[tfi[j]].w, tfp[tfi[j] + 1].w, tfa[j]);
       }
     } else
@@ -381,7 +386,7 @@ constexpr int rc1_waves_per_eu() {
   return (K == 4 && !PHONG && !SKIP && !QUAD) ? 8 : 1;
 #endif
 }
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, bool BUF, int FB>
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rc1_waves_per_eu<K, PHONG, SKIP, QUAD>())))
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
@@ -677,7 +682,7 @@ __global__ void clear_u32_kernel(uint32_t* __restrict__ p, int n) {
 // Kernel variant: K (batch), PHONG, SKIP (empty-space skipping compiled in),
 // QUAD (quad path compiled in), XF (range-free exp).  Paths a frame does not
 // use are compiled out: they would cost the hot loop registers (occupancy).
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, bool BUF, int FB = 0>
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB = 0>
 static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                                  unsigned long long* tile_samples, const int* order,
                                  uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
@@ -696,23 +701,32 @@ template <int K, bool PHONG, bool SKIP>
 static hipError_t launch_kps(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                              unsigned long long* ts, const int* order, uint32_t* tile_cost,
                              const RenderPlan& plan, hipStream_t s) {
+  // buffer loads address the cell grid with 32-bit byte offsets (BUF 2: the
+  // 24-bit multiply-add form, while 16 * pitch_z < 2^23, i.e. up to 723^3)
+  const int buf = c.cells_bytes >= (size_t(1) << 32) ? 0
+                  : (c.cells.bpitch_z > 0 && c.cells.bpitch_z < (1 << 23)) ? 2 : 1;
   if (a.filter_bits == 8) {   // GL texture-unit weights: the ray-parallel march only
-    if (c.cells_bytes < (size_t(1) << 32))
-      return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, true, 8>(c, a, out, samples, ts, order, tile_cost, plan, s)
-                        : launch_variant<K, PHONG, SKIP, false, false, true, 8>(c, a, out, samples, ts, order, tile_cost, plan, s);
-    return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, false, 8>(c, a, out, samples, ts, order, tile_cost, plan, s)
-                      : launch_variant<K, PHONG, SKIP, false, false, false, 8>(c, a, out, samples, ts, order, tile_cost, plan, s);
+    if (buf == 2)
+      return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, 2, 8>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                        : launch_variant<K, PHONG, SKIP, false, false, 2, 8>(c, a, out, samples, ts, order, tile_cost, plan, s);
+    if (buf == 1)
+      return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, 1, 8>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                        : launch_variant<K, PHONG, SKIP, false, false, 1, 8>(c, a, out, samples, ts, order, tile_cost, plan, s);
+    return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, 0, 8>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                      : launch_variant<K, PHONG, SKIP, false, false, 0, 8>(c, a, out, samples, ts, order, tile_cost, plan, s);
   }
   const bool quad = order && plan.quad_pct > 0;
   if (quad)
-    return a.exp_fast ? launch_variant<K, PHONG, SKIP, true, true, false>(c, a, out, samples, ts, order, tile_cost, plan, s)
-                      : launch_variant<K, PHONG, SKIP, true, false, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
-  // buffer loads address the cell grid with 32-bit byte offsets
-  if (c.cells_bytes < (size_t(1) << 32))
-    return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, true>(c, a, out, samples, ts, order, tile_cost, plan, s)
-                      : launch_variant<K, PHONG, SKIP, false, false, true>(c, a, out, samples, ts, order, tile_cost, plan, s);
-  return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, false>(c, a, out, samples, ts, order, tile_cost, plan, s)
-                    : launch_variant<K, PHONG, SKIP, false, false, false>(c, a, out, samples, ts, order, tile_cost, plan, s);
+    return a.exp_fast ? launch_variant<K, PHONG, SKIP, true, true, 0>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                      : launch_variant<K, PHONG, SKIP, true, false, 0>(c, a, out, samples, ts, order, tile_cost, plan, s);
+  if (buf == 2)
+    return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, 2>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                      : launch_variant<K, PHONG, SKIP, false, false, 2>(c, a, out, samples, ts, order, tile_cost, plan, s);
+  if (buf == 1)
+    return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, 1>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                      : launch_variant<K, PHONG, SKIP, false, false, 1>(c, a, out, samples, ts, order, tile_cost, plan, s);
+  return a.exp_fast ? launch_variant<K, PHONG, SKIP, false, true, 0>(c, a, out, samples, ts, order, tile_cost, plan, s)
+                    : launch_variant<K, PHONG, SKIP, false, false, 0>(c, a, out, samples, ts, order, tile_cost, plan, s);
 }
 
 template <int K, bool PHONG>
