@@ -646,11 +646,22 @@ def main():
             roof["vmem_dwordx4_per_s"] = round(vm, 1)
             roof["vmem_peak_dwordx4_per_s"] = vm_peak
             roof["vmem_frac"] = round(vm / vm_peak, 4)
-            pmc = load_pmc(a.pmc.replace("rc1pass", a.renderer), wkey)
-            if pmc.get("td_busy_frac_per_cu") is not None:
-                roof["pmc_td_busy_per_cu"] = round(pmc["td_busy_frac_per_cu"], 3)
-                roof["pmc_l2_hit_rate"] = round(pmc["tcc_hit_rate"], 3)
             roof["alg_over_hbm_peak"] = round(achieved / HBM_PEAK_GBS, 4)
+        # the counters of the same workload's dominant kernel (rocprofv3 --pmc, committed
+        # under profiles/): which pipe is busy, VALU per sample, the bytes written (for
+        # the headline: the frame + ~8 MB of the 8-wave budget's 2 spilled VGPRs)
+        pmc = load_pmc(a.pmc.replace("rc1pass", a.renderer), wkey)
+        if pmc.get("td_busy_frac_per_cu") is not None:
+            roof["pmc"] = {"td_busy_per_cu": round(pmc["td_busy_frac_per_cu"], 3),
+                           "ta_busy_per_cu": round(pmc["ta_busy_frac_per_cu"], 3),
+                           "valu_issue_per_simd": round(pmc["valu_issue_frac_per_simd"], 3),
+                           "l2_hit_rate": round(pmc["tcc_hit_rate"], 3),
+                           "write_bytes_per_launch": int(pmc["write_bytes_per_launch"])}
+            if pmc.get("valu_per_sample") is not None:
+                roof["pmc"]["valu_per_sample"] = round(pmc["valu_per_sample"], 1)
+            if a.renderer == "rc1pass" and not a.phong:
+                roof["pmc"]["scratch_bytes_per_launch_est"] = max(
+                    0, int(pmc["write_bytes_per_launch"]) - px_bytes * pixels)
         if roof["traffic"]:
             # the bytes HBM actually served (PMC) at the kernel's own time: where the
             # algorithmic figure is mostly served from L1/L2 (frac > 1 for EBS), this
