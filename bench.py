@@ -67,7 +67,7 @@ if __name__ == "__main__":
 # unconditionally (not setdefault), before torch initialises HIP, so the bench runs
 # the configuration DESIGN §7 measured whatever the box's environment holds; the
 # value is reported in config.hw_queues.
-HW_QUEUES = 8
+HW_QUEUES = int(sys.argv[sys.argv.index("--hw-queues") + 1]) if "--hw-queues" in sys.argv else 8
 os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 import torch  # noqa: E402
@@ -122,6 +122,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--format", choices=["rgba16f", "rgba32f"], default="rgba16f",
                    help="frame format: RGBA16F (the reference's framebuffer) or RGBA32F")
+    p.add_argument("--hw-queues", type=int, default=8,
+                   help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises)")
     p.add_argument("--streams", type=int, default=4,
                    help="frames in flight (render streams rotated per frame)")
     p.add_argument("--exchange-frames", type=int, default=0,

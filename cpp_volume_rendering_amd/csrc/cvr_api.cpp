@@ -1095,7 +1095,7 @@ cvr_status cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* f, const void*
 extern "C++" {
 template <class Launch>
 static cvr_status render_shaded(Ctx* c, const cvr_output* o, int ntiles, size_t npix,
-                                const Launch& launch) {
+                                const Launch& launch, bool flat_jobs = false) {
   hipStream_t s = c->stream;
   float4* d_out;
   uint32_t* d_samples;
@@ -1112,9 +1112,9 @@ static cvr_status render_shaded(Ctx* c, const cvr_output* o, int ntiles, size_t 
     d_samples = o->samples ? (uint32_t*)((char*)c->d_scratch + rgba_bytes) : nullptr;
     d_total = o->total ? c->d_total : nullptr;
   }
-  // flat shading (c->shade_flat) keeps one job list per context: frames on other
-  // streams wait for it like for the counters
-  const bool use_counters = d_total || c->shade_counters || c->shade_flat;
+  // flat shading (DOS/EBS with c->shade_flat) keeps one job list per context:
+  // frames on other streams wait for it like for the counters
+  const bool use_counters = d_total || c->shade_counters || flat_jobs;
   if (use_counters) {
     cvr_status st = counters_acquire(c, s);
     if (st != CVR_OK) return st;
@@ -1392,7 +1392,7 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   return render_shaded(c, o, ntiles, npix, [&](float4* out, uint32_t* smp, unsigned long long* shade,
                                                 unsigned long long* ts, hipStream_t st) {
     return cvr::launch_dos(*c, Q, out, smp, shade, ts, st);
-  });
+  }, c->shade_flat != 0);
 }
 
 
@@ -1562,7 +1562,7 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
   return render_shaded(c, o, ntiles, npix, [&](float4* out, uint32_t* smp, unsigned long long* shade,
                                                 unsigned long long* ts, hipStream_t st) {
     return cvr::launch_ebs(*c, Q, out, smp, shade, ts, st);
-  });
+  }, c->shade_flat != 0);
 }
 
 

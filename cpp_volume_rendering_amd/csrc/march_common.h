@@ -144,16 +144,24 @@ __device__ __forceinline__ float pair_lerp(uint32_t w, float t) {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+// PK: the two y lerps as one packed subtract and one packed fma, per lane the
+// same two roundings as lerpf (the emission-absorption march: kernel -5 % with
+// the buffer-offset and TF-weight changes of round 3; the Blinn-Phong march
+// keeps the scalar form, where the register pairs cost it 10 %)
+template <bool PK = false>
 __device__ __forceinline__ float trilerp_cell(uint4 raw, float ax, float ay, float az) {
   float c00 = pair_lerp(raw.x, ax);    // (v000, v100)
   float c10 = pair_lerp(raw.y, ax);    // (v010, v110)
   float c01 = pair_lerp(raw.z, ax);    // (v001, v101)
   float c11 = pair_lerp(raw.w, ax);    // (v011, v111)
-  // the two y lerps as one packed subtract and one packed fma: per lane the same
-  // two roundings as lerpf (round 3: headline kernel -5 % with the two changes below)
-  const f2v lo = {c00, c01}, hi = {c10, c11};
-  const f2v c = __builtin_elementwise_fma(f2v{ay, ay}, hi - lo, lo);
-  return lerpf(c.x, c.y, az);
+  if (PK) {
+    const f2v lo = {c00, c01}, hi = {c10, c11};
+    const f2v c = __builtin_elementwise_fma(f2v{ay, ay}, hi - lo, lo);
+    return lerpf(c.x, c.y, az);
+  }
+  float c0 = lerpf(c00, c10, ay);
+  float c1 = lerpf(c01, c11, ay);
+  return lerpf(c0, c1, az);
 }
 
 // A GL_LINEAR weight at FB fraction bits (FB = 0: the exact float weight).

@@ -192,7 +192,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
     if (!PHONG) {
 #pragma unroll
       for (int j = 0; j < K; j++) {
-        const float xd = fmaf(trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az), fn, -0.5f);
+        const float xd = fmaf(trilerp_cell<true>(raw[j], sp[j].ax, sp[j].ay, sp[j].az), fn, -0.5f);
         tfa[j] = filter_weight<FB>(__builtin_amdgcn_fractf(xd));   // see classify
         tfi[j] = cvt_flr(xd) + 1;
         src[j].w = lerpf(tfp[tfi[j]].w, tfp[tfi[j] + 1].w, tfa[j]);

@@ -6,9 +6,17 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 T=${TAG:-r03}
-PMC_STEPS=24 PMC_TIMEOUT=120 bash tools/pmc_bench.sh rc1pass rc1pass_tile_kernel "--streams 1" > gpurun_out/${T}_pmc_rc1pass.log 2>&1 || { tail -20 gpurun_out/${T}_pmc_rc1pass.log; exit 1; }
-PMC_STEPS=12 PMC_TIMEOUT=120 bash tools/pmc_bench.sh phong rc1pass_tile_kernel "--streams 1 --phong" > gpurun_out/${T}_pmc_phong.log 2>&1 || { tail -20 gpurun_out/${T}_pmc_phong.log; exit 1; }
-find gpurun_out/pmc_rc1pass -name "*kernel_trace.csv" | head -1 | xargs -I{} python3 -c "
-import csv, collections
-c = collections.Counter(r['Grid_Size'] for r in csv.DictReader(open('{}')) if 'rc1pass_tile' in r['Kernel_Name'])
-print(c)"
+env | grep -i "GPU_MAX\|HIP_\|HSA_" > gpurun_out/${T}_env.txt || true
+run() {   # name, lib override ('' = in-tree), bench args
+  local name=$1 lib=$2; shift 2
+  if [ -n "$lib" ]; then export CVR_LIB_OVERRIDE=$lib; else unset CVR_LIB_OVERRIDE; fi
+  timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > gpurun_out/${T}_$name.json 2> gpurun_out/${T}_$name.err || { tail -20 gpurun_out/${T}_$name.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/${T}_$name.json')); print('$name', d['ms_per_step'], d['roofline']['kernel_ms'])"
+}
+for i in 1 2; do
+  for q in 4 8; do
+    run ea_q${q}_$i "" --hw-queues $q
+    run phong_q${q}_$i "" --hw-queues $q --phong
+    run iso_q${q}_$i "" --hw-queues $q --renderer iso
+  done
+done
