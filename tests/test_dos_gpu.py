@@ -224,3 +224,36 @@ def test_dosct_screen_tiles_match_full_frame(dev, bonsai_tf, bonsai_tf_rgba, nra
         tot += int(total[0])
     assert tot == full_total
     assert_bitexact(T.unpack(packed, W, H, tile, nranks), full, "dos tiles")
+
+
+@pytest.mark.parametrize("name", ["occlusion", "shadow_spot", "phong_fd", "occ7_ragged", "inside"])
+def test_dosct_flat_equals_per_wave(dev, bonsai_tf, bonsai_tf_rgba, name):
+    """Flat shading (the default: one job list, shaded by its own grid and folded per
+    pixel, shaded_march.h) against the per-wave deferred kernel, bit for bit, for
+    several XCD chunk groupings, counts included."""
+    c = DOS_CASES[name]
+    n = 48
+    vol = D.marschner_lobb_u8(n)
+    scale = D.voxel_scale(n)
+    setup(dev, vol, scale, bonsai_tf, bonsai_tf_rgba, (64, 64, 64), gmode=c.get("gmode", 0))
+    occ = c["occ"]() if "occ" in c else default_cone_params(True)
+    sdw = default_cone_params(False)
+    W, H = c.get("W", 96), c.get("H", 80)
+    kw = dict(apply_occlusion=c.get("apply_occlusion", True),
+              apply_shadow=c.get("apply_shadow", False), shadow_type=c.get("shadow_type", 0),
+              phong=c.get("phong", False))
+    L = N.lib()
+    step = 0.5 / math.sqrt(3.0)
+    try:
+        L.cvr_set_option(dev.handle, b"shade_flat", 0)
+        ref = gpu_dos(dev, c.get("cam", INITIAL), W, H, step, occ, sdw, **kw)
+        L.cvr_set_option(dev.handle, b"shade_flat", 1)
+        for group in (1, 8, 64):
+            L.cvr_set_option(dev.handle, b"flat_group", group)
+            got = gpu_dos(dev, c.get("cam", INITIAL), W, H, step, occ, sdw, **kw)
+            assert_bitexact(got[1], ref[1], f"{name} counts (group {group})")
+            assert_bitexact(got[0], ref[0], f"{name} rgba (group {group})")
+            assert got[2] == ref[2]
+    finally:
+        L.cvr_set_option(dev.handle, b"shade_flat", 1)
+        L.cvr_set_option(dev.handle, b"flat_group", 8)

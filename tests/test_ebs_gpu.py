@@ -7,6 +7,7 @@ oracle, bit for bit (tolerance 0):
     that SAT: ambient occlusion, point / directional shadows, Blinn-Phong.
 """
 import ctypes
+import math
 
 import numpy as np
 import pytest
@@ -192,3 +193,34 @@ def test_ebs_screen_tiles_match_full_frame(dev, bonsai_tf, nranks, tile):
         tot += int(total[0])
     assert tot == full_total
     assert_bitexact(T.unpack(packed, W, H, tile, nranks), full, "ebs tiles")
+
+
+@pytest.mark.parametrize("name", ["defaults_point", "phong", "directional", "ragged_inside"])
+def test_ebs_flat_equals_per_wave(dev, bonsai_tf, name):
+    """Flat shading (the default) against the per-wave deferred kernel, bit for bit,
+    counts included, for several XCD chunk groupings and a screen-tile share."""
+    c = dict(EBS_CASES[name])
+    n = 40
+    vol = D.marschner_lobb_u8(n)
+    scale = D.voxel_scale(n)
+    W, H = c.pop("W", 80), c.pop("H", 64)
+    cam = c.pop("cam", INITIAL)
+    gpu_sat(dev, vol, scale)
+    dev.set_transfer_function(bonsai_tf)
+    dev.set_gradient(1 if c.get("phong", False) else 0)
+    p = ebs_params(step=0.5 / math.sqrt(3.0), **c)
+    L = N.lib()
+    try:
+        for tile, rank, nranks in ((0, 0, 1), (16, 1, 3)):
+            L.cvr_set_option(dev.handle, b"shade_flat", 0)
+            ref = gpu_ebs(dev, cam, W, H, p, tile, rank, nranks)
+            L.cvr_set_option(dev.handle, b"shade_flat", 1)
+            for group in (1, 8, 64):
+                L.cvr_set_option(dev.handle, b"flat_group", group)
+                got = gpu_ebs(dev, cam, W, H, p, tile, rank, nranks)
+                assert_bitexact(got[1], ref[1], f"{name} counts (group {group}, split {nranks})")
+                assert_bitexact(got[0], ref[0], f"{name} rgba (group {group}, split {nranks})")
+                assert got[2] == ref[2]
+    finally:
+        L.cvr_set_option(dev.handle, b"shade_flat", 1)
+        L.cvr_set_option(dev.handle, b"flat_group", 8)
