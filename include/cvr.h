@@ -277,6 +277,13 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *   "sat_chunk"  z planes per work item of the EBS SAT build (1..64, default 32)
  *   "shade_counters" 1: count shaded / shadow-lit samples of cvr_render_dosct
  *                and cvr_render_extbsd (cvr_read_shade_counters; one atomic per wave)
+ *   "shade_flat" cvr_render_dosct / cvr_render_extbsd: 1 (default) = the frame's
+ *                shading jobs in one list, shaded by a grid of their own and folded
+ *                per pixel; the call then synchronizes the context stream once
+ *                (after the counting march, to size the grid) and frames on other
+ *                streams wait for the previous frame's list; 0 = per-wave deferred
+ *                shading inside the march (fully asynchronous)
+ *   "flat_group" flat shading: consecutive 64-job chunks per XCD turn (default 8)
  * One option changes the arithmetic (and so the image) rather than the speed:
  *   "filter_bits" 0: exact float GL_LINEAR weights (CVR-SPEC, the default);
  *                8: every GL_LINEAR weight of cvr_render_rc1pass (volume, gradient,
