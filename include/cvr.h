@@ -89,10 +89,13 @@ typedef struct cvr_frame {
   int width;        /* viewport (RenderingParameters::GetScreenWidth)         */
   int height;
   /* Screen-tile split (multi-GPU): nranks <= 1 renders the whole W x H image
-   * row-major.  nranks > 1: the image is cut into tile_size^2 tiles, global
-   * tile t (row-major over tiles) belongs to rank t % nranks, and this rank
-   * writes its k-th tile (t = rank + k*nranks) packed at offset
-   * k*tile_size*tile_size pixels, row-major inside the tile.               */
+   * row-major.  nranks > 1: the image is cut into tile_size^2 tiles (a multiple
+   * of 16; 16 recommended) on a diagonal lattice: with ntx tiles per row, this
+   * rank's k-th tile is virtual tile v = rank + k*nranks, at row ty = v / ntx
+   * and column tx = (v % ntx - s*ty) mod ntx, s = 3 for nranks >= 4 else 1
+   * (when nranks divides ntx: rank (tx + s*ty) % nranks).  It is written packed
+   * at offset k*tile_size*tile_size pixels, row-major inside the tile.  Every
+   * rank gets cvr_tiles_for_rank tiles, as with plain t % nranks.  (ABI 2.)  */
   int tile_size;
   int rank;
   int nranks;
