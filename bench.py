@@ -67,7 +67,12 @@ if __name__ == "__main__":
 # unconditionally (not setdefault), before torch initialises HIP, so the bench runs
 # the configuration DESIGN §7 measured whatever the box's environment holds; the
 # value is reported in config.hw_queues.
-HW_QUEUES = int(sys.argv[sys.argv.index("--hw-queues") + 1]) if "--hw-queues" in sys.argv else 8
+# Default by world size (WORLD_SIZE is set by the launcher before this process
+# starts): the frames in flight need a queue each, one per render stream and the
+# RCCL stream (32 at 8 ranks: 16 streams; DESIGN §7, profiles/r03_s25_*).
+_WS = int(os.environ.get("WORLD_SIZE", "1"))
+HW_QUEUES = (int(sys.argv[sys.argv.index("--hw-queues") + 1]) if "--hw-queues" in sys.argv
+             else (32 if _WS >= 8 else (24 if _WS >= 4 else 8)))
 os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 import torch  # noqa: E402
@@ -122,15 +127,16 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--format", choices=["rgba16f", "rgba32f"], default="rgba16f",
                    help="frame format: RGBA16F (the reference's framebuffer) or RGBA32F")
-    p.add_argument("--hw-queues", type=int, default=8,
-                   help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises)")
-    p.add_argument("--streams", type=int, default=4,
-                   help="frames in flight (render streams rotated per frame)")
+    p.add_argument("--hw-queues", type=int, default=0,
+                   help="GPU_MAX_HW_QUEUES for this process, set before HIP initialises "
+                        "(default: 8; 24 at 4 GPUs, 32 at >= 8)")
+    p.add_argument("--streams", type=int, default=0,
+                   help="frames in flight, render streams rotated per frame "
+                        "(default: 4; 12 at 4 GPUs, 16 at >= 8)")
     p.add_argument("--exchange-frames", type=int, default=0,
-                   help="frames per gather at N > 1 (default: 4 at >= 8 GPUs, 2 at 4, else 1)")
+                   help="frames per gather at N > 1 (default: 2 at >= 4 GPUs, else 1)")
     p.add_argument("--quad", type=int, default=-1,
-                   help="quad (4 lanes per ray) share of the longest tiles, %% "
-                        "(default: 10 at >= 8 GPUs, else 0)")
+                   help="quad (4 lanes per ray) share of the longest tiles, %% (default 0)")
     p.add_argument("--transport", choices=["rccl", "torch"], default="rccl",
                    help="N > 1 gather: the library's RCCL communicator or dist.gather")
     p.add_argument("--shade-flat", type=int, default=-1, choices=[-1, 0, 1],
@@ -448,9 +454,12 @@ def main():
     tile = a.tile
     fmt = N.FORMAT_RGBA16F if a.format == "rgba16f" else N.FORMAT_RGBA32F
     # the frame (its tiles on this rank at N > 1): render, RCCL gather to rank 0, unpack
-    # the per-GPU share of the frame shrinks with N: at 8 GPUs the longest rays set
-    # a rank's frame time, and 4 lanes per ray on the longest 10 % of tiles pay off
-    quad = a.quad if a.quad >= 0 else (10 if world >= 8 else 0)
+    # the per-GPU share of the frame shrinks with N while its longest rays do not:
+    # at 8 GPUs a rank's frame is ~14 us of throughput and ~50 us of latency, so
+    # more frames fly (16 streams: 0.0188 ms per rank frame against 0.030 with 4
+    # streams and quad 10 %, which the deeper pipeline no longer needs)
+    quad = a.quad if a.quad >= 0 else 0
+    a.streams = a.streams or (16 if world >= 8 else (12 if world >= 4 else 4))
     if a.renderer == "rc1pass":
         N.check(N.lib().cvr_set_option(r.device.handle, b"quad", quad), "quad", r.device.handle)
         if a.batch:
@@ -470,7 +479,7 @@ def main():
     try:
         # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
         # on rank 0) would otherwise rival a rank's share of the frame (~23 us at N = 8)
-        gx = a.exchange_frames or (4 if world >= 8 else (2 if world >= 4 else 1))
+        gx = a.exchange_frames or (2 if world >= 4 else 1)
         split = T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev,
                                   transport=a.transport if world > 1 else None, streams=a.streams,
                                   frames_per_exchange=gx)

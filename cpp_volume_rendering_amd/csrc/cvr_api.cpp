@@ -388,7 +388,7 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     return CVR_OK;
   }
   if (!std::strcmp(key, "split_streams")) {
-    if (value < 1 || value > 8) return fail(c, CVR_ERR_ARG, "split_streams must be 1..8");
+    if (value < 1 || value > 32) return fail(c, CVR_ERR_ARG, "split_streams must be 1..32");
     c->split_streams = value;
     return CVR_OK;
   }

@@ -276,7 +276,7 @@ struct Ctx {
   };
   int stale_deg = 5;               // option "stale_deg": an order learned on a view more than this
                                    // far away (degrees / 1/12 of the eye distance) is not used
-  static constexpr int kOrderSlots = 8;   // async_order uses the first 3
+  static constexpr int kOrderSlots = 32;  // one per render stream (async_order uses the first 3)
   int async_order = 0;             // option "async_order": 1 = sort on a side stream (lag 3)
   int order_interval = 8;          // option "order_interval": rebuild the order every n-th frame
   OrderSlot oslot[kOrderSlots];
