@@ -206,10 +206,10 @@ def test_rccl_gather_two_ranks_one_gpu():
     assert [p.exitcode for p in procs] == [0, 0]
 
 
-@pytest.mark.parametrize("D", [4, 16])
-def test_rccl_one_rank_gather_pipeline(dev, bonsai_tf, D):
+@pytest.mark.parametrize("nstreams", [4, 16])
+def test_rccl_one_rank_gather_pipeline(dev, bonsai_tf, nstreams):
     """A one-rank communicator through cvr_comm_init / cvr_gather_tiles (ncclGather in
-    place + copy), frames rotated over D streams with split_streams = D (16: the
+    place + copy), frames rotated over n streams with split_streams = n (16: the
     bench's default at 8 GPUs): after cvr_gather_sync the image holds the last
     frame, bit-equal to a direct render."""
     import torch
@@ -222,15 +222,15 @@ def test_rccl_one_rank_gather_pipeline(dev, bonsai_tf, D):
     N.check(L.cvr_comm_unique_id(uid), "uid")
     N.check(L.cvr_comm_init(dev.handle, 1, 0, uid.raw), "cvr_comm_init", dev.handle)
     try:
-        N.check(L.cvr_set_option(dev.handle, b"split_streams", D), "opt", dev.handle)
+        N.check(L.cvr_set_option(dev.handle, b"split_streams", nstreams), "opt", dev.handle)
         W, H = 160, 120
-        streams = [torch.cuda.Stream() for _ in range(D)]
-        bufs = [torch.zeros((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(D)]
+        streams = [torch.cuda.Stream() for _ in range(nstreams)]
+        bufs = [torch.zeros((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(nstreams)]
         img = torch.zeros((H, W, 4), dtype=torch.float16, device="cuda")
         p = N.Rc1passParams()
-        seq = [0, 1, 2, 0, 1, 2, 1] * (3 if D > 4 else 1)
+        seq = [0, 1, 2, 0, 1, 2, 1] * (3 if nstreams > 4 else 1)
         for n, ci in enumerate(seq):
-            k = n % D
+            k = n % nstreams
             frame = make_frame(Camera(**CAMS[ci]), W, H)
             dev.set_stream(streams[k].cuda_stream)
             out = N.Output(bufs[k].data_ptr(), None, None, 1, N.FORMAT_RGBA16F)
