@@ -483,7 +483,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
 // ---------------------------------------------------------------------------
 
 #ifndef CVR_DOS_FLAT_WAVES
-#define CVR_DOS_FLAT_WAVES 4   // flat shading: 128 VGPRs (the compiler's choice is 129, 3 waves)
+#define CVR_DOS_FLAT_WAVES 5   // flat shading: 96 VGPRs, 5 waves/SIMD (19 spilled): 11.2 -> 11.0 ms per frame; 4 / 6 waves: 11.2 / 12.6 ms
 #endif
 #ifndef CVR_DOS_WAVES
 #define CVR_DOS_WAVES 3
