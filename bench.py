@@ -708,6 +708,10 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "fps": round(1000.0 / ms_per_step, 1),
+            # fps and ms_per_step are throughput: frames overlap on the device (one
+            # static view, split.nstreams in flight); one frame's own latency is
+            # about roofline.kernel_ms (its launch, with the other frames in flight)
+            "frame_latency_ms_approx": None,
             "higher_is_better": True,
             "scaling": "strong",   # one fixed frame split over the GPUs
             "vs_baseline": None,
@@ -745,6 +749,7 @@ def main():
                                            if macro > 0 else "off"},
             "roofline": roof,
         }
+        res["frame_latency_ms_approx"] = round(kern_ms, 4)
         if world > 1:
             res["config"]["gather"] = (f"{a.transport}: packed {a.format} tiles to rank 0 "
                                        f"({split.G} frame(s) per ncclGather) + unpack of every "
