@@ -108,6 +108,9 @@ static void free_ptr(void*& p) {
 // Blocks the calling thread only when it allocates.
 hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds) {
   hipError_t e = hipSuccess;
+  // growing frees buffers a frame on another stream may still read: let it finish
+  if ((J.tiles < ntiles && J.tiles > 0) || (jobs > J.cap && J.cap > 0) || (rounds > J.rcap && J.rcap > 0))
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
   if (J.tiles < ntiles) {
     void* p = J.tile_off; free_ptr(p); J.tile_off = nullptr;
     p = J.tile_roff; free_ptr(p); J.tile_roff = nullptr;

@@ -349,6 +349,11 @@ flat_shade_kernel(typename SH::Args Q, typename SH::Data data, FlatJobs J, unsig
   }
 }
 
+template <class SH>
+hipError_t launch_shaded_march(const Ctx& c, const typename SH::Args& q, bool phong,
+                               typename SH::Data data, float4* out, uint32_t* samples,
+                               unsigned long long* shade_ctr, unsigned long long* tile_samples,
+                               hipStream_t s);
 hipError_t launch_flat_scan(FlatJobs& J, int ntiles, hipStream_t s);
 hipError_t launch_flat_fold(const Rc1passArgs& a, FlatJobs& J, float4* out, hipStream_t s);
 hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds);
@@ -382,7 +387,14 @@ hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool pho
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
   const unsigned long long total = J.h_total[0], rounds = J.h_total[1];
   if (total > 0) {
-    if ((e = flat_reserve(J, nt, (size_t)total, (size_t)rounds)) != hipSuccess) return e;
+    if (flat_reserve(J, nt, (size_t)total, (size_t)rounds) != hipSuccess) {
+      // more jobs than 32-bit offsets or the free memory hold: the per-wave kernel
+      // renders the same frame, bit for bit, without a job list
+      (void)hipGetLastError();
+      if (shade_ctr && (e = hipMemsetAsync(shade_ctr, 0, 3 * sizeof(unsigned long long), s)) != hipSuccess)
+        return e;
+      return launch_shaded_march<SH>(c, q, phong, data, out, samples, shade_ctr, tile_samples, s);
+    }
     if (phong)
       hipLaunchKernelGGL((shaded_jobs_kernel<SH, true, true>), dim3(nt), dim3(64), lds, s, q, cells,
                          grad, tf, J, nullptr, nullptr, nullptr);
