@@ -765,7 +765,7 @@ def main():
                                          "(double, reference recurrence, bit-exact): sat_ms = wall "
                                          "time of cvr_set_extinction_sat incl. freeing and "
                                          "allocating the SAT buffers, sat_gpu_ms = HIP-event time "
-                                         "of the build + cell8 expansion kernels"}
+                                         "of the build + cell4 expansion kernels"}
         if a.postpass and world == 1:
             res["postpass"] = postpass_bench(r, dev, W, H, a.steps)
         if world == 1 and not a.no_cpu_baseline:

@@ -1409,13 +1409,13 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
     return fail(c, CVR_ERR_ARG, "cvr_set_extinction_sat: need one extinction per voxel value (%d)", nv);
   const int w = c->N[0] + 2, h = c->N[1] + 2, d = c->N[2] + 2;
   const size_t cells = (size_t)w * h * d;
-  // the shader indexes texels with 32-bit / 24-bit products
+  // the shader indexes texels (plus one cell4 plane) with 32-bit / 24-bit products
   if (w > 4096 || h > 4096 || d > 4096 || cells >= ((size_t)1 << 31))
     return fail(c, CVR_ERR_ARG, "cvr_set_extinction_sat: volume too large for the SAT");
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   // Same grid as the last build (a TF change): rebuild into the existing buffers.
-  // Freeing and re-allocating the ~50 GB of a 1024^3 SAT costs seconds.
+  // Freeing and re-allocating the ~30 GB of a 1024^3 SAT costs seconds.
   const bool reuse = c->d_sat && c->d_sat_cells && c->d_sat_scratch &&
                      c->sat_dims[0] == w && c->sat_dims[1] == h && c->sat_dims[2] == d;
   if (!reuse) {
@@ -1441,7 +1441,8 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
   if (e == hipSuccess) e = hipEventRecord(ev[1], c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   (void)hipFree(d_lut);
-  if (e == hipSuccess && !reuse) e = hipMalloc((void**)&c->d_sat_cells, cells * 2 * sizeof(float4));
+  if (e == hipSuccess && !reuse)
+    e = hipMalloc((void**)&c->d_sat_cells, cvr::sat_cells_float4s(w, h, d) * sizeof(float4));
   if (e == hipSuccess) e = hipEventRecord(ev[2], c->stream);
   if (e == hipSuccess) e = cvr::launch_sat_cells(*c, c->d_sat, c->d_sat_cells, c->stream);
   if (e == hipSuccess) e = hipEventRecord(ev[3], c->stream);
@@ -1517,6 +1518,7 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
     Q.G[i] = (float)c->N[i] * c->scale[i];
     Q.inv_vs[i] = 1.0f / (Q.G[i] + Q.S[i] * 2.0f);        // inv_vol_scaled (:75)
     Q.sat_dims[i] = c->sat_dims[i];
+    Q.sat_pz = (uint32_t)c->sat_dims[0] * (uint32_t)c->sat_dims[1];
     Q.nsat[i] = (float)c->sat_dims[i];
     Q.nsat_m1[i] = (float)(c->sat_dims[i] - 1);
     Q.min_sat[i] = Q.S[i] * 0.5f;                        // MinSATPosition (:66)

@@ -136,6 +136,7 @@ struct EbsArgs {
   float inv_vs[3];                   // 1 / (G + 2 S)
   float nsat[3], nsat_m1[3];         // SAT dims as float, and dims - 1
   int sat_dims[3];
+  uint32_t sat_pz;                   // texels per SAT plane (the cell4 layout's z + 1 plane offset)
   float min_sat[3], max_sat[3];      // S / 2, G + 1.5 S
   int apply_occlusion, occ_shells;
   float occ_radius;
@@ -293,7 +294,7 @@ struct Ctx {
   int sat_chunk = 32;                // z planes per SAT work item (option "sat_chunk")
   int sat_build_us = 0;              // GPU time of the last SAT build (option "sat_build_us")
   float* d_sat = nullptr;
-  float4* d_sat_cells = nullptr;   // the same SAT as cell8 (8 float corners per texel)
+  float4* d_sat_cells = nullptr;   // the same SAT as cell4 texels (4 float corners of a plane, sat.hip)
   void* d_sat_scratch = nullptr;   // the double grid of the build (kept for rebuilds)
   int sat_dims[3] = {0, 0, 0};
   int ext_res[3] = {0, 0, 0};
@@ -359,6 +360,7 @@ hipError_t launch_ext_volume(const Ctx& c, const float4* d_tf_rgba, int tf_n, co
 hipError_t launch_sat_build(const Ctx& c, const float* d_lut, double* d_sd, float* d_sf,
                             hipStream_t s);
 hipError_t launch_sat_cells(const Ctx& c, const float* d_sf, float4* d_cells, hipStream_t s);
+size_t sat_cells_float4s(int w, int h, int d);   // the size of that layout, in float4
 hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s);
 hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,

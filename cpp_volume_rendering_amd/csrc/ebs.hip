@@ -21,7 +21,8 @@ namespace cvr {
 namespace {
 
 // GetSummed3Density (:77-83): trilinear of the float SAT at u = p * inv_vol_scaled,
-// from the cell8 copy (two float4 per texel: the 8 corners, x fastest).
+// from the cell4 copy (float4 of a plane's 4 corners per texel, x fastest; the
+// z + 1 corners are the texel one plane above).
 __device__ __forceinline__ float sat_fetch(const EbsArgs& Q, const float4* __restrict__ sat, float x,
                                            float y, float z) {
   const float tx = __builtin_amdgcn_fmed3f(fmaf(x * Q.inv_vs[0], Q.nsat[0], -0.5f), 0.0f, Q.nsat_m1[0]);
@@ -30,8 +31,7 @@ __device__ __forceinline__ float sat_fetch(const EbsArgs& Q, const float4* __res
   // < 2^31 texels (checked on the host): 32-bit index, 24-bit row products
   const uint32_t row = __umul24((uint32_t)tz, (uint32_t)Q.sat_dims[1]) + (uint32_t)ty;
   const uint32_t idx = __umul24(row, (uint32_t)Q.sat_dims[0]) + (uint32_t)tx;
-  const float4* cell = sat + 2 * (size_t)idx;
-  const float4 lo = cell[0], hi = cell[1];
+  const float4 lo = sat[idx], hi = sat[idx + Q.sat_pz];
   const float ax = __builtin_amdgcn_fractf(tx), ay = __builtin_amdgcn_fractf(ty),
               az = __builtin_amdgcn_fractf(tz);
   const float c00 = lerpf(lo.x, lo.y, ax), c10 = lerpf(lo.z, lo.w, ax);
@@ -123,9 +123,8 @@ __device__ __forceinline__ void shadow_half_issue(const EbsArgs& Q, const float4
     const int xi = (k & 1) ? 0 : 1, zi = (k & 2) ? 0 : 1;
     const uint32_t row = __umul24((uint32_t)C.tz[zi], (uint32_t)Q.sat_dims[1]) + ty;
     const uint32_t idx = __umul24(row, (uint32_t)Q.sat_dims[0]) + (uint32_t)C.tx[xi];
-    const float4* cell = sat + 2 * (size_t)idx;
-    c[2 * j] = cell[0];
-    c[2 * j + 1] = cell[1];
+    c[2 * j] = sat[idx];
+    c[2 * j + 1] = sat[idx + Q.sat_pz];
   }
 }
 
@@ -368,7 +367,7 @@ struct EbsShaderT {
   using Args = EbsArgs;
   static constexpr int kMinWavesPerEU = CVR_EBS_WAVES;   // register budget (1: compiler's choice)
   static constexpr int kFlatWavesPerEU = CVR_EBS_FLAT_WAVES;   // flat_shade_kernel
-  using Data = const float4*;   // the float SAT, cell8
+  using Data = const float4*;   // the float SAT, cell4
 
   // ShadeSample (:498-550); `lit` counts the shadow box chains traced.
   __device__ static f3 shade(const EbsArgs& Q, const float4* __restrict__ sat, f3 tx, f3 wp, f3,

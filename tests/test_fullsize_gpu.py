@@ -3,7 +3,7 @@
 The smaller parity suites exercise every code path at toy sizes; these run the
 configured sizes, whose indexing and allocation sizes (a 6.5 GiB gradient grid at
 512^3, 159-section shadow cones at 2048^2, a 1026^3 SAT of 4.3 GB with 289 wavefront
-launches and a 34.6 GiB cell8 copy) no toy case reaches:
+launches and a 17.3 GiB cell4 copy) no toy case reaches:
 
   * C2: a 256^3 u8 volume written as a reference `.raw` file
     (name.<bytes>.<W>x<H>x<D>.raw, reader.cpp:162-225), read back by cvr_read_raw,

@@ -10,12 +10,7 @@ run() {   # name, lib override ('' = in-tree), bench args
   local name=$1 lib=$2; shift 2
   if [ -n "$lib" ]; then export CVR_LIB_OVERRIDE=$lib; else unset CVR_LIB_OVERRIDE; fi
   timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > gpurun_out/${T}_$name.json 2> gpurun_out/${T}_$name.err || { tail -20 gpurun_out/${T}_$name.err; exit 1; }
-  python -c "import json; d=json.load(open('gpurun_out/${T}_$name.json')); print('$name', d['ms_per_step'], d['roofline']['kernel_ms'])"
+  python -c "import json; d=json.load(open('gpurun_out/${T}_$name.json')); p=d.get('precompute',{}); print('$name', d['ms_per_step'], d['roofline']['kernel_ms'], p.get('sat_gpu_ms'), d.get('parity'))"
 }
-CVR_LIB_OVERRIDE=ablib/dw5/libcvr.so timeout -k 10 400 python -u -m pytest tests/test_dos_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || { tail -30 gpurun_out/${T}_tests.log; exit 1; }
-tail -1 gpurun_out/${T}_tests.log
-for i in 1 2; do
-  run w4_$i "" --renderer dos
-  run w5_$i ablib/dw5/libcvr.so --renderer dos
-  run w6_$i ablib/dw6/libcvr.so --renderer dos
-done
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_ebs_gpu.py tests/test_fullsize_gpu.py -m gpu -k "ebs or c5" > gpurun_out/${T}_pytest.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest.log; [ $rc -eq 0 ] || exit 1
+run ebs "" --renderer ebs
