@@ -71,8 +71,20 @@ if __name__ == "__main__":
 # starts): the frames in flight need a queue each, one per render stream and the
 # RCCL stream (32 at 8 ranks: 16 streams; DESIGN §7, profiles/r03_s25_*).
 _WS = int(os.environ.get("WORLD_SIZE", "1"))
-HW_QUEUES = (int(sys.argv[sys.argv.index("--hw-queues") + 1]) if "--hw-queues" in sys.argv
-             else (32 if _WS >= 8 else (24 if _WS >= 4 else 8)))
+
+
+def _hw_queues_arg() -> int:
+    """--hw-queues N / --hw-queues=N, read before torch initialises HIP (argparse
+    proper runs later); 0 = the default by world size.  The box refuses more than 32."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--hw-queues", type=int, default=0)
+    known, _ = pre.parse_known_args()
+    if known.hw_queues and not 1 <= known.hw_queues <= 32:
+        sys.exit(f"bench.py: --hw-queues must be in 1..32 (got {known.hw_queues})")
+    return known.hw_queues
+
+
+HW_QUEUES = _hw_queues_arg() or (32 if _WS >= 8 else (24 if _WS >= 4 else 8))
 os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 import torch  # noqa: E402
@@ -121,6 +133,9 @@ def parse():
     p.add_argument("--skip-min-pct", type=int, default=-1,
                    help="empty-space skipping when >= this %% of macro cells are empty (101: off; "
                         "-1: the library default)")
+    p.add_argument("--cell-skip", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4],
+                   help="rc1pass per-cell skip: 0 off, 1 empty-sample flags, 2 + distance skip "
+                        "(-1: the library default, 2)")
     p.add_argument("--batch", type=int, default=0, choices=[0, 2, 4],
                    help="rc1pass samples per lane per memory round trip (0 = auto: 4, 2 with Phong)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -184,7 +199,8 @@ def dry_run(world, rank, a):
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": ranks,
                           "renderer": a.renderer, "volume": n, "viewport": [W, W],
-                          "tile": a.tile, "tiles_per_rank": tiles, "gather_exact": exact}))
+                          "tile": a.tile, "tiles_per_rank": tiles, "gather_exact": exact,
+                          "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])}))
 
 
 def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgba=None,
@@ -467,6 +483,9 @@ def main():
         if a.tile_order >= 0:
             N.check(N.lib().cvr_set_option(r.device.handle, b"tile_order", a.tile_order), "tile_order",
                     r.device.handle)
+        if a.cell_skip >= 0:
+            N.check(N.lib().cvr_set_option(r.device.handle, b"cell_skip", a.cell_skip), "cell_skip",
+                    r.device.handle)
         if a.skip_min_pct >= 0:
             N.check(N.lib().cvr_set_option(r.device.handle, b"skip_min_pct", a.skip_min_pct),
                     "skip_min_pct", r.device.handle)
@@ -508,7 +527,8 @@ def main():
 
     # samples per frame (this rank) and camera, counted by the kernel; for the shaded
     # renderers also the shaded / shadow-lit samples and the secondary fetches
-    count_shaded = shaded or (a.phong and not iso)
+    # (rc1pass: [0] Phong-shaded samples, [1] samples the per-cell skip stepped over)
+    count_shaded = not iso
     if count_shaded:
         N.check(L.cvr_set_option(r.device.handle, b"shade_counters", 1), "opt", r.device.handle)
     S_cam = []
@@ -681,6 +701,16 @@ def main():
             roof["traffic_frac"] = round(roof["traffic_GBs"] / HBM_PEAK_GBS, 4)
         if a.phong and count_shaded:
             roof["phong_shaded_samples"] = int(shade[0])
+        if a.renderer == "rc1pass":
+            # the per-cell skip (cell_skip 2-4) steps over samples in empty space without
+            # a load: they count in S (the reference's loop iterations) but fetch nothing;
+            # the same roofline on the bytes actually fetched, beside it
+            skipped = int(shade[1])
+            b_fetch = b_alg - 8 * skipped
+            roof.update({"skipped_samples": skipped, "fetched_samples": S_rank - skipped,
+                         "bytes_fetched_per_launch": b_fetch,
+                         "achieved_fetched": round(b_fetch / (kern_ms * 1e-3) / 1e9, 1),
+                         "frac_fetched": round(b_fetch / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
         if dos:
             roof.update({"shaded_samples": shade[0], "shadow_lit_samples": shade[1],
                          "cone_fetches_per_shaded": [f_occ, f_sdw],

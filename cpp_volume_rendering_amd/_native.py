@@ -29,7 +29,7 @@ GRADIENT_NONE, GRADIENT_FINITE_DIFFERENCES, GRADIENT_SOBEL_FELDMAN = 0, 1, 2
 EXPORTED_SYMBOLS = (
     "cvr_abi_version", "cvr_status_string", "cvr_create", "cvr_destroy", "cvr_last_error",
     "cvr_set_stream", "cvr_set_option", "cvr_get_option", "cvr_synchronize", "cvr_set_volume", "cvr_set_volume_device",
-    "cvr_set_transfer_function", "cvr_set_gradient", "cvr_device_bytes", "cvr_tiles_for_rank",
+    "cvr_set_transfer_function", "cvr_set_gradient", "cvr_device_bytes", "cvr_copy_cells", "cvr_tiles_for_rank",
     "cvr_render_rc1pass", "cvr_unpack_tiles_device", "cvr_copy_tile_stats", "cvr_read_kernel_times", "cvr_read_shade_counters", "cvr_selftest_arith", "cvr_camera_lookat", "cvr_default_step",
     "cvr_tf1d_build_rgbt", "cvr_read_tf1d", "cvr_read_raw", "cvr_read_syn", "cvr_read_pvm",
     "cvr_read_camera_state", "cvr_read_light_position", "cvr_read_light", "cvr_build_cone_tables",
@@ -171,6 +171,7 @@ def lib() -> ctypes.CDLL:
         "cvr_set_transfer_function": ([P, FP, I], I),
         "cvr_set_gradient": ([P, I], I),
         "cvr_device_bytes": ([P], ctypes.c_size_t),
+        "cvr_copy_cells": ([P, P, ctypes.c_size_t], I),
         "cvr_tiles_for_rank": ([ctypes.POINTER(Frame), I], I),
         "cvr_render_rc1pass": ([P, ctypes.POINTER(Frame), ctypes.POINTER(Rc1passParams),
                                 ctypes.POINTER(Output)], I),

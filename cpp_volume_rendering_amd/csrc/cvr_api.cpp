@@ -372,6 +372,14 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->occ_valid = 0;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "cell_skip")) {
+    if (value < 0 || value > 4)
+      return fail(c, CVR_ERR_ARG, "cell_skip must be 0 (off), 1 (empty-sample flags), 2 (+ distance "
+                                  "skip per lane), 3 (+ distance skip when every lane can) or 4 (+ "
+                                  "distance skip, equal for the lanes that can)");
+    c->cell_skip = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "skip_min_pct")) {
     if (value < 0 || value > 101) return fail(c, CVR_ERR_ARG, "skip_min_pct must be 0..101");
     c->skip_min_pct = value;
@@ -438,6 +446,8 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "sat_build_us")) return c->sat_build_us;   // read-only
   if (!std::strcmp(key, "order_interval")) return c->order_interval;
   if (!std::strcmp(key, "skip_min_pct")) return c->skip_min_pct;
+  if (!std::strcmp(key, "cell_skip")) return c->cell_skip;
+  if (!std::strcmp(key, "cell_flags_valid")) return c->cell_flags_valid;   // read-only
   if (!std::strcmp(key, "occ_empty_permille"))   // read-only: empty macro cells (after a render)
     return c->occ_valid ? (int)(c->occ_empty * 1000.0f + 0.5f) : -1;
   if (!std::strcmp(key, "tile_stats")) return c->tile_stats;
@@ -464,6 +474,18 @@ size_t cvr_device_bytes(const cvr_ctx* ctx) {
   const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
   if (!c) return 0;
   return c->vox_bytes + c->cells_bytes + c->grad_bytes + (size_t)c->tf_n * 16 + c->scratch_bytes;
+}
+
+cvr_status cvr_copy_cells(cvr_ctx* ctx, void* out, size_t capacity) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c || !out) return CVR_ERR_ARG;
+  if (!c->d_cells) return fail(c, CVR_ERR_STATE, "cvr_copy_cells: no volume set");
+  if (capacity < c->cells_bytes)
+    return fail(c, CVR_ERR_ARG, "cvr_copy_cells: need %zu bytes", c->cells_bytes);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipDeviceSynchronize());
+  HIP_TRY(c, hipMemcpy(out, c->d_cells, c->cells_bytes, hipMemcpyDeviceToHost));
+  return CVR_OK;
 }
 
 static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, int bpv, int w,
@@ -499,6 +521,8 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
   { void* p = c->d_occ; free_dev(p); c->d_occ = nullptr; }
   c->mm_shift = -1;
   c->occ_valid = 0;
+  c->cell_flags_valid = 0;   // the cells are rebuilt without flags
+  c->cell_flags_set = 0;
   { void* p = c->d_ext; free_dev(p); c->d_ext = nullptr; c->ext_levels = 0; }
   { void* p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr; }
   { void* p = c->d_sat; free_dev(p); c->d_sat = nullptr; }
@@ -570,6 +594,7 @@ cvr_status cvr_set_transfer_function(cvr_ctx* ctx, const float* rgbt, int n) {
   HIP_TRY(c, hipMemcpy(c->d_tf_prefix, prefix.data(), prefix.size() * sizeof(int),
                        hipMemcpyHostToDevice));
   c->occ_valid = 0;
+  c->cell_flags_valid = 0;
   return CVR_OK;
 }
 
@@ -662,6 +687,29 @@ static cvr_status ensure_occupancy(Ctx* c) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->occ_empty = (float)n_empty / (float)nm;
   c->occ_valid = 1;
+  return CVR_OK;
+}
+
+// Skip flags of the density cells for the current volume and TF (rebuilt lazily
+// after either changes; on the context stream).  Frames in flight on other
+// streams may still read the cells' old flags, so the device drains first (a
+// TF change is rare); the two scratch bytes per cell are freed after the build.
+static cvr_status ensure_cell_flags(Ctx* c) {
+  if (c->cell_flags_valid) return CVR_OK;
+  if (!c->d_cells || !c->d_tf_prefix) return fail(c, CVR_ERR_STATE, "cell flags: no volume or TF");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipDeviceSynchronize());
+  const size_t n = cvr::cell_count(c->cells);
+  uint8_t* t = nullptr;
+  HIP_TRY(c, hipMalloc((void**)&t, 2 * n));
+  hipError_t e = cvr::launch_cell_flags(*c, false, t, t + n, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(t);
+  if (e != hipSuccess)
+    return fail(c, e == hipErrorOutOfMemory ? CVR_ERR_OOM : CVR_ERR_HIP, "cell flags: %s",
+                hipGetErrorString(e));
+  c->cell_flags_valid = 1;
+  c->cell_flags_set = 1;
   return CVR_OK;
 }
 
@@ -767,7 +815,14 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   A.tile_stats = nullptr;
   A.cost_time = c->cost_time;
   A.occ = nullptr;
-  if (c->macro_shift > 0) {
+  A.cell_skip = 0;
+  if (c->cell_skip > 0) {   // (the quad march ignores it)
+    cvr_status st = ensure_cell_flags(c);
+    if (st != CVR_OK) return st;
+    A.cell_skip = c->cell_skip;
+    A.inv_step = 1.0f / A.step;
+  }
+  if (c->macro_shift > 0 && A.cell_skip == 0) {
     cvr_status st = ensure_occupancy(c);
     if (st != CVR_OK) return st;
     // the skip path costs the march registers and a probe: worth it only
@@ -787,12 +842,12 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     A.tile_stats = c->d_tile_stats;
   }
   A.shade_ctr = nullptr;
-  const bool use_counters = (c->shade_counters && phong) || o->total;
+  const bool use_counters = c->shade_counters || o->total;
   if (use_counters) {
     cvr_status st = counters_acquire(c, c->stream);
     if (st != CVR_OK) return st;
   }
-  if (c->shade_counters && phong) {   // measurement: shaded samples (gradient fetches)
+  if (c->shade_counters) {   // measurement: shaded samples (gradient fetches), skipped samples
     if (!c->d_shade) HIP_TRY(c, hipMalloc((void**)&c->d_shade, 3 * sizeof(unsigned long long)));
     HIP_TRY(c, hipMemsetAsync(c->d_shade, 0, 3 * sizeof(unsigned long long), c->stream));
     A.shade_ctr = c->d_shade;

@@ -69,7 +69,8 @@ struct Rc1passArgs {
   int out_half;                      // 1: store RGBA16F (uint2 per pixel), 0: float4
   int ntiles;                        // 8x8 wave tiles of this launch
   unsigned long long* tile_stats;    // diagnostics (tile_stats option) or null
-  unsigned long long* shade_ctr;     // measurement (shade_counters): [0] += shaded samples (Phong)
+  unsigned long long* shade_ctr;     // measurement (shade_counters): [0] += shaded samples (Phong),
+                                     // [1] += samples the cell skip stepped over without a load
   int cost_time;                     // LPT cost = measured tile time (1) or longest ray (0)
   // empty-space skipping: occupancy byte per macro cell (null = off)
   const uint8_t* occ;
@@ -79,6 +80,10 @@ struct Rc1passArgs {
   // (CVR-SPEC), 8 = every GL_LINEAR weight (volume, gradient, TF) rounded to 8
   // fraction bits, as GPU texture units filter (CVR-SPEC-8)
   int filter_bits;
+  // per-cell skip (march_common.h cell_empty): 0 off, 1 empty-sample flags,
+  // 2 flags + distance skip; inv_step = 1 / step (the full-step bound)
+  int cell_skip;
+  float inv_step;
 };
 
 constexpr int kMaxTfLds = 4096;          // TF entries a kernel stages into LDS
@@ -222,6 +227,13 @@ struct Ctx {
   float occ_empty = 0.0f;         // fraction of empty macro cells
   int skip_min_pct = 15;          // skipping is compiled in when >= this % of cells are empty
   int* d_tf_prefix = nullptr;     // count of padded TF entries with alpha > 0 before k
+  // per-cell skip flags in the cells' sign bits (march_common.h cell_empty /
+  // cell_skip_q; option "cell_skip": 0 off, 1 empty-sample flags, 2 flags + the
+  // distance skip per lane, 3 (default) when every marching lane can, 4 by the
+  // lanes that can; raymarch.hip march_ray); rebuilt lazily after the volume or TF changes
+  int cell_skip = 3;
+  int cell_flags_valid = 0;       // the cells' flags match the current TF
+  int cell_flags_set = 0;         // the cells carry flags (of some TF)
   // transfer function (RGBA16F values as float)
   float* d_tf = nullptr;
   int tf_n = 0;
@@ -353,6 +365,9 @@ hipError_t launch_macro_minmax(const Ctx& c, int shift, const int mdim[3], uint3
 hipError_t launch_occupancy(const uint32_t* minmax, int n_macro, const uint16_t* lut,
                             const int* prefix, int tf_n, uint8_t* occ, unsigned int* n_empty,
                             hipStream_t s);
+// skip flags of the density cells for the current TF (clear: strip them); t0, t1
+// are two scratch bytes per cell
+hipError_t launch_cell_flags(const Ctx& c, bool clear, uint8_t* t0, uint8_t* t1, hipStream_t s);
 hipError_t launch_ext_volume(const Ctx& c, const float4* d_tf_rgba, int tf_n, const int res[3],
                              float sigma0, int nlevels, const long long* off, uint16_t* d_ext,
                              uint4* d_ext_cells,

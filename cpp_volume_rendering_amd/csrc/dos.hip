@@ -256,7 +256,7 @@ __device__ __forceinline__ bool outside_box(const DosArgs& Q, f3 p) {
 
 __device__ __forceinline__ float ext_value(const DosArgs& Q, uint4 raw, const ExtTap& t,
                                            bool outside, float xb) {
-  float rg = trilerp_cell(raw, t.ax, t.ay, t.az);
+  float rg = trilerp_cell<false, false>(raw, t.ax, t.ay, t.az);   // extinction cells: no flags
 #ifdef CVR_DOS_EXPERIMENT_NO_BORDER   // cost probes only (tools/build_variant.sh): wrong images
   return rg;
 #endif

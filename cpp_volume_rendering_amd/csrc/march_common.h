@@ -127,33 +127,58 @@ __device__ __forceinline__ SamplePos sample_pos_clamped(float x, float y, float 
 
 // (float)hi - (float)lo of a packed fp16 pair, in ONE mixed-precision FMA
 // (hi * 1.0 + (-lo), computed exactly then rounded once = the fp32 subtraction
-// of the two exactly-converted halves).
+// of the two exactly-converted halves).  ABS: |hi| - |lo| (the operand modifier
+// is free): a density cell's sign bits carry the skip flags (cell_empty below).
+template <bool ABS = false>
 __device__ __forceinline__ float pair_diff(uint32_t w) {
   float d;
-  asm("v_fma_mix_f32 %0, %1, 1.0, -%1 op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(w));
+  if (ABS)
+    asm("v_fma_mix_f32 %0, |%1|, 1.0, -|%1| op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(w));
+  else
+    asm("v_fma_mix_f32 %0, %1, 1.0, -%1 op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(w));
   return d;
 }
 
 // lerp(lo, hi, t) of a packed fp16 pair = fmaf(t, hi - lo, lo): two
 // v_fma_mix_f32, the second taking lo straight from the low half.
+template <bool ABS = false>
 __device__ __forceinline__ float pair_lerp(uint32_t w, float t) {
   float r;
-  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(t), "v"(pair_diff(w)), "v"(w));
+  if (ABS)
+    asm("v_fma_mix_f32 %0, %1, %2, |%3| op_sel_hi:[0,0,1]" : "=v"(r) : "v"(t), "v"(pair_diff<true>(w)), "v"(w));
+  else
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(t), "v"(pair_diff<false>(w)), "v"(w));
   return r;
 }
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+// Skip flags of the density cells (precompute.hip: build_cell_flags, rebuilt
+// for every TF).  Densities are >= 0, so the 8 fp16 sign bits of a cell are
+// free; every density read takes |corner| (ABS above, no extra instruction):
+//  * bit 31 of .x: the cell is EMPTY — every density its corners can
+//    interpolate to (a lerp stays within its end points) classifies to tau = 0,
+//    so a sample there composites nothing (ray_marching_1p.comp:142);
+//  * bits 31 of .y, .z, .w (an empty cell): q = min(d, 8) - 1, d = the
+//    chessboard distance in cells to the nearest cell that is not empty, so
+//    every cell within q of this one is empty too.
+__device__ __forceinline__ bool cell_empty(uint4 r) { return (int)r.x < 0; }
+__device__ __forceinline__ int cell_skip_q(uint4 r) {
+  return (int)((r.y >> 31) | ((r.z >> 31) << 1) | ((r.w >> 31) << 2));
+}
+constexpr int kCellSkipCap = 8;            // distances stored up to 8 (q <= 7)
+
 // PK: the two y lerps as one packed subtract and one packed fma, per lane the
 // same two roundings as lerpf (the emission-absorption march: kernel -5 % with
 // the buffer-offset and TF-weight changes of round 3; the Blinn-Phong march
-// keeps the scalar form, where the register pairs cost it 10 %)
-template <bool PK = false>
+// keeps the scalar form, where the register pairs cost it 10 %).  ABS (default):
+// a density cell, whose sign bits are flags; the gradient cells are signed.
+template <bool PK = false, bool ABS = true>
 __device__ __forceinline__ float trilerp_cell(uint4 raw, float ax, float ay, float az) {
-  float c00 = pair_lerp(raw.x, ax);    // (v000, v100)
-  float c10 = pair_lerp(raw.y, ax);    // (v010, v110)
-  float c01 = pair_lerp(raw.z, ax);    // (v001, v101)
-  float c11 = pair_lerp(raw.w, ax);    // (v011, v111)
+  float c00 = pair_lerp<ABS>(raw.x, ax);    // (v000, v100)
+  float c10 = pair_lerp<ABS>(raw.y, ax);    // (v010, v110)
+  float c01 = pair_lerp<ABS>(raw.z, ax);    // (v001, v101)
+  float c11 = pair_lerp<ABS>(raw.w, ax);    // (v011, v111)
   if (PK) {
     const f2v lo = {c00, c01}, hi = {c10, c11};
     const f2v c = __builtin_elementwise_fma(f2v{ay, ay}, hi - lo, lo);
@@ -203,8 +228,9 @@ __device__ __forceinline__ f3 sample_gradient_cell(const uint4* __restrict__ gce
                                                    const SamplePos& sp) {
   const uint4* g = gcells + 3 * (size_t)sp.idx;
   const uint4 gx = g[0], gy = g[1], gz = g[2];
-  return f3{trilerp_cell(gx, sp.ax, sp.ay, sp.az), trilerp_cell(gy, sp.ax, sp.ay, sp.az),
-            trilerp_cell(gz, sp.ax, sp.ay, sp.az)};
+  return f3{trilerp_cell<false, false>(gx, sp.ax, sp.ay, sp.az),
+            trilerp_cell<false, false>(gy, sp.ax, sp.ay, sp.az),
+            trilerp_cell<false, false>(gz, sp.ax, sp.ay, sp.az)};
 }
 
 // Blinn-Phong (ray_marching_1p.comp:48-81), CVR-SPEC arithmetic, for gradient g

@@ -5,9 +5,11 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 #include <cstdint>
+#include <utility>
 
 #include "cvr_device.h"
 #include "cvr_internal.h"
+#include "march_common.h"
 
 namespace cvr {
 
@@ -270,6 +272,106 @@ hipError_t launch_occupancy(const uint32_t* minmax, int n_macro, const uint16_t*
   const int bs = 256;
   hipLaunchKernelGGL(occupancy_kernel, dim3((n_macro + bs - 1) / bs), dim3(bs), 0, s, minmax,
                      n_macro, lut, prefix, tf_n, occ, n_empty);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Skip flags of the density cells (march_common.h: cell_empty, cell_skip_q),
+// rebuilt whenever the volume or the TF changes.
+// ---------------------------------------------------------------------------
+
+// Pass 0: is the cell EMPTY?  Its densities lie in [min, max] of its 8 corners
+// (every lerp fmaf(t, b - a, a) with t in [0, 1] stays between a and b), and the
+// TF entries a density reads grow with it (as occupancy_kernel; the range is
+// widened by 2^-10, which also covers 8-bit filter weights).  Non-negative fp16
+// bit patterns order like their values, so min/max run on the integer halves.
+// Writes 0 (not empty) or kCellSkipCap (empty) per cell.
+__global__ void cell_empty_kernel(const uint4* __restrict__ cells, size_t n,
+                                  const int* __restrict__ prefix, int tf_n, uint8_t* __restrict__ d0) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4 r = cells[i];
+  const uint32_t w[4] = {r.x & 0x7fff7fffu, r.y & 0x7fff7fffu, r.z & 0x7fff7fffu, r.w & 0x7fff7fffu};
+  uint32_t lo = 0xffffu, hi = 0u;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    lo = min(lo, min(w[k] & 0xffffu, w[k] >> 16));
+    hi = max(hi, max(w[k] & 0xffffu, w[k] >> 16));
+  }
+  float flo, fhi, dummy;
+  h2f2(lo, flo, dummy);
+  h2f2(hi, fhi, dummy);
+  const float fn = (float)tf_n;
+  int kl = (int)floorf(fmaf(flo - 1.0f / 1024.0f, fn, -0.5f)) + 1;
+  int kh = (int)floorf(fmaf(fhi + 1.0f / 1024.0f, fn, -0.5f)) + 2;
+  kl = max(kl, 0);
+  kh = min(kh, tf_n + 1);
+  const bool occupied = kl <= kh && prefix[kh + 1] - prefix[kl] > 0;
+  d0[i] = occupied ? 0 : (uint8_t)kCellSkipCap;
+}
+
+// One axis of the chessboard distance transform, capped at kCellSkipCap:
+// out(p) = min over |k| < cap (p + k e inside the grid) of max(|k|, in(p + k e)).
+// Applied along x to the 0 / cap map of pass 0, then y, then z, it gives
+// min over non-empty q of max(|dx|, |dy|, |dz|) (max distributes over min).
+// Cells outside the grid count as empty: no sample position leaves the grid.
+__global__ void cell_dist_axis_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                      size_t n, int cx, int cy, int cz, int axis) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t a = (uint32_t)(i % (uint32_t)cx);
+  const uint32_t rest = (uint32_t)(i / (uint32_t)cx);
+  const uint32_t b = rest % (uint32_t)cy, c = rest / (uint32_t)cy;
+  const int pos = axis == 0 ? (int)a : axis == 1 ? (int)b : (int)c;
+  const int dim = axis == 0 ? cx : axis == 1 ? cy : cz;
+  const long long stride = axis == 0 ? 1 : axis == 1 ? (long long)cx : (long long)cx * cy;
+  int d = in[i];
+  for (int k = 1; k < kCellSkipCap && k < d; k++) {
+    if (pos - k >= 0) d = min(d, max(k, (int)in[(long long)i - k * stride]));
+    if (pos + k < dim) d = min(d, max(k, (int)in[(long long)i + k * stride]));
+  }
+  out[i] = (uint8_t)d;
+}
+
+// Final pass: the distance into the cells' sign bits (flag + 3-bit q).
+__global__ void cell_flags_write_kernel(uint4* __restrict__ cells, const uint8_t* __restrict__ dist,
+                                        size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int d = dist[i];
+  const uint32_t e = d >= 1 ? 1u : 0u;
+  const uint32_t q = d >= 1 ? (uint32_t)(min(d, kCellSkipCap) - 1) : 0u;
+  uint4 r = cells[i];
+  r.x = (r.x & 0x7fff7fffu) | (e << 31);
+  r.y = (r.y & 0x7fff7fffu) | ((q & 1u) << 31);
+  r.z = (r.z & 0x7fff7fffu) | (((q >> 1) & 1u) << 31);
+  r.w = (r.w & 0x7fff7fffu) | (((q >> 2) & 1u) << 31);
+  cells[i] = r;
+}
+
+__global__ void fill_u8_kernel(uint8_t* __restrict__ p, size_t n, uint8_t v) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// clear = true: strip every flag (the cells hold plain |densities| again)
+hipError_t launch_cell_flags(const Ctx& c, bool clear, uint8_t* t0, uint8_t* t1, hipStream_t s) {
+  const size_t n = cell_count(c.cells);
+  const int bs = 256;
+  const dim3 grid((unsigned)((n + bs - 1) / bs));
+  uint4* cells = (uint4*)c.d_cells;
+  if (clear) {
+    hipLaunchKernelGGL(fill_u8_kernel, grid, dim3(bs), 0, s, t0, n, (uint8_t)0);
+  } else {
+    hipLaunchKernelGGL(cell_empty_kernel, grid, dim3(bs), 0, s, (const uint4*)cells, n,
+                       c.d_tf_prefix, c.tf_n, t0);
+    for (int axis = 0; axis < 3; axis++) {
+      hipLaunchKernelGGL(cell_dist_axis_kernel, grid, dim3(bs), 0, s, (const uint8_t*)t0, t1, n,
+                         c.cells.cx, c.cells.cy, c.cells.cz, axis);
+      std::swap(t0, t1);
+    }
+  }
+  hipLaunchKernelGGL(cell_flags_write_kernel, grid, dim3(bs), 0, s, cells, (const uint8_t*)t0, n);
   return hipGetLastError();
 }
 

@@ -74,11 +74,27 @@ __device__ __forceinline__ bool skip_empty(const Rc1passArgs& A, const Ray& r, f
 // Ray-parallel march (one lane per ray) of ray_marching_1p.comp:124-172.  The
 // arithmetic per sample is exactly the reference's sequential loop (s
 // accumulates h one step at a time); batching only changes when loads issue.
-template <int K, bool PHONG, bool SKIP, bool XF, int BUF, int FB>
+// Per-cell skip (CS, option "cell_skip", march_common.h cell_empty):
+//  * CS >= 1: when sample j of every marching lane lies in an EMPTY cell (a
+//    wave-uniform ballot of one sign bit per load), its trilinear density, TF
+//    lookup and composite test are skipped: its tau is exactly 0, so the
+//    reference composites nothing (:142) and only counts it;
+//  * CS == 2: after a batch whose last sample lies in an empty cell at chessboard
+//    distance d >= 2 from any non-empty cell, the next m samples are counted and
+//    stepped over with the same s += h recurrence, without loads: m full steps
+//    move the position by at most m * step * max|dt| <= d - 1 - kSkipMargin
+//    texels on every axis, so each of those samples lies in a cell within d - 1
+//    of the last one (all empty), and m stays 2 steps short of the ray's end, so
+//    every skipped h is the full step.
+// Both leave the image and the sample count bit for bit as the plain march.
+constexpr float kSkipMargin = 1.0f / 32.0f;   // texels: absorbs the rounding of s and positions
+
+template <int K, bool PHONG, bool SKIP, bool XF, int BUF, int FB, int CS>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
                                           const uint4* __restrict__ grad,
                                           const float4* __restrict__ tfp, int px, int py,
-                                          float4& dst, uint32_t& cnt, uint32_t& nshade) {
+                                          float4& dst, uint32_t& cnt, uint32_t& nshade,
+                                          uint32_t& nbatch, uint32_t& nskip) {
   dst = make_float4(0.f, 0.f, 0.f, 0.f);
   cnt = 0;
   Ray r;
@@ -106,6 +122,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
     return cells[p.idx];
   };
   while (!done) {
+    if (CS > 0) nbatch++;   // the LPT cost with skipping: loop rounds, not samples
     // Empty-space skipping (bit-exact): if the macro cell holding the next
     // sample is transparent for the current TF (every density its texels can
     // interpolate to classifies to alpha <= 0), the samples whose positions stay
@@ -189,18 +206,34 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
     // 16-B reads) only for visible samples, ~1 in 5 on the headline frame
     int tfi[K];
     float tfa[K];
+    // we[j], wave-uniform: sample j of every marching lane lies in an empty cell.
+    // Each is tested right before its sample's math, so the loads of the later
+    // samples stay in flight behind it (testing all four first waited for all).
+    bool we[K];
+    int qlast = 0;   // the last sample's skip distance (0: no skip), read before raw[] dies
     if (!PHONG) {
 #pragma unroll
       for (int j = 0; j < K; j++) {
-        const float xd = fmaf(trilerp_cell<true>(raw[j], sp[j].ax, sp[j].ay, sp[j].az), fn, -0.5f);
-        tfa[j] = filter_weight<FB>(__builtin_amdgcn_fractf(xd));   // see classify
-        tfi[j] = cvt_flr(xd) + 1;
-        src[j].w = lerpf(tfp[tfi[j]].w, tfp[tfi[j] + 1].w, tfa[j]);
+        we[j] = CS > 0 && __ballot(!cell_empty(raw[j])) == 0;
+        if (CS >= 2 && j == K - 1) qlast = cell_empty(raw[j]) ? cell_skip_q(raw[j]) : 0;
+        if (CS > 0 && we[j]) {
+          tfa[j] = 0.0f; tfi[j] = 0; src[j].w = 0.0f;
+        } else {
+          const float xd = fmaf(trilerp_cell<true>(raw[j], sp[j].ax, sp[j].ay, sp[j].az), fn, -0.5f);
+          tfa[j] = filter_weight<FB>(__builtin_amdgcn_fractf(xd));   // see classify
+          tfi[j] = cvt_flr(xd) + 1;
+          src[j].w = lerpf(tfp[tfi[j]].w, tfp[tfi[j] + 1].w, tfa[j]);
+        }
       }
-    } else
+    } else {
 #pragma unroll
-    for (int j = 0; j < K; j++)
-      src[j] = classify<FB>(tfp, fn, trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az));
+      for (int j = 0; j < K; j++) {
+        we[j] = CS > 0 && __ballot(!cell_empty(raw[j])) == 0;
+        if (CS >= 2 && j == K - 1) qlast = cell_empty(raw[j]) ? cell_skip_q(raw[j]) : 0;
+        if (CS > 0 && we[j]) src[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        else src[j] = classify<FB>(tfp, fn, trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az));
+      }
+    }
     bool visible = false;
     // stage 3: front-to-back composite + ERT, in sample order.  The branches
     // matter: a wave whose samples are all transparent (empty space) skips
@@ -214,7 +247,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
         } else {
           cnt++;
           float4 sc = src[j];
-          if (sc.w > 0.0f) {
+          if (!(CS > 0 && we[j]) && sc.w > 0.0f) {
             visible = true;
             if (!PHONG) {   // classify's rgb, same lerps
               const float4 t0 = tfp[tfi[j]], t1 = tfp[tfi[j] + 1];
@@ -241,6 +274,41 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
     s = ss;
     if (!(s < D)) done = true;
     probe = !visible;
+    if (CS >= 2 && wave_in_box) {
+      const bool ok = !done && qlast > 0 && vj[K - 1];
+      // CS 3: only when every marching lane can skip (one ballot, so a wave with
+      // any lane in occupied space pays nothing more)
+      if ((CS != 3 || __ballot(!ok) == 0) && ok) {
+        // samples per texel of the largest per-axis move: 1 / (step * max|dt|),
+        // recomputed here (the opaque copies keep the compiler from hoisting it
+        // out of the loop, where it took a register and spilled)
+        float dx = r.dt.x, dy = r.dt.y, dz = r.dt.z;
+        asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
+        const float kinv = __builtin_amdgcn_rcpf(step * fmaxf(fmaxf(fabsf(dx), fabsf(dy)), fabsf(dz)));
+        int m = min(cvt_flr(((float)qlast - kSkipMargin) * kinv), cvt_flr((D - s) * A.inv_step) - 2);
+        if (CS == 2) {   // each lane its own m
+          if (m > 0) {
+            cnt += (uint32_t)m;
+            nskip += (uint32_t)m;
+            for (; m >= 4; m -= 4) {
+              s = s + step;
+              s = s + step;
+              s = s + step;
+              s = s + step;
+            }
+            for (; m > 0; m--) s = s + step;
+          }
+        } else {
+          // 3 (every marching lane) / 4 (the lanes that can): they skip the same
+          // number of samples, the fewest any of them may, so they stay at one
+          // sample index and a wave load keeps touching neighbouring cells
+          int i = 0;
+          for (; __all(i < m); i++) s = s + step;
+          cnt += (uint32_t)i;
+          nskip += (uint32_t)i;
+        }
+      }
+    }
   }
 }
 
@@ -386,7 +454,7 @@ constexpr int rc1_waves_per_eu() {
   return (K == 4 && !PHONG && !SKIP && !QUAD) ? 8 : 1;
 #endif
 }
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB>
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB, int CS>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rc1_waves_per_eu<K, PHONG, SKIP, QUAD>())))
 rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
@@ -414,15 +482,27 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   int px, py;
   long long oidx;
   float4 dst;
-  uint32_t cnt, nshade = 0;
+  // nskip: samples stepped over without a load (measurement); the EA march has
+  // no shaded-sample count, so it shares that register
+  uint32_t cnt, nshade = 0, nbatch = 0, nskip_own = 0;
+  uint32_t& nskip = PHONG ? nskip_own : nshade;
   bool writer;
   if (!QUAD || quarter < 0) {   // whole tile, one lane per ray
     tile_pixel(A, t, lane & 7, lane >> 3, px, py, oidx);
     const bool inside = px < A.W && py < A.H;
     dst = make_float4(0.f, 0.f, 0.f, 0.f);
     cnt = 0;
-    if (inside) march_ray<K, PHONG, SKIP, XF, BUF, FB>(A, cells, grad, tfp, px, py, dst, cnt, nshade);
+    if (inside) march_ray<K, PHONG, SKIP, XF, BUF, FB, CS>(A, cells, grad, tfp, px, py, dst, cnt, nshade,
+                                                          nbatch, nskip);
     writer = inside || A.packed;
+    if (CS > 0) {
+      // the output index again, from the lane id (v_mbcnt) and the wave's tile
+      // (scalar) rather than held across the march, where it spilled (16 B per
+      // lane of scratch traffic)
+      const int ln = (int)__lane_id();
+      int px2, py2;
+      tile_pixel(A, t, ln & 7, ln >> 3, px2, py2, oidx);
+    }
   } else {                    // quarter of a tile, four lanes per ray
     const int ray = lane >> 2;
     tile_pixel(A, t, ((quarter & 1) << 2) | (ray & 3), ((quarter >> 1) << 2) | (ray >> 2), px, py,
@@ -436,9 +516,15 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     store_rgba(out, oidx, dst, A.out_half);
     if (samples) samples[oidx] = cnt;
   }
-  if (PHONG && A.shade_ctr) {   // measurement only: shaded samples (the gradient's bytes)
-    const unsigned long long v = wave_sum(nshade);
-    if (lane == 0 && v) atomicAdd(&A.shade_ctr[0], v);
+  if (A.shade_ctr) {   // measurement only: shaded samples (the gradient's bytes), skipped samples
+    if (PHONG) {
+      const unsigned long long v = wave_sum(nshade);
+      if (lane == 0 && v) atomicAdd(&A.shade_ctr[0], v);
+    }
+    if (CS >= 2) {
+      const unsigned long long v = wave_sum(nskip);
+      if (lane == 0 && v) atomicAdd(&A.shade_ctr[1], v);
+    }
   }
   if (tile_samples) {   // per-tile sample count; summed by tile_order_kernel (no hot atomic)
     unsigned long long v = wave_sum(cnt);
@@ -452,8 +538,12 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   }
   uint32_t m = 0;
   if (tile_cost || A.tile_stats) m = wave_max(cnt);
+  // with the per-cell skip the samples no longer measure a tile's time (a skipped
+  // sample costs one add): its march rounds do (x 4, the scale of the samples)
+  uint32_t mb = 0;
+  if (CS > 0 && tile_cost) mb = 4u * wave_max(nbatch);
   if (tile_cost && lane == 0) {   // next frame's order: the tile's measured time or its longest ray
-    uint32_t c = m;
+    uint32_t c = CS > 0 ? mb : m;
     if (A.cost_time) {
       const unsigned long long d = __builtin_amdgcn_s_memrealtime() - t_start;   // 100 MHz ticks
       c = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
@@ -682,7 +772,7 @@ __global__ void clear_u32_kernel(uint32_t* __restrict__ p, int n) {
 // Kernel variant: K (batch), PHONG, SKIP (empty-space skipping compiled in),
 // QUAD (quad path compiled in), XF (range-free exp).  Paths a frame does not
 // use are compiled out: they would cost the hot loop registers (occupancy).
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB = 0>
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB = 0, int CS = 0>
 static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                                  unsigned long long* tile_samples, const int* order,
                                  uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
@@ -691,7 +781,7 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
   // cell (1,1,1) <-> texel (0,0,0)
   const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
   int grid = order ? plan.order_slots : plan.ntiles;
-  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF, FB>), dim3(grid), dim3(64), lds, s,
+  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF, FB, CS>), dim3(grid), dim3(64), lds, s,
                      a, cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, out, samples,
                      tile_samples, order, tile_cost, order ? plan.boost : 0);
   return hipGetLastError();
@@ -716,6 +806,22 @@ static hipError_t launch_kps(const Ctx& c, const Rc1passArgs& a, float4* out, ui
                       : launch_variant<K, PHONG, SKIP, false, false, 0, 8>(c, a, out, samples, ts, order, tile_cost, plan, s);
   }
   const bool quad = order && plan.quad_pct > 0;
+  if (!SKIP && !quad && a.cell_skip > 0) {   // per-cell skip flags (a.occ is null then)
+#define CVR_CS_LAUNCH(CSV)                                                                                 \
+    if (buf == 2)                                                                                          \
+      return a.exp_fast ? launch_variant<K, PHONG, false, false, true, 2, 0, CSV>(c, a, out, samples, ts, order, tile_cost, plan, s) \
+                        : launch_variant<K, PHONG, false, false, false, 2, 0, CSV>(c, a, out, samples, ts, order, tile_cost, plan, s); \
+    if (buf == 1)                                                                                          \
+      return a.exp_fast ? launch_variant<K, PHONG, false, false, true, 1, 0, CSV>(c, a, out, samples, ts, order, tile_cost, plan, s) \
+                        : launch_variant<K, PHONG, false, false, false, 1, 0, CSV>(c, a, out, samples, ts, order, tile_cost, plan, s); \
+    return a.exp_fast ? launch_variant<K, PHONG, false, false, true, 0, 0, CSV>(c, a, out, samples, ts, order, tile_cost, plan, s) \
+                      : launch_variant<K, PHONG, false, false, false, 0, 0, CSV>(c, a, out, samples, ts, order, tile_cost, plan, s);
+    if (a.cell_skip == 1) { CVR_CS_LAUNCH(1) }
+    if (a.cell_skip == 3) { CVR_CS_LAUNCH(3) }
+    if (a.cell_skip == 4) { CVR_CS_LAUNCH(4) }
+    CVR_CS_LAUNCH(2)
+#undef CVR_CS_LAUNCH
+  }
   if (quad)
     return a.exp_fast ? launch_variant<K, PHONG, SKIP, true, true, 0>(c, a, out, samples, ts, order, tile_cost, plan, s)
                       : launch_variant<K, PHONG, SKIP, true, false, 0>(c, a, out, samples, ts, order, tile_cost, plan, s);

@@ -322,6 +322,13 @@ cvr_status  cvr_set_gradient(cvr_ctx* ctx, int mode);
 /* Device bytes held by the context (volume layouts, TF, gradient, ...). */
 size_t      cvr_device_bytes(const cvr_ctx* ctx);
 
+/* Copy the volume's cell grid back (diagnostics and tests): (W+1)(H+1)(D+1)
+ * cells, x-fastest, 16 B each = the 8 R16F corners GL_LINEAR reads for a
+ * sample in the cell.  The corners' sign bits carry the per-cell skip flags of
+ * the current TF (option "cell_skip").  No reference counterpart:
+ * the reference keeps the volume in a GL_R16F texture (utils.cpp:20-56). */
+cvr_status  cvr_copy_cells(cvr_ctx* ctx, void* out, size_t capacity);
+
 /* ----------------------------------------------------------------------------
  * Rendering
  * -------------------------------------------------------------------------- */

@@ -56,3 +56,19 @@ def test_gpus_disagreeing_with_world_size_fails():
                                                 "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert "WORLD_SIZE" in p.stderr
+
+
+@pytest.mark.parametrize("args,want", [([], 8), (["--hw-queues", "16"], 16), (["--hw-queues=12"], 12)])
+def test_hw_queues_both_forms(args, want):
+    """GPU_MAX_HW_QUEUES is set before HIP initialises from either spelling of the flag."""
+    p = _run(["--dry-run", *args])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert _json_line(p.stdout)["hw_queues"] == want
+
+
+@pytest.mark.parametrize("bad", [["--hw-queues=40"], ["--hw-queues", "33"], ["--hw-queues"]])
+def test_hw_queues_rejects_bad_values(bad):
+    """Outside 1..32 (the box refuses more than 32) or without a value: a clear exit."""
+    p = _run(["--dry-run", *bad])
+    assert p.returncode != 0
+    assert "hw-queues" in p.stderr

@@ -233,10 +233,19 @@ SCHEDULES = [
     dict(tile_order=1, quad=100, boost=0, batch=2),
     dict(tile_order=1, quad=0, boost=50, batch=2),
     dict(tile_order=1, quad=35, boost=5, batch=4),
-    # empty-space skipping forced on (any fraction of empty macro cells)
-    dict(tile_order=1, batch=4, macro=3, skip_min_pct=0),
-    dict(tile_order=0, batch=2, macro=2, skip_min_pct=0),
-    dict(tile_order=1, batch=4, macro=5, skip_min_pct=0, quad=10),
+    # macro-cell empty-space skipping forced on (any fraction of empty macro cells;
+    # it runs only with the per-cell skip off)
+    dict(tile_order=1, batch=4, macro=3, skip_min_pct=0, cell_skip=0),
+    dict(tile_order=0, batch=2, macro=2, skip_min_pct=0, cell_skip=0),
+    dict(tile_order=1, batch=4, macro=5, skip_min_pct=0, quad=10, cell_skip=0),
+    # per-cell skip: off, empty-sample flags only (the default, 2, runs in every other row)
+    dict(tile_order=1, batch=4, cell_skip=0, macro=0),
+    dict(tile_order=1, batch=2, cell_skip=1),
+    dict(tile_order=0, batch=4, cell_skip=1),
+    dict(tile_order=1, batch=4, cell_skip=3),
+    dict(tile_order=1, batch=2, cell_skip=3, boost=0),
+    dict(tile_order=1, batch=4, cell_skip=4),
+    dict(tile_order=2, batch=2, cell_skip=4),
     # order built on a side stream (lag 3) / rebuilt every frame
     dict(tile_order=1, batch=4, async_order=1, quad=10),
     dict(tile_order=1, batch=2, order_interval=1, boost=0),
@@ -264,7 +273,7 @@ def test_schedules_bitexact(oracle, bonsai_tf, name, sched):
     d = Device(0)
     try:
         for k in ("tile_order", "quad", "boost", "batch", "macro", "skip_min_pct", "async_order",
-                  "order_interval"):
+                  "order_interval", "cell_skip"):
             if k in opts:
                 N.check(N.lib().cvr_set_option(d.handle, k.encode(), opts[k]), k)
         for frame in range(5):
@@ -273,6 +282,94 @@ def test_schedules_bitexact(oracle, bonsai_tf, name, sched):
             assert_bitexact(g_cnt, o_cnt, f"{name} frame {frame} counts")
             assert_bitexact(g_rgba, o_rgba, f"{name} frame {frame} rgba")
             assert g_total == o_total
+    finally:
+        d.close()
+
+
+def _cell_flags(d, n):
+    """The skip flags the library wrote into the cells (cvr_copy_cells), as
+    (empty bool, q int) arrays over the (n+1)^3 cell grid (z, y, x)."""
+    cells = np.zeros(((n + 1) ** 3, 4), np.uint32)
+    N.check(N.lib().cvr_copy_cells(d.handle, cells.ctypes.data, cells.nbytes), "copy cells", d.handle)
+    empty = (cells[:, 0] >> 31).astype(bool)
+    q = ((cells[:, 1] >> 31) | ((cells[:, 2] >> 31) << 1) | ((cells[:, 3] >> 31) << 2)).astype(int)
+    return empty.reshape((n + 1,) * 3), q.reshape((n + 1,) * 3), cells
+
+
+def test_cell_flags_match_host_restatement(oracle, bonsai_tf):
+    """The per-cell skip flags (precompute.hip build_cell_flags): EMPTY exactly where every
+    density the cell's corners can interpolate to reads only TF entries with tau = 0
+    (recomputed here in numpy, with the same 2^-10 margin), and q = min(d, 8) - 1 for the
+    chessboard distance d to the nearest non-empty cell (scipy's distance transform, cells
+    outside the grid ignored).  The flags change with the TF and vanish with cell_skip 0
+    on a new volume; the densities (the low 15 bits of every half) never change."""
+    from scipy import ndimage
+    n = 40
+    vol = D.blobs_u8(n, count=5)
+    sc = D.voxel_scale(n)
+    d = Device(0)
+    try:
+        for tf in (bonsai_tf, case_tf(dict(tf_alpha_scale=0.0), bonsai_tf)):
+            gpu_render(d, vol, sc, tf, INITIAL, 32, 32)
+            empty, q, cells = _cell_flags(d, n)
+            v16 = oracle.volume_r16f(vol)
+            idx = np.clip(np.arange(n + 1) - 1, 0, n - 1); idx2 = np.clip(np.arange(n + 1), 0, n - 1)
+
+            def mm(f):
+                a = f(v16[idx], v16[idx2]); a = f(a[:, idx], a[:, idx2])
+                return f(a[:, :, idx], a[:, :, idx2])
+            vmin, vmax = mm(np.minimum), mm(np.maximum)
+            t16 = tf.astype(np.float16).astype(np.float32)
+            tau = np.concatenate([[t16[0, 3]], t16[:, 3], [t16[-1, 3]]])
+            pre = np.concatenate([[0], np.cumsum((tau > 0) | np.isnan(tau))])
+            fn = np.float32(tf.shape[0])
+            kl = np.maximum(np.floor((vmin - np.float32(1 / 1024)) * fn - 0.5).astype(int) + 1, 0)
+            kh = np.minimum(np.floor((vmax + np.float32(1 / 1024)) * fn - 0.5).astype(int) + 2,
+                            tf.shape[0] + 1)
+            want_empty = ~((kl <= kh) & (pre[np.maximum(kh, 0) + 1] - pre[kl] > 0))
+            assert np.array_equal(empty, want_empty)
+            dist = (ndimage.distance_transform_cdt(want_empty, metric="chessboard")
+                    if (~want_empty).any() else np.full(want_empty.shape, 99))   # all empty
+            want_q = np.where(want_empty, np.minimum(dist, 8) - 1, 0)
+            assert np.array_equal(q, want_q)
+            assert want_empty.any()
+        # the densities are untouched by the flags
+        fresh = Device(0)
+        try:
+            N.check(N.lib().cvr_set_option(fresh.handle, b"cell_skip", 0), "cell_skip")
+            gpu_render(fresh, vol, sc, bonsai_tf, INITIAL, 32, 32)
+            e0, q0, c0 = _cell_flags(fresh, n)
+            assert not e0.any() and not q0.any()
+            assert np.array_equal(c0 & 0x7fff7fff, cells & 0x7fff7fff)
+        finally:
+            fresh.close()
+    finally:
+        d.close()
+
+
+def test_cell_skip_modes_bitexact_headline_band(oracle, bonsai_tf):
+    """cell_skip 0 / 1 / 2 / 3 / 4 render the headline field identically (RGBA bits and per-pixel
+    counts); a TF change rebuilds the flags (long-ray TF: alpha x 0.02)."""
+    vol = _ml(256)
+    sc = D.voxel_scale(256)
+    W = H = 256
+    d = Device(0)
+    try:
+        for tfs in (1.0, 0.02):
+            tf = bonsai_tf.copy(); tf[:, 3] *= tfs
+            res = []
+            for cs in (0, 1, 2, 3, 4):
+                N.check(N.lib().cvr_set_option(d.handle, b"cell_skip", cs), "cell_skip")
+                res.append(gpu_render(d, vol, sc, tf, INITIAL, W, H, set_data=(cs == 0)))
+            for cs in (1, 2, 3, 4):
+                assert_bitexact(res[cs][0], res[0][0], f"cell_skip {cs} rgba (tf x{tfs})")
+                assert_bitexact(res[cs][1], res[0][1], f"cell_skip {cs} counts (tf x{tfs})")
+                assert res[cs][2] == res[0][2]
+            rows = (120, 136)
+            o_rgba, o_cnt, _ = oracle.render_rc1pass(oracle.volume_r16f(vol), sc, tf, INITIAL, W, H,
+                                                     oracle.default_step(sc), rows=rows)
+            assert_bitexact(res[2][0][rows[0]:rows[1]], o_rgba[rows[0]:rows[1]], "rows rgba")
+            assert_bitexact(res[2][1][rows[0]:rows[1]], o_cnt[rows[0]:rows[1]], "rows counts")
     finally:
         d.close()
 

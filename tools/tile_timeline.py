@@ -26,13 +26,15 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--quad", type=int, default=0)
     ap.add_argument("--keep", type=int, default=0, help="render only the longest N entries per band")
+    ap.add_argument("--cell-skip", type=int, default=2)
     ap.add_argument("--tag", default="run")
     a = ap.parse_args()
     n, W = a.size, a.res
     dev = Device(0)
     L = N.lib()
     for k, v in (("tile_order", a.order), ("boost", a.boost),
-                 ("batch", a.batch), ("quad", a.quad), ("debug_keep", a.keep), ("tile_stats", 1)):
+                 ("batch", a.batch), ("quad", a.quad), ("debug_keep", a.keep), ("tile_stats", 1),
+                 ("cell_skip", a.cell_skip)):
         N.check(L.cvr_set_option(dev.handle, k.encode(), v), k)
     dev.set_volume(D.marschner_lobb_u8(n), D.voxel_scale(n))
     dev.set_transfer_function(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
