@@ -156,6 +156,9 @@ def parse():
                    help="N > 1 gather: the library's RCCL communicator or dist.gather")
     p.add_argument("--shade-flat", type=int, default=-1, choices=[-1, 0, 1],
                    help="dos/ebs: 1 flat job list (library default), 0 per-wave shading batches")
+    p.add_argument("--sat-layout", type=int, default=-1, choices=[-1, 0, 1],
+                   help="ebs: the SAT the frame reads, 0 the cell4 copy, 1 the plain float SAT "
+                        "(-1: the library default)")
     p.add_argument("--flat-group", type=int, default=0,
                    help="dos/ebs flat shading: 64-job chunks per XCD turn (0: library default)")
     p.add_argument("--postpass", action="store_true",
@@ -457,6 +460,9 @@ def main():
     r.SetExternalResources(dm, rp)
     assert r.Init(W, H)
     r.PrepareRender(cam)
+    if ebs and a.sat_layout >= 0:
+        N.check(N.lib().cvr_set_option(r.device.handle, b"sat_layout", a.sat_layout), "sat_layout",
+                r.device.handle)
     if ebs:
         # the SAT precompute on its own (Init built it once already): GPU wall time
         torch.cuda.synchronize()
@@ -768,7 +774,10 @@ def main():
                        "settle_frames": settle,
                        "parallelism": f"screen tiles {tile}x{tile} over {world} GPU(s)"
                                       if world > 1 else "1 GPU",
-                       "storage": "cell8 fp16 (16 B/cell, x-fastest)",
+                       "storage": "cell8 fp16 (16 B/cell, x-fastest; skip flags in the sign bits)"
+                                  + ((", SAT " + ("plain float" if N.lib().cvr_get_option(
+                                      r.device.handle, b"sat_layout") == 1 else "cell4 float4"))
+                                     if ebs else ""),
                        "frame_format": a.format,
                        "frames_in_flight": split.nstreams,
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),

@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "cvr_tf1d_build_rgbt", "cvr_read_tf1d", "cvr_read_raw", "cvr_read_syn", "cvr_read_pvm",
     "cvr_read_camera_state", "cvr_read_light_position", "cvr_read_light", "cvr_build_cone_tables",
     "cvr_set_extinction_volume", "cvr_copy_extinction_level", "cvr_render_dosct",
-    "cvr_tf1d_ext_lut", "cvr_set_extinction_sat", "cvr_copy_extinction_sat", "cvr_render_extbsd",
+    "cvr_tf1d_ext_lut", "cvr_set_extinction_sat", "cvr_copy_extinction_sat", "cvr_sat_layout_check", "cvr_render_extbsd",
     "cvr_comm_unique_id", "cvr_comm_init", "cvr_comm_destroy", "cvr_gather_tiles",
     "cvr_gather_tiles_n", "cvr_unpack_tiles_device_n",
     "cvr_gather_sync", "cvr_multiscale_resolution", "cvr_multiscale_filter",
@@ -210,6 +210,7 @@ def lib() -> ctypes.CDLL:
         "cvr_tf1d_ext_lut": ([DP, I, DP, I, I, I, I, FP], I),
         "cvr_set_extinction_sat": ([P, FP, I], I),
         "cvr_copy_extinction_sat": ([P, FP, ctypes.c_size_t, IP], I),
+        "cvr_sat_layout_check": ([IP, I, I, ctypes.POINTER(ctypes.c_ulonglong)], I),
         "cvr_render_extbsd": ([P, ctypes.POINTER(Frame), ctypes.POINTER(EbsParams),
                                ctypes.POINTER(Output)], I),
         "cvr_iso_params_default": ([I, ctypes.POINTER(IsoParams)], None),

@@ -255,7 +255,7 @@ void cvr_destroy(cvr_ctx* ctx) {
   p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr;
   p = c->d_sat_scratch; free_dev(p); c->d_sat_scratch = nullptr;
   p = c->d_shade; free_dev(p); c->d_shade = nullptr;
-  cvr::flat_release(c->flat);
+  for (auto& J : c->flat) cvr::flat_release(J);
   p = c->d_cones; free_dev(p); c->d_cones = nullptr;
   delete[] c->cone_tab;
   p = c->d_total; free_dev(p); c->d_total = nullptr;
@@ -329,6 +329,27 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->sat_chunk = value;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "sat_layout")) {
+    if (value < 0 || value > 1)
+      return fail(c, CVR_ERR_ARG, "sat_layout must be 0 (cell4 copy) or 1 (the plain float SAT)");
+    if (value == 1 && c->d_sat_cells) {   // the copy is not needed any more (17 GiB at 1024^3)
+      HIP_TRY(c, hipSetDevice(c->device));
+      HIP_TRY(c, hipDeviceSynchronize());
+      void* p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr;
+    }
+    c->sat_layout = value;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "sat_keep_scratch")) {
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "sat_keep_scratch must be 0 or 1");
+    c->sat_keep_scratch = value;
+    if (!value && c->d_sat_scratch) {
+      HIP_TRY(c, hipSetDevice(c->device));
+      HIP_TRY(c, hipDeviceSynchronize());
+      void* p = c->d_sat_scratch; free_dev(p); c->d_sat_scratch = nullptr;
+    }
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "shade_flat")) {
     if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "shade_flat must be 0 or 1");
     c->shade_flat = value;
@@ -337,6 +358,11 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
   if (!std::strcmp(key, "flat_group")) {
     if (value < 1 || value > 4096) return fail(c, CVR_ERR_ARG, "flat_group must be in [1, 4096]");
     c->flat_group = value;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "debug_flat_limit")) {   // tests: force the flat pipeline's fallback
+    if (value < 0) return fail(c, CVR_ERR_ARG, "debug_flat_limit must be >= 0");
+    c->debug_flat_limit = value;
     return CVR_OK;
   }
   if (!std::strcmp(key, "shade_counters")) {
@@ -454,7 +480,15 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "shade_counters")) return c->shade_counters;
   if (!std::strcmp(key, "shade_flat")) return c->shade_flat;
   if (!std::strcmp(key, "flat_group")) return c->flat_group;
+  if (!std::strcmp(key, "debug_flat_limit")) return c->debug_flat_limit;
+  if (!std::strcmp(key, "flat_cap_kjobs")) {   // read-only: the context stream's job-list capacity
+    for (const auto& J : c->flat)
+      if (J.owned && J.stream == c->stream) return (int)(J.cap / 1000);
+    return 0;
+  }
   if (!std::strcmp(key, "sat_chunk")) return c->sat_chunk;
+  if (!std::strcmp(key, "sat_layout")) return c->sat_layout;
+  if (!std::strcmp(key, "sat_keep_scratch")) return c->sat_keep_scratch;
   if (!std::strcmp(key, "quad")) return c->quad_pct;
   if (!std::strcmp(key, "filter_bits")) return c->filter_bits;
   if (!std::strcmp(key, "kernel_timing")) return (int)c->ev_start.size();
@@ -1167,9 +1201,9 @@ static cvr_status render_shaded(Ctx* c, const cvr_output* o, int ntiles, size_t 
     d_samples = o->samples ? (uint32_t*)((char*)c->d_scratch + rgba_bytes) : nullptr;
     d_total = o->total ? c->d_total : nullptr;
   }
-  // flat shading (DOS/EBS with c->shade_flat) keeps one job list per context:
-  // frames on other streams wait for it like for the counters
-  const bool use_counters = d_total || c->shade_counters || flat_jobs;
+  // (flat shading keeps one job-list set per render stream: no wait for it here)
+  (void)flat_jobs;
+  const bool use_counters = d_total || c->shade_counters;
   if (use_counters) {
     cvr_status st = counters_acquire(c, s);
     if (st != CVR_OK) return st;
@@ -1471,9 +1505,8 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   // Same grid as the last build (a TF change): rebuild into the existing buffers.
   // Freeing and re-allocating the ~30 GB of a 1024^3 SAT costs seconds.
-  const bool reuse = c->d_sat && c->d_sat_cells && c->d_sat_scratch &&
-                     c->sat_dims[0] == w && c->sat_dims[1] == h && c->sat_dims[2] == d;
-  if (!reuse) {
+  const bool same = c->d_sat && c->sat_dims[0] == w && c->sat_dims[1] == h && c->sat_dims[2] == d;
+  if (!same) {
     void* p = c->d_sat; free_dev(p); c->d_sat = nullptr;
     p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr;
     p = c->d_sat_scratch; free_dev(p); c->d_sat_scratch = nullptr;
@@ -1482,10 +1515,15 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
   float* d_lut = nullptr;
   hipError_t e = hipMalloc((void**)&d_lut, (size_t)nv * sizeof(float));
   if (e == hipSuccess) e = hipMemcpy(d_lut, ext_lut, (size_t)nv * sizeof(float), hipMemcpyHostToDevice);
-  // the double recurrence's grid stays allocated with the SAT (for rebuilds)
-  if (e == hipSuccess && !reuse) e = hipMalloc(&c->d_sat_scratch, cells * sizeof(double));
+  // the double recurrence's grid: kept with the SAT for rebuilds (sat_keep_scratch,
+  // 8.6 GB at 1024^3) or allocated for this build only
+  if (e == hipSuccess && !c->d_sat_scratch) e = hipMalloc(&c->d_sat_scratch, cells * sizeof(double));
   double* d_sd = (double*)c->d_sat_scratch;
-  if (e == hipSuccess && !reuse) e = hipMalloc((void**)&c->d_sat, cells * sizeof(float));
+  // the float SAT plus kSatPlainPadPlanes zero planes (the plain layout's clamped
+  // +1 neighbours: cvr_sat_layout_check)
+  const size_t pad_floats = cvr::sat_plain_floats(w, h, d) - cells;
+  if (e == hipSuccess && !same) e = hipMalloc((void**)&c->d_sat, cvr::sat_plain_floats(w, h, d) * sizeof(float));
+  if (e == hipSuccess && !same) e = hipMemsetAsync(c->d_sat + cells, 0, pad_floats * sizeof(float), c->stream);
   // GPU time of the two compute phases (option "sat_build_us"): the wall time of
   // this call also holds the allocations of ~50 GB at 1024^3
   hipEvent_t ev[4] = {};
@@ -1496,10 +1534,12 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
   if (e == hipSuccess) e = hipEventRecord(ev[1], c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   (void)hipFree(d_lut);
-  if (e == hipSuccess && !reuse)
+  if (!c->sat_keep_scratch) { void* p = c->d_sat_scratch; free_dev(p); c->d_sat_scratch = nullptr; }
+  // the cell4 copy only for the layout that reads it
+  if (e == hipSuccess && c->sat_layout == 0 && !c->d_sat_cells)
     e = hipMalloc((void**)&c->d_sat_cells, cvr::sat_cells_float4s(w, h, d) * sizeof(float4));
   if (e == hipSuccess) e = hipEventRecord(ev[2], c->stream);
-  if (e == hipSuccess) e = cvr::launch_sat_cells(*c, c->d_sat, c->d_sat_cells, c->stream);
+  if (e == hipSuccess && c->sat_layout == 0) e = cvr::launch_sat_cells(*c, c->d_sat, c->d_sat_cells, c->stream);
   if (e == hipSuccess) e = hipEventRecord(ev[3], c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess) {
@@ -1507,6 +1547,9 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
     if (hipEventElapsedTime(&a, ev[0], ev[1]) == hipSuccess &&
         hipEventElapsedTime(&b, ev[2], ev[3]) == hipSuccess)
       c->sat_build_us = (int)((a + b) * 1000.0f);
+  }
+  if (e == hipSuccess && c->sat_layout == 1) {   // a copy from an earlier layout is stale now
+    void* p = c->d_sat_cells; free_dev(p); c->d_sat_cells = nullptr;
   }
   for (hipEvent_t x : ev)
     if (x) (void)hipEventDestroy(x);
@@ -1519,6 +1562,43 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
                 "cvr_set_extinction_sat: %s", hipGetErrorString(e));
   }
   c->sat_dims[0] = w; c->sat_dims[1] = h; c->sat_dims[2] = d;
+  return CVR_OK;
+}
+
+cvr_status cvr_sat_layout_check(const int dims[3], int layout, int pad_planes, unsigned long long out[4]) {
+  if (!dims || !out || (layout != 0 && layout != 1)) return CVR_ERR_ARG;
+  const long long w = dims[0], h = dims[1], d = dims[2];
+  if (w < 1 || h < 1 || d < 1) return CVR_ERR_ARG;
+  const int pad = pad_planes >= 0 ? pad_planes : cvr::kSatPlainPadPlanes;
+  // bytes allocated: cell4 = float4 per texel of d + 1 planes (sat_cells_float4s);
+  // plain = floats of d + pad planes (sat_plain_floats)
+  const unsigned long long alloc = layout == 0 ? (unsigned long long)cvr::sat_cells_float4s((int)w, (int)h, (int)d) * 16ull
+                                               : (unsigned long long)(w * h * (d + pad)) * 4ull;
+  bool wrap = (w * h) >= (1ll << 24) || h >= (1ll << 24) || w >= (1ll << 24) || (d - 1) * h + (h - 1) >= (1ll << 24);
+  unsigned long long end = 0;
+  const uint32_t pz = (uint32_t)(w * h);
+  for (int c = 0; c < 8; c++) {   // the clamped extremes of every axis
+    const uint32_t tx = (c & 1) ? (uint32_t)(w - 1) : 0u, ty = (c & 2) ? (uint32_t)(h - 1) : 0u,
+                   tz = (c & 4) ? (uint32_t)(d - 1) : 0u;
+    const uint32_t idx = cvr::sat_texel_index(tx, ty, tz, (uint32_t)w, (uint32_t)h);
+    const unsigned long long exact = ((unsigned long long)tz * h + ty) * w + tx;
+    if (idx != exact) wrap = true;
+    if (layout == 0) {
+      for (unsigned long long e : {exact, exact + pz}) {
+        if (e + 1 > 0xffffffffull) wrap = true;
+        end = std::max(end, (e + 1) * 16ull);
+      }
+    } else {
+      for (unsigned long long e : {exact, exact + w, exact + pz, exact + pz + w}) {
+        if (e + 2 > 0xffffffffull) wrap = true;   // the 32-bit element index of the pair
+        end = std::max(end, (e + 2) * 4ull);      // a float pair: elements e, e + 1
+      }
+    }
+  }
+  out[0] = end;
+  out[1] = alloc;
+  out[2] = wrap ? 1ull : 0ull;
+  out[3] = (!wrap && end <= alloc) ? 1ull : 0ull;
   return CVR_OK;
 }
 
@@ -1549,6 +1629,12 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
     return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: bad viewport %dx%d", f->width, f->height);
   if (!c->d_cells || !c->d_tf) return fail(c, CVR_ERR_STATE, "cvr_render_extbsd: no volume or TF");
   if (!c->d_sat) return fail(c, CVR_ERR_STATE, "cvr_render_extbsd: needs cvr_set_extinction_sat");
+  if (c->sat_layout == 0 && !c->d_sat_cells) {   // switched back to the cell4 copy: build it
+    const int w = c->sat_dims[0], h = c->sat_dims[1], d = c->sat_dims[2];
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMalloc((void**)&c->d_sat_cells, cvr::sat_cells_float4s(w, h, d) * sizeof(float4)));
+    HIP_TRY(c, cvr::launch_sat_cells(*c, c->d_sat, c->d_sat_cells, c->stream));
+  }
   const bool phong = p->apply_gradient_shading != 0;
   if (phong && !c->d_grad) return fail(c, CVR_ERR_STATE, "cvr_render_extbsd: Phong needs cvr_set_gradient");
   if (p->shadow_type < 0 || p->shadow_type > 1) return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: bad shadow type");

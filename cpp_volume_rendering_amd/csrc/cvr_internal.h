@@ -188,18 +188,31 @@ constexpr int kMaxBandTiles = 8192;
 // Flat shading of the DOS/EBS renderers (option "shade_flat", shaded_march.h):
 // one frame's shading jobs in a single global list, shaded by a grid of their own
 // and folded into the pixels afterwards.  Buffers grow on demand, one set per context.
+// One set of flat-shading buffers (shaded_march.h launch_shaded_flat).  Each
+// render stream gets its own set (Ctx::flat), so DOS/EBS frames on different
+// streams pipeline; a set is sized from the totals of its earlier frames, read
+// back without blocking (ev_read), and a frame whose list would not fit renders
+// through the per-wave kernel instead, decided on the device (flag).
 struct FlatJobs {
   uint32_t* tile_off = nullptr;             // jobs per 8x8 tile, scanned in place to offsets [tiles + 1]
   uint32_t* tile_roff = nullptr;            // march rounds with a job per tile, scanned likewise
   unsigned long long* masks = nullptr;      // per such round: the lanes that made a job (ballot)
-  unsigned long long* total = nullptr;      // [2]: the frame's jobs and rounds (device)
-  unsigned long long* h_total = nullptr;    // pinned host copy
+  unsigned long long* total = nullptr;      // [3]: the frame's jobs, rounds, overflow flag (device)
+  unsigned long long* h_total = nullptr;    // pinned host copy of an earlier frame's [3]
   float4* cam = nullptr;                    // the ray's camera direction per pixel slot
   float4* jobs = nullptr;                   // 2 float4 per job (+1 with Phong)
   float4* res = nullptr;                    // shaded rgb * alpha, alpha, per job
   int tiles = 0;                            // allocated 8x8 tiles
   size_t cap = 0;                           // allocated jobs (float4 units: cap * 3)
   size_t rcap = 0;                          // allocated round masks
+  // host side of the set
+  hipEvent_t ev_read = nullptr;             // h_total holds the totals of the frame recorded last
+  hipEvent_t ev_done = nullptr;             // the set's last frame is done with its buffers
+  bool pending_read = false;
+  size_t want_jobs = 0, want_rounds = 0;    // the largest totals read back so far
+  hipStream_t stream = nullptr;             // the render stream the set serves
+  bool owned = false;
+  long long last_use = -1;
 };    // the epilogue sorts a band in LDS (32 KiB + group prefixes)
 
 struct Ctx {
@@ -255,7 +268,10 @@ struct Ctx {
   int shade_counters = 0;          // DOS/EBS: count shaded and shadow-lit samples
   int shade_flat = 1;              // DOS/EBS: 1 = flat job list (FlatJobs), 0 = per-wave batches
   int flat_group = 8;              // flat shading: 64-job chunks per XCD turn (XCD-aware order)
-  mutable FlatJobs flat;
+  int debug_flat_limit = 0;        // tests: a frame with more jobs takes the per-wave fallback
+  static constexpr int kFlatSets = 16;    // flat-shading buffer sets, one per render stream
+  mutable FlatJobs flat[kFlatSets];
+  mutable long long flat_clock = 0;
   unsigned long long* d_shade = nullptr;   // [3]: shaded, lit, secondary fetches (last frame)
   int tile_stats = 0;              // record per-tile timing (diagnostics)
   unsigned long long* d_tile_stats = nullptr;
@@ -307,6 +323,8 @@ struct Ctx {
   int sat_build_us = 0;              // GPU time of the last SAT build (option "sat_build_us")
   float* d_sat = nullptr;
   float4* d_sat_cells = nullptr;   // the same SAT as cell4 texels (4 float corners of a plane, sat.hip)
+  int sat_layout = 0;              // option "sat_layout": the frame reads 0 = cell4 copy, 1 = the plain SAT
+  int sat_keep_scratch = 1;        // option "sat_keep_scratch": keep the double build grid for rebuilds
   void* d_sat_scratch = nullptr;   // the double grid of the build (kept for rebuilds)
   int sat_dims[3] = {0, 0, 0};
   int ext_res[3] = {0, 0, 0};
@@ -403,5 +421,35 @@ inline CellGrid make_cell_grid(const int N[3]) {
 }
 
 inline size_t cell_count(const CellGrid& g) { return (size_t)g.cx * g.cy * g.cz; }
+
+// ---------------------------------------------------------------------------
+// Addressing of a SAT fetch (ebs.hip), shared by the kernels and the host check
+// cvr_sat_layout_check.  The texel (tx, ty, tz) is clamped to [0, dims - 1]; its
+// element index (tz * h + ty) * w + tx is formed with 24-bit products (both
+// operands < 2^24, the result < 2^32: checked on the host).  A fetch reads:
+//  * layout 0 (cell4, float4 per texel): elements idx and idx + w*h;
+//  * layout 1 (plain float SAT): the float pairs at idx, idx + w, idx + w*h and
+//    idx + w*h + w (x, x + 1 of rows y, y + 1 of planes z, z + 1).  A clamped
+//    texel's +1 neighbours have weight 0 but are still read; at the far corner
+//    (w-1, h-1, d-1) the last one is element w*h*d + w*h + w, so the buffer
+//    carries kSatPlainPadPlanes planes of zeros after the SAT.  (Round 3's
+//    variant padded one plane: that read ran w + 1 floats past its allocation,
+//    4108 B at 1026^3 — always into the next 4 KiB page — and faulted there.)
+// ---------------------------------------------------------------------------
+constexpr int kSatPlainPadPlanes = 2;
+
+__host__ __device__ inline uint32_t sat_texel_index(uint32_t tx, uint32_t ty, uint32_t tz, uint32_t w,
+                                                    uint32_t h) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __umul24(__umul24(tz, h) + ty, w) + tx;
+#else
+  return ((tz * h + ty) & 0xffffffu) * w + tx;   // the 24-bit product's operand, as the device
+#endif
+}
+
+// floats the plain layout allocates for a w x h x d SAT
+inline size_t sat_plain_floats(int w, int h, int d) {
+  return (size_t)w * h * (size_t)(d + kSatPlainPadPlanes);
+}
 
 }  // namespace cvr

@@ -20,18 +20,51 @@ namespace cvr {
 
 namespace {
 
-// GetSummed3Density (:77-83): trilinear of the float SAT at u = p * inv_vol_scaled,
-// from the cell4 copy (float4 of a plane's 4 corners per texel, x fastest; the
-// z + 1 corners are the texel one plane above).
-__device__ __forceinline__ float sat_fetch(const EbsArgs& Q, const float4* __restrict__ sat, float x,
+// The two device layouts of the float SAT (option "sat_layout"; addressing:
+// sat_texel_index, cvr_internal.h).  corners(idx) gives a texel's 8 GL_LINEAR
+// corners as lo = (x, x+1 of row y; x, x+1 of row y+1) of plane z and hi, the
+// same of plane z + 1.
+//  * SatCell4: the cell4 copy (a float4 of a plane's 4 corners per texel, plus
+//    one repeated top plane; sat.hip sat_cells_kernel): two dwordx4 loads;
+//  * SatPlain: the plain x-fastest float SAT (4x smaller), four float pairs.  A
+//    clamped texel's +1 neighbours (weight exactly 0) are the next row / plane's
+//    first element or the zero planes past the SAT (kSatPlainPadPlanes), all
+//    finite, so each lerp returns its first operand as the cell4 copy's
+//    repeated corner does: the same bits.
+struct SatCell4 {
+  using Ptr = const float4*;
+  __device__ static __forceinline__ void corners(Ptr sat, uint32_t idx, uint32_t w, uint32_t pz,
+                                                 float4& lo, float4& hi) {
+    lo = sat[idx];
+    hi = sat[idx + pz];
+  }
+};
+struct SatPlain {
+  using Ptr = const float*;
+  typedef float f2a __attribute__((ext_vector_type(2), aligned(4)));   // dwordx2 at 4-byte alignment
+  __device__ static __forceinline__ void corners(Ptr sat, uint32_t idx, uint32_t w, uint32_t pz,
+                                                 float4& lo, float4& hi) {
+    const f2a a = *reinterpret_cast<const f2a*>(sat + idx);
+    const f2a b = *reinterpret_cast<const f2a*>(sat + (idx + w));
+    const f2a c = *reinterpret_cast<const f2a*>(sat + (idx + pz));
+    const f2a d = *reinterpret_cast<const f2a*>(sat + (idx + pz + w));
+    lo = make_float4(a.x, a.y, b.x, b.y);
+    hi = make_float4(c.x, c.y, d.x, d.y);
+  }
+};
+
+// GetSummed3Density (:77-83): trilinear of the float SAT at u = p * inv_vol_scaled.
+template <class L>
+__device__ __forceinline__ float sat_fetch(const EbsArgs& Q, typename L::Ptr __restrict__ sat, float x,
                                            float y, float z) {
   const float tx = __builtin_amdgcn_fmed3f(fmaf(x * Q.inv_vs[0], Q.nsat[0], -0.5f), 0.0f, Q.nsat_m1[0]);
   const float ty = __builtin_amdgcn_fmed3f(fmaf(y * Q.inv_vs[1], Q.nsat[1], -0.5f), 0.0f, Q.nsat_m1[1]);
   const float tz = __builtin_amdgcn_fmed3f(fmaf(z * Q.inv_vs[2], Q.nsat[2], -0.5f), 0.0f, Q.nsat_m1[2]);
   // < 2^31 texels (checked on the host): 32-bit index, 24-bit row products
-  const uint32_t row = __umul24((uint32_t)tz, (uint32_t)Q.sat_dims[1]) + (uint32_t)ty;
-  const uint32_t idx = __umul24(row, (uint32_t)Q.sat_dims[0]) + (uint32_t)tx;
-  const float4 lo = sat[idx], hi = sat[idx + Q.sat_pz];
+  const uint32_t idx = sat_texel_index((uint32_t)tx, (uint32_t)ty, (uint32_t)tz, (uint32_t)Q.sat_dims[0],
+                                       (uint32_t)Q.sat_dims[1]);
+  float4 lo, hi;
+  L::corners(sat, idx, (uint32_t)Q.sat_dims[0], Q.sat_pz, lo, hi);
   const float ax = __builtin_amdgcn_fractf(tx), ay = __builtin_amdgcn_fractf(ty),
               az = __builtin_amdgcn_fractf(tz);
   const float c00 = lerpf(lo.x, lo.y, ax), c10 = lerpf(lo.z, lo.w, ax);
@@ -40,11 +73,12 @@ __device__ __forceinline__ float sat_fetch(const EbsArgs& Q, const float4* __res
 }
 
 // EvaluateSAT3D (:85-99)
-__device__ __forceinline__ float sat_box(const EbsArgs& Q, const float4* __restrict__ sat, f3 p1, f3 p2) {
-  const float V1 = sat_fetch(Q, sat, p2.x, p2.y, p2.z), V2 = sat_fetch(Q, sat, p1.x, p2.y, p2.z);
-  const float V3 = sat_fetch(Q, sat, p2.x, p2.y, p1.z), V4 = sat_fetch(Q, sat, p1.x, p2.y, p1.z);
-  const float V5 = sat_fetch(Q, sat, p2.x, p1.y, p2.z), V6 = sat_fetch(Q, sat, p1.x, p1.y, p2.z);
-  const float V7 = sat_fetch(Q, sat, p2.x, p1.y, p1.z), V8 = sat_fetch(Q, sat, p1.x, p1.y, p1.z);
+template <class L>
+__device__ __forceinline__ float sat_box(const EbsArgs& Q, typename L::Ptr __restrict__ sat, f3 p1, f3 p2) {
+  const float V1 = sat_fetch<L>(Q, sat, p2.x, p2.y, p2.z), V2 = sat_fetch<L>(Q, sat, p1.x, p2.y, p2.z);
+  const float V3 = sat_fetch<L>(Q, sat, p2.x, p2.y, p1.z), V4 = sat_fetch<L>(Q, sat, p1.x, p2.y, p1.z);
+  const float V5 = sat_fetch<L>(Q, sat, p2.x, p1.y, p2.z), V6 = sat_fetch<L>(Q, sat, p1.x, p1.y, p2.z);
+  const float V7 = sat_fetch<L>(Q, sat, p2.x, p1.y, p1.z), V8 = sat_fetch<L>(Q, sat, p1.x, p1.y, p1.z);
   return (V1 - V2 - V3 + V4 - V5 + V6 + V7 - V8);
 }
 
@@ -67,12 +101,13 @@ __device__ __forceinline__ float cone_div(float a, float d, float rd) {
 }
 
 // EvaluateShadowSAT3D (:148-185, the texture path)
-__device__ __forceinline__ float shadow_box(const EbsArgs& Q, const float4* __restrict__ sat, f3 p1, f3 p2,
+template <class L>
+__device__ __forceinline__ float shadow_box(const EbsArgs& Q, typename L::Ptr __restrict__ sat, f3 p1, f3 p2,
                                            f3 rS) {
   const float volquery = (div_by_recip(fabsf(p1.x - p2.x), Q.S[0], rS.x)) *
                          (div_by_recip(fabsf(p1.y - p2.y), Q.S[1], rS.y)) *
                          (div_by_recip(fabsf(p1.z - p2.z), Q.S[2], rS.z));
-  return ((sat_box(Q, sat, sat_offset(Q, p1), sat_offset(Q, p2)) / volquery)) * Q.ui_weight;
+  return ((sat_box<L>(Q, sat, sat_offset(Q, p1), sat_offset(Q, p2)) / volquery)) * Q.ui_weight;
 }
 
 // The same shadow box as a software pipeline, half a box deep.  A box's eight
@@ -113,18 +148,17 @@ __device__ __forceinline__ SatBoxCoord shadow_box_coord(const EbsArgs& Q, f3 p1,
 
 // V_k (k = 0..7 for V1..V8) is the fetch at p1.x if k & 1, p1.z if k & 2,
 // p1.y if k & 4 (else p2): half H holds k = 4H .. 4H+3.
-template <int H>
-__device__ __forceinline__ void shadow_half_issue(const EbsArgs& Q, const float4* __restrict__ sat,
+template <int H, class L>
+__device__ __forceinline__ void shadow_half_issue(const EbsArgs& Q, typename L::Ptr __restrict__ sat,
                                                   const SatBoxCoord& C, float4 (&c)[8]) {
   const uint32_t ty = (uint32_t)C.ty[H ? 0 : 1];
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int k = 4 * H + j;
     const int xi = (k & 1) ? 0 : 1, zi = (k & 2) ? 0 : 1;
-    const uint32_t row = __umul24((uint32_t)C.tz[zi], (uint32_t)Q.sat_dims[1]) + ty;
-    const uint32_t idx = __umul24(row, (uint32_t)Q.sat_dims[0]) + (uint32_t)C.tx[xi];
-    c[2 * j] = sat[idx];
-    c[2 * j + 1] = sat[idx + Q.sat_pz];
+    const uint32_t idx = sat_texel_index((uint32_t)C.tx[xi], ty, (uint32_t)C.tz[zi],
+                                         (uint32_t)Q.sat_dims[0], (uint32_t)Q.sat_dims[1]);
+    L::corners(sat, idx, (uint32_t)Q.sat_dims[0], Q.sat_pz, c[2 * j], c[2 * j + 1]);
   }
 }
 
@@ -150,8 +184,8 @@ __device__ __forceinline__ void shadow_half_finish(const SatBoxCoord& C, const f
 // The box chain of a cone: while cond(w) { Stau += box(w); w += si }, with
 // box_at(w, p1, p2) giving the box corners at axis position w (ConeZAxis
 // :240-272 and its Y / X twins).  Pipelined half a box deep (CVR_EBS_PIPE).
-template <class Cond, class BoxAt>
-__device__ __forceinline__ float shadow_chain(const EbsArgs& Q, const float4* __restrict__ sat, f3 rS,
+template <class L, class Cond, class BoxAt>
+__device__ __forceinline__ float shadow_chain(const EbsArgs& Q, typename L::Ptr __restrict__ sat, f3 rS,
                                               float w, float si, Cond cond, BoxAt box_at,
                                               uint32_t& boxes) {
   float Stau = 0.0f;
@@ -159,7 +193,7 @@ __device__ __forceinline__ float shadow_chain(const EbsArgs& Q, const float4* __
   if (!CVR_EBS_PIPE) {
     while (cond(w)) {
       box_at(w, p1, p2);
-      Stau += shadow_box(Q, sat, p1, p2, rS);
+      Stau += shadow_box<L>(Q, sat, p1, p2, rS);
       boxes++;
       w = w + si;
     }
@@ -170,9 +204,9 @@ __device__ __forceinline__ float shadow_chain(const EbsArgs& Q, const float4* __
   SatBoxCoord C = shadow_box_coord(Q, p1, p2, rS);
   float4 F[8], S[8];
   float V[4];
-  shadow_half_issue<0>(Q, sat, C, F);
+  shadow_half_issue<0, L>(Q, sat, C, F);
   for (;;) {
-    shadow_half_issue<1>(Q, sat, C, S);
+    shadow_half_issue<1, L>(Q, sat, C, S);
     __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the lerps
     shadow_half_finish<0>(C, F, V);
     float sum = V[0] - V[1] - V[2] + V[3];
@@ -180,7 +214,7 @@ __device__ __forceinline__ float shadow_chain(const EbsArgs& Q, const float4* __
     const bool more = cond(wn);
     box_at(wn, p1, p2);
     const SatBoxCoord Cn = shadow_box_coord(Q, p1, p2, rS);
-    shadow_half_issue<0>(Q, sat, Cn, F);
+    shadow_half_issue<0, L>(Q, sat, Cn, F);
     __builtin_amdgcn_sched_barrier(0);
     shadow_half_finish<1>(C, S, V);
     sum = sum - V[0] + V[1] + V[2] - V[3];
@@ -194,10 +228,11 @@ __device__ __forceinline__ float shadow_chain(const EbsArgs& Q, const float4* __
 }
 
 // ExtinctionAmbientOcclusion (:109-146)
-__device__ float ebs_occlusion(const EbsArgs& Q, const float4* __restrict__ sat, f3 tx) {
+template <class L>
+__device__ float ebs_occlusion(const EbsArgs& Q, typename L::Ptr __restrict__ sat, f3 tx) {
   const float R = Q.occ_radius;
   const f3 r0{R * Q.S[0], R * Q.S[1], R * Q.S[2]};
-  const float SAT_Sh0 = sat_box(Q, sat, sat_offset(Q, f3{tx.x - r0.x, tx.y - r0.y, tx.z - r0.z}),
+  const float SAT_Sh0 = sat_box<L>(Q, sat, sat_offset(Q, f3{tx.x - r0.x, tx.y - r0.y, tx.z - r0.z}),
                                 sat_offset(Q, f3{tx.x + r0.x, tx.y + r0.y, tx.z + r0.z}));
   // the weights 1 / r^2 and W_A are the same for every sample: Q.ao_w / Q.ao_wa,
   // computed on the host by the same float expressions
@@ -207,7 +242,7 @@ __device__ float ebs_occlusion(const EbsArgs& Q, const float4* __restrict__ sat,
   for (int i = 1; i < Q.occ_shells; i++) {
     const float r1 = R * (float)(i + 1);
     const f3 ri{r1 * Q.S[0], r1 * Q.S[1], r1 * Q.S[2]};
-    const float SAT_Shi_1 = sat_box(Q, sat, sat_offset(Q, f3{tx.x - ri.x, tx.y - ri.y, tx.z - ri.z}),
+    const float SAT_Shi_1 = sat_box<L>(Q, sat, sat_offset(Q, f3{tx.x - ri.x, tx.y - ri.y, tx.z - ri.z}),
                                     sat_offset(Q, f3{tx.x + ri.x, tx.y + ri.y, tx.z + ri.z}));
     const float tshi_1 = tshi + (SAT_Shi_1 - SAT_Shi) * (tab ? Q.ao_w[i] : 1.0f / (r1 * r1));
     SAT_Shi = SAT_Shi_1;
@@ -220,8 +255,8 @@ __device__ float ebs_occlusion(const EbsArgs& Q, const float4* __restrict__ sat,
 }
 
 // ConeZAxis (:187-275)
-template <bool R>
-__device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
+template <class L, bool R>
+__device__ float cone_z(const EbsArgs& Q, typename L::Ptr __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
   float signal = 1.0f;
   if (cv.z < 0) signal = -1.0f;
@@ -261,12 +296,12 @@ __device__ float cone_z(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
     p1 = f3{pos.x + x1, pos.y + y1, pos.z + z1};
     p2 = f3{pos.x + x2, pos.y + y2, pos.z + z2};
   };
-  return shadow_chain(Q, sat, rS, z_pos, si, cond, box_at, boxes);
+  return shadow_chain<L>(Q, sat, rS, z_pos, si, cond, box_at, boxes);
 }
 
 // ConeYAxis (:277-364)
-template <bool R>
-__device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
+template <class L, bool R>
+__device__ float cone_y(const EbsArgs& Q, typename L::Ptr __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
   float signal = 1.0f;
   if (cv.y < 0) signal = -1.0f;
@@ -306,12 +341,12 @@ __device__ float cone_y(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
     p1 = f3{pos.x + x1, pos.y + y1, pos.z + z1};
     p2 = f3{pos.x + x2, pos.y + y2, pos.z + z2};
   };
-  return shadow_chain(Q, sat, rS, y_pos, si, cond, box_at, boxes);
+  return shadow_chain<L>(Q, sat, rS, y_pos, si, cond, box_at, boxes);
 }
 
 // ConeXAxis (:366-453)
-template <bool R>
-__device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos, f3 cv,
+template <class L, bool R>
+__device__ float cone_x(const EbsArgs& Q, typename L::Ptr __restrict__ sat, f3 pos, f3 cv,
                         uint32_t& boxes) {
   float signal = 1.0f;
   if (cv.x < 0) signal = -1.0f;
@@ -351,7 +386,7 @@ __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
     p1 = f3{pos.x + x1, pos.y + y1, pos.z + z1};
     p2 = f3{pos.x + x2, pos.y + y2, pos.z + z2};
   };
-  return shadow_chain(Q, sat, rS, x_pos, si, cond, box_at, boxes);
+  return shadow_chain<L>(Q, sat, rS, x_pos, si, cond, box_at, boxes);
 }
 
 }  // namespace
@@ -362,22 +397,22 @@ __device__ float cone_x(const EbsArgs& Q, const float4* __restrict__ sat, f3 pos
 #ifndef CVR_EBS_WAVES
 #define CVR_EBS_WAVES 1
 #endif
-template <bool RECIP_CONE>
+template <bool RECIP_CONE, class LY>
 struct EbsShaderT {
   using Args = EbsArgs;
   static constexpr int kMinWavesPerEU = CVR_EBS_WAVES;   // register budget (1: compiler's choice)
   static constexpr int kFlatWavesPerEU = CVR_EBS_FLAT_WAVES;   // flat_shade_kernel
-  using Data = const float4*;   // the float SAT, cell4
+  using Data = typename LY::Ptr;   // the float SAT, cell4 or plain
 
   // ShadeSample (:498-550); `lit` counts the shadow box chains traced.
-  __device__ static f3 shade(const EbsArgs& Q, const float4* __restrict__ sat, f3 tx, f3 wp, f3,
+  __device__ static f3 shade(const EbsArgs& Q, typename LY::Ptr __restrict__ sat, f3 tx, f3 wp, f3,
                              f3 rgb, const f3* g, uint32_t& lit, uint32_t& fetches) {
     const Rc1passArgs& A = Q.a;
     const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
     const f3 light{A.light[0], A.light[1], A.light[2]};
     float iocc = 0.0f, isdw = 0.0f;
     if (Q.apply_occlusion) {
-      iocc = ebs_occlusion(Q, sat, tx);
+      iocc = ebs_occlusion<LY>(Q, sat, tx);
       fetches += 8 * Q.occ_shells;
     }
     if (Q.apply_shadow) {
@@ -387,9 +422,9 @@ struct EbsShaderT {
       const f3 ac{fabsf(cv.x), fabsf(cv.y), fabsf(cv.z)};
       float Stau;
       uint32_t boxes = 0;
-      if (ac.z > ac.x && ac.z > ac.y) Stau = cone_z<RECIP_CONE>(Q, sat, tx, cv, boxes);
-      else if (ac.y > ac.x) Stau = cone_y<RECIP_CONE>(Q, sat, tx, cv, boxes);
-      else Stau = cone_x<RECIP_CONE>(Q, sat, tx, cv, boxes);
+      if (ac.z > ac.x && ac.z > ac.y) Stau = cone_z<LY, RECIP_CONE>(Q, sat, tx, cv, boxes);
+      else if (ac.y > ac.x) Stau = cone_y<LY, RECIP_CONE>(Q, sat, tx, cv, boxes);
+      else Stau = cone_x<LY, RECIP_CONE>(Q, sat, tx, cv, boxes);
       fetches += 8 * boxes;
       isdw = cvr_expf(-Stau);
       lit++;
@@ -417,20 +452,25 @@ struct EbsShaderT {
   }
 };
 
-hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* samples,
-                      unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
+template <class L>
+static hipError_t launch_ebs_layout(const Ctx& c, const EbsArgs& q, typename L::Ptr sat, float4* out,
+                                    uint32_t* samples, unsigned long long* shade,
+                                    unsigned long long* tile_samples, hipStream_t s) {
   const bool ph = q.phong != 0;
   if (c.shade_flat)
     return q.recip_cone
-               ? launch_shaded_flat<EbsShaderT<true>>(c, q, ph, c.d_sat_cells, out, samples, shade,
-                                                      tile_samples, s)
-               : launch_shaded_flat<EbsShaderT<false>>(c, q, ph, c.d_sat_cells, out, samples, shade,
-                                                       tile_samples, s);
+               ? launch_shaded_flat<EbsShaderT<true, L>>(c, q, ph, sat, out, samples, shade, tile_samples, s)
+               : launch_shaded_flat<EbsShaderT<false, L>>(c, q, ph, sat, out, samples, shade, tile_samples, s);
   if (q.recip_cone)
-    return launch_shaded_march<EbsShaderT<true>>(c, q, ph, c.d_sat_cells, out, samples, shade,
-                                                 tile_samples, s);
-  return launch_shaded_march<EbsShaderT<false>>(c, q, ph, c.d_sat_cells, out, samples, shade,
-                                                tile_samples, s);
+    return launch_shaded_march<EbsShaderT<true, L>>(c, q, ph, sat, out, samples, shade, tile_samples, s);
+  return launch_shaded_march<EbsShaderT<false, L>>(c, q, ph, sat, out, samples, shade, tile_samples, s);
+}
+
+hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* samples,
+                      unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
+  if (c.sat_layout == 1)
+    return launch_ebs_layout<SatPlain>(c, q, c.d_sat, out, samples, shade, tile_samples, s);
+  return launch_ebs_layout<SatCell4>(c, q, c.d_sat_cells, out, samples, shade, tile_samples, s);
 }
 
 }  // namespace cvr

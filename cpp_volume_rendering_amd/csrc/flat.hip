@@ -48,12 +48,24 @@ __device__ void flat_scan_one(uint32_t* __restrict__ a, int n, unsigned long lon
   __syncthreads();
 }
 
+// After the scans: total[2] = 1 when the frame's jobs or rounds exceed the
+// set's capacity.  The emit, shade and fold kernels then do nothing and the
+// per-wave kernel renders the frame (the same bits); the count kernel's shade
+// counters (measurement) are cleared for it.
 __global__ void __launch_bounds__(1024) flat_scan_kernel(uint32_t* __restrict__ tile_off,
                                                          uint32_t* __restrict__ tile_roff, int n,
-                                                         unsigned long long* __restrict__ total) {
+                                                         unsigned long long* __restrict__ total,
+                                                         unsigned long long cap,
+                                                         unsigned long long rcap,
+                                                         unsigned long long* __restrict__ shade_ctr) {
   __shared__ unsigned long long part[1024];
   flat_scan_one(tile_off, n, total + 0, part);
   flat_scan_one(tile_roff, n, total + 1, part);
+  if (threadIdx.x == 0) {
+    const bool over = total[0] > cap || total[1] > rcap;
+    total[2] = over ? 1ull : 0ull;
+    if (over && shade_ctr) shade_ctr[0] = shade_ctr[1] = shade_ctr[2] = 0ull;
+  }
 }
 
 // Per pixel: its jobs' results folded in sample order, dst.a replayed from the
@@ -62,6 +74,7 @@ __global__ void __launch_bounds__(1024) flat_scan_kernel(uint32_t* __restrict__ 
 // from their ballot masks: round r's results sit contiguously in lane order.
 __global__ void __launch_bounds__(64) flat_fold_kernel(Rc1passArgs A, FlatJobs J,
                                                        float4* __restrict__ out) {
+  if (J.total[2]) return;   // the list did not fit: the per-wave kernel writes the frame
   const int t = blockIdx.x, lane = threadIdx.x;
   const unsigned long long lt = (1ull << lane) - 1ull;
   int px, py;
@@ -85,9 +98,10 @@ __global__ void __launch_bounds__(64) flat_fold_kernel(Rc1passArgs A, FlatJobs J
   if ((px < A.W && py < A.H) || A.packed) store_rgba(out, oidx, dst, A.out_half);
 }
 
-hipError_t launch_flat_scan(FlatJobs& J, int ntiles, hipStream_t s) {
+hipError_t launch_flat_scan(FlatJobs& J, int ntiles, unsigned long long cap, unsigned long long rcap,
+                            unsigned long long* shade_ctr, hipStream_t s) {
   hipLaunchKernelGGL(flat_scan_kernel, dim3(1), dim3(1024), 0, s, J.tile_off, J.tile_roff, ntiles,
-                     J.total);
+                     J.total, cap, rcap, shade_ctr);
   return hipGetLastError();
 }
 
@@ -108,9 +122,12 @@ static void free_ptr(void*& p) {
 // Blocks the calling thread only when it allocates.
 hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds) {
   hipError_t e = hipSuccess;
-  // growing frees buffers a frame on another stream may still read: let it finish
+  // growing frees buffers the set's last frame may still read: wait for that
+  // frame only (its own event), not for the device
   if ((J.tiles < ntiles && J.tiles > 0) || (jobs > J.cap && J.cap > 0) || (rounds > J.rcap && J.rcap > 0))
-    if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+    if (J.ev_done && (e = hipEventSynchronize(J.ev_done)) != hipSuccess) return e;
+  if (!J.ev_done && (e = hipEventCreateWithFlags(&J.ev_done, hipEventDisableTiming)) != hipSuccess) return e;
+  if (!J.ev_read && (e = hipEventCreateWithFlags(&J.ev_read, hipEventDisableTiming)) != hipSuccess) return e;
   if (J.tiles < ntiles) {
     void* p = J.tile_off; free_ptr(p); J.tile_off = nullptr;
     p = J.tile_roff; free_ptr(p); J.tile_roff = nullptr;
@@ -122,8 +139,11 @@ hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds) {
     if ((e = hipMalloc((void**)&J.cam, slots * sizeof(float4))) != hipSuccess) return e;
     J.tiles = ntiles;
   }
-  if (!J.total && (e = hipMalloc((void**)&J.total, 2 * sizeof(unsigned long long))) != hipSuccess) return e;
-  if (!J.h_total && (e = hipHostMalloc((void**)&J.h_total, 2 * sizeof(unsigned long long))) != hipSuccess)
+  if (!J.total) {
+    if ((e = hipMalloc((void**)&J.total, 3 * sizeof(unsigned long long))) != hipSuccess) return e;
+    if ((e = hipMemset(J.total, 0, 3 * sizeof(unsigned long long))) != hipSuccess) return e;
+  }
+  if (!J.h_total && (e = hipHostMalloc((void**)&J.h_total, 3 * sizeof(unsigned long long))) != hipSuccess)
     return e;
   if (jobs >= (1ull << 32) || rounds >= (1ull << 32)) return hipErrorInvalidValue;   // 32-bit offsets
   if (jobs > J.cap) {
@@ -145,7 +165,28 @@ hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds) {
   return hipSuccess;
 }
 
+// The buffer set of render stream s: the one it used before, else the least
+// recently used set (a set taken over from another stream first waits, on the
+// device, for that stream's last frame with it).
+FlatJobs& flat_set(const Ctx& c, hipStream_t s) {
+  FlatJobs* best = nullptr;
+  for (auto& J : c.flat)
+    if (J.owned && J.stream == s) best = &J;
+  if (!best) {
+    for (auto& J : c.flat)
+      if (!best || J.last_use < best->last_use) best = &J;
+    if (best->owned && best->ev_done) (void)hipStreamWaitEvent(s, best->ev_done, 0);
+    best->owned = true;
+    best->stream = s;
+  }
+  best->last_use = ++c.flat_clock;
+  return *best;
+}
+
 void flat_release(FlatJobs& J) {
+  if (J.ev_done) (void)hipEventSynchronize(J.ev_done);
+  if (J.ev_done) (void)hipEventDestroy(J.ev_done);
+  if (J.ev_read) (void)hipEventDestroy(J.ev_read);
   void* p = J.tile_off; free_ptr(p);
   p = J.tile_roff; free_ptr(p);
   p = J.masks; free_ptr(p);

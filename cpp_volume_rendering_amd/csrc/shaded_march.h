@@ -26,6 +26,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 
 #include "cvr_device.h"
@@ -55,7 +56,11 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
                     typename SH::Data data, float4* __restrict__ out,
                     uint32_t* __restrict__ samples, unsigned long long* __restrict__ shade_ctr,
-                    unsigned long long* __restrict__ tile_samples) {
+                    unsigned long long* __restrict__ tile_samples,
+                    const unsigned long long* __restrict__ run_if) {
+  // run_if: the flat pipeline's totals; this kernel is its fallback and renders
+  // only a frame whose job list did not fit (run_if[2] set by flat_scan_kernel)
+  if (run_if && !run_if[2]) return;
   extern __shared__ float4 tfp[];
   __shared__ float jpx[kJobSlots], jpy[kJobSlots], jpz[kJobSlots];   // tx_pos
   __shared__ float jr[kJobSlots], jg[kJobSlots], jb[kJobSlots];      // TF rgb -> shaded rgb * a
@@ -206,7 +211,10 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
 //      shading, so the march is exact without it) and the march rounds in which
 //      at least one lane made a job;
 //   2. flat_scan_kernel: both counts to exclusive offsets and frame totals,
-//      which the host reads to size the grid (one stream sync per frame);
+//      and whether they fit the stream's buffer set (sized from earlier
+//      frames' totals, read back without blocking; a frame that does not fit
+//      is rendered by the per-wave kernel, launched behind the fold with the
+//      flag as its condition, so the host never waits on a frame);
 //   3. shaded_jobs_kernel<emit>: the same march; each round's jobs are written
 //      contiguously (lane order, so the stores coalesce: position, alpha, TF
 //      rgb, pixel slot; + gradient with Phong) and the round's ballot mask kept;
@@ -225,6 +233,7 @@ shaded_jobs_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
                    const uint4* __restrict__ grad, const float4* __restrict__ tf_g, FlatJobs J,
                    uint32_t* __restrict__ samples, unsigned long long* __restrict__ shade_ctr,
                    unsigned long long* __restrict__ tile_samples) {
+  if (EMIT && J.total[2]) return;   // the list does not fit: the per-wave fallback renders
   extern __shared__ float4 tfp[];
   load_tf_lds(tfp, tf_g, Q.a.tf_n);
   const Rc1passArgs& A = Q.a;
@@ -313,12 +322,15 @@ shaded_jobs_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
 
 template <class SH, bool PHONG>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SH::kFlatWavesPerEU)))
-flat_shade_kernel(typename SH::Args Q, typename SH::Data data, FlatJobs J, unsigned long long total,
-                  int nchunks, int group, unsigned long long* __restrict__ shade_ctr) {
+flat_shade_kernel(typename SH::Args Q, typename SH::Data data, FlatJobs J, int nchunks, int group,
+                  unsigned long long* __restrict__ shade_ctr) {
+  // the grid covers the set's capacity; this frame's total is on the device
+  const unsigned long long total = J.total[0];
+  if (J.total[2]) return;   // did not fit: the per-wave fallback renders the frame
   // block b runs on XCD b % 8; XCD x takes chunk groups x, x + 8, ... in order
   const int b = blockIdx.x, x = b & 7, k = b >> 3;
   const int chunk = ((k / group) * 8 + x) * group + (k % group);
-  if (chunk >= nchunks) return;
+  if (chunk >= nchunks || (unsigned long long)chunk * 64 >= total) return;
   const int lane = threadIdx.x;
   const unsigned long long i = (unsigned long long)chunk * 64 + lane;
   uint32_t nlit = 0, nfetch = 0;
@@ -353,10 +365,12 @@ template <class SH>
 hipError_t launch_shaded_march(const Ctx& c, const typename SH::Args& q, bool phong,
                                typename SH::Data data, float4* out, uint32_t* samples,
                                unsigned long long* shade_ctr, unsigned long long* tile_samples,
-                               hipStream_t s);
-hipError_t launch_flat_scan(FlatJobs& J, int ntiles, hipStream_t s);
+                               hipStream_t s, const unsigned long long* run_if = nullptr);
+hipError_t launch_flat_scan(FlatJobs& J, int ntiles, unsigned long long cap, unsigned long long rcap,
+                            unsigned long long* shade_ctr, hipStream_t s);
 hipError_t launch_flat_fold(const Rc1passArgs& a, FlatJobs& J, float4* out, hipStream_t s);
 hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds);
+FlatJobs& flat_set(const Ctx& c, hipStream_t s);
 
 template <class SH>
 hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool phong,
@@ -366,13 +380,29 @@ hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool pho
   const int nt = q.a.ntiles;
   if (nt <= 0) return hipSuccess;
   if (q.a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
-  FlatJobs& J = c.flat;
+  FlatJobs& J = flat_set(c, s);
   hipError_t e = flat_reserve(J, nt, 0, 0);
   if (e != hipSuccess) return e;
   const size_t lds = (size_t)(q.a.tf_n + 2) * sizeof(float4);
   const uint4* cells = (const uint4*)c.d_cells;
   const uint4* grad = (const uint4*)c.d_grad;
   const float4* tf = (const float4*)c.d_tf;
+  // The set's capacity from the totals of its earlier frames, read back without
+  // blocking: the copy of a frame's totals lands in pinned memory behind it
+  // (ev_read), and is read by a later call once it has.
+  if (J.pending_read && hipEventQuery(J.ev_read) == hipSuccess) {
+    J.want_jobs = std::max(J.want_jobs, (size_t)J.h_total[0]);
+    J.want_rounds = std::max(J.want_rounds, (size_t)J.h_total[1]);
+    J.pending_read = false;
+  }
+  const bool first = J.cap == 0;   // no estimate yet: this frame reads its totals synchronously
+  if (!first && (J.want_jobs > J.cap || J.want_rounds > J.rcap)) {
+    if (flat_reserve(J, nt, J.want_jobs, J.want_rounds) != hipSuccess) {
+      (void)hipGetLastError();   // too large to hold: keep the old size (frames fall back)
+      J.want_jobs = std::min(J.want_jobs, J.cap);
+      J.want_rounds = std::min(J.want_rounds, J.rcap);
+    }
+  }
   if (phong)
     hipLaunchKernelGGL((shaded_jobs_kernel<SH, true, false>), dim3(nt), dim3(64), lds, s, q, cells,
                        grad, tf, J, samples, shade_ctr, tile_samples);
@@ -380,14 +410,22 @@ hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool pho
     hipLaunchKernelGGL((shaded_jobs_kernel<SH, false, false>), dim3(nt), dim3(64), lds, s, q, cells,
                        grad, tf, J, samples, shade_ctr, tile_samples);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = launch_flat_scan(J, nt, s)) != hipSuccess) return e;
-  if ((e = hipMemcpyAsync(J.h_total, J.total, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                          s)) != hipSuccess)
+  const unsigned long long kNoLimit = ~0ull;
+  // (debug_flat_limit: a smaller capacity, to exercise the device-side fallback)
+  const unsigned long long lim = c.debug_flat_limit > 0 ? (unsigned long long)c.debug_flat_limit : kNoLimit;
+  if ((e = launch_flat_scan(J, nt, first ? kNoLimit : std::min<unsigned long long>(J.cap, lim),
+                            first ? kNoLimit : J.rcap, shade_ctr, s)) != hipSuccess)
     return e;
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-  const unsigned long long total = J.h_total[0], rounds = J.h_total[1];
-  if (total > 0) {
-    if (flat_reserve(J, nt, (size_t)total, (size_t)rounds) != hipSuccess) {
+  if (first) {
+    if ((e = hipMemcpyAsync(J.h_total, J.total, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                            s)) != hipSuccess)
+      return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const unsigned long long total = J.h_total[0], rounds = J.h_total[1];
+    J.want_jobs = (size_t)total;
+    J.want_rounds = (size_t)rounds;
+    if (flat_reserve(J, nt, std::max<size_t>((size_t)total, 1), std::max<size_t>((size_t)rounds, 1)) !=
+        hipSuccess) {
       // more jobs than 32-bit offsets or the free memory hold: the per-wave kernel
       // renders the same frame, bit for bit, without a job list
       (void)hipGetLastError();
@@ -395,34 +433,47 @@ hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool pho
         return e;
       return launch_shaded_march<SH>(c, q, phong, data, out, samples, shade_ctr, tile_samples, s);
     }
-    if (phong)
-      hipLaunchKernelGGL((shaded_jobs_kernel<SH, true, true>), dim3(nt), dim3(64), lds, s, q, cells,
-                         grad, tf, J, nullptr, nullptr, nullptr);
-    else
-      hipLaunchKernelGGL((shaded_jobs_kernel<SH, false, true>), dim3(nt), dim3(64), lds, s, q, cells,
-                         grad, tf, J, nullptr, nullptr, nullptr);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    const unsigned long long nch = (total + 63) / 64;
-    if (nch > (1ull << 30)) return hipErrorInvalidValue;
-    const int nchunks = (int)nch, group = c.flat_group;
-    const long long span = 8LL * group;                           // chunks per round of the XCDs
-    const long long nb = (nchunks + span - 1) / span * span;      // every XCD gets whole groups
-    if (phong)
-      hipLaunchKernelGGL((flat_shade_kernel<SH, true>), dim3((unsigned)nb), dim3(64), 0, s, q, data, J,
-                         total, nchunks, group, shade_ctr);
-    else
-      hipLaunchKernelGGL((flat_shade_kernel<SH, false>), dim3((unsigned)nb), dim3(64), 0, s, q, data, J,
-                         total, nchunks, group, shade_ctr);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  return launch_flat_fold(q.a, J, out, s);
+  if (phong)
+    hipLaunchKernelGGL((shaded_jobs_kernel<SH, true, true>), dim3(nt), dim3(64), lds, s, q, cells,
+                       grad, tf, J, nullptr, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL((shaded_jobs_kernel<SH, false, true>), dim3(nt), dim3(64), lds, s, q, cells,
+                       grad, tf, J, nullptr, nullptr, nullptr);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // the shade grid covers the set's capacity; blocks past the frame's total exit
+  const unsigned long long nch = ((unsigned long long)J.cap + 63) / 64;
+  if (nch > (1ull << 30)) return hipErrorInvalidValue;
+  const int nchunks = (int)nch, group = c.flat_group;
+  const long long span = 8LL * group;                           // chunks per round of the XCDs
+  const long long nb = (nchunks + span - 1) / span * span;      // every XCD gets whole groups
+  if (phong)
+    hipLaunchKernelGGL((flat_shade_kernel<SH, true>), dim3((unsigned)nb), dim3(64), 0, s, q, data, J,
+                       nchunks, group, shade_ctr);
+  else
+    hipLaunchKernelGGL((flat_shade_kernel<SH, false>), dim3((unsigned)nb), dim3(64), 0, s, q, data, J,
+                       nchunks, group, shade_ctr);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = launch_flat_fold(q.a, J, out, s)) != hipSuccess) return e;
+  // the device-side fallback: renders the frame only if its list did not fit
+  if ((e = launch_shaded_march<SH>(c, q, phong, data, out, samples, shade_ctr, tile_samples, s,
+                                   J.total)) != hipSuccess)
+    return e;
+  if (!first) {
+    if ((e = hipMemcpyAsync(J.h_total, J.total, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                            s)) != hipSuccess)
+      return e;
+    if ((e = hipEventRecord(J.ev_read, s)) != hipSuccess) return e;
+    J.pending_read = true;
+  }
+  return hipEventRecord(J.ev_done, s);
 }
 
 template <class SH>
 hipError_t launch_shaded_march(const Ctx& c, const typename SH::Args& q, bool phong,
                                typename SH::Data data, float4* out, uint32_t* samples,
                                unsigned long long* shade_ctr, unsigned long long* tile_samples,
-                               hipStream_t s) {
+                               hipStream_t s, const unsigned long long* run_if) {
   if (q.a.ntiles <= 0) return hipSuccess;
   if (q.a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
   const size_t lds = (size_t)(q.a.tf_n + 2) * sizeof(float4);
@@ -430,11 +481,11 @@ hipError_t launch_shaded_march(const Ctx& c, const typename SH::Args& q, bool ph
   if (phong)
     hipLaunchKernelGGL((shaded_march_kernel<SH, true>), dim3(q.a.ntiles), dim3(64), lds, s, q,
                        cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, data, out, samples,
-                       shade_ctr, tile_samples);
+                       shade_ctr, tile_samples, run_if);
   else
     hipLaunchKernelGGL((shaded_march_kernel<SH, false>), dim3(q.a.ntiles), dim3(64), lds, s, q,
                        cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, data, out, samples,
-                       shade_ctr, tile_samples);
+                       shade_ctr, tile_samples, run_if);
   return hipGetLastError();
 }
 

@@ -366,6 +366,19 @@ cvr_status  cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n
 /* Copy the float SAT back (x-fastest); out = NULL: dims only. */
 cvr_status  cvr_copy_extinction_sat(cvr_ctx* ctx, float* out, size_t capacity, int dims[3]);
 
+/* Host check of the SAT fetch addressing (no device work): for a SAT of
+ * sat_dims = (W+2, H+2, D+2) texels in `layout` (0 = cell4 copy, 1 = the plain
+ * float SAT; option "sat_layout"), evaluates every load of a fetch at every
+ * clamped corner texel with the kernels' own index arithmetic and reports
+ * out[0] = one past the last byte read, out[1] = bytes the library allocates
+ * for that layout, out[2] = 1 if any 24-bit operand or 32-bit index would
+ * wrap, out[3] = 1 if the addressing is safe (out[0] <= out[1] and no wrap).
+ * pad_planes < 0 = the library's padding; >= 0 evaluates another padding (the
+ * round-3 variant's one plane: tests/test_ebs.py).  No reference counterpart:
+ * the reference samples the SAT through a GL texture (ebsrenderer.cpp:700-716). */
+cvr_status  cvr_sat_layout_check(const int sat_dims[3], int layout, int pad_planes,
+                                 unsigned long long out[4]);
+
 /* One extinction-based shading frame: the ray-march with each sample shaded by
  * a SAT ambient occlusion and a SAT box-chain shadow.  Needs
  * cvr_set_extinction_sat. */

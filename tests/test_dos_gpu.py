@@ -257,3 +257,98 @@ def test_dosct_flat_equals_per_wave(dev, bonsai_tf, bonsai_tf_rgba, name):
     finally:
         L.cvr_set_option(dev.handle, b"shade_flat", 1)
         L.cvr_set_option(dev.handle, b"flat_group", 8)
+
+
+def _dos_params(occ, sdw, step, apply_shadow=True):
+    p = N.DosParams()
+    p.step = step
+    p.ka, p.kd, p.ks, p.shininess = 0.5, 0.5, 0.8, 30.0
+    p.ispecular[:] = [1.0, 1.0, 1.0]
+    for k in ("position", "forward", "up", "right"):
+        getattr(p.light, k)[:] = list(LIGHT0[k])
+    p.light.spot_angle_deg = LIGHT0["spot_angle_deg"]
+    p.apply_occlusion, p.apply_shadow, p.shadow_type = 1, int(apply_shadow), 0
+    p.occlusion, p.shadow = occ, sdw
+    return p
+
+
+FAR = dict(eye=(700.0, 600.0, 1400.0), center=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0))
+
+
+def test_dosct_flat_fallback_and_growth(dev, bonsai_tf, bonsai_tf_rgba):
+    """The flat pipeline without host round trips (shaded_march.h launch_shaded_flat): a
+    stream's job-list set is sized from its earlier frames' totals; a frame with more jobs
+    than the set holds is rendered by the per-wave kernel, chosen on the device, and the
+    set grows for the frames after it.  Every frame equals the per-wave kernel bit for
+    bit: far view (sizes the set), near view (does not fit: fallback), near again (grown),
+    and near with debug_flat_limit = 1 (fallback forced)."""
+    n = 48
+    vol = D.marschner_lobb_u8(n)
+    scale = D.voxel_scale(n)
+    setup(dev, vol, scale, bonsai_tf, bonsai_tf_rgba, (64, 64, 64))
+    occ, sdw = default_cone_params(True), default_cone_params(False)
+    W, H = 96, 80
+    step = 0.5 / math.sqrt(3.0)
+    L = N.lib()
+    try:
+        L.cvr_set_option(dev.handle, b"shade_flat", 0)
+        ref = {k: gpu_dos(dev, cam, W, H, step, occ, sdw, apply_shadow=True)
+               for k, cam in (("far", FAR), ("near", INITIAL))}
+        assert ref["near"][0][..., 3].sum() > 4 * ref["far"][0][..., 3].sum()
+        L.cvr_set_option(dev.handle, b"shade_flat", 1)
+        d2 = Device(0)   # a fresh context: its stream's set starts empty
+        try:
+            setup(d2, vol, scale, bonsai_tf, bonsai_tf_rgba, (64, 64, 64))
+            caps = []
+            for k, lim in (("far", 0), ("near", 0), ("near", 0), ("far", 0), ("near", 1)):
+                N.check(L.cvr_set_option(d2.handle, b"debug_flat_limit", lim), "limit")
+                got = gpu_dos(d2, FAR if k == "far" else INITIAL, W, H, step, occ, sdw,
+                              apply_shadow=True)
+                assert_bitexact(got[1], ref[k][1], f"{k} counts (limit {lim})")
+                assert_bitexact(got[0], ref[k][0], f"{k} rgba (limit {lim})")
+                assert got[2] == ref[k][2]
+                caps.append(L.cvr_get_option(d2.handle, b"flat_cap_kjobs"))
+            assert caps[2] > caps[1] >= caps[0] > 0, caps   # grew after the near frame
+        finally:
+            d2.close()
+    finally:
+        L.cvr_set_option(dev.handle, b"shade_flat", 1)
+
+
+def test_dosct_frames_in_flight_on_streams(bonsai_tf, bonsai_tf_rgba):
+    """Device outputs on three render streams, frames submitted back to back with no
+    host synchronisation in between (each stream has its own job-list set): every frame
+    equals the per-wave kernel's image of its view bit for bit."""
+    import torch
+    n = 48
+    vol = D.marschner_lobb_u8(n)
+    scale = D.voxel_scale(n)
+    dev = Device(0)
+    setup(dev, vol, scale, bonsai_tf, bonsai_tf_rgba, (64, 64, 64))
+    occ, sdw = default_cone_params(True), default_cone_params(False)
+    W, H = 96, 80
+    step = 0.5 / math.sqrt(3.0)
+    cams = [INITIAL, FAR, dict(eye=(-300.0, 120.0, 420.0), center=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0))]
+    L = N.lib()
+    L.cvr_set_option(dev.handle, b"shade_flat", 0)
+    ref = [gpu_dos(dev, c, W, H, step, occ, sdw, apply_shadow=True)[0] for c in cams]
+    L.cvr_set_option(dev.handle, b"shade_flat", 1)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    p = _dos_params(occ, sdw, step)
+    # the images are zeroed on torch's stream: let that finish before the renders
+    outs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(12)]
+    torch.cuda.synchronize()
+    try:
+        for i in range(12):
+            s = streams[i % 3]
+            img = outs[i]
+            dev.set_stream(s.cuda_stream)
+            frame = make_frame(Camera(**cams[i % 3]), W, H)
+            o = N.Output(img.data_ptr(), None, None, 1)
+            N.check(L.cvr_render_dosct(dev.handle, ctypes.byref(frame), ctypes.byref(p),
+                                       ctypes.byref(o)), "render", dev.handle)
+        torch.cuda.synchronize()
+        for i, img in enumerate(outs):
+            assert_bitexact(img.cpu().numpy(), ref[i % 3], f"frame {i} (stream {i % 3})")
+    finally:
+        dev.close()

@@ -88,3 +88,46 @@ def test_sat_planes_stream_equals_build(oracle, shape, bpv):
     zs = sorted({0, 1, 2, shape[0] // 2, shape[0], shape[0] + 1})
     got = oracle.sat_planes(vox, lut, zs)
     assert np.array_equal(got.view(np.uint32), full[zs].view(np.uint32))
+
+
+def _sat_check(dims, layout, pad=-1):
+    import ctypes
+    o = (ctypes.c_ulonglong * 4)()
+    d = (ctypes.c_int * 3)(*dims)
+    assert N.lib().cvr_sat_layout_check(d, layout, pad, o) == 0
+    return list(o)
+
+
+def test_sat_layout_check_round3_fault():
+    """Round 3's plain-SAT variant (one zero plane of padding) read w + 1 floats past its
+    allocation at the clamped far corner (w-1, h-1, d-1): its +1 row of the +1 plane.  At
+    the 1026^3 SAT of config 5 that is 4108 B, more than a 4 KiB page, so the read always
+    left the allocation's last page; at toy sizes it stayed inside the rounding slack.
+    The library's layout pads kSatPlainPadPlanes = 2 planes; the cell4 copy reads inside
+    its d + 1 planes."""
+    end, alloc, wrap, ok = _sat_check((1026, 1026, 1026), 1, pad=1)
+    assert not ok and not wrap and end - alloc == 4 * (1026 + 1) == 4108
+    end, alloc, wrap, ok = _sat_check((42, 42, 42), 1, pad=1)
+    assert not ok and end - alloc == 4 * 43 < 4096        # inside a page: no fault at toy sizes
+    for layout in (0, 1):
+        end, alloc, wrap, ok = _sat_check((1026, 1026, 1026), layout)
+        assert ok and not wrap and end <= alloc
+    # the plain SAT at 1026^3 reads past 2^32 bytes: 64-bit addresses (global loads), not
+    # 32-bit buffer offsets
+    assert _sat_check((1026, 1026, 1026), 1)[0] > 2 ** 32
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_sat_layout_check_random_dims(seed):
+    """Every SAT the library accepts (sides <= 4096, < 2^31 texels) addresses safely in both
+    layouts: no 24-bit operand or 32-bit index wraps, nothing is read past the allocation."""
+    rng = np.random.default_rng(seed)
+    for _ in range(200):
+        w, h = rng.integers(3, 4097, size=2)
+        dmax = min(4096, (2 ** 31 - 1) // (int(w) * int(h)))
+        if dmax < 3:
+            continue
+        d = int(rng.integers(3, dmax + 1))
+        for layout in (0, 1):
+            end, alloc, wrap, ok = _sat_check((int(w), int(h), d), layout)
+            assert ok and not wrap and end <= alloc, (w, h, d, layout, end, alloc)

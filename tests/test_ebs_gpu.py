@@ -224,3 +224,107 @@ def test_ebs_flat_equals_per_wave(dev, bonsai_tf, name):
     finally:
         L.cvr_set_option(dev.handle, b"shade_flat", 1)
         L.cvr_set_option(dev.handle, b"flat_group", 8)
+
+
+def test_ebs_flat_fallback_growth_and_streams(bonsai_tf):
+    """EBS through the flat pipeline without host round trips: a far view sizes the
+    stream's set, a near view does not fit (device-side per-wave fallback), the set grows;
+    then frames on three streams in flight with device outputs.  All bit-exact with the
+    per-wave kernel."""
+    import torch
+    n = 40
+    vol = D.marschner_lobb_u8(n)
+    scale = D.voxel_scale(n)
+    far = dict(eye=(700.0, 600.0, 1400.0), center=(0.0, 0.0, 0.0), up=(0.0, 1.0, 0.0))
+    cams = [far, INITIAL, INITIAL, far]
+    W, H = 80, 64
+    L = N.lib()
+    d = Device(0)
+    try:
+        gpu_sat(d, vol, scale)
+        d.set_transfer_function(bonsai_tf)
+        p = ebs_params(step=0.5 / math.sqrt(3.0))
+        L.cvr_set_option(d.handle, b"shade_flat", 0)
+        ref = [gpu_ebs(d, c, W, H, p) for c in (far, INITIAL)]
+        L.cvr_set_option(d.handle, b"shade_flat", 1)
+        for i, c in enumerate(cams):
+            got = gpu_ebs(d, c, W, H, p)
+            r = ref[0] if c is far else ref[1]
+            assert_bitexact(got[1], r[1], f"frame {i} counts")
+            assert_bitexact(got[0], r[0], f"frame {i} rgba")
+            assert got[2] == r[2]
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        # the images are zeroed on torch's stream: let that finish before the renders
+        outs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(9)]
+        torch.cuda.synchronize()
+        for i in range(9):
+            img = outs[i]
+            d.set_stream(streams[i % 3].cuda_stream)
+            frame = make_frame(Camera(**cams[i % 2]), W, H)
+            o = N.Output(img.data_ptr(), None, None, 1)
+            N.check(L.cvr_render_extbsd(d.handle, ctypes.byref(frame), ctypes.byref(p),
+                                        ctypes.byref(o)), "render", d.handle)
+        torch.cuda.synchronize()
+        for i, img in enumerate(outs):
+            assert_bitexact(img.cpu().numpy(), ref[0 if i % 2 == 0 else 1][0], f"stream frame {i}")
+    finally:
+        d.close()
+
+
+@pytest.mark.parametrize("name", ["defaults_point", "phong", "directional", "ragged_inside", "cone_60"])
+def test_ebs_sat_layouts_bitexact(dev, bonsai_tf, name):
+    """The frame read from the plain float SAT (sat_layout 1, its clamped +1 neighbours in
+    the zero padding) equals the cell4 copy's frame bit for bit, flat and per-wave, and
+    switching back rebuilds the copy."""
+    c = dict(EBS_CASES[name])
+    n = 40
+    vol = D.marschner_lobb_u8(n)
+    scale = D.voxel_scale(n)
+    W, H = c.pop("W", 80), c.pop("H", 64)
+    cam = c.pop("cam", INITIAL)
+    gpu_sat(dev, vol, scale)
+    dev.set_transfer_function(bonsai_tf)
+    dev.set_gradient(1 if c.get("phong", False) else 0)
+    p = ebs_params(step=0.5 / math.sqrt(3.0), **c)
+    L = N.lib()
+    try:
+        for flat in (1, 0):
+            L.cvr_set_option(dev.handle, b"shade_flat", flat)
+            L.cvr_set_option(dev.handle, b"sat_layout", 0)
+            ref = gpu_ebs(dev, cam, W, H, p)
+            N.check(L.cvr_set_option(dev.handle, b"sat_layout", 1), "sat_layout", dev.handle)
+            got = gpu_ebs(dev, cam, W, H, p)
+            assert_bitexact(got[1], ref[1], f"{name} counts (flat {flat})")
+            assert_bitexact(got[0], ref[0], f"{name} rgba (flat {flat})")
+            L.cvr_set_option(dev.handle, b"sat_layout", 0)
+            back = gpu_ebs(dev, cam, W, H, p)
+            assert_bitexact(back[0], ref[0], f"{name} rgba after switching back (flat {flat})")
+    finally:
+        L.cvr_set_option(dev.handle, b"shade_flat", 1)
+        L.cvr_set_option(dev.handle, b"sat_layout", 0)
+
+
+def test_ebs_sat_plain_layout_fresh_build(bonsai_tf):
+    """sat_layout 1 set before the build: no cell4 copy is made (device bytes), the frame
+    equals the cell4 build's, and the scratch can be dropped (sat_keep_scratch 0)."""
+    n = 36
+    vol = D.marschner_lobb_u8(n)
+    scale = D.voxel_scale(n)
+    p = ebs_params(step=0.5 / math.sqrt(3.0))
+    L = N.lib()
+    imgs = []
+    for layout in (0, 1):
+        d = Device(0)
+        try:
+            N.check(L.cvr_set_option(d.handle, b"sat_layout", layout), "sat_layout", d.handle)
+            N.check(L.cvr_set_option(d.handle, b"sat_keep_scratch", 0), "keep", d.handle)
+            gpu_sat(d, vol, scale)
+            d.set_transfer_function(bonsai_tf)
+            imgs.append(gpu_ebs(d, INITIAL, 64, 48, p))
+            gpu_sat(d, vol, scale)            # a rebuild after the scratch was freed
+            again = gpu_ebs(d, INITIAL, 64, 48, p)
+            assert_bitexact(again[0], imgs[-1][0], f"layout {layout} rebuild")
+        finally:
+            d.close()
+    assert_bitexact(imgs[1][0], imgs[0][0], "plain vs cell4 rgba")
+    assert_bitexact(imgs[1][1], imgs[0][1], "plain vs cell4 counts")

@@ -162,6 +162,17 @@ def test_c5_sat_and_ebs_1024(fresh_dev, oracle, bonsai_tf):
     _, e_cnt, e_S = oracle.render_rc1pass(v16, sc, bonsai_tf, INITIAL, W, W, step)
     assert_bitexact(g_cnt, e_cnt, "C5 full-frame counts")
     assert g_S == e_S
+    # the plain float SAT (sat_layout 1: no 17 GiB cell4 copy; its +1 reads at the far
+    # corner stay inside the padding, cvr_sat_layout_check): the same frame, bit for bit
+    from cpp_volume_rendering_amd import _native as N
+    N.check(N.lib().cvr_set_option(fresh_dev.handle, b"sat_layout", 1), "sat_layout", fresh_dev.handle)
+    try:
+        p_rgba, p_cnt, p_S = gpu_ebs(fresh_dev, INITIAL, W, W, p)
+        assert_bitexact(p_cnt, g_cnt, "C5 plain-SAT counts")
+        assert_bitexact(p_rgba, g_rgba, "C5 plain-SAT rgba")
+        assert p_S == g_S
+    finally:
+        N.lib().cvr_set_option(fresh_dev.handle, b"sat_layout", 0)
 
 
 def test_view_matrix_frame_equals_lookat_frame(fresh_dev, bonsai_tf):

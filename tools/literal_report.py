@@ -1,29 +1,98 @@
 #!/usr/bin/env python3
-"""Prints the CVR-SPEC vs literal-GLSL distances that tests/test_literal.py asserts
-(BASELINE.md gate: |dRGBA| <= 2e-3 for >= 99.9 % of pixels, max 2e-2, SSIM >= 0.99)."""
+"""CVR-SPEC vs the literal GLSL reading (oracle/glsl_literal.cpp) at BASELINE's config
+sizes, against BASELINE.md's gate (|dRGBA| <= 2e-3 for >= 99.9 % of pixels, max 2e-2,
+SSIM >= 0.99).  CPU only; writes the table as JSON (profiles/r04/literal_config_sizes.json).
+
+  rc1pass  512^3 / 1024^2 (config 2's march, the headline), full frame: float and 8-bit weights
+  phong    512^3 / 1024^2 (config 3), full frame: float weights, and CVR-SPEC-8 vs literal-8
+  dos      512^3 / 2048^2 (config 4), the 128-row centre band: cone AO + point-light shadows
+           (and CVR-SPEC-8 vs literal-8 when the oracle supports filter_bits for DOS)
+tests/test_literal.py asserts the same gate at the smaller sizes the CPU suite can afford."""
+import argparse
 import json
+import math
 import os
 import sys
+import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 import oracle as O  # noqa: E402
 import test_literal as T  # noqa: E402
 
 from cpp_volume_rendering_amd import datasets as D  # noqa: E402
+from cpp_volume_rendering_amd.renderer import default_cone_params  # noqa: E402
 
-t = O.tf_table_double(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA)
-tables = (t, O.tf_rgbt(t), O.tf_rgbt(t, extinction_input=True))
-out = {}
-vol, sc, v16, st = T._vol(O, 512)
-spec = O.render_rc1pass(v16, sc, tables[1], T.CAM, 1024, 1024, st)[0]
-for w in (0, 8):
-    lit = O.render_rc1pass(v16, sc, tables[1], T.CAM, 1024, 1024, st, literal=w)[0]
-    out[f"rc1pass_512_1024_w{w}"] = T.gate(spec, lit)
-vol, sc, v16, st = T._vol(O, 128)
-g = O.gradient(vol, "fd")
-kw = dict(grad=g, phong=True, light=D.LIGHT_LIST0_POSITION)
-a = O.render_rc1pass(v16, sc, tables[1], T.CAM, 512, 512, st, **kw)[0]
-b = O.render_rc1pass(v16, sc, tables[1], T.CAM, 512, 512, st, literal=0, **kw)[0]
-out["phong_128_512"] = T.gate(a, b)
-print(json.dumps(out, indent=1))
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="rc1pass,phong,dos")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04", "literal_config_sizes.json"))
+    a = ap.parse_args()
+    only = set(a.only.split(","))
+    t = O.tf_table_double(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA)
+    tables = (t, O.tf_rgbt(t), O.tf_rgbt(t, extinction_input=True))
+    out = {"gate": "max|dRGBA| <= 2e-2, <= 0.1 % of pixels over 2e-3, SSIM >= 0.99 (BASELINE.md)"}
+
+    def rec(name, a_, b_, **extra):
+        r = T.gate(a_, b_)
+        r["inside_gate"] = bool(r["frac_over"] <= 1e-3 and r["max"] <= 2e-2 and r["ssim"] >= 0.99)
+        r.update(extra)
+        out[name] = r
+        print(name, json.dumps(r), flush=True)
+
+    vol, sc, v16, st = T._vol(O, 512)
+    if "rc1pass" in only:
+        spec = O.render_rc1pass(v16, sc, tables[1], T.CAM, 1024, 1024, st)[0]
+        rec("rc1pass_512_1024_w0", spec,
+            O.render_rc1pass(v16, sc, tables[1], T.CAM, 1024, 1024, st, literal=0)[0], rows="full frame")
+        spec8 = O.render_rc1pass(v16, sc, tables[1], T.CAM, 1024, 1024, st, filter_bits=8)[0]
+        rec("rc1pass_512_1024_spec8_vs_lit8", spec8,
+            O.render_rc1pass(v16, sc, tables[1], T.CAM, 1024, 1024, st, literal=8)[0], rows="full frame")
+    if "phong" in only:
+        g = O.gradient(vol, "fd")
+        kw = dict(grad=g, phong=True, light=D.LIGHT_LIST0_POSITION)
+        t0 = time.time()
+        spec = O.render_rc1pass(v16, sc, tables[1], T.CAM, 1024, 1024, st, **kw)[0]
+        rec("phong_512_1024_w0", spec, O.render_rc1pass(v16, sc, tables[1], T.CAM, 1024, 1024, st,
+                                                        literal=0, **kw)[0], rows="full frame")
+        spec8 = O.render_rc1pass(v16, sc, tables[1], T.CAM, 1024, 1024, st, filter_bits=8, **kw)[0]
+        rec("phong_512_1024_spec8_vs_lit8", spec8,
+            O.render_rc1pass(v16, sc, tables[1], T.CAM, 1024, 1024, st, literal=8, **kw)[0],
+            rows="full frame", seconds=round(time.time() - t0, 1))
+        del g
+    if "dos" in only:
+        W = 2048
+        rows = (W // 2 - 64, W // 2 + 64)
+        levels = O.ext_volume(v16, sc, tables[2], (128, 128, 128))
+        diag = math.sqrt(sum((512 * s) ** 2 for s in sc))
+        occ = T._cones(default_cone_params(True), diag, 0.50)
+        sdw = T._cones(default_cone_params(False), diag, 0.75)
+        kw = dict(apply_shadow=True, shadow_type=0, light=T.LIGHT0, rows=rows)
+        t0 = time.time()
+        spec = O.render_dos(v16, sc, tables[1], levels, T.CAM, W, W, st, occ, sdw, **kw)[0]
+        lit = O.render_dos(v16, sc, tables[1], levels, T.CAM, W, W, st, occ, sdw, literal=0, **kw)[0]
+        rec("dos_512_2048_band128_w0", spec[rows[0]:rows[1]], lit[rows[0]:rows[1]],
+            rows=list(rows), seconds=round(time.time() - t0, 1))
+        try:
+            spec8 = O.render_dos(v16, sc, tables[1], levels, T.CAM, W, W, st, occ, sdw,
+                                 filter_bits=8, **kw)[0]
+        except TypeError:
+            spec8 = None
+        if spec8 is not None:
+            lit8 = O.render_dos(v16, sc, tables[1], levels, T.CAM, W, W, st, occ, sdw, literal=8, **kw)[0]
+            rec("dos_512_2048_band128_spec8_vs_lit8", spec8[rows[0]:rows[1]], lit8[rows[0]:rows[1]],
+                rows=list(rows))
+    prev = {}
+    if os.path.exists(a.out):
+        with open(a.out) as f:
+            prev = json.load(f)
+    prev.update(out)
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(prev, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
