@@ -336,9 +336,17 @@ def cone_fetches(r, n, scale):
     return out
 
 
-def load_pmc(path, workload_key):
-    """The PMC record (tools/pmc_traffic.py, tools/pmc_bench.sh) of this exact workload:
-    `path` or any profiles/pmc_<renderer>*.json beside it; {} if none."""
+def lib_sha16():
+    """The running libcvr.so's build: the first 16 hex digits of its sha256."""
+    import hashlib
+    with open(N.lib()._name, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_pmc(path, workload_key, kernel, sha):
+    """The PMC record (tools/pmc_record.py) of this exact workload, dominant kernel and
+    library build: `path` or any profiles/pmc_<renderer>*.json beside it; {} if none.
+    A record counted on another build or kernel is not this run's and is never used."""
     import glob
     stem = os.path.splitext(path)[0]
     for f in [path] + sorted(glob.glob(stem + "_*.json")):
@@ -347,14 +355,10 @@ def load_pmc(path, workload_key):
                 d = json.load(fh)
         except (OSError, ValueError):
             continue
-        if d.get("workload_key") == workload_key:
+        if (d.get("workload_key") == workload_key and d.get("kernel") == kernel
+                and d.get("lib_sha16") == sha):
             return d
     return {}
-
-
-def load_traffic(path, workload_key):
-    """HBM bytes per launch measured by PMC for this exact workload (or None)."""
-    return load_pmc(path, workload_key).get("hbm_bytes_per_launch")
 
 
 def postpass_bench(r, dev, W, H, reps):
@@ -661,19 +665,24 @@ def main():
                  "shaded_march_kernel<EbsShader>" if ebs else
                  f"iso_tile_kernel<{iso_variant}, {str(a.phong).lower()}>" if iso else
                  f"rc1pass_tile_kernel<{batch}, {str(a.phong).lower()}, *, false, true, *>")
-        # EBS moves ~2 TB of SAT corners per frame through the vector-memory pipe, far
-        # above what HBM could serve at this frame time: its roofline is the L2's, and
-        # the HBM figures (PMC traffic) are reported beside it
-        peak = L2_PEAK_GBS if ebs else HBM_PEAK_GBS
-        roof = {"bound": "l2" if ebs else "hbm", "achieved": round(achieved, 1), "peak": peak,
+        # DOS and EBS move their secondary fetches (DOS: 85 GB of pyramid corners per
+        # frame, a 37 MiB pyramid; EBS: ~2 TB of SAT corners) through the vector-memory
+        # pipe from L1/L2/MALL, far above what HBM could serve at these frame times:
+        # their roofline is the L2's, with the HBM figures (PMC traffic) beside it
+        peak = L2_PEAK_GBS if shaded else HBM_PEAK_GBS
+        sha = lib_sha16()
+        pmc = load_pmc(a.pmc.replace("rc1pass", a.renderer), wkey, kname, sha)
+        roof = {"bound": "l2" if shaded else "hbm", "achieved": round(achieved, 1), "peak": peak,
                 "unit": "GB/s", "frac": round(achieved / peak, 4),
-                "traffic": load_traffic(a.pmc.replace("rc1pass", a.renderer), wkey),
+                "traffic": pmc.get("hbm_bytes_per_launch"),
                 "kernel": kname,
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank,
                 # the same bytes over the frame time of the timed region (frames in
                 # flight overlap, so a frame takes less than one launch's duration)
                 "frac_frame": round(b_alg / (ms_per_step * 1e-3) / 1e9 / peak, 4)}
+        if shaded:
+            roof["alg_over_hbm_peak"] = round(achieved / HBM_PEAK_GBS, 4)
         if ebs:
             # the vector-memory pipe: 2 dwordx4 wave-loads (2 x 1 KiB) per 64 SAT fetches,
             # against 256 CUs x one 1-KiB wave-load per 16 clocks (64 B/clk per CU L1) at
@@ -683,11 +692,9 @@ def main():
             roof["vmem_dwordx4_per_s"] = round(vm, 1)
             roof["vmem_peak_dwordx4_per_s"] = vm_peak
             roof["vmem_frac"] = round(vm / vm_peak, 4)
-            roof["alg_over_hbm_peak"] = round(achieved / HBM_PEAK_GBS, 4)
-        # the counters of the same workload's dominant kernel (rocprofv3 --pmc, committed
-        # under profiles/): which pipe is busy, VALU per sample, the bytes written (for
-        # the headline: the frame + ~8 MB of the 8-wave budget's 2 spilled VGPRs)
-        pmc = load_pmc(a.pmc.replace("rc1pass", a.renderer), wkey)
+        # the counters of the same workload's dominant kernel on this library build
+        # (rocprofv3 --pmc, committed under profiles/): which pipe is busy, VALU per
+        # sample, the bytes written
         if pmc.get("td_busy_frac_per_cu") is not None:
             roof["pmc"] = {"td_busy_per_cu": round(pmc["td_busy_frac_per_cu"], 3),
                            "ta_busy_per_cu": round(pmc["ta_busy_frac_per_cu"], 3),
@@ -699,6 +706,8 @@ def main():
             if a.renderer == "rc1pass" and not a.phong:
                 roof["pmc"]["scratch_bytes_per_launch_est"] = max(
                     0, int(pmc["write_bytes_per_launch"]) - px_bytes * pixels)
+            roof["pmc"]["kernel_ns_under_pmc"] = pmc.get("kernel_ns_avg_under_pmc")
+            roof["pmc"]["record"] = f"profiles/pmc_{a.renderer}*.json, lib {sha}"
         if roof["traffic"]:
             # the bytes HBM actually served (PMC) at the kernel's own time: where the
             # algorithmic figure is mostly served from L1/L2 (frac > 1 for EBS), this
@@ -771,6 +780,7 @@ def main():
                                    + ("" if iso else ", step 0.5, ERT 0.99")
                                    + (", Blinn-Phong FD gradient" if a.phong else ""),
                        "volume": n, "viewport": [W, H], "samples_per_frame": S_all,
+                       "workload_key": wkey, "lib_sha16": sha,
                        "settle_frames": settle,
                        "parallelism": f"screen tiles {tile}x{tile} over {world} GPU(s)"
                                       if world > 1 else "1 GPU",
