@@ -1363,8 +1363,7 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_dosct: null argument");
-  if (c->filter_bits)
-    return fail(c, CVR_ERR_ARG, "cvr_render_dosct: filter_bits %d is implemented for cvr_render_rc1pass only", c->filter_bits);
+
   if (o->format != CVR_FORMAT_RGBA32F && o->format != CVR_FORMAT_RGBA16F)
     return fail(c, CVR_ERR_ARG, "cvr_render_dosct: unknown output format %d", o->format);
   if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
@@ -1412,6 +1411,13 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   int ntiles = 0;
   size_t npix = 0;
   fill_frame_args(c, f, p->step, Q.a, ntiles, npix);
+  Q.a.filter_bits = c->filter_bits;   // GL_LINEAR weights of every fetch (CVR-SPEC-8 at 8)
+  if (c->cell_skip > 0) {   // the per-cell skip flags in the count / emit march
+    cvr_status st = ensure_cell_flags(c);
+    if (st != CVR_OK) return st;
+    Q.a.cell_skip = 1;
+    Q.a.inv_step = 1.0f / Q.a.step;
+  }
   Q.a.out_half = o->format == CVR_FORMAT_RGBA16F;
   Q.a.ka = p->ka;   // Phong ambient/diffuse/specular weights of the surface term
   Q.a.kd = p->kd;
@@ -1621,8 +1627,9 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: null argument");
-  if (c->filter_bits)
-    return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: filter_bits %d is implemented for cvr_render_rc1pass only", c->filter_bits);
+  if (c->filter_bits && c->sat_layout != 0)
+    return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: filter_bits %d needs sat_layout 0 (the cell4 copy)",
+                c->filter_bits);
   if (o->format != CVR_FORMAT_RGBA32F && o->format != CVR_FORMAT_RGBA16F)
     return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: unknown output format %d", o->format);
   if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
@@ -1650,6 +1657,13 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
   int ntiles = 0;
   size_t npix = 0;
   fill_frame_args(c, f, p->step, Q.a, ntiles, npix);
+  Q.a.filter_bits = c->filter_bits;   // GL_LINEAR weights of every fetch (CVR-SPEC-8 at 8)
+  if (c->cell_skip > 0) {   // the per-cell skip flags in the count / emit march
+    cvr_status st = ensure_cell_flags(c);
+    if (st != CVR_OK) return st;
+    Q.a.cell_skip = 1;
+    Q.a.inv_step = 1.0f / Q.a.step;
+  }
   Q.a.out_half = o->format == CVR_FORMAT_RGBA16F;
   Q.a.ka = p->ka; Q.a.kd = p->kd; Q.a.ks = p->ks;
   Q.a.shininess = p->shininess;

@@ -222,6 +222,7 @@ __device__ __forceinline__ ExtLevel load_level(const ExtLevel* lv, int L) {
 #endif
 }
 
+template <int FB>   // FB: GL_LINEAR weights at FB fraction bits (filter_bits; 0 = exact)
 __device__ __forceinline__ ExtTap ext_tap(const ExtLevel& l, f3 p) {
   const float x = __builtin_amdgcn_fmed3f(fmaf(p.x, l.sx, -0.5f), 0.0f, l.mx);
   const float y = __builtin_amdgcn_fmed3f(fmaf(p.y, l.sy, -0.5f), 0.0f, l.my);
@@ -230,9 +231,9 @@ __device__ __forceinline__ ExtTap ext_tap(const ExtLevel& l, f3 p) {
   // dims <= 2^12 and < 2^28 cells in all (checked on the host): 24-bit multiplies
   const uint32_t row = __umul24((uint32_t)z, (uint32_t)l.dy) + (uint32_t)y;
   t.off = (__umul24(row, (uint32_t)l.dx) + (uint32_t)x + (uint32_t)l.off) << 4;
-  t.ax = __builtin_amdgcn_fractf(x);
-  t.ay = __builtin_amdgcn_fractf(y);
-  t.az = __builtin_amdgcn_fractf(z);
+  t.ax = filter_weight<FB>(__builtin_amdgcn_fractf(x));
+  t.ay = filter_weight<FB>(__builtin_amdgcn_fractf(y));
+  t.az = filter_weight<FB>(__builtin_amdgcn_fractf(z));
   return t;
 }
 
@@ -289,7 +290,7 @@ __device__ __forceinline__ float4 load_section(const float4* sec, int i) {
 }
 typedef const float4* ConstSections;
 
-template <int J, int U, int J0 = 0, int JN = J>
+template <int J, int U, int J0, int JN, int FB>
 __device__ __forceinline__ void cone_sections(const DosArgs& Q, const DosCone& C,
                                               const uint4* __restrict__ ext, const float4 (&e)[U],
                                               const float (&tr)[U], const f3 (&vk)[J], f3 pos,
@@ -304,7 +305,7 @@ __device__ __forceinline__ void cone_sections(const DosArgs& Q, const DosCone& C
 #pragma unroll
     for (int j = 0; j < JN; j++) {
       const f3 p = vmad(vk[J0 + j], tr[q], pos);
-      tap[q][j] = ext_tap(l, p);
+      tap[q][j] = ext_tap<FB>(l, p);
       // The border exponent is -0 inside the box, so "outside" is xb < 0: a tap
       // outside whose exponent is still -0 (a distance that underflows) gets the
       // factor exp(-0) = 1 exactly, the inside value (no 6-compare box test)
@@ -339,7 +340,7 @@ __device__ __forceinline__ void cone_sections(const DosArgs& Q, const DosCone& C
 
 // U sections of a J-ray stage starting at table entry s (uniform).  The 7-ray
 // stage is split 4 + 3 rays to bound the fetches (registers) in flight.
-template <int J, int U>
+template <int J, int U, int FB>
 __device__ __forceinline__ void cone_step(const DosArgs& Q, const DosCone& C,
                                           const uint4* __restrict__ ext, ConstSections sec, int s,
                                           float& track, const f3 (&vk)[J], f3 pos,
@@ -353,10 +354,10 @@ __device__ __forceinline__ void cone_step(const DosArgs& Q, const DosCone& C,
     track += e[q].x;
   }
   if (J == 7) {
-    cone_sections<J, U, 0, 4>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
-    cone_sections<J, U, 4, 3>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+    cone_sections<J, U, 0, 4, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+    cone_sections<J, U, 4, 3, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
   } else {
-    cone_sections<J, U>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+    cone_sections<J, U, 0, J, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
   }
 }
 
@@ -395,7 +396,7 @@ __device__ __forceinline__ bool ray_gone(const DosArgs& Q, const ConeStageExit& 
   return true;
 }
 
-template <int J, int U>
+template <int J, int U, int FB>
 __device__ __forceinline__ void cone_stage(const DosArgs& Q, const DosCone& C,
                                            const uint4* __restrict__ ext, ConstSections sec, int& s,
                                            int n, float& track, const f3 (&vk)[J], f3 pos,
@@ -403,7 +404,7 @@ __device__ __forceinline__ void cone_stage(const DosArgs& Q, const DosCone& C,
                                            const ConeStageExit& X) {
   int i = 0;
   for (; i + U <= n; i += U, s += U) {
-    cone_step<J, U>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last,
+    cone_step<J, U, FB>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last,
                     nf);
     if (X.nruns > 0 && i + U < n) {
       bool zero = true;
@@ -425,13 +426,14 @@ __device__ __forceinline__ void cone_stage(const DosArgs& Q, const DosCone& C,
     }
   }
   for (; i < n; i++, s++)
-    cone_step<J, 1>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last,
+    cone_step<J, 1, FB>(Q, C, ext, sec, __builtin_amdgcn_readfirstlane(s), track, vk, pos, rays, last,
                     nf);
 }
 
 // Cone1/3/7 RayOcclusion and Cone1/3/7 RayShadow (the same accumulation): the
 // visibility exp(-sum) of a cone from `pos` along k, split 1 -> 3 -> 7 rays.
 // Every lane walks the same section table (wave-uniform loads and levels).
+template <int FB>
 __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __restrict__ ext,
                             f3 pos, f3 k, f3 u, f3 v, uint32_t& nf) {
   float rays[7], last[7];
@@ -442,7 +444,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
   int s = 0;
   {
     const f3 vk[1] = {k};
-    cone_stage<1, 4>(Q, C, ext, sec, s, C.counts[0], track, vk, pos, rays, last, nf, C.exit[0]);
+    cone_stage<1, 4, FB>(Q, C, ext, sec, s, C.counts[0], track, vk, pos, rays, last, nf, C.exit[0]);
   }
   if (C.counts[1] + C.counts[2] == 0) return cvr_expf(-rays[0]);
   rays[2] = rays[0]; rays[1] = rays[0];
@@ -451,7 +453,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
     f3 vk[3];
 #pragma unroll
     for (int j = 0; j < 3; j++) vk[j] = cone_axis(C.axes + 3 * j, k, u, v);
-    cone_stage<3, 2>(Q, C, ext, sec, s, C.counts[1], track, vk, pos, rays, last, nf, C.exit[1]);
+    cone_stage<3, 2, FB>(Q, C, ext, sec, s, C.counts[1], track, vk, pos, rays, last, nf, C.exit[1]);
   }
   if (C.counts[2] == 0)
     return ((cvr_expf(-rays[0]) + cvr_expf(-rays[1])) + cvr_expf(-rays[2])) / 3.0f;
@@ -470,7 +472,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
     f3 vk[7];
 #pragma unroll
     for (int j = 0; j < 7; j++) vk[j] = cone_axis(C.axes + 3 * (3 + j), k, u, v);
-    cone_stage<7, 1>(Q, C, ext, sec, s, C.counts[2], track, vk, pos, rays, last, nf, C.exit[2]);
+    cone_stage<7, 1, FB>(Q, C, ext, sec, s, C.counts[2], track, vk, pos, rays, last, nf, C.exit[2]);
   }
   float side = cvr_expf(-rays[1]);
 #pragma unroll
@@ -488,8 +490,10 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
 #ifndef CVR_DOS_WAVES
 #define CVR_DOS_WAVES 3
 #endif
-struct DosShader {
+template <int FB>
+struct DosShaderT {
   using Args = DosArgs;
+  static constexpr int kFB = FB;   // GL_LINEAR weights of every fetch (filter_bits)
   // register budget: 3 waves/SIMD (168 VGPRs; the compiler alone takes 172 -> 2 waves):
   // kernel 21.1 -> 18.0 ms, 4 waves 18.8 ms (spills)
   static constexpr int kMinWavesPerEU = CVR_DOS_WAVES;
@@ -510,7 +514,7 @@ struct DosShader {
       const f3 v_right = normalize3(cross3(cam, f3{0.0f, 1.0f, 0.0f}));
       const f3 v_up = normalize3(cross3(f3{-cam.x, -cam.y, -cam.z}, v_right));
       const f3 k = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
-      iocc = cone_trace(Q, Q.occ, ext, tx, k, v_up, v_right, fetches);
+      iocc = cone_trace<FB>(Q, Q.occ, ext, tx, k, v_up, v_right, fetches);
     }
     if (Q.apply_shadow) {
       f3 k, u, v;
@@ -528,7 +532,7 @@ struct DosShader {
       }
       // Cone1RayShadow(pos, k, v, u) is called as (pos, k, u, v): swapped (:559-561)
       if (on) {
-        isdw = cone_trace(Q, Q.sdw, ext, tx, k, v, u, fetches);
+        isdw = cone_trace<FB>(Q, Q.sdw, ext, tx, k, v, u, fetches);
         lit++;
       }
     }
@@ -554,13 +558,19 @@ struct DosShader {
   }
 };
 
+template <class SH>
+static hipError_t launch_dos_fb(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,
+                                unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
+  if (c.shade_flat)
+    return launch_shaded_flat<SH>(c, q, q.phong != 0, c.d_ext_cells, out, samples, shade, tile_samples, s);
+  return launch_shaded_march<SH>(c, q, q.phong != 0, c.d_ext_cells, out, samples, shade, tile_samples, s);
+}
+
 hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
-  if (c.shade_flat)
-    return launch_shaded_flat<DosShader>(c, q, q.phong != 0, c.d_ext_cells, out, samples, shade,
-                                         tile_samples, s);
-  return launch_shaded_march<DosShader>(c, q, q.phong != 0, c.d_ext_cells, out, samples, shade,
-                                        tile_samples, s);
+  if (q.a.filter_bits == 8)   // GL texture-unit weights (CVR-SPEC-8)
+    return launch_dos_fb<DosShaderT<8>>(c, q, out, samples, shade, tile_samples, s);
+  return launch_dos_fb<DosShaderT<0>>(c, q, out, samples, shade, tile_samples, s);
 }
 
 }  // namespace cvr

@@ -33,6 +33,7 @@ namespace {
 //    repeated corner does: the same bits.
 struct SatCell4 {
   using Ptr = const float4*;
+  static constexpr int kFB = 0;   // GL_LINEAR weights at kFB fraction bits (filter_bits; 0 = exact)
   __device__ static __forceinline__ void corners(Ptr sat, uint32_t idx, uint32_t w, uint32_t pz,
                                                  float4& lo, float4& hi) {
     lo = sat[idx];
@@ -41,6 +42,7 @@ struct SatCell4 {
 };
 struct SatPlain {
   using Ptr = const float*;
+  static constexpr int kFB = 0;
   typedef float f2a __attribute__((ext_vector_type(2), aligned(4)));   // dwordx2 at 4-byte alignment
   __device__ static __forceinline__ void corners(Ptr sat, uint32_t idx, uint32_t w, uint32_t pz,
                                                  float4& lo, float4& hi) {
@@ -51,6 +53,13 @@ struct SatPlain {
     lo = make_float4(a.x, a.y, b.x, b.y);
     hi = make_float4(c.x, c.y, d.x, d.y);
   }
+};
+
+// A layout whose fetches round their GL_LINEAR weights to FB fraction bits
+// (option filter_bits, CVR-SPEC-8: as a GPU texture unit filters texture()).
+template <class Base, int FB>
+struct SatFB : Base {
+  static constexpr int kFB = FB;
 };
 
 // GetSummed3Density (:77-83): trilinear of the float SAT at u = p * inv_vol_scaled.
@@ -65,8 +74,9 @@ __device__ __forceinline__ float sat_fetch(const EbsArgs& Q, typename L::Ptr __r
                                        (uint32_t)Q.sat_dims[1]);
   float4 lo, hi;
   L::corners(sat, idx, (uint32_t)Q.sat_dims[0], Q.sat_pz, lo, hi);
-  const float ax = __builtin_amdgcn_fractf(tx), ay = __builtin_amdgcn_fractf(ty),
-              az = __builtin_amdgcn_fractf(tz);
+  const float ax = filter_weight<L::kFB>(__builtin_amdgcn_fractf(tx)),
+              ay = filter_weight<L::kFB>(__builtin_amdgcn_fractf(ty)),
+              az = filter_weight<L::kFB>(__builtin_amdgcn_fractf(tz));
   const float c00 = lerpf(lo.x, lo.y, ax), c10 = lerpf(lo.z, lo.w, ax);
   const float c01 = lerpf(hi.x, hi.y, ax), c11 = lerpf(hi.z, hi.w, ax);
   return lerpf(lerpf(c00, c10, ay), lerpf(c01, c11, ay), az);
@@ -162,14 +172,15 @@ __device__ __forceinline__ void shadow_half_issue(const EbsArgs& Q, typename L::
   }
 }
 
-template <int H>
+template <int H, int FB>
 __device__ __forceinline__ void shadow_half_finish(const SatBoxCoord& C, const float4 (&c)[8], float (&V)[4]) {
-  const float ay = __builtin_amdgcn_fractf(C.ty[H ? 0 : 1]);
+  const float ay = filter_weight<FB>(__builtin_amdgcn_fractf(C.ty[H ? 0 : 1]));
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int k = 4 * H + j;
     const int xi = (k & 1) ? 0 : 1, zi = (k & 2) ? 0 : 1;
-    const float ax = __builtin_amdgcn_fractf(C.tx[xi]), az = __builtin_amdgcn_fractf(C.tz[zi]);
+    const float ax = filter_weight<FB>(__builtin_amdgcn_fractf(C.tx[xi])),
+                az = filter_weight<FB>(__builtin_amdgcn_fractf(C.tz[zi]));
     const float4 lo = c[2 * j], hi = c[2 * j + 1];
     const float c00 = lerpf(lo.x, lo.y, ax), c10 = lerpf(lo.z, lo.w, ax);
     const float c01 = lerpf(hi.x, hi.y, ax), c11 = lerpf(hi.z, hi.w, ax);
@@ -208,7 +219,7 @@ __device__ __forceinline__ float shadow_chain(const EbsArgs& Q, typename L::Ptr 
   for (;;) {
     shadow_half_issue<1, L>(Q, sat, C, S);
     __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the lerps
-    shadow_half_finish<0>(C, F, V);
+    shadow_half_finish<0, L::kFB>(C, F, V);
     float sum = V[0] - V[1] - V[2] + V[3];
     const float wn = w + si;
     const bool more = cond(wn);
@@ -216,7 +227,7 @@ __device__ __forceinline__ float shadow_chain(const EbsArgs& Q, typename L::Ptr 
     const SatBoxCoord Cn = shadow_box_coord(Q, p1, p2, rS);
     shadow_half_issue<0, L>(Q, sat, Cn, F);
     __builtin_amdgcn_sched_barrier(0);
-    shadow_half_finish<1>(C, S, V);
+    shadow_half_finish<1, L::kFB>(C, S, V);
     sum = sum - V[0] + V[1] + V[2] - V[3];
     Stau += (sum / C.vq) * Q.ui_weight;
     boxes++;
@@ -403,6 +414,7 @@ struct EbsShaderT {
   static constexpr int kMinWavesPerEU = CVR_EBS_WAVES;   // register budget (1: compiler's choice)
   static constexpr int kFlatWavesPerEU = CVR_EBS_FLAT_WAVES;   // flat_shade_kernel
   using Data = typename LY::Ptr;   // the float SAT, cell4 or plain
+  static constexpr int kFB = LY::kFB;   // GL_LINEAR weights of every fetch (filter_bits)
 
   // ShadeSample (:498-550); `lit` counts the shadow box chains traced.
   __device__ static f3 shade(const EbsArgs& Q, typename LY::Ptr __restrict__ sat, f3 tx, f3 wp, f3,
@@ -468,6 +480,10 @@ static hipError_t launch_ebs_layout(const Ctx& c, const EbsArgs& q, typename L::
 
 hipError_t launch_ebs(const Ctx& c, const EbsArgs& q, float4* out, uint32_t* samples,
                       unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
+  if (q.a.filter_bits == 8)   // GL texture-unit weights (CVR-SPEC-8): the cell4 copy only
+    return c.sat_layout == 1 ? hipErrorInvalidValue
+                             : launch_ebs_layout<SatFB<SatCell4, 8>>(c, q, c.d_sat_cells, out, samples,
+                                                                     shade, tile_samples, s);
   if (c.sat_layout == 1)
     return launch_ebs_layout<SatPlain>(c, q, c.d_sat, out, samples, shade, tile_samples, s);
   return launch_ebs_layout<SatCell4>(c, q, c.d_sat_cells, out, samples, shade, tile_samples, s);

@@ -167,6 +167,9 @@ __device__ __forceinline__ int cell_skip_q(uint4 r) {
   return (int)((r.y >> 31) | ((r.z >> 31) << 1) | ((r.w >> 31) << 2));
 }
 constexpr int kCellSkipCap = 8;            // distances stored up to 8 (q <= 7)
+// The distance skip's margin in texels: absorbs the rounding of s and of the
+// sample positions (raymarch.hip march_ray, shaded_march.h shaded_jobs_kernel).
+constexpr float kSkipMarginTexels = 1.0f / 32.0f;
 
 // PK: the two y lerps as one packed subtract and one packed fma, per lane the
 // same two roundings as lerpf (the emission-absorption march: kernel -5 % with

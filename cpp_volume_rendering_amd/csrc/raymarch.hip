@@ -82,12 +82,11 @@ __device__ __forceinline__ bool skip_empty(const Rc1passArgs& A, const Ray& r, f
 //  * CS == 2: after a batch whose last sample lies in an empty cell at chessboard
 //    distance d >= 2 from any non-empty cell, the next m samples are counted and
 //    stepped over with the same s += h recurrence, without loads: m full steps
-//    move the position by at most m * step * max|dt| <= d - 1 - kSkipMargin
+//    move the position by at most m * step * max|dt| <= d - 1 - kSkipMarginTexels
 //    texels on every axis, so each of those samples lies in a cell within d - 1
 //    of the last one (all empty), and m stays 2 steps short of the ray's end, so
 //    every skipped h is the full step.
 // Both leave the image and the sample count bit for bit as the plain march.
-constexpr float kSkipMargin = 1.0f / 32.0f;   // texels: absorbs the rounding of s and positions
 
 template <int K, bool PHONG, bool SKIP, bool XF, int BUF, int FB, int CS>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
@@ -285,7 +284,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
         float dx = r.dt.x, dy = r.dt.y, dz = r.dt.z;
         asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
         const float kinv = __builtin_amdgcn_rcpf(step * fmaxf(fmaxf(fabsf(dx), fabsf(dy)), fabsf(dz)));
-        int m = min(cvt_flr(((float)qlast - kSkipMargin) * kinv), cvt_flr((D - s) * A.inv_step) - 2);
+        int m = min(cvt_flr(((float)qlast - kSkipMarginTexels) * kinv), cvt_flr((D - s) * A.inv_step) - 2);
         if (CS == 2) {   // each lane its own m
           if (m > 0) {
             cnt += (uint32_t)m;

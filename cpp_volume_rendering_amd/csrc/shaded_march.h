@@ -109,8 +109,9 @@ shaded_march_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
         const float tt = fmaf(h, 0.5f, s);
         const float x = fmaf(r.dt.x, tt, r.o.x), y = fmaf(r.dt.y, tt, r.o.y),
                     z = fmaf(r.dt.z, tt, r.o.z);
-        const SamplePos sp = wave_in_box ? sample_pos(x, y, z, A) : sample_pos_clamped(x, y, z, A);
-        const float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
+        SamplePos sp = wave_in_box ? sample_pos(x, y, z, A) : sample_pos_clamped(x, y, z, A);
+        if (SH::kFB) quantise_weights<SH::kFB>(sp);   // filter_bits: volume and gradient weights
+        const float4 sc = classify<SH::kFB>(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
         cnt++;
         if (sc.w > 0.0f) {
           const int slot = lane * kJobsPerLane + n;
@@ -258,16 +259,32 @@ shaded_jobs_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
   float s = 0.0f, dst_a = 0.0f;
   uint32_t cnt = 0, rounds = 0, tjobs = 0;   // rounds, tjobs: wave-uniform
   bool any_job = false;
+  const bool skip = A.cell_skip > 0;   // per-cell skip flags (march_common.h cell_empty)
   for (;;) {   // one sample per live lane per round (wave-uniform loop)
     if (__ballot(active) == 0) break;
     bool pushed = false;
     float4 q0, q1, q2;
+    float h = 0.0f, tt = 0.0f;
+    SamplePos sp;
+    uint4 raw;
+    bool empty = true;
     if (active) {
-      const float h = fminf(step, r.D - s);
-      const float tt = fmaf(h, 0.5f, s);
+      h = fminf(step, r.D - s);
+      tt = fmaf(h, 0.5f, s);
       const float x = fmaf(r.dt.x, tt, r.o.x), y = fmaf(r.dt.y, tt, r.o.y), z = fmaf(r.dt.z, tt, r.o.z);
-      const SamplePos sp = wave_in_box ? sample_pos(x, y, z, A) : sample_pos_clamped(x, y, z, A);
-      const float4 sc = classify(tfp, fn, trilerp_cell(cells[sp.idx], sp.ax, sp.ay, sp.az));
+      sp = wave_in_box ? sample_pos(x, y, z, A) : sample_pos_clamped(x, y, z, A);
+      raw = cells[sp.idx];
+      empty = cell_empty(raw);
+    }
+    // every marching lane's sample in an empty cell: tau is exactly 0 for all of
+    // them (no job, no alpha), so the round only counts and steps (bit-exact)
+    const bool wave_empty = skip && __ballot(!empty) == 0;
+    if (active) {
+      float4 sc = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!wave_empty) {
+        if (SH::kFB) quantise_weights<SH::kFB>(sp);   // filter_bits: volume and gradient weights
+        sc = classify<SH::kFB>(tfp, fn, trilerp_cell(raw, sp.ax, sp.ay, sp.az));
+      }
       cnt++;
       if (sc.w > 0.0f) {
         const float a = 1.0f - cvr_expf(-(sc.w * h));
@@ -288,6 +305,24 @@ shaded_jobs_kernel(typename SH::Args Q, const uint4* __restrict__ cells,
       if (active) {
         s = s + h;
         active = s < r.D;
+      }
+    }
+    // the distance skip of an all-empty round (raymarch.hip march_ray, CS 3): when
+    // every lane still marching sits in an empty cell at distance >= 2 from any
+    // occupied one, all of them step over the same number of samples without
+    // loads (the fewest any may: lanes stay at one sample index).  Skipped samples
+    // make no job and no round, so the job list and its masks are unchanged.
+    if (wave_empty && wave_in_box) {
+      const int q = active ? cell_skip_q(raw) : 0;
+      if (__ballot(active && q == 0) == 0 && __ballot(active) != 0 && active) {
+        float dx = r.dt.x, dy = r.dt.y, dz = r.dt.z;
+        asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
+        const float kinv = __builtin_amdgcn_rcpf(step * fmaxf(fmaxf(fabsf(dx), fabsf(dy)), fabsf(dz)));
+        const int msk = min(cvt_flr(((float)q - kSkipMarginTexels) * kinv),
+                            cvt_flr((r.D - s) * A.inv_step) - 2);
+        int i = 0;
+        for (; __all(i < msk); i++) s = s + step;
+        cnt += (uint32_t)i;
       }
     }
     const unsigned long long m = __ballot(pushed);

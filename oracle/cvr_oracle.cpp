@@ -652,6 +652,7 @@ namespace {
 struct ExtVol {
   const float* v; int res[3]; int nl; v3 G;
   std::vector<int64_t> off;
+  int wbits = 0;   // GL_LINEAR weights at this many fraction bits (filter_bits)
   // GetGaussianExtinction (:92-112): textureLod at an integer level, clamp-to-edge,
   // plus the CONSIDER_BORDERS attenuation outside the box
   float gge(v3 p, float mip) const {
@@ -659,7 +660,7 @@ struct ExtVol {
     L = std::min(std::max(L, 0), nl - 1);
     int d[3];
     ext_level_dims(res, L, d);
-    Tex t{v + off[L], {d[0], d[1], d[2]}, 1};
+    Tex t{v + off[L], {d[0], d[1], d[2]}, 1, wbits};
     // texel coordinate p/G*d - 0.5 as fma(p, d/G, -0.5) with d/G rounded once
     // (the convention of the volume fetch, n_over_g in the march)
     const v3 s = mk((float)d[0] / G.x, (float)d[1] / G.y, (float)d[2] / G.z);
@@ -762,7 +763,7 @@ uint64_t shaded_march_rows(const OracleRc1pass& P, int y0, int y1, float* out_rg
   const v3 G = mk((float)P.N[0] * P.scale[0], (float)P.N[1] * P.scale[1], (float)P.N[2] * P.scale[2]);
   const v3 half = mk(G.x * 0.5f, G.y * 0.5f, G.z * 0.5f);
   const v3 NoG = mk((float)P.N[0] / G.x, (float)P.N[1] / G.y, (float)P.N[2] / G.z);
-  Tex vol{P.vol, {P.N[0], P.N[1], P.N[2]}, 1};
+  Tex vol{P.vol, {P.N[0], P.N[1], P.N[2]}, 1, P.filter_bits};
   const int W = P.W, H = P.H;
   std::vector<uint32_t> tmp;
   uint32_t* counts = out_counts;
@@ -807,7 +808,7 @@ uint64_t shaded_march_rows(const OracleRc1pass& P, int y0, int y1, float* out_rg
           float dens;
           vol.sample(x, y, z, &dens);
           float src[4];
-          tf_lookup(P.tf, P.tf_n, dens, src);
+          tf_lookup(P.tf, P.tf_n, dens, src, P.filter_bits);
           cnt++;
           if (src[3] > 0.0f) {
             const v3 tx = vmad(dir, t, tpos);              // tx_pos, volume box at [0, G]
@@ -845,8 +846,8 @@ ORACLE_API uint64_t oracle_render_dos_rows(const OracleDos* Q, int y0, int y1, f
   const v3 lfwd = mk(Q->light_forward[0], Q->light_forward[1], Q->light_forward[2]);
   const v3 lup = mk(Q->light_up[0], Q->light_up[1], Q->light_up[2]);
   const v3 lright = mk(Q->light_right[0], Q->light_right[1], Q->light_right[2]);
-  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3};
-  ExtVol E{Q->ext, {Q->ext_res[0], Q->ext_res[1], Q->ext_res[2]}, Q->ext_levels, G, {}};
+  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3, P.filter_bits};
+  ExtVol E{Q->ext, {Q->ext_res[0], Q->ext_res[1], Q->ext_res[2]}, Q->ext_levels, G, {}, P.filter_bits};
   E.off.assign(E.nl + 1, 0);
   for (int L = 0; L < E.nl; L++) {
     int d[3];
@@ -1205,7 +1206,7 @@ ORACLE_API uint64_t oracle_render_ebs_rows(const OracleEbs* Q, int y0, int y1, f
   const v3 eye = mk(P.eye[0], P.eye[1], P.eye[2]);
   const v3 light = mk(P.light[0], P.light[1], P.light[2]);
   Sat T;
-  T.t = Tex{Q->sat, {Q->sat_dims[0], Q->sat_dims[1], Q->sat_dims[2]}, 1};
+  T.t = Tex{Q->sat, {Q->sat_dims[0], Q->sat_dims[1], Q->sat_dims[2]}, 1, P.filter_bits};
   T.S = mk(P.scale[0], P.scale[1], P.scale[2]);
   T.G = mk((float)P.N[0] * P.scale[0], (float)P.N[1] * P.scale[1], (float)P.N[2] * P.scale[2]);
   // inv_vol_scaled = 1.0f / (VolumeScaledSizes + VolumeScales * 2.0) (:75)
@@ -1216,7 +1217,7 @@ ORACLE_API uint64_t oracle_render_ebs_rows(const OracleEbs* Q, int y0, int y1, f
   ConeCS cs{std::cos(Q->cone_angle), std::sin(Q->cone_angle), std::cos(-Q->cone_angle),
             std::sin(-Q->cone_angle)};
   const v3 lfwd = mk(Q->light_forward[0], Q->light_forward[1], Q->light_forward[2]);
-  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3};
+  Tex grd{P.grad, {P.N[0], P.N[1], P.N[2]}, 3, P.filter_bits};
   const float ka = Q->apply_occlusion ? P.ka : 0.0f;
   const float kd = Q->apply_shadow ? P.kd : 0.0f;
   const float ks = Q->apply_shadow ? P.ks : 0.0f;

@@ -312,10 +312,12 @@ def _cone(tables, keep):
 def render_dos(vol16, scale, tf_rgbt, ext_levels, camera, W, H, step, occ_tables, sdw_tables,
                apply_occlusion=True, apply_shadow=False, shadow_type=0, light=None,
                grad=None, phong=False, ka=0.5, kd=0.5, ks=0.8, shininess=30.0,
-               ispec=(1.0, 1.0, 1.0), threads: int = 0, rows=None, literal=None):
+               ispec=(1.0, 1.0, 1.0), threads: int = 0, rows=None, literal=None,
+               filter_bits: int = 0):
     """Directional-occlusion shading frame (ray_bbox_marching.comp), or rows=(y0, y1) of
-    it.  light = dict with position/forward/up/right/spot_angle_deg.  literal: as
-    render_rc1pass.
+    it.  light = dict with position/forward/up/right/spot_angle_deg.  literal,
+    filter_bits: as render_rc1pass (filter_bits rounds the weights of the volume, TF,
+    gradient and extinction-pyramid fetches).
     Returns (rgba, counts, S)."""
     vol16 = np.ascontiguousarray(vol16, np.float32)
     tf = _q16_array(tf_rgbt)
@@ -326,6 +328,7 @@ def render_dos(vol16, scale, tf_rgbt, ext_levels, camera, W, H, step, occ_tables
     Q = OracleDos()
     Q.base = _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shininess,
                      ispec, pos)
+    Q.base.filter_bits = int(filter_bits)
     res = list(ext_levels[0].shape[::-1])
     flat = np.ascontiguousarray(np.concatenate([l.ravel() for l in ext_levels]), np.float32)
     Q.ext = _p(flat)
@@ -397,9 +400,11 @@ def render_ebs(vol16, scale, tf_rgbt, sat_f32, camera, W, H, step, apply_occlusi
                cone_angle_deg=1.0, interval=2.0, initial_step=2.0, ui_weight=1.0,
                max_distance=None, light=(0.0, 0.0, 0.0), light_forward=(0.0, 0.0, -1.0),
                grad=None, phong=False, ka=0.5, kd=0.5, ks=0.8, shininess=30.0,
-               ispec=(1.0, 1.0, 1.0), threads: int = 0, rows=None, literal=None):
+               ispec=(1.0, 1.0, 1.0), threads: int = 0, rows=None, literal=None,
+               filter_bits: int = 0):
     """Extinction-based shading frame (ebs_ray_bbox_marching.comp).  Returns (rgba, counts, S).
-    literal: as render_rc1pass."""
+    literal, filter_bits: as render_rc1pass (filter_bits rounds the weights of the volume,
+    TF, gradient and every SAT fetch)."""
     vol16 = np.ascontiguousarray(vol16, np.float32)
     tf = _q16_array(tf_rgbt)
     sat = np.ascontiguousarray(sat_f32, np.float32)
@@ -408,6 +413,7 @@ def render_ebs(vol16, scale, tf_rgbt, sat_f32, camera, W, H, step, apply_occlusi
     Q = OracleEbs()
     Q.base = _params(vol16, scale, tf, grad, camera, W, H, step, phong, ka, kd, ks, shininess,
                      ispec, light)
+    Q.base.filter_bits = int(filter_bits)
     Q.sat = _p(sat)
     Q.sat_dims[:] = list(sat.shape[::-1])
     Q.apply_occlusion, Q.occ_shells, Q.occ_radius = int(apply_occlusion), int(occ_shells), float(occ_radius)

@@ -15,7 +15,7 @@ struct OracleRc1pass {
   int W, H;
   float step;
   int phong; float ka, kd, ks, shininess; float ispec[3]; float light[3];
-  int filter_bits;                     // GL_LINEAR weights at this many fraction bits (0: exact); rc1pass only
+  int filter_bits;                     // GL_LINEAR weights at this many fraction bits (0: exact): every fetch of rc1pass, DOS, EBS
 };
 
 struct OracleDosCone {

@@ -2,8 +2,11 @@
 GL_LINEAR weight of the rc1pass march (volume, gradient, TF; ray_marching_1p.comp:133,
 :138) rounded to 8 fraction bits, as GPU texture units filter.  The HIP kernel against the
 oracle with the same weights (oracle.render_rc1pass(filter_bits=8)), bit for bit, over the
-rc1pass cases and schedules; the shaded renderers refuse the mode.  (That CVR-SPEC-8 sits
-inside BASELINE's image gate against the literal 8-bit reading: tests/test_literal.py.)"""
+rc1pass cases and schedules, and the shaded renderers' frames (DOS: the march, the gradient
+and every extinction-pyramid textureLod, ray_bbox_marching.comp:92-112; EBS: the march and
+every SAT texture() fetch, ebs_ray_bbox_marching.comp:77-83) against
+oracle.render_dos / render_ebs(filter_bits=8).  (That CVR-SPEC-8 sits inside BASELINE's
+image gate against the literal 8-bit reading: tests/test_literal.py.)"""
 import ctypes
 
 import numpy as np
@@ -92,6 +95,10 @@ def test_filter_bits_option_errors(bonsai_tf):
         out = N.Output(rgba.ctypes.data, None, None, 0)
         f = make_frame(Camera(**INITIAL), 16, 16)
         p = N.EbsParams()
+        # EBS filters the cell4 copy only: with the plain SAT the mode is refused
+        from test_ebs import lib_ext_lut
+        d.set_extinction_sat(lib_ext_lut(1))
+        N.check(L.cvr_set_option(d.handle, b"sat_layout", 1), "sat_layout", d.handle)
         assert L.cvr_render_extbsd(d.handle, ctypes.byref(f), ctypes.byref(p),
                                    ctypes.byref(out)) == N.CVR_ERR_ARG
         assert b"filter_bits" in L.cvr_last_error(d.handle)
@@ -101,3 +108,76 @@ def test_filter_bits_option_errors(bonsai_tf):
                                 ctypes.byref(out)) == N.CVR_ERR_ARG
     finally:
         d.close()
+
+
+@pytest.mark.parametrize("case", ["ao_shadow", "phong", "occ7_spot"])
+@pytest.mark.parametrize("flat", [1, 0])
+def test_filter8_dos_bitexact_vs_oracle(oracle, bonsai_tf, bonsai_tf_rgba, case, flat):
+    import math
+    from cpp_volume_rendering_amd.renderer import default_cone_params
+    from test_dos_gpu import LIGHT0, _occ7, cone_tables, gpu_dos, setup
+    n, W, H = 48, 96, 80
+    vol = D.marschner_lobb_u8(n)
+    sc = D.voxel_scale(n)
+    phong = case == "phong"
+    occ = _occ7() if case == "occ7_spot" else default_cone_params(True)
+    sdw = default_cone_params(False)
+    stype = 1 if case == "occ7_spot" else 0
+    step = 0.5 / math.sqrt(3.0)
+    d = Device(0)
+    try:
+        setup(d, vol, sc, bonsai_tf, bonsai_tf_rgba, (64, 64, 64), gmode=1 if phong else 0)
+        L = N.lib()
+        N.check(L.cvr_set_option(d.handle, b"shade_flat", flat), "shade_flat", d.handle)
+        g0 = gpu_dos(d, INITIAL, W, H, step, occ, sdw, apply_shadow=True, shadow_type=stype,
+                     phong=phong)
+        N.check(L.cvr_set_option(d.handle, b"filter_bits", 8), "filter_bits", d.handle)
+        g8 = gpu_dos(d, INITIAL, W, H, step, occ, sdw, apply_shadow=True, shadow_type=stype,
+                     phong=phong)
+        levels = d.extinction_levels()
+    finally:
+        d.close()
+    diag = math.sqrt(sum((n * s_) ** 2 for s_ in sc))
+    t_occ, t_sdw = cone_tables(occ, diag, 0.50), cone_tables(sdw, diag, 0.75)
+    v16 = oracle.volume_r16f(vol)
+    o8 = oracle.render_dos(v16, sc, bonsai_tf, levels, INITIAL, W, H, step, t_occ, t_sdw,
+                           apply_shadow=True, shadow_type=stype, light=LIGHT0,
+                           grad=oracle.gradient(vol, "fd") if phong else None, phong=phong,
+                           filter_bits=8)
+    assert_bitexact(g8[1], o8[1], f"DOS {case} counts (8-bit weights)")
+    assert_bitexact(g8[0], o8[0], f"DOS {case} rgba (8-bit weights)")
+    assert (g8[0].view(np.uint32) != g0[0].view(np.uint32)).mean() > 0.05
+
+
+@pytest.mark.parametrize("case", ["defaults_point", "phong", "directional"])
+@pytest.mark.parametrize("flat", [1, 0])
+def test_filter8_ebs_bitexact_vs_oracle(oracle, bonsai_tf, case, flat):
+    import math
+    from test_ebs_gpu import EBS_CASES, LIGHT_FWD, LIGHT_POS, ebs_params, gpu_ebs, gpu_sat
+    c = dict(EBS_CASES[case])
+    n, W, H = 40, 80, 64
+    vol = D.marschner_lobb_u8(n)
+    sc = D.voxel_scale(n)
+    phong = c.get("phong", False)
+    step = 0.5 / math.sqrt(3.0)
+    p = ebs_params(step=step, **c)
+    d = Device(0)
+    try:
+        sat, lut = gpu_sat(d, vol, sc)
+        d.set_transfer_function(bonsai_tf)
+        d.set_gradient(1 if phong else 0)
+        L = N.lib()
+        N.check(L.cvr_set_option(d.handle, b"shade_flat", flat), "shade_flat", d.handle)
+        g0 = gpu_ebs(d, INITIAL, W, H, p)
+        N.check(L.cvr_set_option(d.handle, b"filter_bits", 8), "filter_bits", d.handle)
+        g8 = gpu_ebs(d, INITIAL, W, H, p)
+    finally:
+        d.close()
+    o8 = oracle.render_ebs(oracle.volume_r16f(vol), sc, bonsai_tf, sat, INITIAL, W, H, step,
+                           apply_occlusion=p.apply_occlusion, apply_shadow=p.apply_shadow,
+                           shadow_type=p.shadow_type, light=LIGHT_POS, light_forward=LIGHT_FWD,
+                           grad=oracle.gradient(vol, "fd") if phong else None, phong=phong,
+                           filter_bits=8)
+    assert_bitexact(g8[1], o8[1], f"EBS {case} counts (8-bit weights)")
+    assert_bitexact(g8[0], o8[0], f"EBS {case} rgba (8-bit weights)")
+    assert (g8[0].view(np.uint32) != g0[0].view(np.uint32)).mean() > 0.05

@@ -106,6 +106,12 @@ def test_dos(oracle, tables, n, W, res):
     spec = oracle.render_dos(v16, sc, tables[1], levels, CAM, W, W, st, occ, sdw, **kw)[0]
     lit = oracle.render_dos(v16, sc, tables[1], levels, CAM, W, W, st, occ, sdw, literal=0, **kw)[0]
     assert_gate(gate(spec, lit), f"DOS {n}^3/{W}^2 (cone AO + point shadows)")
+    # texture-unit weights on both sides: CVR-SPEC-8 (filter_bits = 8: the volume, TF and
+    # every extinction-pyramid textureLod) against the literal reading with 8-bit weights
+    spec8 = oracle.render_dos(v16, sc, tables[1], levels, CAM, W, W, st, occ, sdw, filter_bits=8,
+                              **kw)[0]
+    lit8 = oracle.render_dos(v16, sc, tables[1], levels, CAM, W, W, st, occ, sdw, literal=8, **kw)[0]
+    assert_gate(gate(spec8, lit8), f"DOS {n}^3/{W}^2, 8-bit weights")
 
 
 def test_ebs_occlusion_and_shadow_conditioning(oracle, tables):
