@@ -324,7 +324,7 @@ struct Ctx {
   float* d_sat = nullptr;
   float4* d_sat_cells = nullptr;   // the same SAT as cell4 texels (4 float corners of a plane, sat.hip)
   int sat_layout = 0;              // option "sat_layout": the frame reads 0 = cell4 copy, 1 = the plain SAT
-  int sat_keep_scratch = 1;        // option "sat_keep_scratch": keep the double build grid for rebuilds
+  int sat_keep_scratch = 0;        // option "sat_keep_scratch": 1 keeps the double build grid for rebuilds
   void* d_sat_scratch = nullptr;   // the double grid of the build (kept for rebuilds)
   int sat_dims[3] = {0, 0, 0};
   int ext_res[3] = {0, 0, 0};

@@ -32,6 +32,16 @@
 namespace cvr {
 
 constexpr int kQuadFlag = 1 << 28;   // order entry = tile | (quarter + 1) << 28 for quad tiles
+#ifdef CVR_PHONG_CLASSIFY_FULL
+constexpr bool kPhongClassifyFull = true;
+#else
+constexpr bool kPhongClassifyFull = false;
+#endif
+#ifdef CVR_PHONG_GRAD_EARLY
+constexpr bool kPhongGradEarly = true;
+#else
+constexpr bool kPhongGradEarly = false;
+#endif
 
 // Macro-cell skip.  The macro cell m (2^mshift texels a side) of a sample is
 // taken from its clamped texel coordinate exactly as sample_pos computes it; its
@@ -210,7 +220,10 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
     // samples stay in flight behind it (testing all four first waited for all).
     bool we[K];
     int qlast = 0;   // the last sample's skip distance (0: no skip), read before raw[] dies
-    if (!PHONG) {
+    // Blinn-Phong too (CVR_PHONG_CLASSIFY_FULL: the round-3 full classify of every
+    // sample): its shading needs the rgb only for the visible samples as well
+    constexpr bool kAlphaFirst = !PHONG || !kPhongClassifyFull;
+    if (kAlphaFirst) {
 #pragma unroll
       for (int j = 0; j < K; j++) {
         we[j] = CS > 0 && __ballot(!cell_empty(raw[j])) == 0;
@@ -218,7 +231,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
         if (CS > 0 && we[j]) {
           tfa[j] = 0.0f; tfi[j] = 0; src[j].w = 0.0f;
         } else {
-          const float xd = fmaf(trilerp_cell<true>(raw[j], sp[j].ax, sp[j].ay, sp[j].az), fn, -0.5f);
+          const float xd = fmaf(trilerp_cell<!PHONG>(raw[j], sp[j].ax, sp[j].ay, sp[j].az), fn, -0.5f);
           tfa[j] = filter_weight<FB>(__builtin_amdgcn_fractf(xd));   // see classify
           tfi[j] = cvt_flr(xd) + 1;
           src[j].w = lerpf(tfp[tfi[j]].w, tfp[tfi[j] + 1].w, tfa[j]);
@@ -231,6 +244,22 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
         if (CS >= 2 && j == K - 1) qlast = cell_empty(raw[j]) ? cell_skip_q(raw[j]) : 0;
         if (CS > 0 && we[j]) src[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         else src[j] = classify<FB>(tfp, fn, trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az));
+      }
+    }
+    // Blinn-Phong: the gradient cells of the batch's visible samples are loaded
+    // here, together, so that their round trip overlaps the batch's other
+    // samples instead of stalling the composite once per shaded sample
+    // (CVR_PHONG_GRAD_LATE: loaded where each sample is shaded, round 3)
+    uint4 gq[PHONG ? K : 1][3];
+    if (PHONG && kPhongGradEarly) {
+#pragma unroll
+      for (int j = 0; j < K; j++) {
+        if (!(CS > 0 && we[j]) && src[j].w > 0.0f) {
+          const uint4* g = grad + 3 * (size_t)sp[j].idx;
+          gq[j][0] = g[0];
+          gq[j][1] = g[1];
+          gq[j][2] = g[2];
+        }
       }
     }
     bool visible = false;
@@ -248,14 +277,21 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
           float4 sc = src[j];
           if (!(CS > 0 && we[j]) && sc.w > 0.0f) {
             visible = true;
-            if (!PHONG) {   // classify's rgb, same lerps
+            if (kAlphaFirst) {   // classify's rgb, same lerps
               const float4 t0 = tfp[tfi[j]], t1 = tfp[tfi[j] + 1];
               sc.x = lerpf(t0.x, t1.x, tfa[j]);
               sc.y = lerpf(t0.y, t1.y, tfa[j]);
               sc.z = lerpf(t0.z, t1.z, tfa[j]);
             }
             if (PHONG) {
-              shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
+              if (kPhongGradEarly) {
+                const f3 g{trilerp_cell<false, false>(gq[j][0], sp[j].ax, sp[j].ay, sp[j].az),
+                           trilerp_cell<false, false>(gq[j][1], sp[j].ax, sp[j].ay, sp[j].az),
+                           trilerp_cell<false, false>(gq[j][2], sp[j].ax, sp[j].ay, sp[j].az)};
+                phong_rgb(A, g, phong_wpos(r.dir, tj[j], r.tpos, hg), eye, sc);
+              } else {
+                shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
+              }
               nshade++;
             }
             const float x = -(sc.w * hj[j]);
@@ -461,7 +497,11 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
                     unsigned long long* __restrict__ tile_samples, const int* __restrict__ order,
                     uint32_t* __restrict__ tile_cost, int boost) {
   extern __shared__ float4 tfp[];
+#ifdef CVR_PROBE_FRAMES   // cost probe only: one launch marches the same frame CVR_PROBE_FRAMES times
+  const int b = (int)(blockIdx.x % (gridDim.x / CVR_PROBE_FRAMES)), nt = A.ntiles;
+#else
   const int b = blockIdx.x, nt = A.ntiles;
+#endif
   int t, quarter = -1;
   if (order) {
     const int e = order[b];
@@ -780,6 +820,9 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
   // cell (1,1,1) <-> texel (0,0,0)
   const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
   int grid = order ? plan.order_slots : plan.ntiles;
+#ifdef CVR_PROBE_FRAMES
+  grid *= CVR_PROBE_FRAMES;
+#endif
   hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF, FB, CS>), dim3(grid), dim3(64), lds, s,
                      a, cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, out, samples,
                      tile_samples, order, tile_cost, order ? plan.boost : 0);

@@ -277,22 +277,36 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *   "tile_stats" 1: record per-tile timing of every frame (diagnostics)
  *   "kernel_timing" N > 0: time the ray-march kernel of the last N frames
  *                (cvr_read_kernel_times); 0 off (default)
+ *   "cell_skip"  per-cell skip flags kept in the density cells' fp16 sign bits
+ *                (rebuilt after a volume or TF change): 0 off; 1 a sample in an
+ *                EMPTY cell (no density its corners interpolate to has tau > 0) skips
+ *                its classification; 2 also steps over the next samples that stay
+ *                within the cell's chessboard distance to non-empty cells, per lane;
+ *                3 (default) the same when every marching lane of the wave can;
+ *                4 the fewest steps any lane may, for the lanes that can
  *   "sat_chunk"  z planes per work item of the EBS SAT build (1..64, default 32)
+ *   "sat_layout" EBS: 0 (default) = frames read a cell4 copy of the SAT (4 float
+ *                corners of a plane per texel, 16 B per texel more); 1 = frames read
+ *                the plain float SAT (no copy; slower)
+ *   "sat_keep_scratch" EBS: 1 keeps the SAT build's double grid (8 B per texel)
+ *                allocated for rebuilds; 0 (default) frees it after each build
  *   "shade_counters" 1: count shaded / shadow-lit samples of cvr_render_dosct
  *                and cvr_render_extbsd (cvr_read_shade_counters; one atomic per wave)
  *   "shade_flat" cvr_render_dosct / cvr_render_extbsd: 1 (default) = the frame's
  *                shading jobs in one list, shaded by a grid of their own and folded
- *                per pixel; the call then synchronizes the context stream once
- *                (after the counting march, to size the grid) and frames on other
- *                streams wait for the previous frame's list; 0 = per-wave deferred
- *                shading inside the march (fully asynchronous)
+ *                per pixel; one list per render stream, sized from earlier frames'
+ *                totals (read back without blocking); a frame whose list would not
+ *                fit renders through the per-wave kernel, decided on the device;
+ *                0 = per-wave deferred shading inside the march
  *   "flat_group" flat shading: consecutive 64-job chunks per XCD turn (default 8)
+ *   "debug_flat_limit" tests: a smaller job-list capacity, to exercise the fallback
  * One option changes the arithmetic (and so the image) rather than the speed:
  *   "filter_bits" 0: exact float GL_LINEAR weights (CVR-SPEC, the default);
- *                8: every GL_LINEAR weight of cvr_render_rc1pass (volume, gradient,
- *                TF; ray_marching_1p.comp:133, :138) rounded to 8 fraction bits, the
- *                fixed-point weights of GPU texture units (CVR-SPEC-8).  The other
- *                renderers return CVR_ERR_ARG while it is set. */
+ *                8: every GL_LINEAR weight (volume, gradient, TF; ray_marching_1p.comp:133,
+ *                :138; the DOS extinction pyramid, ray_bbox_marching.comp:92-112; the
+ *                EBS SAT, ebs_ray_bbox_marching.comp:77-83) rounded to 8 fraction
+ *                bits, the fixed-point weights of GPU texture units (CVR-SPEC-8).
+ *                cvr_render_extbsd needs sat_layout 0 for it. */
 cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
 int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);

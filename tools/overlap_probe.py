@@ -37,6 +37,9 @@ ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks")
 ap.add_argument("--renderer", choices=["rc1pass", "dos", "ebs"], default="rc1pass")
 ap.add_argument("--out", default="")
 ap.add_argument("--hwq", default="8")
+ap.add_argument("--frames-per-launch", type=int, default=1,
+                help="a CVR_PROBE_FRAMES=G library build (CVR_LIB_OVERRIDE): each call marches G frames")
+ap.add_argument("--tile-order", type=int, default=-1, help="rc1pass tile_order option (-1: default)")
 ap.add_argument("--boost", default="-1", help="rc1pass: comma list of boost percentages (-1: library default)")
 a = ap.parse_args()
 
@@ -72,6 +75,8 @@ for q, bst in itertools.product([int(x) for x in a.quad.split(",")], [int(x) for
         L.cvr_set_option(handle, b"quad", q)
         if bst >= 0:
             L.cvr_set_option(handle, b"boost", bst)
+        if a.tile_order >= 0:
+            L.cvr_set_option(handle, b"tile_order", a.tile_order)
     for nr in [int(x) for x in a.nranks.split(",")]:
         for tile in [int(x) for x in a.tile.split(",")]:
             ranks = range(nr) if a.ranks == "all" else [int(x) for x in a.ranks.split(",") if int(x) < nr]
@@ -92,9 +97,10 @@ for q, bst in itertools.product([int(x) for x in a.quad.split(",")], [int(x) for
                             L.cvr_set_stream(handle, ctypes.c_void_p(pool[i % ns].cuda_stream))
                             render(frame, outs[i % ns])
                         torch.cuda.synchronize()
-                        best = min(best, (time.perf_counter() - t0) / a.frames * 1e3)
+                        best = min(best, (time.perf_counter() - t0) / (a.frames * a.frames_per_launch) * 1e3)
                     per.append(best)
-                line = dict(renderer=a.renderer, nranks=nr, tile=tile, quad=q, boost=bst, streams=ns, hwq=int(a.hwq),
+                line = dict(renderer=a.renderer, frames_per_launch=a.frames_per_launch, tile_order=a.tile_order,
+                            lib=os.environ.get("CVR_LIB_OVERRIDE", "in-tree"), nranks=nr, tile=tile, quad=q, boost=bst, streams=ns, hwq=int(a.hwq),
                             ms_per_rank=[round(x, 5) for x in per], max_ms=round(max(per), 5),
                             mean_ms=round(sum(per) / len(per), 5),
                             max_over_mean=round(max(per) / (sum(per) / len(per)), 4))
