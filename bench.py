@@ -146,10 +146,14 @@ def parse():
                    help="GPU_MAX_HW_QUEUES for this process, set before HIP initialises "
                         "(default: 8; 24 at 4 GPUs, 32 at >= 8)")
     p.add_argument("--streams", type=int, default=0,
-                   help="frames in flight, render streams rotated per frame "
-                        "(default: 4; 12 at 4 GPUs, 16 at >= 8)")
+                   help="render streams, rotated per launch (default with multi-frame launches: "
+                        "3, 4 at N > 1; one frame per launch: 4, 12 at 4 GPUs, 16 at >= 8)")
     p.add_argument("--exchange-frames", type=int, default=0,
-                   help="frames per gather at N > 1 (default: 2 at >= 4 GPUs, else 1)")
+                   help="frames per gather at N > 1 (default: 2 at >= 4 GPUs, else 1; "
+                        "the launch group with --frames-per-launch > 1)")
+    p.add_argument("--frames-per-launch", type=int, default=0,
+                   help="rc1pass: consecutive frames rendered in ONE launch "
+                        "(cvr_render_rc1pass_frames, 1..8; default 4, other renderers 1)")
     p.add_argument("--quad", type=int, default=-1,
                    help="quad (4 lanes per ray) share of the longest tiles, %% (default 0)")
     p.add_argument("--transport", choices=["rccl", "torch"], default="rccl",
@@ -485,7 +489,21 @@ def main():
     # more frames fly (16 streams: 0.0188 ms per rank frame against 0.030 with 4
     # streams and quad 10 %, which the deeper pipeline no longer needs)
     quad = a.quad if a.quad >= 0 else 0
-    a.streams = a.streams or (16 if world >= 8 else (12 if world >= 4 else 4))
+    # Several frames per launch (rc1pass): one launch fills the GPU with 4 frames'
+    # waves, so a frame's tail overlaps the next frame inside the launch and rank 0's
+    # host pays one call per 4 frames.  Measured (profiles/r04/s11_*, s12_*):
+    # the driver's 20-frame command at N = 1, 0.0808 ms per frame (1 frame per launch,
+    # 4 streams) -> 0.0778 (4 per launch, 3 streams); rank shares at N = 8 over 20
+    # frames 0.0254 -> 0.0154 ms, in steady state 0.0224 -> 0.0122-0.0131 ms
+    if a.frames_per_launch <= 0:
+        a.frames_per_launch = 4 if a.renderer == "rc1pass" else 1
+    if a.renderer != "rc1pass" and a.frames_per_launch != 1:
+        sys.exit("bench.py: --frames-per-launch > 1 needs --renderer rc1pass")
+    if not 1 <= a.frames_per_launch <= 8:
+        sys.exit("bench.py: --frames-per-launch must be in 1..8")
+    FPL = a.frames_per_launch
+    a.streams = a.streams or ((4 if world >= 2 else 3) if FPL > 1 else
+                              (16 if world >= 8 else (12 if world >= 4 else 4)))
     if a.renderer == "rc1pass":
         N.check(N.lib().cvr_set_option(r.device.handle, b"quad", quad), "quad", r.device.handle)
         if a.batch:
@@ -508,10 +526,10 @@ def main():
     try:
         # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
         # on rank 0) would otherwise rival a rank's share of the frame (~23 us at N = 8)
-        gx = a.exchange_frames or (2 if world >= 4 else 1)
+        gx = FPL if FPL > 1 else (a.exchange_frames or (2 if world >= 4 else 1))
         split = T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev,
                                   transport=a.transport if world > 1 else None, streams=a.streams,
-                                  frames_per_exchange=gx)
+                                  frames_per_exchange=gx, frames_per_launch=FPL)
     except N.CvrError as e:     # no native communicator: torch's dist.gather instead
         if world == 1 or a.transport != "rccl":
             raise
@@ -605,19 +623,32 @@ def main():
 
     # Kernel-only time for the roofline: HIP events the library records on its
     # own stream around the ray-march launch (kernel_timing), in a separate pass.
-    N.check(L.cvr_set_option(r.device.handle, b"kernel_timing", a.steps), "kernel_timing",
+    # With multi-frame launches the pass times the same launches as the timed region:
+    # floor(steps / FPL) launches of FPL frames (the roofline's bytes are per launch).
+    n_launch = max(1, a.steps // FPL)
+    N.check(L.cvr_set_option(r.device.handle, b"kernel_timing", n_launch), "kernel_timing",
             r.device.handle)
     total.zero_()
-    for i in range(a.steps):
-        step_once(i)
+    if FPL > 1:
+        mf_bufs = [out_buf] + [torch.empty_like(out_buf) for _ in range(FPL - 1)]
+        mf_outs = [N.Output(mf_bufs[j].data_ptr(), None, total.data_ptr() if j == 0 else None, 1, fmt)
+                   for j in range(FPL)]
+        for k in range(n_launch):
+            r.render_frames_to([frames[(k * FPL + j) % len(frames)] for j in range(FPL)], mf_outs)
+        S_timed = sum(S_cam[i % len(S_cam)] for i in range(n_launch * FPL))
+    else:
+        for i in range(a.steps):
+            step_once(i)
+        S_timed = S_rank_steps
     torch.cuda.synchronize(dev)
-    kt = (ctypes.c_float * a.steps)()
+    kt = (ctypes.c_float * n_launch)()
     nkt = ctypes.c_int()
-    N.check(L.cvr_read_kernel_times(r.device.handle, kt, a.steps, ctypes.byref(nkt)),
+    N.check(L.cvr_read_kernel_times(r.device.handle, kt, n_launch, ctypes.byref(nkt)),
             "cvr_read_kernel_times", r.device.handle)
-    assert nkt.value == a.steps
+    assert nkt.value == n_launch
     kern_ms = float(np.mean(kt[:nkt.value]))
-    assert int(total.item()) == S_rank_steps, "sample count changed between frames"
+    assert int(total.item()) == S_timed, "sample count changed between frames"
+    S_launch = int(round(S_timed / n_launch))            # samples per launch (FPL frames)
     batch = L.cvr_get_option(r.device.handle, b"batch") or (2 if a.phong else 4)   # 0 = auto
     macro = L.cvr_get_option(r.device.handle, b"macro")
 
@@ -640,7 +671,8 @@ def main():
         # sample for the Phong gradient: 8 corners x 3 fp16, counted by the kernel)
         px_bytes = 8 if fmt == N.FORMAT_RGBA16F else 16
         # (iso: 8 B per volume fetch + the pixel; the <= 1 gradient fetch per hit is left out)
-        b_alg = 8 * 1 * S_rank + px_bytes * pixels + (48 * int(shade[0]) if count_shaded and a.phong else 0)
+        b_alg = (8 * 1 * S_launch + FPL * px_bytes * pixels
+                 + (FPL * 48 * int(shade[0]) if count_shaded and a.phong else 0))
         fetches = int(shade[2])
         if dos:
             # + 8 fp16 corners (16 B) per trilinear extinction fetch the kernel issues.
@@ -677,12 +709,20 @@ def main():
                 "traffic": pmc.get("hbm_bytes_per_launch"),
                 "kernel": kname,
                 "kernel_ms": round(kern_ms, 4),
-                "bytes_alg_per_launch": b_alg, "samples_per_launch": S_rank,
+                "frames_per_launch": FPL,
+                "bytes_alg_per_launch": b_alg, "samples_per_launch": S_launch,
                 # the same bytes over the frame time of the timed region (frames in
                 # flight overlap, so a frame takes less than one launch's duration)
-                "frac_frame": round(b_alg / (ms_per_step * 1e-3) / 1e9 / peak, 4)}
+                "frac_frame": round(b_alg / FPL / (ms_per_step * 1e-3) / 1e9 / peak, 4)}
         if shaded:
             roof["alg_over_hbm_peak"] = round(achieved / HBM_PEAK_GBS, 4)
+        else:
+            # "an *effective* bandwidth" -- B_alg counts 8 corners per
+            # sample of the reference's loop; most of them come from L1/L2 (traffic
+            # below is what HBM served), so frac near or above 1 means the march is
+            # past the HBM roofline of its algorithmic bytes (VALU issue and vector-
+            # memory latency bound it)
+            roof["definition"] = "effective: B_alg / launch time (SURVEY 8d); HBM bytes in traffic"
         if ebs:
             # the vector-memory pipe: 2 dwordx4 wave-loads (2 x 1 KiB) per 64 SAT fetches,
             # against 256 CUs x one 1-KiB wave-load per 16 clocks (64 B/clk per CU L1) at
@@ -720,9 +760,9 @@ def main():
             # the per-cell skip (cell_skip 2-4) steps over samples in empty space without
             # a load: they count in S (the reference's loop iterations) but fetch nothing;
             # the same roofline on the bytes actually fetched, beside it
-            skipped = int(shade[1])
+            skipped = int(shade[1]) * FPL
             b_fetch = b_alg - 8 * skipped
-            roof.update({"skipped_samples": skipped, "fetched_samples": S_rank - skipped,
+            roof.update({"skipped_samples": skipped, "fetched_samples": S_launch - skipped,
                          "bytes_fetched_per_launch": b_fetch,
                          "achieved_fetched": round(b_fetch / (kern_ms * 1e-3) / 1e9, 1),
                          "frac_fetched": round(b_fetch / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
@@ -754,8 +794,9 @@ def main():
             "ms_per_step": round(ms_per_step, 4),
             "fps": round(1000.0 / ms_per_step, 1),
             # fps and ms_per_step are throughput: frames overlap on the device (one
-            # static view, split.nstreams in flight); one frame's own latency is
-            # about roofline.kernel_ms (its launch, with the other frames in flight)
+            # static view, split.nstreams launches of frames_per_launch frames in
+            # flight); a frame is delivered when its launch ends, so its latency is
+            # about roofline.kernel_ms (its launch, with the other launches in flight)
             "frame_latency_ms_approx": None,
             "higher_is_better": True,
             "scaling": "strong",   # one fixed frame split over the GPUs
@@ -789,7 +830,9 @@ def main():
                                       r.device.handle, b"sat_layout") == 1 else "cell4 float4"))
                                      if ebs else ""),
                        "frame_format": a.format,
-                       "frames_in_flight": split.nstreams,
+                       "frames_in_flight": split.nstreams * FPL,
+                       "frames_per_launch": FPL,
+                       "render_streams": split.nstreams,
                        "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
                        "quad_pct": quad if a.renderer == "rc1pass" else 0,
                        "shading": ("flat job list" if N.lib().cvr_get_option(r.device.handle, b"shade_flat")

@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "cvr_abi_version", "cvr_status_string", "cvr_create", "cvr_destroy", "cvr_last_error",
     "cvr_set_stream", "cvr_set_option", "cvr_get_option", "cvr_synchronize", "cvr_set_volume", "cvr_set_volume_device",
     "cvr_set_transfer_function", "cvr_set_gradient", "cvr_device_bytes", "cvr_copy_cells", "cvr_tiles_for_rank",
-    "cvr_render_rc1pass", "cvr_unpack_tiles_device", "cvr_copy_tile_stats", "cvr_read_kernel_times", "cvr_read_shade_counters", "cvr_selftest_arith", "cvr_camera_lookat", "cvr_default_step",
+    "cvr_render_rc1pass", "cvr_render_rc1pass_frames", "cvr_unpack_tiles_device", "cvr_copy_tile_stats", "cvr_read_kernel_times", "cvr_read_shade_counters", "cvr_selftest_arith", "cvr_camera_lookat", "cvr_default_step",
     "cvr_tf1d_build_rgbt", "cvr_read_tf1d", "cvr_read_raw", "cvr_read_syn", "cvr_read_pvm",
     "cvr_read_camera_state", "cvr_read_light_position", "cvr_read_light", "cvr_build_cone_tables",
     "cvr_set_extinction_volume", "cvr_copy_extinction_level", "cvr_render_dosct",
@@ -175,6 +175,8 @@ def lib() -> ctypes.CDLL:
         "cvr_tiles_for_rank": ([ctypes.POINTER(Frame), I], I),
         "cvr_render_rc1pass": ([P, ctypes.POINTER(Frame), ctypes.POINTER(Rc1passParams),
                                 ctypes.POINTER(Output)], I),
+        "cvr_render_rc1pass_frames": ([P, ctypes.POINTER(Frame), I, ctypes.POINTER(Rc1passParams),
+                                       ctypes.POINTER(Output)], I),
         "cvr_unpack_tiles_device": ([P, ctypes.POINTER(Frame), P, I, I, P], I),
         "cvr_comm_unique_id": ([ctypes.c_char_p], I),
         "cvr_comm_init": ([P, I, I, ctypes.c_char_p], I),

@@ -820,11 +820,27 @@ static bool view_close(const float a[7], const float b[7], int deg) {
   return std::fabs((double)a[6] - b[6]) <= rad * std::fabs((double)b[6]);
 }
 
-cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pass_params* p,
-                              const cvr_output* o) {
-  Ctx* c = reinterpret_cast<Ctx*>(ctx);
-  if (!c) return CVR_ERR_ARG;
+// nf frames (1..kMaxLaunchFrames) in one ray-march launch; nf = 1 is cvr_render_rc1pass.
+static cvr_status render_rc1pass_frames(Ctx* c, const cvr_frame* frames, int nf,
+                                        const cvr_rc1pass_params* p, const cvr_output* outs) {
+  const cvr_frame* f = frames;
+  const cvr_output* o = outs;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: null argument");
+  if (nf < 1 || nf > cvr::kMaxLaunchFrames)
+    return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass_frames: nframes %d not in 1..%d", nf,
+                cvr::kMaxLaunchFrames);
+  for (int i = 1; i < nf; i++) {
+    const cvr_frame& g = frames[i];
+    if (g.width != f->width || g.height != f->height || g.tile_size != f->tile_size ||
+        g.rank != f->rank || g.nranks != f->nranks)
+      return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass_frames: frame %d differs from frame 0 in "
+                                  "viewport or screen split", i);
+    if (!outs[i].rgba || !outs[i].on_device || outs[i].format != o->format || outs[i].total)
+      return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass_frames: output %d must be a device buffer of "
+                                  "frame 0's format, without a total", i);
+  }
+  if (nf > 1 && !o->on_device)
+    return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass_frames: the outputs must be device buffers");
   if (o->format != CVR_FORMAT_RGBA32F && o->format != CVR_FORMAT_RGBA16F)
     return fail(c, CVR_ERR_ARG, "cvr_render_rc1pass: unknown output format %d", o->format);
   if (f->width < 1 || f->height < 1 || f->width > 32768 || f->height > 32768)
@@ -931,6 +947,34 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   A.interleave = c->use_order == 2;
   float vsig[7];
   view_signature(A, vsig);
+  // frames 1.. of a multi-frame launch: their views (the rest of A is frame 0's)
+  cvr::LaunchFrames lf;
+  lf.n = nf;
+  lf.grid = 0;
+  bool views_close = true;   // every frame of the launch near frame 0's view (one launch order)
+  for (int i = 0; i < nf; i++) {
+    cvr::Rc1passArgs Ai = A;
+    if (i > 0) {
+      int nti;
+      size_t npi;
+      fill_frame_args(c, &frames[i], p->step, Ai, nti, npi);
+      float vi[7];
+      view_signature(Ai, vi);
+      if (!view_close(vi, vsig, c->stale_deg)) views_close = false;
+    }
+    cvr::FrameView& v = lf.view[i];
+    for (int k = 0; k < 3; k++) {
+      v.eye[k] = Ai.eye[k];
+      v.col0[k] = Ai.col0[k];
+      v.col1[k] = Ai.col1[k];
+      v.col2[k] = Ai.col2[k];
+    }
+    v.tan_half_fovy = Ai.tan_half_fovy;
+    v.aspect = Ai.aspect;
+    lf.out[i] = (float4*)outs[i].rgba;
+    lf.samples[i] = (uint32_t*)outs[i].samples;
+  }
+  if (nf > 1) plan.frames = &lf;
   const int key = (plan.ntiles << 2) ^ (plan.quad_pct << 24) ^
                   (packed ? (f->rank << 8) ^ (f->nranks << 12) ^ 1 : 0);
   const int* order = nullptr;
@@ -982,6 +1026,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     // an order learned on a distant view costs more than none (interleaved
     // screen order): measured +18 % mean over the 24 reference views
     if (order && os.has_view && !view_close(vsig, os.view, c->stale_deg)) order = nullptr;
+    if (!views_close) order = nullptr;   // frames far apart in one launch: no shared order
     tile_cost = os.d_cost;
   }
   // without an order, tiles go to the XCDs interleaved (tile t on XCD t mod 8):
@@ -1014,7 +1059,7 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
   // ... and only while the camera holds still (or moves little) from frame to
   // frame: when every frame jumps to a distant view, a new order would never be
   // used and its rebuild (~15 us on the frame's stream) is skipped
-  const bool steady = !os.has_last || view_close(vsig, os.last_view, c->stale_deg);
+  const bool steady = views_close && (!os.has_last || view_close(vsig, os.last_view, c->stale_deg));
   std::memcpy(os.last_view, vsig, sizeof(vsig));
   os.has_last = true;
   const bool rebuild = tile_cost && !c->async_order && steady &&
@@ -1054,6 +1099,20 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
     HIP_TRY(c, hipStreamSynchronize(s));
   }
   return CVR_OK;
+}
+
+cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pass_params* p,
+                              const cvr_output* o) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  return render_rc1pass_frames(c, f, 1, p, o);
+}
+
+cvr_status cvr_render_rc1pass_frames(cvr_ctx* ctx, const cvr_frame* frames, int nframes,
+                                     const cvr_rc1pass_params* p, const cvr_output* outs) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  return render_rc1pass_frames(c, frames, nframes, p, outs);
 }
 
 cvr_status cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int* out_tiles) {

@@ -172,6 +172,24 @@ struct IsoArgs {
   float color[4];
 };
 
+// Several frames in one ray-march launch (cvr_render_rc1pass_frames): frame f
+// takes workgroups [f * grid, (f + 1) * grid) and differs from frame 0 only in
+// its view (camera) and its outputs.  grid is a multiple of 8 whenever the
+// single-frame grid is, so workgroup b keeps XCD b % 8's share of the frame.
+constexpr int kMaxLaunchFrames = 8;
+struct FrameView {
+  float eye[3];
+  float col0[3], col1[3], col2[3];   // columns of mat3(View)
+  float tan_half_fovy, aspect;
+};
+struct LaunchFrames {
+  int n;                             // frames in the launch (1: a plain launch, the rest unused)
+  int grid;                          // workgroups per frame
+  FrameView view[kMaxLaunchFrames];
+  float4* out[kMaxLaunchFrames];
+  uint32_t* samples[kMaxLaunchFrames];
+};
+
 // How one frame is cut into work: one 8x8 wave tile per workgroup.
 struct RenderPlan {
   int ntiles;                        // 8x8 wave tiles (one workgroup each)
@@ -181,9 +199,11 @@ struct RenderPlan {
   int keep;                          // diagnostics: >0 keeps only the first `keep` entries per band
   int max_seg;                       // most tiles one (work-balanced) band may take
   int epi_stop;                      // diagnostics: the epilogue stops after phase k (0 = full)
+  const LaunchFrames* frames;        // null: one frame; else frames->n frames in one launch
 };
 
 constexpr int kMaxBandTiles = 8192;
+
 
 // Flat shading of the DOS/EBS renderers (option "shade_flat", shaded_march.h):
 // one frame's shading jobs in a single global list, shaded by a grid of their own
@@ -371,6 +391,8 @@ hipError_t launch_build_cells_impl(const void* vox, int bpv, const uint16_t* lut
 hipError_t launch_gradient(const Ctx& c, int mode, uint2* tmp, hipStream_t s);
 hipError_t launch_selftest_arith(int e_rcp_lo, int e_rcp_n, int e_sqrt_lo, int e_sqrt_n,
                                  unsigned long long* bad, hipStream_t s);
+// plan.frames: null for one frame, else plan.frames->n frames in one launch
+// (out / samples: frame 0's)
 hipError_t launch_rc1pass(const Ctx& c, const Rc1passArgs& a, bool phong, float4* out,
                           uint32_t* samples, unsigned long long* tile_samples, const int* order,
                           uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s);

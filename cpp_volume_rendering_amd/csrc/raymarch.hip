@@ -491,17 +491,38 @@ constexpr int rc1_waves_per_eu() {
 }
 template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB, int CS>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rc1_waves_per_eu<K, PHONG, SKIP, QUAD>())))
-rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
+rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
-                    float4* __restrict__ out, uint32_t* __restrict__ samples,
+                    float4* __restrict__ out0, uint32_t* __restrict__ samples0,
                     unsigned long long* __restrict__ tile_samples, const int* __restrict__ order,
-                    uint32_t* __restrict__ tile_cost, int boost) {
+                    uint32_t* __restrict__ tile_cost, int boost, LaunchFrames LF) {
   extern __shared__ float4 tfp[];
-#ifdef CVR_PROBE_FRAMES   // cost probe only: one launch marches the same frame CVR_PROBE_FRAMES times
-  const int b = (int)(blockIdx.x % (gridDim.x / CVR_PROBE_FRAMES)), nt = A.ntiles;
-#else
-  const int b = blockIdx.x, nt = A.ntiles;
-#endif
+  // Several frames per launch (LF.n > 1, cvr_render_rc1pass_frames): workgroup
+  // blockIdx.x marches block b of frame f with that frame's view and outputs.
+  // Only frame 0 records the tile costs of the next launch order; the per-tile
+  // sample counts of all frames add up (the launch's total).
+  Rc1passArgs A = A0;
+  float4* __restrict__ out = out0;
+  uint32_t* __restrict__ samples = samples0;
+  int b = blockIdx.x, f = 0;
+  const int nt = A.ntiles;
+  if (LF.n > 1) {
+    f = b / LF.grid;
+    b -= f * LF.grid;
+    const FrameView& v = LF.view[f];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      A.eye[i] = v.eye[i];
+      A.col0[i] = v.col0[i];
+      A.col1[i] = v.col1[i];
+      A.col2[i] = v.col2[i];
+    }
+    A.tan_half_fovy = v.tan_half_fovy;
+    A.aspect = v.aspect;
+    out = LF.out[f];
+    samples = LF.samples[f];
+    if (f != 0) tile_cost = nullptr;
+  }
   int t, quarter = -1;
   if (order) {
     const int e = order[b];
@@ -568,7 +589,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
   if (tile_samples) {   // per-tile sample count; summed by tile_order_kernel (no hot atomic)
     unsigned long long v = wave_sum(cnt);
     if (lane == 0) {
-      if (QUAD && quarter >= 0) {
+      if ((QUAD && quarter >= 0) || LF.n > 1) {
         if (v) atomicAdd(&tile_samples[t], v);
       } else {
         tile_samples[t] = v;
@@ -594,7 +615,7 @@ rc1pass_tile_kernel(Rc1passArgs A, const uint4* __restrict__ cells,
     unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     unsigned hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    if (lane == 0 && quarter <= 0) {
+    if (lane == 0 && quarter <= 0 && f == 0) {
       A.tile_stats[t * 4 + 0] = t_start;
       A.tile_stats[t * 4 + 1] = t_end;
       A.tile_stats[t * 4 + 2] = m;
@@ -820,12 +841,16 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
   // cell (1,1,1) <-> texel (0,0,0)
   const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
   int grid = order ? plan.order_slots : plan.ntiles;
-#ifdef CVR_PROBE_FRAMES
-  grid *= CVR_PROBE_FRAMES;
-#endif
+  LaunchFrames lf;
+  lf.n = 1;
+  if (plan.frames && plan.frames->n > 1) {
+    lf = *plan.frames;
+    lf.grid = grid;
+    grid *= lf.n;
+  }
   hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF, FB, CS>), dim3(grid), dim3(64), lds, s,
                      a, cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, out, samples,
-                     tile_samples, order, tile_cost, order ? plan.boost : 0);
+                     tile_samples, order, tile_cost, order ? plan.boost : 0, lf);
   return hipGetLastError();
 }
 

@@ -554,6 +554,19 @@ class RayCasting1Pass(BaseVolumeRenderer):
                                               ctypes.byref(self._params), ctypes.byref(out)),
                 self._ENTRY, self.device.handle)
 
+    def render_frames_to(self, frames, outs):
+        """Several frames in ONE launch (cvr_render_rc1pass_frames): frames[i] into
+        outs[i] (device outputs; outs[0].total gets the samples of all of them), the
+        same pixels as len(frames) render_to calls."""
+        if self._ENTRY != "cvr_render_rc1pass":
+            raise NotImplementedError(f"{type(self).__name__}: one frame per call")
+        n = len(frames)
+        fa = (N.Frame * n)(*frames)
+        oa = (N.Output * n)(*outs)
+        N.check(N.lib().cvr_render_rc1pass_frames(self.device.handle, fa, n,
+                                                  ctypes.byref(self._params), oa),
+                "cvr_render_rc1pass_frames", self.device.handle)
+
     def FillParameterSpace(self, pspace: dict):
         pspace.clear()
         pspace["StepSize"] = (0.2, 2.0, 0.1)        # rc1prenderer.cpp:225-229

@@ -96,6 +96,12 @@ def gather_to_root(packed: torch.Tensor, tpr_max: int, group=None) -> torch.Tens
     return None
 
 
+def _copy_frame(f):
+    g = N.Frame()
+    ctypes.pointer(g)[0] = f
+    return g
+
+
 class ScreenTileSplit:
     """One renderer's frames split over the ranks of a process group.
 
@@ -119,6 +125,12 @@ class ScreenTileSplit:
     Streams sharing a hardware queue serialise: give the process enough queues
     (GPU_MAX_HW_QUEUES, bench.py sets 8).
 
+    ``frames_per_launch`` = L > 1 (rc1pass with the library render only): L
+    consecutive frames render in ONE launch (cvr_render_rc1pass_frames), issued when
+    the L-th is submitted (or at flush); at world > 1 the launch is the exchange group
+    (frames_per_exchange = L).  At world 1 the groups rotate over the D streams with
+    L images each.
+
     Transport ``"rccl"`` (default on GPUs at world > 1): the library's own
     communicator (cvr_comm_init, id broadcast over the process group) and
     cvr_gather_tiles, two C calls per frame; rank 0 renders straight into its block
@@ -131,7 +143,8 @@ class ScreenTileSplit:
     def __init__(self, renderer=None, width: int = None, height: int = None, tile: int = 16,
                  fmt: int = N.FORMAT_RGBA16F, group=None, device=None, render_fn=None,
                  unpack_fn=None, count_samples: bool = False, transport: str = None,
-                 streams: int = None, frames_per_exchange: int = 1, stream_factory=None):
+                 streams: int = None, frames_per_exchange: int = 1, stream_factory=None,
+                 frames_per_launch: int = 1):
         self.r = renderer
         self.width = width if width is not None else renderer.width
         self.height = height if height is not None else renderer.height
@@ -163,7 +176,14 @@ class ScreenTileSplit:
         self.streams = [mk() for _ in range(streams)] if streams > 1 else None
         self.k = tiles_for_rank(w, h, tile, self.rank, self.world) if self.split else 0
         self.tpr_max = max_tiles_per_rank(w, h, tile, self.world) if self.split else 0
-        nimg = streams if not self.split else 1
+        # frames per launch: rc1pass through the library's own render call only
+        self.L = max(1, int(frames_per_launch))
+        if (self.L > 1 and (render_fn is not None or renderer is None or
+                            getattr(renderer, "_ENTRY", "") != "cvr_render_rc1pass")):
+            self.L = 1
+        if self.split and self.L > 1:
+            frames_per_exchange = self.L
+        nimg = streams * self.L if not self.split else 1
         self._images = ([torch.zeros((h, w, 4), dtype=dtype, device=self.device)
                          for _ in range(nimg)] if self.rank == 0 else None)
         # buffer sets: frame n uses set n % nbuf (one per stream; two for one stream).
@@ -172,6 +192,9 @@ class ScreenTileSplit:
         self.nbuf = max(2, streams)
         self.G = max(1, int(frames_per_exchange)) if (self.transport == "rccl" and
                                                        self.streams is not None) else 1
+        if self.split and self.G == 1:
+            self.L = 1
+        self._batch = []            # frames of the open launch (L > 1)
         if self.split:
             # padded to tpr_max tiles (gather needs equal sizes); padding stays zero
             self.packed = [torch.zeros((self.G, self.tpr_max, tile, tile, 4), dtype=dtype,
@@ -201,7 +224,8 @@ class ScreenTileSplit:
                 g = self.gathered[i] if self.rank == 0 else None
                 blk = g[0] if self.rank == 0 else self.packed[i]     # (G, tpr, T, T, 4)
                 outs = [N.Output(blk[j].data_ptr(), None,
-                                 self.total.data_ptr() if self.total is not None else None, 1,
+                                 self.total.data_ptr() if self.total is not None and
+                                 (self.L == 1 or j == 0) else None, 1,
                                  fmt) for j in range(self.G)]
                 slots.append((self.streams[i % self.nstreams].cuda_stream, outs, blk.data_ptr(),
                               g.data_ptr() if g is not None else None))
@@ -211,12 +235,20 @@ class ScreenTileSplit:
                           slots)
             self._group = 0      # frames rendered into the open exchange group
 
+    def _image_index(self, n):
+        """World 1: the image of frame n (launch group g = n // L on stream g % D)."""
+        if self.L == 1:
+            return n % len(self._images)
+        return ((n // self.L) % self.nstreams) * self.L + n % self.L
+
     @property
     def image(self):
         """Rank 0: the frame ``completed`` (None on other ranks)."""
         if self._images is None:
             return None
-        return self._images[max(self.completed, 0) % len(self._images)]
+        if self.split:
+            return self._images[0]
+        return self._images[self._image_index(max(self.completed, 0))]
 
     def _init_comm(self):
         L = N.lib()
@@ -272,6 +304,13 @@ class ScreenTileSplit:
         """Render this rank's tiles of one frame and start their gather."""
         n = self.submitted
         frame = self._frame_for(camera)
+        if self.L > 1:
+            # the launch group's frames are rendered together when the last arrives
+            self._batch.append(_copy_frame(frame))
+            self.submitted += 1
+            if len(self._batch) == self.L:
+                self._launch_batch()
+            return
         self._stream_for(n)
         if not self.split:
             self.render_fn(frame, self._images[n % len(self._images)], self.total)
@@ -322,6 +361,34 @@ class ScreenTileSplit:
         while len(self._pending) > 1:
             self._complete_oldest()
 
+    def _launch_batch(self):
+        """Render the open launch group (frames submitted - len(batch) .. submitted - 1)
+        in one cvr_render_rc1pass_frames call on the group's stream; at world > 1
+        start its gather."""
+        frames, self._batch = self._batch, []
+        nb = len(frames)
+        n0 = self.submitted - nb
+        g = n0 // self.L
+        self._stream_for(g)
+        if not self.split:
+            outs = [N.Output(self._images[self._image_index(n0 + j)].data_ptr(), None,
+                             self.total.data_ptr() if (self.total is not None and j == 0) else None,
+                             1, self.fmt) for j in range(nb)]
+            self.r.render_frames_to(frames, outs)
+            self.completed = n0 + nb - 1 if self.streams is None else n0 - 1
+            return
+        L, h, entry, params, imgs, slots = self._fast
+        sptr, outs, buf, gb = slots[g % self.nbuf]
+        L.cvr_set_stream(h, sptr)
+        fa = (N.Frame * nb)(*frames)
+        oa = (N.Output * nb)(*outs[:nb])
+        st = L.cvr_render_rc1pass_frames(h, fa, nb, params, oa)
+        if st:
+            N.check(st, "cvr_render_rc1pass_frames", h)
+        self._frame = frames[-1]
+        self._exchange(nb, n0 + nb - 1)
+        self.completed = n0 - 1
+
     def _exchange(self, nframes, n_last):
         """Gather the open group's `nframes` frames, the last of which is frame
         `n_last`, in one ncclGather on the group's stream."""
@@ -356,6 +423,8 @@ class ScreenTileSplit:
     def flush(self):
         """Complete every submitted frame: work queued on the current stream afterwards
         sees the last frame in `image`."""
+        if self._batch:
+            self._launch_batch()                              # a partly filled launch group
         if self._fast is not None and self._group:
             self._exchange(self._group, self.submitted - 1)   # a partly filled group
         if self.device.type == "cuda":

@@ -352,6 +352,20 @@ int         cvr_tiles_for_rank(const cvr_frame* frame, int rank);
 cvr_status  cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* frame,
                                const cvr_rc1pass_params* params, const cvr_output* out);
 
+/* nframes frames (1..8) in ONE ray-march launch: frames[i] is rendered into
+ * outs[i] exactly as nframes calls of cvr_render_rc1pass would render it (same
+ * pixels, same per-pixel counts).  The frames share the viewport and the screen
+ * split (width, height, tile_size, rank, nranks) and may differ in camera; the
+ * outputs are device buffers of one format.  outs[0].total (if set) receives the
+ * samples of all the frames; the other totals must be NULL.  One launch holds
+ * nframes x the waves of a frame, so the tail of one frame's longest rays
+ * overlaps the next frame's, and the host pays one call.  The
+ * launch order learned on frame 0's view is used when every frame is within
+ * "stale_deg" of it.  No reference counterpart: the reference draws one frame
+ * per Redraw (rc1prenderer.cpp:100-151); this is the batch form of that call. */
+cvr_status  cvr_render_rc1pass_frames(cvr_ctx* ctx, const cvr_frame* frames, int nframes,
+                                      const cvr_rc1pass_params* params, const cvr_output* outs);
+
 /* Extinction-coefficient mip pyramid of the current volume for the DOS
  * renderer (ExtinctionCoefficientVolume, extcoefvolumegenerator.cpp:230-408): level 0 at
  * res (NULL: 128^3) is a 7^3 Gaussian (sigma0, default 1) of the opacity TF

@@ -205,6 +205,11 @@ class _FakeLib:
         self.calls.append(("render", self.stream, out._obj.rgba))
         return 0
 
+    def cvr_render_rc1pass_frames(self, h, frames, n, params, outs):
+        self.calls.append(("render_n", self.stream, n, [outs[j].rgba for j in range(n)],
+                           [outs[j].total for j in range(n)]))
+        return 0
+
     def cvr_gather_tiles_n(self, h, fr, nframes, buf, tpr, fmt, g, imgs):
         self.calls.append(("gather", self.stream, nframes, buf, g is not None))
         return 0
@@ -277,11 +282,69 @@ def _native_flow_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_native_split_control_flow_gloo():
+def _native_batch_worker(rank, world, port, q):
+    """The same fast path with frames_per_launch = 4: a group's frames render in ONE
+    cvr_render_rc1pass_frames call (slots 0..3 of the group's buffer, only frame 0
+    with the total), then its gather; the partial group at flush renders its 2."""
+    from cpp_volume_rendering_amd import _native as N
+    from cpp_volume_rendering_amd.renderer import Camera
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fake = _FakeLib()
+        N._lib = fake
+
+        class R:
+            _ENTRY = "cvr_render_rc1pass"
+            _params = N.Rc1passParams()
+
+            class device:
+                handle = 1
+
+                @staticmethod
+                def set_stream(s):
+                    fake.stream = s
+
+        D_, L = 3, 4
+        sp = T.ScreenTileSplit(R(), 96, 64, tile=32, fmt=N.FORMAT_RGBA16F, device="cpu",
+                               transport="rccl", streams=D_, frames_per_exchange=2,
+                               stream_factory=_FakeStream, count_samples=True,
+                               frames_per_launch=L)
+        assert sp._fast is not None and sp.G == L and sp.L == L
+        cam = Camera(**D.INITIAL_STATE_CAMERA)
+        for _ in range(10):
+            sp.submit(cam)
+        assert [c[0] for c in fake.calls if c[0] in ("render", "render_n", "gather")] == \
+            ["render_n", "gather", "render_n", "gather"]
+        sp.flush()
+        calls = [c for c in fake.calls if c[0] in ("render", "render_n", "gather")]
+        assert [c[0] for c in calls] == ["render_n", "gather"] * 3
+        renders = [c for c in calls if c[0] == "render_n"]
+        gathers = [c for c in calls if c[0] == "gather"]
+        assert [r[2] for r in renders] == [4, 4, 2] and [g[2] for g in gathers] == [4, 4, 2]
+        streams = [s.cuda_stream for s in sp.streams]
+        for grp, (rc, g) in enumerate(zip(renders, gathers)):
+            assert rc[1] == streams[grp % D_] and g[1] == streams[grp % D_]
+            blk = (sp.gathered[grp % D_][0] if rank == 0 else sp.packed[grp % D_])
+            assert rc[3] == [blk[j].data_ptr() for j in range(rc[2])]
+            assert rc[4][0] == sp.total.data_ptr() and not any(rc[4][1:])
+        sp.close()
+        q.put(("ok", rank, len(gathers)))
+    except Exception as e:   # noqa: BLE001  (reported to the parent)
+        q.put(("fail", rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("worker", ["flow", "batch"])
+def test_native_split_control_flow_gloo(worker):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_native_flow_worker, args=(r, 2, port, q)) for r in range(2)]
+    target = _native_flow_worker if worker == "flow" else _native_batch_worker
+    procs = [ctx.Process(target=target, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

@@ -87,17 +87,25 @@ for q, bst in itertools.product([int(x) for x in a.quad.split(",")], [int(x) for
                     frame = make_frame(Camera(**D.INITIAL_STATE_CAMERA), W, W, tile, rk, nr) \
                         if nr > 1 else make_frame(Camera(**D.INITIAL_STATE_CAMERA), W, W)
                     npx = T.tiles_for_rank(W, W, tile, rk, nr) * tile * tile if nr > 1 else W * W
-                    bufs = [torch.zeros((npx, 4), dtype=torch.float16, device="cuda") for _ in range(ns)]
+                    G = a.frames_per_launch
+                    real_mf = G > 1 and "CVR_LIB_OVERRIDE" not in os.environ   # else a probe build
+                    nb = ns * (G if real_mf else 1)
+                    bufs = [torch.zeros((npx, 4), dtype=torch.float16, device="cuda") for _ in range(nb)]
                     outs = [N.Output(b.data_ptr(), None, None, 1, 1) for b in bufs]
                     best = 1e9
+                    nl = a.frames // G if real_mf else a.frames       # launches
                     for rep in range(3):
                         torch.cuda.synchronize()
                         t0 = time.perf_counter()
-                        for i in range(a.frames):
+                        for i in range(nl):
                             L.cvr_set_stream(handle, ctypes.c_void_p(pool[i % ns].cuda_stream))
-                            render(frame, outs[i % ns])
+                            if real_mf:   # cvr_render_rc1pass_frames: G frames per call
+                                k = i % ns
+                                r.render_frames_to([frame] * G, outs[k * G:(k + 1) * G])
+                            else:
+                                render(frame, outs[i % ns])
                         torch.cuda.synchronize()
-                        best = min(best, (time.perf_counter() - t0) / (a.frames * a.frames_per_launch) * 1e3)
+                        best = min(best, (time.perf_counter() - t0) / (nl * G) * 1e3)
                     per.append(best)
                 line = dict(renderer=a.renderer, frames_per_launch=a.frames_per_launch, tile_order=a.tile_order,
                             lib=os.environ.get("CVR_LIB_OVERRIDE", "in-tree"), nranks=nr, tile=tile, quad=q, boost=bst, streams=ns, hwq=int(a.hwq),
