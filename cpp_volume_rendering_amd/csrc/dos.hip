@@ -290,6 +290,17 @@ __device__ __forceinline__ float4 load_section(const float4* sec, int i) {
 }
 typedef const float4* ConstSections;
 
+// Sections per batch of the 1-ray and 3-ray stages (loads in flight per lane:
+// U and 3U; the 7-ray stage issues 4 + 3)
+#ifndef CVR_DOS_U1
+#define CVR_DOS_U1 4
+#endif
+#ifndef CVR_DOS_SPLIT7
+#define CVR_DOS_SPLIT7 4   // the 7-ray stage's fetches in groups of 4 + 3 rays (3: 3+2+2, 2: 2+2+2+1)
+#endif
+#ifndef CVR_DOS_U3
+#define CVR_DOS_U3 2
+#endif
 template <int J, int U, int J0, int JN, int FB>
 __device__ __forceinline__ void cone_sections(const DosArgs& Q, const DosCone& C,
                                               const uint4* __restrict__ ext, const float4 (&e)[U],
@@ -353,7 +364,16 @@ __device__ __forceinline__ void cone_step(const DosArgs& Q, const DosCone& C,
     tr[q] = track;
     track += e[q].x;
   }
-  if (J == 7) {
+  if (J == 7 && CVR_DOS_SPLIT7 == 2) {
+    cone_sections<J, U, 0, 2, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+    cone_sections<J, U, 2, 2, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+    cone_sections<J, U, 4, 2, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+    cone_sections<J, U, 6, 1, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+  } else if (J == 7 && CVR_DOS_SPLIT7 == 3) {
+    cone_sections<J, U, 0, 3, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+    cone_sections<J, U, 3, 2, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+    cone_sections<J, U, 5, 2, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
+  } else if (J == 7) {
     cone_sections<J, U, 0, 4, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
     cone_sections<J, U, 4, 3, FB>(Q, C, ext, e, tr, vk, pos, rays, last, nf);
   } else {
@@ -444,7 +464,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
   int s = 0;
   {
     const f3 vk[1] = {k};
-    cone_stage<1, 4, FB>(Q, C, ext, sec, s, C.counts[0], track, vk, pos, rays, last, nf, C.exit[0]);
+    cone_stage<1, CVR_DOS_U1, FB>(Q, C, ext, sec, s, C.counts[0], track, vk, pos, rays, last, nf, C.exit[0]);
   }
   if (C.counts[1] + C.counts[2] == 0) return cvr_expf(-rays[0]);
   rays[2] = rays[0]; rays[1] = rays[0];
@@ -453,7 +473,7 @@ __device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __r
     f3 vk[3];
 #pragma unroll
     for (int j = 0; j < 3; j++) vk[j] = cone_axis(C.axes + 3 * j, k, u, v);
-    cone_stage<3, 2, FB>(Q, C, ext, sec, s, C.counts[1], track, vk, pos, rays, last, nf, C.exit[1]);
+    cone_stage<3, CVR_DOS_U3, FB>(Q, C, ext, sec, s, C.counts[1], track, vk, pos, rays, last, nf, C.exit[1]);
   }
   if (C.counts[2] == 0)
     return ((cvr_expf(-rays[0]) + cvr_expf(-rays[1])) + cvr_expf(-rays[2])) / 3.0f;

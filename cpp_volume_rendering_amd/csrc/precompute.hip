@@ -160,39 +160,47 @@ hipError_t launch_gradient(const Ctx& c, int mode, uint2* tmp, hipStream_t s) {
 // Rank r's k-th tile sits at tile slot r * rank_stride + k of `packed` (rank_stride
 // = tpr_max for one frame per exchange; nframes * tpr_max when several frames
 // travel together and `packed` points at frame j's first slot).
+// One workgroup per tile slot: the slot's rank, index and screen position are
+// worked out once (wave-uniform 32-bit math; round 3 did it per pixel with 64-bit
+// divisions, ~10 us per 1024^2 frame), then 256 lanes copy the tile's pixels,
+// coalesced on both sides (a 16-pixel row is 128 B of RGBA16F).
 template <typename PX>
-__global__ void unpack_tiles_kernel(const PX* __restrict__ packed, PX* __restrict__ out,
-                                    int W, int H, int tile, int nranks, int tpr_max,
-                                    size_t rank_stride, int ntx, size_t n) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  size_t tt = (size_t)tile * tile;
-  size_t slot = i / tt;                     // rank * tpr_max + k
-  int inner = (int)(i - slot * tt);
-  int r = (int)(slot / (size_t)tpr_max), k = (int)(slot % (size_t)tpr_max);
+__global__ void __launch_bounds__(256)
+unpack_tiles_kernel(const PX* __restrict__ packed, PX* __restrict__ out, int W, int H, int tile,
+                    int nranks, int tpr_max, size_t rank_stride, int ntx) {
+  const int slot = blockIdx.x;                       // rank * tpr_max + k
+  const int r = slot / tpr_max, k = slot - r * tpr_max;
   int tx, ty;
   split_tile(r, nranks, k, ntx, tx, ty);
-  int px = tx * tile + inner % tile, py = ty * tile + inner / tile;
-  if (px < W && py < H && ty * tile < H)
-    out[(size_t)py * W + px] = packed[((size_t)r * rank_stride + k) * tt + inner];
+  if (ty * tile >= H) return;                        // a padding slot past the rank's tiles
+  const PX* __restrict__ src = packed + ((size_t)r * rank_stride + k) * ((size_t)tile * tile);
+  const int x0 = tx * tile, y0 = ty * tile;
+  if (tile == 16) {
+    const int inner = threadIdx.x, px = x0 + (inner & 15), py = y0 + (inner >> 4);
+    if (px < W && py < H) out[(size_t)py * W + px] = src[inner];
+    return;
+  }
+  for (int inner = threadIdx.x; inner < tile * tile; inner += blockDim.x) {
+    const int px = x0 + inner % tile, py = y0 + inner / tile;
+    if (px < W && py < H) out[(size_t)py * W + px] = src[inner];
+  }
 }
 
 hipError_t launch_unpack_tiles(const void* packed, void* out, int half, int W, int H, int tile,
                                int nranks, int tpr_max, hipStream_t s, size_t rank_stride) {
   int ntx = (W + tile - 1) / tile;
-  size_t n = (size_t)nranks * tpr_max * tile * tile;
-  int bs = 256;
-  size_t nb = (n + bs - 1) / bs;
-  if (n == 0) return hipSuccess;
+  const long long nslots = (long long)nranks * tpr_max;
+  if (nslots == 0) return hipSuccess;
+  if (nslots > 0x7fffffffLL) return hipErrorInvalidValue;
   if (rank_stride == 0) rank_stride = (size_t)tpr_max;
   if (half)
-    hipLaunchKernelGGL(unpack_tiles_kernel<uint2>, dim3((unsigned)nb), dim3(bs), 0, s,
+    hipLaunchKernelGGL(unpack_tiles_kernel<uint2>, dim3((unsigned)nslots), dim3(256), 0, s,
                        (const uint2*)packed, (uint2*)out, W, H, tile, nranks, tpr_max, rank_stride,
-                       ntx, n);
+                       ntx);
   else
-    hipLaunchKernelGGL(unpack_tiles_kernel<float4>, dim3((unsigned)nb), dim3(bs), 0, s,
+    hipLaunchKernelGGL(unpack_tiles_kernel<float4>, dim3((unsigned)nslots), dim3(256), 0, s,
                        (const float4*)packed, (float4*)out, W, H, tile, nranks, tpr_max,
-                       rank_stride, ntx, n);
+                       rank_stride, ntx);
   return hipGetLastError();
 }
 

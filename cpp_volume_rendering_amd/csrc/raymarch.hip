@@ -37,11 +37,7 @@ constexpr bool kPhongClassifyFull = true;
 #else
 constexpr bool kPhongClassifyFull = false;
 #endif
-#ifdef CVR_PHONG_GRAD_EARLY
-constexpr bool kPhongGradEarly = true;
-#else
-constexpr bool kPhongGradEarly = false;
-#endif
+
 
 // Macro-cell skip.  The macro cell m (2^mshift texels a side) of a sample is
 // taken from its clamped texel coordinate exactly as sample_pos computes it; its
@@ -246,22 +242,6 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
         else src[j] = classify<FB>(tfp, fn, trilerp_cell(raw[j], sp[j].ax, sp[j].ay, sp[j].az));
       }
     }
-    // Blinn-Phong: the gradient cells of the batch's visible samples are loaded
-    // here, together, so that their round trip overlaps the batch's other
-    // samples instead of stalling the composite once per shaded sample
-    // (CVR_PHONG_GRAD_LATE: loaded where each sample is shaded, round 3)
-    uint4 gq[PHONG ? K : 1][3];
-    if (PHONG && kPhongGradEarly) {
-#pragma unroll
-      for (int j = 0; j < K; j++) {
-        if (!(CS > 0 && we[j]) && src[j].w > 0.0f) {
-          const uint4* g = grad + 3 * (size_t)sp[j].idx;
-          gq[j][0] = g[0];
-          gq[j][1] = g[1];
-          gq[j][2] = g[2];
-        }
-      }
-    }
     bool visible = false;
     // stage 3: front-to-back composite + ERT, in sample order.  The branches
     // matter: a wave whose samples are all transparent (empty space) skips
@@ -284,14 +264,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
               sc.z = lerpf(t0.z, t1.z, tfa[j]);
             }
             if (PHONG) {
-              if (kPhongGradEarly) {
-                const f3 g{trilerp_cell<false, false>(gq[j][0], sp[j].ax, sp[j].ay, sp[j].az),
-                           trilerp_cell<false, false>(gq[j][1], sp[j].ax, sp[j].ay, sp[j].az),
-                           trilerp_cell<false, false>(gq[j][2], sp[j].ax, sp[j].ay, sp[j].az)};
-                phong_rgb(A, g, phong_wpos(r.dir, tj[j], r.tpos, hg), eye, sc);
-              } else {
-                shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
-              }
+              shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
               nshade++;
             }
             const float x = -(sc.w * hj[j]);

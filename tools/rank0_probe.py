@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Rank 0's whole frame loop at N ranks, emulated on one GPU: rank 0's
+share of the headline frame (512^3 ML, 1024^2) rendered L frames per launch
+(cvr_render_rc1pass_frames) into its block of the gather buffer, then on a
+separate communication stream the other N-1 ranks' bytes LANDING in the gather
+buffer (a device-to-device copy of the same size stands in for RCCL's receive;
+the xGMI transfer time itself is not on one GPU and is bounded separately) and
+the unpack of every frame into the image (cvr_unpack_tiles_device_n), with the
+render stream of a buffer set waiting for its previous exchange, as
+cvr_gather_tiles_n orders them.  Host calls included.  Prints ms per frame with
+and without the exchange, for F frames (20 = the driver's command; 96 = steady).
+Usage: python tools/rank0_probe.py [--nranks 8] [--streams 4] [--frames-per-launch 4]
+       [--frames 20,96] [--out FILE]"""
+import os
+import sys
+
+os.environ["GPU_MAX_HW_QUEUES"] = (sys.argv[sys.argv.index("--hwq") + 1]
+                                   if "--hwq" in sys.argv else "32")
+import argparse  # noqa: E402
+import ctypes  # noqa: E402
+import json  # noqa: E402
+import time  # noqa: E402
+
+import torch  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cpp_volume_rendering_amd import _native as N  # noqa: E402
+from cpp_volume_rendering_amd import datasets as D  # noqa: E402
+from cpp_volume_rendering_amd import screen_tiles as T  # noqa: E402
+from cpp_volume_rendering_amd.renderer import (Camera, DataManager, RayCasting1Pass,  # noqa: E402
+                                               RenderingParameters, build_tf_rgbt, make_frame)
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--nranks", type=int, default=8)
+ap.add_argument("--streams", default="4")
+ap.add_argument("--frames-per-launch", default="4")
+ap.add_argument("--frames", default="20,96")
+ap.add_argument("--tile", type=int, default=16)
+ap.add_argument("--hwq", default="32")
+ap.add_argument("--out", default="")
+ap.add_argument("--parts", default="both", choices=["both", "copy", "unpack"],
+                help="which part of the emulated exchange runs (diagnostics)")
+a = ap.parse_args()
+
+n, W = 512, 1024
+dm = DataManager()
+dm.SetVolume(D.marschner_lobb_u8(n), D.voxel_scale(n))
+dm.SetTransferFunction(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
+r = RayCasting1Pass(0)
+r.SetExternalResources(dm, RenderingParameters(W, W, light_position=D.LIGHT_LIST0_POSITION))
+assert r.Init(W, W)
+cam = Camera(**D.INITIAL_STATE_CAMERA)
+r.PrepareRender(cam)
+L = N.lib()
+h = r.device.handle
+NR, tile = a.nranks, a.tile
+tpr = T.max_tiles_per_rank(W, W, tile, NR)
+frame = make_frame(cam, W, W, tile, 0, NR)
+comm = torch.cuda.Stream(priority=-1)
+res = []
+for G in [int(x) for x in a.frames_per_launch.split(",")]:
+    for ns in [int(x) for x in a.streams.split(",")]:
+        pool = [torch.cuda.Stream() for _ in range(ns)]
+        # buffer set per stream: the gather buffer (NR blocks of G frames) + an image
+        gathered = [torch.zeros((NR, G, tpr, tile, tile, 4), dtype=torch.float16, device="cuda")
+                    for _ in range(ns)]
+        remote = torch.ones((NR - 1, G, tpr, tile, tile, 4), dtype=torch.float16, device="cuda")
+        image = torch.zeros((W, W, 4), dtype=torch.float16, device="cuda")
+        outs = [[N.Output(g[0, j].data_ptr(), None, None, 1, N.FORMAT_RGBA16F) for j in range(G)]
+                for g in gathered]
+        done = [None] * ns
+        for F in [int(x) for x in a.frames.split(",")]:
+            for exch in (False, True):
+                best = 1e9
+                for rep in range(3):
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    for i in range(F // G):
+                        k = i % ns
+                        s = pool[k]
+                        if done[k] is not None:
+                            s.wait_event(done[k])          # the set's previous exchange
+                        L.cvr_set_stream(h, ctypes.c_void_p(s.cuda_stream))
+                        r.render_frames_to([frame] * G, outs[k])
+                        if not exch:
+                            continue
+                        ev = torch.cuda.Event()
+                        ev.record(s)
+                        comm.wait_event(ev)
+                        if a.parts != "unpack":
+                            with torch.cuda.stream(comm):
+                                gathered[k][1:].copy_(remote)   # the other ranks' bytes landing
+                        L.cvr_set_stream(h, ctypes.c_void_p(comm.cuda_stream))
+                        for j in range(G if a.parts != "copy" else 0):
+                            N.check(L.cvr_unpack_tiles_device_n(h, ctypes.byref(frame),
+                                                                gathered[k].data_ptr(), tpr, G, j,
+                                                                N.FORMAT_RGBA16F, image.data_ptr()),
+                                    "unpack", h)
+                        d = torch.cuda.Event()
+                        d.record(comm)
+                        done[k] = d
+                    torch.cuda.synchronize()
+                    best = min(best, (time.perf_counter() - t0) / (F // G * G) * 1e3)
+                    done = [None] * ns
+                line = dict(nranks=NR, frames_per_launch=G, streams=ns, frames=F, exchange=exch,
+                            parts=a.parts,
+                            ms_per_frame=round(best, 5),
+                            inbound_bytes_per_frame=(NR - 1) * tpr * tile * tile * 8)
+                print(json.dumps(line), flush=True)
+                res.append(line)
+if a.out:
+    json.dump(res, open(a.out, "w"), indent=1)
