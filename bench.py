@@ -154,6 +154,9 @@ def parse():
     p.add_argument("--frames-per-launch", type=int, default=0,
                    help="rc1pass: consecutive frames rendered in ONE launch "
                         "(cvr_render_rc1pass_frames, 1..8; default 4, other renderers 1)")
+    p.add_argument("--buffer-sets", type=int, default=0,
+                   help="N > 1: exchange buffer sets rotated over the render streams (default 4 per "
+                        "stream: a render waits for the exchange of its set 4 rounds back)")
     p.add_argument("--quad", type=int, default=-1,
                    help="quad (4 lanes per ray) share of the longest tiles, %% (default 0)")
     p.add_argument("--transport", choices=["rccl", "torch"], default="rccl",
@@ -529,7 +532,8 @@ def main():
         gx = FPL if FPL > 1 else (a.exchange_frames or (2 if world >= 4 else 1))
         split = T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev,
                                   transport=a.transport if world > 1 else None, streams=a.streams,
-                                  frames_per_exchange=gx, frames_per_launch=FPL)
+                                  frames_per_exchange=gx, frames_per_launch=FPL,
+                                  buffer_sets=a.buffer_sets or 4 * a.streams)
     except N.CvrError as e:     # no native communicator: torch's dist.gather instead
         if world == 1 or a.transport != "rccl":
             raise
@@ -845,7 +849,8 @@ def main():
         if world > 1:
             res["config"]["gather"] = (f"{a.transport}: packed {a.format} tiles to rank 0 "
                                        f"({split.G} frame(s) per ncclGather) + unpack of every "
-                                       f"frame, {split.nstreams} render streams")
+                                       f"frame, {split.nstreams} render streams, {split.nbuf} "
+                                       f"buffer sets")
             res["multi_gpu_bit_exact_vs_1gpu_frame"] = split_exact
         if ebs:
             cells = (n + 2) ** 3

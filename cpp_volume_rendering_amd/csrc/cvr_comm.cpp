@@ -26,7 +26,10 @@ struct Comm {
   int nranks = 0, rank = 0;
   hipStream_t stream = nullptr;        // communication stream (gathers + rank-0 unpack)
   hipEvent_t ev_render = nullptr;      // end of the render whose tiles are gathered
-  hipEvent_t ev_gather[2] = {nullptr, nullptr};
+  // end of exchange g at ev_gather[g % kRing]: a render stream waits for the
+  // exchange that last used the buffer set its next render writes
+  static constexpr int kRing = 64;
+  hipEvent_t ev_gather[kRing] = {};
   long long ngather = 0;
 };
 
@@ -173,17 +176,24 @@ cvr_status cvr_gather_tiles_n(cvr_ctx* ctx, const cvr_frame* f, int nframes, con
   } else {
     CNCCL(c, ncclGather(d_packed, nullptr, bytes, ncclChar, 0, m->comm, m->stream));
   }
-  const int k = (int)(m->ngather & 1);
-  CHIP(c, hipEventRecord(m->ev_gather[k], m->stream));
+  const long long g = m->ngather;
+  CHIP(c, hipEventRecord(m->ev_gather[g % Comm::kRing], m->stream));
   // One render stream and two buffers: the next render reuses the buffers of the
   // previous exchange, so the stream waits for the previous gather (this gather
-  // overlaps the next render).  D >= 2 streams rotated with D buffer sets: the
-  // next render on this stream reuses this exchange's buffers, so it waits for
-  // this gather (the other streams render the next frames meanwhile).
-  if (c->split_streams >= 2)
-    CHIP(c, hipStreamWaitEvent(s, m->ev_gather[k], 0));
-  else if (m->ngather > 0)
-    CHIP(c, hipStreamWaitEvent(s, m->ev_gather[k ^ 1], 0));
+  // overlaps the next render).  D >= 2 streams rotated with B >= D buffer sets
+  // (option "gather_sets", a multiple of D; exchange g uses set g % B on stream
+  // g % D): this stream's next render (exchange g + D) writes set (g + D) % B,
+  // last used by exchange g + D - B, so the stream waits for that one -- with
+  // B = D this exchange, with B = 4D one issued three rounds earlier, which has
+  // usually finished, so a slow exchange no longer stalls the render pipeline.
+  if (c->split_streams >= 2) {
+    const int D = c->split_streams;
+    const int B = c->gather_sets > D ? c->gather_sets : D;
+    const long long w = g + D - B;
+    if (w >= 0) CHIP(c, hipStreamWaitEvent(s, m->ev_gather[w % Comm::kRing], 0));
+  } else if (g > 0) {
+    CHIP(c, hipStreamWaitEvent(s, m->ev_gather[(g - 1) % Comm::kRing], 0));
+  }
   m->ngather++;
   return CVR_OK;
 }
@@ -201,7 +211,7 @@ cvr_status cvr_gather_sync(cvr_ctx* ctx) {
   if (!m) return cfail(c, CVR_ERR_STATE, "cvr_gather_sync: cvr_comm_init not called");
   if (m->ngather == 0) return CVR_OK;
   CHIP(c, hipSetDevice(c->device));
-  CHIP(c, hipStreamWaitEvent(c->stream, m->ev_gather[(m->ngather - 1) & 1], 0));
+  CHIP(c, hipStreamWaitEvent(c->stream, m->ev_gather[(m->ngather - 1) % Comm::kRing], 0));
   return CVR_OK;
 }
 

@@ -370,6 +370,7 @@ struct Ctx {
   // multi-GPU gather (cvr_comm.cpp): RCCL communicator, its stream and events
   void* comm = nullptr;
   int split_streams = 1;           // option "split_streams": render streams the caller rotates
+  int gather_sets = 0;             // option "gather_sets": buffer sets the caller rotates (>= split_streams)
   // scratch
   unsigned long long* d_total = nullptr;
   void* d_scratch = nullptr;      // host-output staging

@@ -175,6 +175,20 @@ unpack_tiles_kernel(const PX* __restrict__ packed, PX* __restrict__ out, int W, 
   if (ty * tile >= H) return;                        // a padding slot past the rank's tiles
   const PX* __restrict__ src = packed + ((size_t)r * rank_stride + k) * ((size_t)tile * tile);
   const int x0 = tx * tile, y0 = ty * tile;
+  if (tile == 16 && sizeof(PX) == 8 && (W & 1) == 0) {
+    // RGBA16F: 16 B (two pixels) per lane, 128 lanes per tile (a 16-pixel row = 8 lanes)
+    const int t = threadIdx.x;
+    if (t >= 128) return;
+    const int px = x0 + ((t & 7) << 1), py = y0 + (t >> 3);
+    if (py < H) {
+      const uint4 v = reinterpret_cast<const uint4*>(src)[t];
+      if (px + 1 < W)
+        *reinterpret_cast<uint4*>(out + (size_t)py * W + px) = v;
+      else if (px < W)
+        *reinterpret_cast<uint2*>(out + (size_t)py * W + px) = make_uint2(v.x, v.y);
+    }
+    return;
+  }
   if (tile == 16) {
     const int inner = threadIdx.x, px = x0 + (inner & 15), py = y0 + (inner >> 4);
     if (px < W && py < H) out[(size_t)py * W + px] = src[inner];

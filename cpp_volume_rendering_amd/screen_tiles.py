@@ -144,7 +144,7 @@ class ScreenTileSplit:
                  fmt: int = N.FORMAT_RGBA16F, group=None, device=None, render_fn=None,
                  unpack_fn=None, count_samples: bool = False, transport: str = None,
                  streams: int = None, frames_per_exchange: int = 1, stream_factory=None,
-                 frames_per_launch: int = 1):
+                 frames_per_launch: int = 1, buffer_sets: int = 0):
         self.r = renderer
         self.width = width if width is not None else renderer.width
         self.height = height if height is not None else renderer.height
@@ -190,6 +190,11 @@ class ScreenTileSplit:
         # With the native transport, G = frames_per_exchange consecutive frames share
         # one set (one slot each), render on its stream and travel in ONE gather.
         self.nbuf = max(2, streams)
+        if buffer_sets > self.nbuf:
+            # more buffer sets than streams (a multiple of them): a render stream then
+            # waits for the exchange that used its next set rounds earlier, not for
+            # its own last one (library option gather_sets)
+            self.nbuf = -(-int(buffer_sets) // streams) * streams
         self.G = max(1, int(frames_per_exchange)) if (self.transport == "rccl" and
                                                        self.streams is not None) else 1
         if self.split and self.G == 1:
@@ -264,6 +269,7 @@ class ScreenTileSplit:
         N.check(L.cvr_comm_init(h, self.world, self.rank, uid), "cvr_comm_init", h)
         self._comm = True
         N.check(L.cvr_set_option(h, b"split_streams", self.nstreams), "split_streams", h)
+        N.check(L.cvr_set_option(h, b"gather_sets", self.nbuf), "gather_sets", h)
 
     def close(self):
         if self._comm:

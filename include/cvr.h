@@ -300,6 +300,12 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                0 = per-wave deferred shading inside the march
  *   "flat_group" flat shading: consecutive 64-job chunks per XCD turn (default 8)
  *   "debug_flat_limit" tests: a smaller job-list capacity, to exercise the fallback
+ *   "split_streams" screen-tile split: render streams the caller rotates over its
+ *                cvr_gather_tiles_n calls (1..32, default 1)
+ *   "gather_sets" buffer sets the caller rotates over those calls (a multiple of
+ *                split_streams; 0 = one per stream): exchange g uses set g % B on
+ *                stream g % D, and the stream's next render waits for exchange
+ *                g + D - B, the last user of the set it writes next (0..48)
  * One option changes the arithmetic (and so the image) rather than the speed:
  *   "filter_bits" 0: exact float GL_LINEAR weights (CVR-SPEC, the default);
  *                8: every GL_LINEAR weight (volume, gradient, TF; ray_marching_1p.comp:133,

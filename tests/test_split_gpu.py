@@ -316,3 +316,63 @@ def test_rccl_one_rank_grouped_gather(dev, bonsai_tf):
     finally:
         N.check(L.cvr_comm_destroy(dev.handle), "cvr_comm_destroy", dev.handle)
         dev.set_stream(None)
+
+
+@pytest.mark.parametrize("nstreams,nsets", [(4, 16), (2, 8), (4, 4)])
+def test_rccl_one_rank_buffer_sets(dev, bonsai_tf, nstreams, nsets):
+    """More exchange buffer sets than render streams (option gather_sets, the bench's
+    N > 1 default 4 per stream): groups of G = 4 frames rendered in one launch
+    (cvr_render_rc1pass_frames) into set g % B on stream g % D, exchanged with
+    cvr_gather_tiles_n into images of their own.  Cameras change every frame, so a
+    render that overwrote a set before its exchange had read it would deliver
+    another frame's pixels: every frame of every group is checked bit for bit."""
+    import torch
+    L = N.lib()
+    vol = D.marschner_lobb_u8(64)
+    dev.set_volume(vol, D.voxel_scale(64))
+    dev.set_transfer_function(bonsai_tf)
+    dev.set_gradient(N.GRADIENT_NONE)
+    uid = ctypes.create_string_buffer(N.COMM_ID_BYTES)
+    N.check(L.cvr_comm_unique_id(uid), "uid")
+    N.check(L.cvr_comm_init(dev.handle, 1, 0, uid.raw), "cvr_comm_init", dev.handle)
+    try:
+        N.check(L.cvr_set_option(dev.handle, b"split_streams", nstreams), "opt", dev.handle)
+        N.check(L.cvr_set_option(dev.handle, b"gather_sets", nsets), "opt", dev.handle)
+        W, H, G, ngroups = 96, 80, 4, 3 * nsets // 2
+        streams = [torch.cuda.Stream() for _ in range(nstreams)]
+        sets = [torch.zeros((G, H, W, 4), dtype=torch.float16, device="cuda") for _ in range(nsets)]
+        imgs_t = [[torch.zeros((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(G)]
+                  for _ in range(ngroups)]
+        p = N.Rc1passParams()
+        cams = []
+        for g in range(ngroups):
+            k = g % nsets
+            dev.set_stream(streams[g % nstreams].cuda_stream)
+            frames = []
+            for j in range(G):
+                c = dict(CAMS[(g * G + j) % len(CAMS)])
+                c["eye"] = tuple(e + 3.0 * ((g * G + j) // len(CAMS)) for e in c["eye"])
+                cams.append(c)
+                frames.append(make_frame(Camera(**c), W, H))
+            fa = (N.Frame * G)(*frames)
+            oa = (N.Output * G)(*[N.Output(sets[k][j].data_ptr(), None, None, 1, N.FORMAT_RGBA16F)
+                                  for j in range(G)])
+            N.check(L.cvr_render_rc1pass_frames(dev.handle, fa, G, ctypes.byref(p), oa), "frames",
+                    dev.handle)
+            imgs = (ctypes.c_void_p * G)(*[t.data_ptr() for t in imgs_t[g]])
+            N.check(L.cvr_gather_tiles_n(dev.handle, ctypes.byref(frames[0]), G, sets[k].data_ptr(), 0,
+                                         N.FORMAT_RGBA16F, sets[k].data_ptr(), imgs), "gather_n",
+                    dev.handle)
+        dev.set_stream(torch.cuda.current_stream().cuda_stream)
+        N.check(L.cvr_gather_sync(dev.handle), "sync", dev.handle)
+        torch.cuda.synchronize()
+        for g in range(ngroups):
+            for j in range(G):
+                want = _render(dev, N.FORMAT_RGBA16F, W, H, cam=cams[g * G + j])
+                assert np.array_equal(imgs_t[g][j].cpu().numpy().view(np.uint16),
+                                      want.view(np.uint16)), (g, j)
+    finally:
+        N.check(L.cvr_set_option(dev.handle, b"split_streams", 1), "opt", dev.handle)
+        N.check(L.cvr_set_option(dev.handle, b"gather_sets", 0), "opt", dev.handle)
+        N.check(L.cvr_comm_destroy(dev.handle), "cvr_comm_destroy", dev.handle)
+        dev.set_stream(None)

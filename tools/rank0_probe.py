@@ -38,6 +38,14 @@ ap.add_argument("--frames", default="20,96")
 ap.add_argument("--tile", type=int, default=16)
 ap.add_argument("--hwq", default="32")
 ap.add_argument("--out", default="")
+ap.add_argument("--sets", default="0", help="buffer sets (0: one per stream); a set is reused "
+                "after its previous exchange")
+ap.add_argument("--reserve-cus", default="0",
+                help="render streams created with a CU mask that leaves this many CUs "
+                     "(the mask's top bits) to the exchange (hipExtStreamCreateWithCUMask)")
+ap.add_argument("--render-nranks", default="0",
+                help="rank 0 renders its share of a split over this many ranks (0: --nranks; "
+                     "-1: renders nothing, a gather-only root) -- a lighter root share")
 ap.add_argument("--parts", default="both", choices=["both", "copy", "unpack"],
                 help="which part of the emulated exchange runs (diagnostics)")
 a = ap.parse_args()
@@ -58,17 +66,42 @@ tpr = T.max_tiles_per_rank(W, W, tile, NR)
 frame = make_frame(cam, W, W, tile, 0, NR)
 comm = torch.cuda.Stream(priority=-1)
 res = []
-for G in [int(x) for x in a.frames_per_launch.split(",")]:
-    for ns in [int(x) for x in a.streams.split(",")]:
-        pool = [torch.cuda.Stream() for _ in range(ns)]
+import itertools  # noqa: E402
+_hip = ctypes.CDLL("libamdhip64.so")
+NCU = torch.cuda.get_device_properties(0).multi_processor_count
+
+
+def masked_stream(reserve):
+    """A HIP stream whose kernels run on all CUs but the mask's top `reserve` bits."""
+    if reserve <= 0:
+        return torch.cuda.Stream()
+    words = (NCU + 31) // 32
+    bits = [1 if i < NCU - reserve else 0 for i in range(words * 32)]
+    mask = (ctypes.c_uint32 * words)(*[sum(bits[w * 32 + b] << b for b in range(32)) for w in range(words)])
+    st = ctypes.c_void_p()
+    rc = _hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
+    assert rc == 0, f"hipExtStreamCreateWithCUMask: {rc}"
+    return torch.cuda.ExternalStream(st.value)
+
+
+for G, ns, nsets, rsv, rn in itertools.product([int(x) for x in a.frames_per_launch.split(",")],
+                                               [int(x) for x in a.streams.split(",")],
+                                               [int(x) for x in a.sets.split(",")],
+                                               [int(x) for x in a.reserve_cus.split(",")],
+                                               [int(x) for x in a.render_nranks.split(",")]):
+    if True:
+        rframe = make_frame(cam, W, W, tile, 0, rn if rn > 0 else NR)
+        pool = [masked_stream(rsv) for _ in range(ns)]
+        nsets = nsets or ns
         # buffer set per stream: the gather buffer (NR blocks of G frames) + an image
         gathered = [torch.zeros((NR, G, tpr, tile, tile, 4), dtype=torch.float16, device="cuda")
-                    for _ in range(ns)]
+                    for _ in range(nsets)]
         remote = torch.ones((NR - 1, G, tpr, tile, tile, 4), dtype=torch.float16, device="cuda")
         image = torch.zeros((W, W, 4), dtype=torch.float16, device="cuda")
+        # rank 0 renders into the start of its block (a lighter share fits in it)
         outs = [[N.Output(g[0, j].data_ptr(), None, None, 1, N.FORMAT_RGBA16F) for j in range(G)]
                 for g in gathered]
-        done = [None] * ns
+        done = [None] * nsets
         for F in [int(x) for x in a.frames.split(",")]:
             for exch in (False, True):
                 best = 1e9
@@ -76,17 +109,19 @@ for G in [int(x) for x in a.frames_per_launch.split(",")]:
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
                     for i in range(F // G):
-                        k = i % ns
-                        s = pool[k]
+                        k = i % nsets
+                        s = pool[i % ns]
                         if done[k] is not None:
                             s.wait_event(done[k])          # the set's previous exchange
                         L.cvr_set_stream(h, ctypes.c_void_p(s.cuda_stream))
-                        r.render_frames_to([frame] * G, outs[k])
+                        if rn >= 0:
+                            r.render_frames_to([rframe] * G, outs[k])
                         if not exch:
                             continue
-                        ev = torch.cuda.Event()
-                        ev.record(s)
-                        comm.wait_event(ev)
+                        if rn >= 0:
+                            ev = torch.cuda.Event()
+                            ev.record(s)
+                            comm.wait_event(ev)
                         if a.parts != "unpack":
                             with torch.cuda.stream(comm):
                                 gathered[k][1:].copy_(remote)   # the other ranks' bytes landing
@@ -101,8 +136,11 @@ for G in [int(x) for x in a.frames_per_launch.split(",")]:
                         done[k] = d
                     torch.cuda.synchronize()
                     best = min(best, (time.perf_counter() - t0) / (F // G * G) * 1e3)
-                    done = [None] * ns
-                line = dict(nranks=NR, frames_per_launch=G, streams=ns, frames=F, exchange=exch,
+                    done = [None] * nsets
+                line = dict(nranks=NR, render_nranks=rn, frames_per_launch=G, streams=ns, sets=nsets,
+                            reserve_cus=rsv,
+                            frames=F,
+                            exchange=exch,
                             parts=a.parts,
                             ms_per_frame=round(best, 5),
                             inbound_bytes_per_frame=(NR - 1) * tpr * tile * tile * 8)

@@ -5,10 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=${TAG:-r04_s15}
-for p in copy unpack both; do
-  timeout -k 10 300 python -u tools/rank0_probe.py --nranks 8 --streams 4 --frames-per-launch 4 --frames 96 --parts $p > gpurun_out/${T}_rank0_$p.log 2>&1 || { tail -5 gpurun_out/${T}_rank0_$p.log; exit 1; }
-  grep -v amdgpu.ids gpurun_out/${T}_rank0_$p.log
-done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o rank0 --output-format csv -- python3 tools/rank0_probe.py --nranks 8 --streams 4 --frames-per-launch 4 --frames 96 > gpurun_out/${T}_rank0_prof.log 2>&1 || { tail -5 gpurun_out/${T}_rank0_prof.log; exit 1; }
-find gpurun_out/${T}_prof -name "*kernel_stats*" -exec head -12 {} \;
+T=${TAG:-r04_s17}
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_split_gpu.py -m gpu > gpurun_out/${T}_pytest.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/${T}_pytest.log | head -20; exit 1; }
+timeout -k 10 600 python -u tools/rank0_probe.py --nranks 8 --streams 4 --sets 16 --reserve-cus 0,32 --render-nranks 0,12,16,-1 --frames-per-launch 4 --frames 20,96 > gpurun_out/${T}_rank0.log 2>&1 || { tail -5 gpurun_out/${T}_rank0.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/${T}_rank0.log
