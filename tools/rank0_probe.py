@@ -28,7 +28,9 @@ from cpp_volume_rendering_amd import _native as N  # noqa: E402
 from cpp_volume_rendering_amd import datasets as D  # noqa: E402
 from cpp_volume_rendering_amd import screen_tiles as T  # noqa: E402
 from cpp_volume_rendering_amd.renderer import (Camera, DataManager, RayCasting1Pass,  # noqa: E402
-                                               RenderingParameters, build_tf_rgbt, make_frame)
+                                               RC1PConeTracingDirOcclusionShading,
+                                               RC1PExtinctionBasedShading, RenderingParameters,
+                                               build_ext_lut, build_tf_rgbt, make_frame)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--nranks", type=int, default=8)
@@ -46,15 +48,25 @@ ap.add_argument("--reserve-cus", default="0",
 ap.add_argument("--render-nranks", default="0",
                 help="rank 0 renders its share of a split over this many ranks (0: --nranks; "
                      "-1: renders nothing, a gather-only root) -- a lighter root share")
+ap.add_argument("--renderer", choices=["rc1pass", "dos", "ebs"], default="rc1pass",
+                help="dos / ebs: configs 4 / 5 (one frame per launch)")
 ap.add_argument("--parts", default="both", choices=["both", "copy", "unpack"],
                 help="which part of the emulated exchange runs (diagnostics)")
 a = ap.parse_args()
 
-n, W = 512, 1024
+n, W = (1024, 1024) if a.renderer == "ebs" else ((512, 2048) if a.renderer == "dos" else (512, 1024))
 dm = DataManager()
 dm.SetVolume(D.marschner_lobb_u8(n), D.voxel_scale(n))
-dm.SetTransferFunction(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
-r = RayCasting1Pass(0)
+dm.SetTransferFunction(build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA),
+                       build_tf_rgbt(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA, extinction_input=True))
+if a.renderer == "dos":                      # bench.py --renderer dos (config 4)
+    r = RC1PConeTracingDirOcclusionShading(0)
+    r.glsl_apply_shadow = True
+elif a.renderer == "ebs":                    # bench.py --renderer ebs (config 5)
+    dm.SetExtinctionTable(build_ext_lut(D.BONSAI_TF_RGB, D.BONSAI_TF_ALPHA))
+    r = RC1PExtinctionBasedShading(0)
+else:
+    r = RayCasting1Pass(0)
 r.SetExternalResources(dm, RenderingParameters(W, W, light_position=D.LIGHT_LIST0_POSITION))
 assert r.Init(W, W)
 cam = Camera(**D.INITIAL_STATE_CAMERA)
@@ -114,8 +126,10 @@ for G, ns, nsets, rsv, rn in itertools.product([int(x) for x in a.frames_per_lau
                         if done[k] is not None:
                             s.wait_event(done[k])          # the set's previous exchange
                         L.cvr_set_stream(h, ctypes.c_void_p(s.cuda_stream))
-                        if rn >= 0:
+                        if rn >= 0 and G > 1:
                             r.render_frames_to([rframe] * G, outs[k])
+                        elif rn >= 0:
+                            r.render_to(rframe, outs[k][0])
                         if not exch:
                             continue
                         if rn >= 0:
