@@ -157,6 +157,9 @@ def parse():
     p.add_argument("--buffer-sets", type=int, default=0,
                    help="N > 1: exchange buffer sets rotated over the render streams (default 4 per "
                         "stream: a render waits for the exchange of its set 4 rounds back)")
+    p.add_argument("--root-renders", type=int, default=-1, choices=[-1, 0, 1],
+                   help="N > 1: 0 = rank 0 only gathers and unpacks, ranks 1..N-1 render the split "
+                        "(-1: 0 for rc1pass at >= 4 GPUs, else 1; DESIGN §7a)")
     p.add_argument("--quad", type=int, default=-1,
                    help="quad (4 lanes per ray) share of the longest tiles, %% (default 0)")
     p.add_argument("--transport", choices=["rccl", "torch"], default="rccl",
@@ -530,10 +533,39 @@ def main():
         # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
         # on rank 0) would otherwise rival a rank's share of the frame (~23 us at N = 8)
         gx = FPL if FPL > 1 else (a.exchange_frames or (2 if world >= 4 else 1))
-        split = T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev,
-                                  transport=a.transport if world > 1 else None, streams=a.streams,
-                                  frames_per_exchange=gx, frames_per_launch=FPL,
-                                  buffer_sets=a.buffer_sets or 4 * a.streams)
+        # rank 0's exchange (receive + unpack of 7/8 of every frame at N = 8) competes
+        # with its own render and stalls it (tools/rank0_probe.py: 0.0295 ms per
+        # frame against 0.0125 for a render-only rank); with 3+ render ranks the root
+        # only gathers (0.0094 ms per frame) and N - 1 ranks render
+        root_renders = (a.root_renders == 1 or world < 4 or a.renderer != "rc1pass"
+                        or a.transport != "rccl") if a.root_renders != 0 else False
+
+        def make_split(root):
+            return T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev,
+                                     transport=a.transport if world > 1 else None,
+                                     streams=a.streams, frames_per_exchange=gx,
+                                     frames_per_launch=FPL,
+                                     buffer_sets=a.buffer_sets or 4 * a.streams,
+                                     root_renders=root)
+        split = make_split(root_renders)
+        if world > 1 and not root_renders:
+            # pre-flight: one frame through the idle-root exchange must equal rank 0's
+            # own render of the whole frame, else the bench falls back to a rendering root
+            split.render(cam)
+            ok = torch.ones((1,), dtype=torch.int32, device=dev)
+            if rank == 0:
+                full = torch.zeros_like(split.image)
+                r.render_to(make_frame(cam, W, H), N.Output(full.data_ptr(), None, None, 1, fmt))
+                torch.cuda.synchronize(dev)
+                view = torch.int16 if fmt else torch.int32
+                ok[0] = int(torch.equal(full.view(view), split.image.view(view)))
+            dist.broadcast(ok, src=0)
+            if not int(ok.item()):
+                print(f"rank {rank}: the idle-root exchange did not reproduce the frame; "
+                      f"rank 0 renders its share instead", file=sys.stderr)
+                split.close()
+                root_renders = True
+                split = make_split(True)
     except N.CvrError as e:     # no native communicator: torch's dist.gather instead
         if world == 1 or a.transport != "rccl":
             raise
@@ -541,9 +573,10 @@ def main():
               file=sys.stderr)
         a.transport = "torch"
         split = T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev, transport="torch")
+    renders = split.renders if world > 1 else True       # False: rank 0 only gathers
     if world > 1:
-        frames = [make_frame(c, W, H, tile, rank, world) for c in cams]
-        k = T.tiles_for_rank(W, H, tile, rank, world)
+        frames = [make_frame(c, W, H, tile, split.srank, split.sworld) for c in cams]
+        k = split.k
         pixels = k * tile * tile
         out_buf = split.packed[0]
     else:
@@ -566,6 +599,9 @@ def main():
     S_cam = []
     shade = (ctypes.c_uint64 * 3)()
     for i in range(len(frames)):
+        if not renders:
+            S_cam.append(0)
+            continue
         total.zero_()
         step_once(i)
         torch.cuda.synchronize(dev)
@@ -630,10 +666,12 @@ def main():
     # With multi-frame launches the pass times the same launches as the timed region:
     # floor(steps / FPL) launches of FPL frames (the roofline's bytes are per launch).
     n_launch = max(1, a.steps // FPL)
-    N.check(L.cvr_set_option(r.device.handle, b"kernel_timing", n_launch), "kernel_timing",
-            r.device.handle)
+    N.check(L.cvr_set_option(r.device.handle, b"kernel_timing", n_launch if renders else 0),
+            "kernel_timing", r.device.handle)
     total.zero_()
-    if FPL > 1:
+    if not renders:
+        S_timed = 0
+    elif FPL > 1:
         mf_bufs = [out_buf] + [torch.empty_like(out_buf) for _ in range(FPL - 1)]
         mf_outs = [N.Output(mf_bufs[j].data_ptr(), None, total.data_ptr() if j == 0 else None, 1, fmt)
                    for j in range(FPL)]
@@ -645,14 +683,26 @@ def main():
             step_once(i)
         S_timed = S_rank_steps
     torch.cuda.synchronize(dev)
-    kt = (ctypes.c_float * n_launch)()
-    nkt = ctypes.c_int()
-    N.check(L.cvr_read_kernel_times(r.device.handle, kt, n_launch, ctypes.byref(nkt)),
-            "cvr_read_kernel_times", r.device.handle)
-    assert nkt.value == n_launch
-    kern_ms = float(np.mean(kt[:nkt.value]))
+    kern_ms = 0.0
+    if renders:
+        kt = (ctypes.c_float * n_launch)()
+        nkt = ctypes.c_int()
+        N.check(L.cvr_read_kernel_times(r.device.handle, kt, n_launch, ctypes.byref(nkt)),
+                "cvr_read_kernel_times", r.device.handle)
+        assert nkt.value == n_launch
+        kern_ms = float(np.mean(kt[:nkt.value]))
     assert int(total.item()) == S_timed, "sample count changed between frames"
     S_launch = int(round(S_timed / n_launch))            # samples per launch (FPL frames)
+    roof_src = "this rank"
+    if world > 1 and split.idle_root:
+        # an idle root renders nothing: the roofline is rank 1's share (same launches)
+        v = torch.tensor([kern_ms, S_launch, pixels, shade[0], shade[1], shade[2]],
+                         dtype=torch.float64, device=dev)
+        dist.broadcast(v, src=1)
+        kern_ms, S_launch, pixels = float(v[0]), int(v[1]), int(v[2])
+        for q in range(3):
+            shade[q] = int(v[3 + q])
+        roof_src = "rank 1 (rank 0 only gathers)"
     batch = L.cvr_get_option(r.device.handle, b"batch") or (2 if a.phong else 4)   # 0 = auto
     macro = L.cvr_get_option(r.device.handle, b"macro")
 
@@ -713,7 +763,7 @@ def main():
                 "traffic": pmc.get("hbm_bytes_per_launch"),
                 "kernel": kname,
                 "kernel_ms": round(kern_ms, 4),
-                "frames_per_launch": FPL,
+                "frames_per_launch": FPL, "share": roof_src,
                 "bytes_alg_per_launch": b_alg, "samples_per_launch": S_launch,
                 # the same bytes over the frame time of the timed region (frames in
                 # flight overlap, so a frame takes less than one launch's duration)
@@ -850,7 +900,9 @@ def main():
             res["config"]["gather"] = (f"{a.transport}: packed {a.format} tiles to rank 0 "
                                        f"({split.G} frame(s) per ncclGather) + unpack of every "
                                        f"frame, {split.nstreams} render streams, {split.nbuf} "
-                                       f"buffer sets")
+                                       f"buffer sets, "
+                                       + ("rank 0 only gathers (N - 1 render ranks)"
+                                          if split.idle_root else "every rank renders"))
             res["multi_gpu_bit_exact_vs_1gpu_frame"] = split_exact
         if ebs:
             cells = (n + 2) ** 3

@@ -421,6 +421,11 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->max_waves_cu = value;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "gather_root_idle")) {
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "gather_root_idle must be 0 or 1");
+    c->gather_root_idle = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "gather_sets")) {
     if (value < 0 || value > 48) return fail(c, CVR_ERR_ARG, "gather_sets must be 0..48");
     c->gather_sets = value;
@@ -475,6 +480,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "async_order")) return c->async_order;
   if (!std::strcmp(key, "split_streams")) return c->split_streams;
   if (!std::strcmp(key, "gather_sets")) return c->gather_sets;
+  if (!std::strcmp(key, "gather_root_idle")) return c->gather_root_idle;
   if (!std::strcmp(key, "sat_build_us")) return c->sat_build_us;   // read-only
   if (!std::strcmp(key, "order_interval")) return c->order_interval;
   if (!std::strcmp(key, "skip_min_pct")) return c->skip_min_pct;

@@ -136,12 +136,17 @@ cvr_status cvr_gather_tiles_n(cvr_ctx* ctx, const cvr_frame* f, int nframes, con
   if (!f || !d_packed || nframes < 1 || tpr_max < 0 || (f->nranks > 1 && f->tile_size < 16) ||
       (format != CVR_FORMAT_RGBA32F && format != CVR_FORMAT_RGBA16F))
     return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: bad arguments");
-  if (f->nranks != m->nranks || f->rank != m->rank)
-    return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: frame rank %d/%d, communicator %d/%d",
-                 f->rank, f->nranks, m->rank, m->nranks);
+  // gather_root_idle: rank 0 renders nothing; communicator ranks 1..N-1 render the
+  // split over N-1 render ranks (frame rank = communicator rank - 1)
+  const bool idle_root = c->gather_root_idle && m->nranks > 2;
+  const int want_nranks = idle_root ? m->nranks - 1 : m->nranks;
+  const int want_rank = idle_root ? m->rank - 1 : m->rank;
+  if (f->nranks != want_nranks || (f->rank != want_rank && !(idle_root && m->rank == 0)))
+    return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: frame rank %d/%d, communicator %d/%d%s",
+                 f->rank, f->nranks, m->rank, m->nranks, idle_root ? " (idle root)" : "");
   if (m->rank == 0 && (!d_gathered || !d_images))
     return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: rank 0 needs the gather buffer and images");
-  if (m->nranks > 1 && cvr_tiles_for_rank(f, f->rank) > tpr_max)
+  if (m->nranks > 1 && !(idle_root && m->rank == 0) && cvr_tiles_for_rank(f, f->rank) > tpr_max)
     return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: tiles_per_rank_max too small");
   CHIP(c, hipSetDevice(c->device));
   const size_t px = format == CVR_FORMAT_RGBA16F ? 8 : 16;
@@ -157,19 +162,22 @@ cvr_status cvr_gather_tiles_n(cvr_ctx* ctx, const cvr_frame* f, int nframes, con
   // its part in place.
   if (m->rank == 0) {
     char* g = static_cast<char*>(d_gathered);
-    if (d_packed != d_gathered)
+    if (d_packed != d_gathered && !idle_root)
       CHIP(c, hipMemcpyAsync(g, d_packed, bytes, hipMemcpyDeviceToDevice, m->stream));
     CNCCL(c, ncclGather(g, g, bytes, ncclChar, 0, m->comm, m->stream));
+    // idle root: block 0 (its own, in place) holds nothing; render rank v's frames
+    // are block v + 1
+    const char* g0 = idle_root ? g + bytes : g;
     for (int j = 0; j < nframes; j++) {
       void* img = d_images[j];
       if (!img) continue;
-      const char* fj = g + (size_t)j * fbytes;
+      const char* fj = g0 + (size_t)j * fbytes;
       if (m->nranks == 1) {
         if (img != (const void*)fj)
           CHIP(c, hipMemcpyAsync(img, fj, fbytes, hipMemcpyDeviceToDevice, m->stream));
       } else {
         CHIP(c, cvr::launch_unpack_tiles(fj, img, format == CVR_FORMAT_RGBA16F, f->width,
-                                         f->height, f->tile_size, m->nranks, tpr_max, m->stream,
+                                         f->height, f->tile_size, f->nranks, tpr_max, m->stream,
                                          (size_t)nframes * tpr_max));
       }
     }

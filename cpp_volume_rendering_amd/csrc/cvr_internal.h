@@ -371,6 +371,7 @@ struct Ctx {
   void* comm = nullptr;
   int split_streams = 1;           // option "split_streams": render streams the caller rotates
   int gather_sets = 0;             // option "gather_sets": buffer sets the caller rotates (>= split_streams)
+  int gather_root_idle = 0;        // option "gather_root_idle": rank 0 only gathers (renders nothing)
   // scratch
   unsigned long long* d_total = nullptr;
   void* d_scratch = nullptr;      // host-output staging

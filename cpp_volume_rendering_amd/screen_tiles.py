@@ -144,7 +144,7 @@ class ScreenTileSplit:
                  fmt: int = N.FORMAT_RGBA16F, group=None, device=None, render_fn=None,
                  unpack_fn=None, count_samples: bool = False, transport: str = None,
                  streams: int = None, frames_per_exchange: int = 1, stream_factory=None,
-                 frames_per_launch: int = 1, buffer_sets: int = 0):
+                 frames_per_launch: int = 1, buffer_sets: int = 0, root_renders: bool = True):
         self.r = renderer
         self.width = width if width is not None else renderer.width
         self.height = height if height is not None else renderer.height
@@ -174,8 +174,20 @@ class ScreenTileSplit:
         # streams on CPU
         mk = stream_factory or (lambda: torch.cuda.Stream(self.device))
         self.streams = [mk() for _ in range(streams)] if streams > 1 else None
-        self.k = tiles_for_rank(w, h, tile, self.rank, self.world) if self.split else 0
-        self.tpr_max = max_tiles_per_rank(w, h, tile, self.world) if self.split else 0
+        # root_renders=False (native transport, world >= 3): rank 0 only gathers and
+        # unpacks; ranks 1..N-1 render the split over N-1 render ranks (library
+        # option gather_root_idle)
+        self.idle_root = not root_renders and self.split and self.world >= 3
+        if self.idle_root and (self.transport != "rccl" or render_fn is not None or
+                               self.streams is None):
+            raise ValueError("root_renders=False needs the native transport, the library "
+                             "render and >= 2 streams")
+        self.sworld = self.world - 1 if self.idle_root else self.world     # the render split
+        self.srank = max(self.rank - 1, 0) if self.idle_root else self.rank
+        self.renders = not (self.idle_root and self.rank == 0)
+        self.k = (tiles_for_rank(w, h, tile, self.srank, self.sworld)
+                  if self.split and self.renders else 0)
+        self.tpr_max = max_tiles_per_rank(w, h, tile, self.sworld) if self.split else 0
         # frames per launch: rc1pass through the library's own render call only
         self.L = max(1, int(frames_per_launch))
         if (self.L > 1 and (render_fn is not None or renderer is None or
@@ -270,6 +282,7 @@ class ScreenTileSplit:
         self._comm = True
         N.check(L.cvr_set_option(h, b"split_streams", self.nstreams), "split_streams", h)
         N.check(L.cvr_set_option(h, b"gather_sets", self.nbuf), "gather_sets", h)
+        N.check(L.cvr_set_option(h, b"gather_root_idle", int(self.idle_root)), "gather_root_idle", h)
 
     def close(self):
         if self._comm:
@@ -332,10 +345,10 @@ class ScreenTileSplit:
             sptr, outs, buf, g = slots[(n // G) % self.nbuf]
             j = n % G
             L.cvr_set_stream(h, sptr)
-            fr = ctypes.byref(frame)
-            st = entry(h, fr, params, ctypes.byref(outs[j]))
-            if st:
-                N.check(st, self.r._ENTRY, h)
+            if self.renders:
+                st = entry(h, ctypes.byref(frame), params, ctypes.byref(outs[j]))
+                if st:
+                    N.check(st, self.r._ENTRY, h)
             self._group = j + 1
             if self._group == G:
                 self._exchange(G, n)
@@ -386,11 +399,12 @@ class ScreenTileSplit:
         L, h, entry, params, imgs, slots = self._fast
         sptr, outs, buf, gb = slots[g % self.nbuf]
         L.cvr_set_stream(h, sptr)
-        fa = (N.Frame * nb)(*frames)
-        oa = (N.Output * nb)(*outs[:nb])
-        st = L.cvr_render_rc1pass_frames(h, fa, nb, params, oa)
-        if st:
-            N.check(st, "cvr_render_rc1pass_frames", h)
+        if self.renders:
+            fa = (N.Frame * nb)(*frames)
+            oa = (N.Output * nb)(*outs[:nb])
+            st = L.cvr_render_rc1pass_frames(h, fa, nb, params, oa)
+            if st:
+                N.check(st, "cvr_render_rc1pass_frames", h)
         self._frame = frames[-1]
         self._exchange(nb, n0 + nb - 1)
         self.completed = n0 - 1
@@ -413,8 +427,8 @@ class ScreenTileSplit:
         key = (tuple(camera.eye), tuple(camera.center), tuple(camera.up), camera.fovy_deg,
                camera.aspect)
         if key != self._fkey:
-            self._frame = (make_frame(camera, self.width, self.height, self.tile, self.rank,
-                                      self.world) if self.split else
+            self._frame = (make_frame(camera, self.width, self.height, self.tile, self.srank,
+                                      self.sworld) if self.split else
                            make_frame(camera, self.width, self.height))
             self._fkey = key
         return self._frame

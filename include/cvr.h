@@ -306,6 +306,11 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                split_streams; 0 = one per stream): exchange g uses set g % B on
  *                stream g % D, and the stream's next render waits for exchange
  *                g + D - B, the last user of the set it writes next (0..48)
+ *   "gather_root_idle" 1 (communicators of N >= 3 ranks): rank 0 renders nothing and
+ *                only gathers and unpacks; ranks 1..N-1 render the split over N-1
+ *                render ranks (their cvr_frame: rank = communicator rank - 1,
+ *                nranks = N - 1; rank 0 passes a frame of that geometry).  Rank 0's
+ *                block of the gather buffer stays unused.  
  * One option changes the arithmetic (and so the image) rather than the speed:
  *   "filter_bits" 0: exact float GL_LINEAR weights (CVR-SPEC, the default);
  *                8: every GL_LINEAR weight (volume, gradient, TF; ray_marching_1p.comp:133,

@@ -207,7 +207,8 @@ class _FakeLib:
 
     def cvr_render_rc1pass_frames(self, h, frames, n, params, outs):
         self.calls.append(("render_n", self.stream, n, [outs[j].rgba for j in range(n)],
-                           [outs[j].total for j in range(n)]))
+                           [outs[j].total for j in range(n)],
+                           [(frames[j].rank, frames[j].nranks) for j in range(n)]))
         return 0
 
     def cvr_gather_tiles_n(self, h, fr, nframes, buf, tpr, fmt, g, imgs):
@@ -338,20 +339,75 @@ def _native_batch_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("worker", ["flow", "batch"])
+def _native_idle_root_worker(rank, world, port, q):
+    """root_renders=False (library option gather_root_idle): rank 0 renders nothing and
+    only exchanges; ranks 1..N-1 render the split over N-1 render ranks (frame rank =
+    rank - 1), 4 frames per launch; every rank issues the same gathers."""
+    from cpp_volume_rendering_amd import _native as N
+    from cpp_volume_rendering_amd.renderer import Camera
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fake = _FakeLib()
+        N._lib = fake
+
+        class R:
+            _ENTRY = "cvr_render_rc1pass"
+            _params = N.Rc1passParams()
+
+            class device:
+                handle = 1
+
+                @staticmethod
+                def set_stream(s):
+                    fake.stream = s
+
+        sp = T.ScreenTileSplit(R(), 96, 64, tile=16, fmt=N.FORMAT_RGBA16F, device="cpu",
+                               transport="rccl", streams=2, stream_factory=_FakeStream,
+                               frames_per_launch=4, buffer_sets=8, root_renders=False)
+        assert sp.idle_root and sp.sworld == world - 1 and sp.nbuf == 8
+        assert sp.k == (0 if rank == 0 else T.tiles_for_rank(96, 64, 16, rank - 1, world - 1))
+        assert sp.tpr_max == T.max_tiles_per_rank(96, 64, 16, world - 1)
+        cam = Camera(**D.INITIAL_STATE_CAMERA)
+        for _ in range(9):
+            sp.submit(cam)
+        sp.flush()
+        renders = [c for c in fake.calls if c[0] == "render_n"]
+        gathers = [c for c in fake.calls if c[0] == "gather"]
+        assert [g[2] for g in gathers] == [4, 4, 1]
+        if rank == 0:
+            assert renders == []
+        else:
+            assert [r[2] for r in renders] == [4, 4, 1]
+            assert all(fr == (rank - 1, world - 1) for r in renders for fr in r[5])
+        assert ("opt", b"gather_root_idle", 1) in fake.calls
+        assert ("opt", b"gather_sets", 8) in fake.calls
+        sp.close()
+        q.put(("ok", rank, len(gathers)))
+    except Exception as e:   # noqa: BLE001  (reported to the parent)
+        q.put(("fail", rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("worker", ["flow", "batch", "idle_root"])
 def test_native_split_control_flow_gloo(worker):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    target = _native_flow_worker if worker == "flow" else _native_batch_worker
-    procs = [ctx.Process(target=target, args=(r, 2, port, q)) for r in range(2)]
+    target = {"flow": _native_flow_worker, "batch": _native_batch_worker,
+              "idle_root": _native_idle_root_worker}[worker]
+    world = 3 if worker == "idle_root" else 2
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=240)
-    res = [q.get(timeout=10) for _ in range(2)]
+    res = [q.get(timeout=10) for _ in range(world)]
     assert all(r[0] == "ok" for r in res), res
-    assert [p.exitcode for p in procs] == [0, 0]
+    assert [p.exitcode for p in procs] == [0] * world
 
 
 @pytest.mark.parametrize("W,H,tile,world", [(1024, 1024, 16, 8), (1024, 1024, 32, 4),

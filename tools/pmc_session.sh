@@ -10,13 +10,13 @@ export TMPDIR=/tmp
 GRPS="FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum;SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_ANY;TD_TD_BUSY TA_TA_BUSY"
 for w in "$@"; do
   case $w in
-    rc1pass) ARGS="--streams 1"; K=rc1pass_tile_kernel; export PMC_GRID=2097152; OUT=pmc_rc1pass.json;;
-    phong)   ARGS="--streams 1 --phong"; K=rc1pass_tile_kernel; export PMC_GRID=2097152; OUT=pmc_rc1pass_phong.json;;
-    longray) ARGS="--streams 1 --tf-alpha 0.02"; K=rc1pass_tile_kernel; export PMC_GRID=2097152; OUT=pmc_rc1pass_longray.json;;
-    dos)     ARGS="--renderer dos --streams 1"; K=flat_shade_kernel; unset PMC_GRID; OUT=pmc_dos.json;;
-    ebs)     ARGS="--renderer ebs --streams 1"; K=flat_shade_kernel; unset PMC_GRID; OUT=pmc_ebs.json;;
+    rc1pass) ARGS="--streams 1"; K=rc1pass_tile_kernel; export PMC_GRID=8388608 PMC_STEPS=8; OUT=pmc_rc1pass.json;;   # 4 frames per launch x 32768 ordered slots x 64
+    phong)   ARGS="--streams 1 --phong"; K=rc1pass_tile_kernel; export PMC_GRID=8388608 PMC_STEPS=8; OUT=pmc_rc1pass_phong.json;;
+    longray) ARGS="--streams 1 --tf-alpha 0.02"; K=rc1pass_tile_kernel; export PMC_GRID=8388608 PMC_STEPS=8; OUT=pmc_rc1pass_longray.json;;
+    dos)     ARGS="--renderer dos --streams 1"; K=flat_shade_kernel; unset PMC_GRID; export PMC_STEPS=3; OUT=pmc_dos.json;;
+    ebs)     ARGS="--renderer ebs --streams 1"; K=flat_shade_kernel; unset PMC_GRID; export PMC_STEPS=3; OUT=pmc_ebs.json;;
   esac
-  timeout -k 10 400 python3 bench.py $ARGS --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/pmcline_$w.json 2> gpurun_out/pmcline_$w.err || { tail -5 gpurun_out/pmcline_$w.err; exit 1; }
+  timeout -k 10 400 python3 bench.py $ARGS --no-cpu-baseline --steps $PMC_STEPS --warmup 1 > gpurun_out/pmcline_$w.json 2> gpurun_out/pmcline_$w.err || { tail -5 gpurun_out/pmcline_$w.err; exit 1; }
   PMC_TIMEOUT=${PMC_TIMEOUT:-240} bash tools/pmc_bench.sh $w $K "$ARGS" "$GRPS" > gpurun_out/pmc_$w.log 2>&1 || { tail -5 gpurun_out/pmc_$w.log; exit 1; }
   python3 tools/pmc_record.py gpurun_out/pmc_$w/summary.json gpurun_out/pmcline_$w.json gpurun_out/$OUT > /dev/null || exit 1
   python3 -c "import json; d=json.load(open('gpurun_out/$OUT')); print('$w', {k: d.get(k) for k in ('kernel_ns_avg_under_pmc','hbm_bytes_per_launch','tcc_hit_rate','td_busy_frac_per_cu','valu_issue_frac_per_simd','valu_per_sample')})"
