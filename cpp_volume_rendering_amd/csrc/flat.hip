@@ -117,10 +117,10 @@ static void free_ptr(void*& p) {
 }
 
 // Buffers for `ntiles` 8x8 tiles, `jobs` jobs and `rounds` round masks (0: the
-// per-tile part only).  Grows, never shrinks; the job list and the masks get
+// per-tile part only), for frames on stream s.  Grows, never shrinks; the job list and the masks get
 // 1/4 headroom so a slowly moving camera does not re-allocate every frame.
 // Blocks the calling thread only when it allocates.
-hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds) {
+hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds, hipStream_t s) {
   hipError_t e = hipSuccess;
   // growing frees buffers the set's last frame may still read: wait for that
   // frame only (its own event), not for the device
@@ -141,7 +141,11 @@ hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds) {
   }
   if (!J.total) {
     if ((e = hipMalloc((void**)&J.total, 3 * sizeof(unsigned long long))) != hipSuccess) return e;
-    if ((e = hipMemset(J.total, 0, 3 * sizeof(unsigned long long))) != hipSuccess) return e;
+    // on the render stream, ordered before the set's first count/scan: a plain
+    // hipMemset runs on the null stream, which the caller's non-blocking render
+    // streams do not wait for -- it could land after the first frame's scan and
+    // zero its totals (round 4: a DOS frame on a fresh stream came out empty)
+    if ((e = hipMemsetAsync(J.total, 0, 3 * sizeof(unsigned long long), s)) != hipSuccess) return e;
   }
   if (!J.h_total && (e = hipHostMalloc((void**)&J.h_total, 3 * sizeof(unsigned long long))) != hipSuccess)
     return e;

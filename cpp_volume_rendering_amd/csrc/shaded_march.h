@@ -404,7 +404,7 @@ hipError_t launch_shaded_march(const Ctx& c, const typename SH::Args& q, bool ph
 hipError_t launch_flat_scan(FlatJobs& J, int ntiles, unsigned long long cap, unsigned long long rcap,
                             unsigned long long* shade_ctr, hipStream_t s);
 hipError_t launch_flat_fold(const Rc1passArgs& a, FlatJobs& J, float4* out, hipStream_t s);
-hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds);
+hipError_t flat_reserve(FlatJobs& J, int ntiles, size_t jobs, size_t rounds, hipStream_t s);
 FlatJobs& flat_set(const Ctx& c, hipStream_t s);
 
 template <class SH>
@@ -416,7 +416,7 @@ hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool pho
   if (nt <= 0) return hipSuccess;
   if (q.a.tf_n > kMaxTfLds) return hipErrorInvalidValue;
   FlatJobs& J = flat_set(c, s);
-  hipError_t e = flat_reserve(J, nt, 0, 0);
+  hipError_t e = flat_reserve(J, nt, 0, 0, s);
   if (e != hipSuccess) return e;
   const size_t lds = (size_t)(q.a.tf_n + 2) * sizeof(float4);
   const uint4* cells = (const uint4*)c.d_cells;
@@ -432,7 +432,7 @@ hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool pho
   }
   const bool first = J.cap == 0;   // no estimate yet: this frame reads its totals synchronously
   if (!first && (J.want_jobs > J.cap || J.want_rounds > J.rcap)) {
-    if (flat_reserve(J, nt, J.want_jobs, J.want_rounds) != hipSuccess) {
+    if (flat_reserve(J, nt, J.want_jobs, J.want_rounds, s) != hipSuccess) {
       (void)hipGetLastError();   // too large to hold: keep the old size (frames fall back)
       J.want_jobs = std::min(J.want_jobs, J.cap);
       J.want_rounds = std::min(J.want_rounds, J.rcap);
@@ -459,7 +459,7 @@ hipError_t launch_shaded_flat(const Ctx& c, const typename SH::Args& q, bool pho
     const unsigned long long total = J.h_total[0], rounds = J.h_total[1];
     J.want_jobs = (size_t)total;
     J.want_rounds = (size_t)rounds;
-    if (flat_reserve(J, nt, std::max<size_t>((size_t)total, 1), std::max<size_t>((size_t)rounds, 1)) !=
+    if (flat_reserve(J, nt, std::max<size_t>((size_t)total, 1), std::max<size_t>((size_t)rounds, 1), s) !=
         hipSuccess) {
       // more jobs than 32-bit offsets or the free memory hold: the per-wave kernel
       // renders the same frame, bit for bit, without a job list

@@ -58,4 +58,35 @@ for rep in range(3):
     print(f"rep {rep}: host {t_host / a.frames * 1e6:.1f} us/frame (render call "
           f"{t_render / a.frames * 1e6:.1f}, gather call {t_gather / a.frames * 1e6:.1f}); "
           f"with GPU {t_all / a.frames * 1e6:.1f} us/frame", flush=True)
+# The bench's form since round 4: 4 frames per cvr_render_rc1pass_frames call and one
+# cvr_gather_tiles_n per 4 frames (host cost per frame = the two calls / 4)
+G = 4
+blk = [torch.zeros((G, H, W, 4), dtype=torch.float16, device="cuda") for _ in range(4)]
+frames4 = (N.Frame * G)(*([frame] * G))
+outs4 = [(N.Output * G)(*[N.Output(b[j].data_ptr(), None, None, 1, N.FORMAT_RGBA16F)
+                          for j in range(G)]) for b in blk]
+imgs4 = (ctypes.c_void_p * G)(*([img.data_ptr()] * G))
+ngroups = max(1, a.frames // G)
+for rep in range(3):
+    torch.cuda.synchronize()
+    t_render = t_gather = 0.0
+    t0 = time.perf_counter()
+    for n in range(ngroups):
+        k = n % 4
+        L.cvr_set_stream(dev.handle, sptr[k])
+        h0 = time.perf_counter()
+        L.cvr_render_rc1pass_frames(dev.handle, frames4, G, pr, outs4[k])
+        h1 = time.perf_counter()
+        L.cvr_gather_tiles_n(dev.handle, fr, G, blk[k].data_ptr(), 0, N.FORMAT_RGBA16F,
+                             blk[k].data_ptr(), imgs4)
+        h2 = time.perf_counter()
+        t_render += h1 - h0
+        t_gather += h2 - h1
+    t_host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    t_all = time.perf_counter() - t0
+    nf = ngroups * G
+    print(f"rep {rep}, {G} frames per call: host {t_host / nf * 1e6:.1f} us/frame (render call "
+          f"{t_render / ngroups * 1e6:.1f} us, gather call {t_gather / ngroups * 1e6:.1f} us per "
+          f"{G} frames); with GPU {t_all / nf * 1e6:.1f} us/frame", flush=True)
 N.check(L.cvr_comm_destroy(dev.handle), "destroy", dev.handle)

@@ -5,11 +5,14 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=${TAG:-r04_s17}
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_split_gpu.py tests/test_frames_gpu.py -m gpu > gpurun_out/${T}_pytest.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/${T}_pytest.log | head -20; exit 1; }
-timeout -k 10 600 python -u tools/rank0_probe.py --nranks 8 --streams 4 --sets 16 --reserve-cus 0,32 --render-nranks 0,12,16,-1 --frames-per-launch 4 --frames 20,96 > gpurun_out/${T}_rank0.log 2>&1 || { tail -5 gpurun_out/${T}_rank0.log; exit 1; }
-grep -v amdgpu.ids gpurun_out/${T}_rank0.log
-timeout -k 10 400 python -u tools/rank0_probe.py --renderer dos --nranks 8 --streams 1,4 --frames-per-launch 1 --frames 8 > gpurun_out/${T}_rank0_dos.log 2>&1 || { tail -5 gpurun_out/${T}_rank0_dos.log; exit 1; }
-grep -v amdgpu.ids gpurun_out/${T}_rank0_dos.log
-timeout -k 10 500 python -u tools/rank0_probe.py --renderer ebs --nranks 8 --streams 1,4 --frames-per-launch 1 --frames 4 > gpurun_out/${T}_rank0_ebs.log 2>&1 || { tail -5 gpurun_out/${T}_rank0_ebs.log; exit 1; }
-grep -v amdgpu.ids gpurun_out/${T}_rank0_ebs.log
+T=${TAG:-r04_s18}
+bash tools/gpu_round.sh all || exit 1
+for i in 1 2; do
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${T}_driver$i.json 2> gpurun_out/${T}_driver$i.err || { tail -5 gpurun_out/${T}_driver$i.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/${T}_driver$i.json')); print('driver', d['ms_per_step'], d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])"
+done
+timeout -k 10 300 python -u tools/overlap_probe.py --hwq 32 --nranks 7 --streams 4 --frames 96 --frames-per-launch 4 > gpurun_out/${T}_split7.log 2>&1 || { tail -5 gpurun_out/${T}_split7.log; exit 1; }
+timeout -k 10 300 python -u tools/overlap_probe.py --hwq 32 --nranks 7 --streams 4 --frames 20 --frames-per-launch 4 >> gpurun_out/${T}_split7.log 2>&1 || { tail -5 gpurun_out/${T}_split7.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/${T}_split7.log
+timeout -k 10 300 python -u tools/host_overhead.py --frames 200 > gpurun_out/${T}_host.log 2>&1 || { tail -5 gpurun_out/${T}_host.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/${T}_host.log
