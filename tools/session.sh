@@ -5,14 +5,14 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=${TAG:-r04_s18}
-bash tools/gpu_round.sh all || exit 1
-for i in 1 2; do
-  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${T}_driver$i.json 2> gpurun_out/${T}_driver$i.err || { tail -5 gpurun_out/${T}_driver$i.err; exit 1; }
-  python -c "import json; d=json.load(open('gpurun_out/${T}_driver$i.json')); print('driver', d['ms_per_step'], d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'])"
-done
-timeout -k 10 300 python -u tools/overlap_probe.py --hwq 32 --nranks 7 --streams 4 --frames 96 --frames-per-launch 4 > gpurun_out/${T}_split7.log 2>&1 || { tail -5 gpurun_out/${T}_split7.log; exit 1; }
-timeout -k 10 300 python -u tools/overlap_probe.py --hwq 32 --nranks 7 --streams 4 --frames 20 --frames-per-launch 4 >> gpurun_out/${T}_split7.log 2>&1 || { tail -5 gpurun_out/${T}_split7.log; exit 1; }
-grep -v amdgpu.ids gpurun_out/${T}_split7.log
-timeout -k 10 300 python -u tools/host_overhead.py --frames 200 > gpurun_out/${T}_host.log 2>&1 || { tail -5 gpurun_out/${T}_host.log; exit 1; }
-grep -v amdgpu.ids gpurun_out/${T}_host.log
+T=${TAG:-r04_s20}
+run() {   # name, bench args
+  local name=$1; shift
+  timeout -k 10 400 python bench.py "$@" > gpurun_out/${T}_$name.json 2> gpurun_out/${T}_$name.err || { tail -20 gpurun_out/${T}_$name.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/${T}_$name.json')); r=d['roofline']; print('$name', d['ms_per_step'], r['kernel_ms'], d['value'], r['frac'], r.get('traffic'), r.get('traffic_frac'))"
+}
+run driver --gpus 1 --steps 20 --warmup 5
+run phong --phong --no-cpu-baseline
+run dos --renderer dos --no-cpu-baseline
+run ebs --renderer ebs --no-cpu-baseline
+run longray --tf-alpha 0.02 --no-cpu-baseline --steps 40
