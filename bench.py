@@ -799,7 +799,7 @@ def main():
                 roof["pmc"]["valu_per_sample"] = round(pmc["valu_per_sample"], 1)
             if a.renderer == "rc1pass" and not a.phong:
                 roof["pmc"]["scratch_bytes_per_launch_est"] = max(
-                    0, int(pmc["write_bytes_per_launch"]) - px_bytes * pixels)
+                    0, int(pmc["write_bytes_per_launch"]) - FPL * px_bytes * pixels)
             roof["pmc"]["kernel_ns_under_pmc"] = pmc.get("kernel_ns_avg_under_pmc")
             roof["pmc"]["record"] = f"profiles/pmc_{a.renderer}*.json, lib {sha}"
         if roof["traffic"]:
