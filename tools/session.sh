@@ -5,14 +5,14 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=${TAG:-r04_s20}
+T=${TAG:-r04_s22}
 run() {   # name, bench args
   local name=$1; shift
-  timeout -k 10 400 python bench.py "$@" > gpurun_out/${T}_$name.json 2> gpurun_out/${T}_$name.err || { tail -20 gpurun_out/${T}_$name.err; exit 1; }
-  python -c "import json; d=json.load(open('gpurun_out/${T}_$name.json')); r=d['roofline']; print('$name', d['ms_per_step'], r['kernel_ms'], d['value'], r['frac'], r.get('traffic'), r.get('traffic_frac'))"
+  timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > gpurun_out/${T}_$name.json 2> gpurun_out/${T}_$name.err || { tail -20 gpurun_out/${T}_$name.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/${T}_$name.json')); r=d['roofline']; print('$name', d['ms_per_step'], r['kernel_ms'], d['value'])"
 }
-run driver --gpus 1 --steps 20 --warmup 5
-run phong --phong --no-cpu-baseline
-run dos --renderer dos --no-cpu-baseline
-run ebs --renderer ebs --no-cpu-baseline
-run longray --tf-alpha 0.02 --no-cpu-baseline --steps 40
+for rep in 1 2; do
+for LS in 4:3 5:2 5:3 5:4 4:2 8:2; do
+  L=${LS%:*}; S=${LS#*:}
+  run L${L}s${S}_$rep --gpus 1 --steps 20 --warmup 5 --frames-per-launch $L --streams $S
+done; done
