@@ -130,6 +130,9 @@ def parse():
     p.add_argument("--phong", action="store_true")
     p.add_argument("--tile-order", type=int, default=-1, choices=[-1, 0, 1, 2],
                    help="rc1pass launch order: 0 XCD bands, 1 learned LPT (default), 2 interleaved")
+    p.add_argument("--launch-interleave", type=int, default=-1,
+                   help="multi-frame launches: 1 deals the frames' launch-order entries "
+                        "interleaved, 0 frame after frame (-1: library default)")
     p.add_argument("--skip-min-pct", type=int, default=-1,
                    help="empty-space skipping when >= this %% of macro cells are empty (101: off; "
                         "-1: the library default)")
@@ -520,6 +523,9 @@ def main():
         if a.cell_skip >= 0:
             N.check(N.lib().cvr_set_option(r.device.handle, b"cell_skip", a.cell_skip), "cell_skip",
                     r.device.handle)
+        if a.launch_interleave >= 0:
+            N.check(N.lib().cvr_set_option(r.device.handle, b"launch_interleave", a.launch_interleave),
+                    "launch_interleave", r.device.handle)
         if a.skip_min_pct >= 0:
             N.check(N.lib().cvr_set_option(r.device.handle, b"skip_min_pct", a.skip_min_pct),
                     "skip_min_pct", r.device.handle)

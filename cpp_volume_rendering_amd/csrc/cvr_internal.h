@@ -176,6 +176,10 @@ struct IsoArgs {
 // takes workgroups [f * grid, (f + 1) * grid) and differs from frame 0 only in
 // its view (camera) and its outputs.  grid is a multiple of 8 whenever the
 // single-frame grid is, so workgroup b keeps XCD b % 8's share of the frame.
+// interleave (under a launch order, grid a multiple of 8): workgroup
+// 8 (n e + f) + x runs entry e of XCD band x of frame f, so the dispatcher hands
+// out entry e of every frame before entry e + 1 of any -- each band's longest
+// tiles of ALL frames start first (LPT over the launch, not per frame).
 constexpr int kMaxLaunchFrames = 8;
 struct FrameView {
   float eye[3];
@@ -185,6 +189,7 @@ struct FrameView {
 struct LaunchFrames {
   int n;                             // frames in the launch (1: a plain launch, the rest unused)
   int grid;                          // workgroups per frame
+  int interleave;                    // 1: the frames' entries interleaved by launch-order entry (below)
   FrameView view[kMaxLaunchFrames];
   float4* out[kMaxLaunchFrames];
   uint32_t* samples[kMaxLaunchFrames];
@@ -371,6 +376,8 @@ struct Ctx {
   void* comm = nullptr;
   int split_streams = 1;           // option "split_streams": render streams the caller rotates
   int gather_sets = 0;             // option "gather_sets": buffer sets the caller rotates (>= split_streams)
+  int launch_interleave = 1;       // option "launch_interleave": multi-frame launches deal the frames'
+                                   // launch-order entries interleaved (LaunchFrames::interleave)
   int gather_root_idle = 0;        // option "gather_root_idle": rank 0 only gathers (renders nothing)
   // scratch
   unsigned long long* d_total = nullptr;

@@ -189,6 +189,11 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
           raw[j] = make_uint4((v.x & 0x01ff01ffu) | 0x00000000u, (v.y & 0x01ff01ffu) | 0x00000000u,
                               (v.z & 0x01ff01ffu) | 0x00000000u, (v.w & 0x01ff01ffu) | 0x00000000u);
         }
+#elif defined(CVR_CELL_REUSE)   // probe: a sample in its predecessor's cell reuses that load
+        if (j > 0 && sp[j].ix == sp[j - 1].ix && sp[j].iy == sp[j - 1].iy && sp[j].iz == sp[j - 1].iz)
+          raw[j] = raw[j - 1];
+        else
+          raw[j] = load_cell(sp[j]);
 #else
         raw[j] = load_cell(sp[j]);
 #endif
@@ -480,8 +485,15 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
   int b = blockIdx.x, f = 0;
   const int nt = A.ntiles;
   if (LF.n > 1) {
-    f = b / LF.grid;
-    b -= f * LF.grid;
+    if (LF.interleave) {          // b = 8 (n e + f) + x -> frame f, block 8 e + x
+      const int x = b & 7, q = b >> 3;
+      const int e = q / LF.n;
+      f = q - e * LF.n;
+      b = (e << 3) | x;
+    } else {
+      f = b / LF.grid;
+      b -= f * LF.grid;
+    }
     const FrameView& v = LF.view[f];
 #pragma unroll
     for (int i = 0; i < 3; i++) {
@@ -816,9 +828,11 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
   int grid = order ? plan.order_slots : plan.ntiles;
   LaunchFrames lf;
   lf.n = 1;
+  lf.interleave = 0;
   if (plan.frames && plan.frames->n > 1) {
     lf = *plan.frames;
     lf.grid = grid;
+    lf.interleave = (order && (grid & 7) == 0 && c.launch_interleave) ? 1 : 0;
     grid *= lf.n;
   }
   hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF, FB, CS>), dim3(grid), dim3(64), lds, s,

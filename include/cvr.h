@@ -311,6 +311,10 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                render ranks (their cvr_frame: rank = communicator rank - 1,
  *                nranks = N - 1; rank 0 passes a frame of that geometry).  Rank 0's
  *                block of the gather buffer stays unused.  
+ *   "launch_interleave" cvr_render_rc1pass_frames under a launch order (tile_order
+ *                1/2): 1 (default) = the launch deals entry e of every frame's XCD
+ *                bands before entry e + 1 of any (the longest tiles of all frames
+ *                first); 0 = frame after frame.  Images identical either way.
  * One option changes the arithmetic (and so the image) rather than the speed:
  *   "filter_bits" 0: exact float GL_LINEAR weights (CVR-SPEC, the default);
  *                8: every GL_LINEAR weight (volume, gradient, TF; ray_marching_1p.comp:133,
