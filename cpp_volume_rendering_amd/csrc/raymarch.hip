@@ -189,11 +189,6 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
           raw[j] = make_uint4((v.x & 0x01ff01ffu) | 0x00000000u, (v.y & 0x01ff01ffu) | 0x00000000u,
                               (v.z & 0x01ff01ffu) | 0x00000000u, (v.w & 0x01ff01ffu) | 0x00000000u);
         }
-#elif defined(CVR_CELL_REUSE)   // probe: a sample in its predecessor's cell reuses that load
-        if (j > 0 && sp[j].ix == sp[j - 1].ix && sp[j].iy == sp[j - 1].iy && sp[j].iz == sp[j - 1].iz)
-          raw[j] = raw[j - 1];
-        else
-          raw[j] = load_cell(sp[j]);
 #else
         raw[j] = load_cell(sp[j]);
 #endif
