@@ -40,6 +40,8 @@ ap.add_argument("--hwq", default="8")
 ap.add_argument("--frames-per-launch", type=int, default=1,
                 help="a CVR_PROBE_FRAMES=G library build (CVR_LIB_OVERRIDE): each call marches G frames")
 ap.add_argument("--tile-order", type=int, default=-1, help="rc1pass tile_order option (-1: default)")
+ap.add_argument("--interleave", default="-1",
+                help="comma list of launch_interleave settings (-1: library default)")
 ap.add_argument("--boost", default="-1", help="rc1pass: comma list of boost percentages (-1: library default)")
 a = ap.parse_args()
 
@@ -70,13 +72,16 @@ def render(frame, out):
 
 res = []
 import itertools  # noqa: E402
-for q, bst in itertools.product([int(x) for x in a.quad.split(",")], [int(x) for x in a.boost.split(",")]):
+for q, bst, il in itertools.product([int(x) for x in a.quad.split(",")], [int(x) for x in a.boost.split(",")],
+                                   [int(x) for x in a.interleave.split(",")]):
     if a.renderer == "rc1pass":
         L.cvr_set_option(handle, b"quad", q)
         if bst >= 0:
             L.cvr_set_option(handle, b"boost", bst)
         if a.tile_order >= 0:
             L.cvr_set_option(handle, b"tile_order", a.tile_order)
+        if il >= 0:
+            L.cvr_set_option(handle, b"launch_interleave", il)
     for nr in [int(x) for x in a.nranks.split(",")]:
         for tile in [int(x) for x in a.tile.split(",")]:
             ranks = range(nr) if a.ranks == "all" else [int(x) for x in a.ranks.split(",") if int(x) < nr]
@@ -108,6 +113,7 @@ for q, bst in itertools.product([int(x) for x in a.quad.split(",")], [int(x) for
                         best = min(best, (time.perf_counter() - t0) / (nl * G) * 1e3)
                     per.append(best)
                 line = dict(renderer=a.renderer, frames_per_launch=a.frames_per_launch, tile_order=a.tile_order,
+                            interleave=il,
                             lib=os.environ.get("CVR_LIB_OVERRIDE", "in-tree"), nranks=nr, tile=tile, quad=q, boost=bst, streams=ns, hwq=int(a.hwq),
                             ms_per_rank=[round(x, 5) for x in per], max_ms=round(max(per), 5),
                             mean_ms=round(sum(per) / len(per), 5),
