@@ -5,17 +5,13 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=${TAG:-r04_s26}
+T=${TAG:-r04_s27}
 run() {   # name, bench args
   local name=$1; shift
   timeout -k 10 300 python bench.py "$@" > gpurun_out/${T}_$name.json 2> gpurun_out/${T}_$name.err || { tail -20 gpurun_out/${T}_$name.err; exit 1; }
   python -c "import json; d=json.load(open('gpurun_out/${T}_$name.json')); r=d['roofline']; print('$name', d['ms_per_step'], r['kernel_ms'], r['frac'], d['value'])"
 }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof -o run -- python3 bench.py --no-cpu-baseline --streams 1 > gpurun_out/${T}_prof_bench_1stream.json 2> gpurun_out/${T}_prof.err || { tail -20 gpurun_out/${T}_prof.err; exit 1; }
-echo prof done
-run driver
-for rep in 1 2; do for IL in 0 1; do
-  run orbit_il${IL}_$rep --no-cpu-baseline --orbit --launch-interleave $IL
+for rep in 1 2; do for F in 20 96; do
+timeout -k 10 300 python tools/overlap_probe.py --nranks 7,8 --frames-per-launch 4 --streams 4 --hwq 32 --frames $F --interleave 0,1 > gpurun_out/${T}_split_F${F}_$rep.jsonl 2> gpurun_out/${T}_split.err || { tail -20 gpurun_out/${T}_split.err; exit 1; }
+cat gpurun_out/${T}_split_F${F}_$rep.jsonl | python3 -c "import sys,json; [print($F, d['nranks'], d['interleave'], d['max_ms'], d['mean_ms']) for d in map(json.loads, sys.stdin)]"
 done; done
-timeout -k 10 400 python tools/overlap_probe.py --nranks 7,8 --frames-per-launch 4 --streams 4 --hwq 32 --frames 96 --interleave 0,1 > gpurun_out/${T}_split_interleave.jsonl 2> gpurun_out/${T}_split.err || { tail -20 gpurun_out/${T}_split.err; exit 1; }
-cat gpurun_out/${T}_split_interleave.jsonl | python3 -c "import sys,json; [print(d['nranks'], d['interleave'], d['max_ms'], d['mean_ms']) for d in map(json.loads, sys.stdin)]"
