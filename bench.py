@@ -110,9 +110,66 @@ HBM_PEAK_GBS = 8000.0    # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md 
 # the bound for EBS, whose 32-B SAT fetches (2.2 TB per 1024^3 frame) are served by
 # L1/L2/MALL, not HBM (PMC: ~220 GB of HBM traffic per frame)
 L2_PEAK_GBS = 34500.0
+# The pipes of one CU at the peak engine clock (MI355X_MICROARCH.md; under load DVFS
+# gives some of it back, the PMC record's effective clock says how much):
+CLOCK_GHZ = 2.4
+N_CU, N_SIMD = 256, 1024
+# a wave64 VALU instruction issues over 2 cycles per SIMD (constants table)
+VALU_PEAK_GWIPS = N_SIMD * CLOCK_GHZ / 2.0
+# the texture-data return path: 64 B/clk per CU, one 1-KiB dwordx4 wave-load per 16 clk
+# (tools/ta_probe.hip: 16.5 clk for any wave-load whose lanes share lines in runs, L1-hot)
+VMEM_PEAK_GBS = N_CU * 64 * CLOCK_GHZ
 
 
-def parse():
+def pipe_roofline(kern_ms, fpl, pmc, live_wave_loads):
+    """The rc1pass march's roofline on the pipe that binds.  Two pipes
+    are priced for one launch of `fpl` frames over its kernel time:
+      * vmem: dwordx4 wave-loads x 1 KiB through the L1 -> VGPR return path (64 B/clk/CU);
+      * valu: VALU wave-instructions x 2 issue cycles per SIMD.
+    Counts come from the PMC record of this library build (per launch of the record's
+    frames, scaled to `fpl`); without one, the vmem pipe uses the kernel's own count of
+    its march rounds (live_wave_loads).  `bound` is the pipe with the larger fraction."""
+    t = kern_ms * 1e-3
+    rec_fpl = (pmc.get("frames_per_launch") or 4) if pmc else None
+    pipes = {}
+    wl, src = None, None
+    if pmc.get("sq_insts_vmem_rd"):
+        wl, src = pmc["sq_insts_vmem_rd"] * fpl / rec_fpl, "PMC SQ_INSTS_VMEM_RD"
+    elif live_wave_loads:
+        wl, src = live_wave_loads, "kernel count: K x march rounds + TF staging loads"
+    if wl:
+        pipes["vmem"] = {"achieved": round(wl * 1024 / t / 1e9, 1), "peak": VMEM_PEAK_GBS,
+                         "unit": "GB/s", "wave_loads_per_launch": int(wl), "count": src}
+    if pmc.get("valu_wave_insts"):
+        v = pmc["valu_wave_insts"] * fpl / rec_fpl
+        pipes["valu"] = {"achieved": round(v / t / 1e9, 2), "peak": VALU_PEAK_GWIPS,
+                         "unit": "G wave-instr/s", "wave_insts_per_launch": int(v),
+                         "count": "PMC SQ_INSTS_VALU"}
+    for p in pipes.values():
+        p["frac"] = round(p["achieved"] / p["peak"], 4)
+    if not pipes:
+        return {}
+    bound = max(pipes, key=lambda k: pipes[k]["frac"])
+    out = {"bound": bound, "achieved": pipes[bound]["achieved"], "peak": pipes[bound]["peak"],
+           "unit": pipes[bound]["unit"], "frac": pipes[bound]["frac"], "pipes": pipes}
+    if pmc.get("td_busy_frac_per_cu") is not None and pmc.get("td_tc_stall_frac_per_cu") is not None:
+        out["vmem_detail"] = {
+            "td_busy_per_cu": round(pmc["td_busy_frac_per_cu"], 3),
+            "td_stalled_on_cache_per_cu": round(pmc["td_tc_stall_frac_per_cu"], 3),
+            "td_work_clk_per_wave_load": round(pmc.get("td_work_cycles_per_wave_load", 0), 2),
+            "coalesced_clk_per_wave_load": 16,
+            "tcp_accesses_per_wave_load": round(pmc.get("tcp_accesses_per_wave_load", 0), 2),
+            "coalesced_tcp_accesses": 16,
+            "l1_miss_requests_per_wave_load": round(pmc.get("l1_miss_requests_per_wave_load", 0), 2),
+            "what": "TD busy = its own work + cycles stalled waiting for L1 misses (TD_TC_STALL); "
+                    "per wave-load the work is the coalesced cost, the stall is miss latency "
+                    "(DESIGN §5)"}
+    if pmc.get("effective_clock_ghz_under_pmc"):
+        out["effective_clock_ghz_under_pmc"] = round(pmc["effective_clock_ghz_under_pmc"], 3)
+    return out
+
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=0,
@@ -138,7 +195,7 @@ def parse():
                         "-1: the library default)")
     p.add_argument("--cell-skip", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4],
                    help="rc1pass per-cell skip: 0 off, 1 empty-sample flags, 2 + distance skip "
-                        "(-1: the library default, 2)")
+                        "(-1: the library default, 3: + the distance skip when every lane can)")
     p.add_argument("--batch", type=int, default=0, choices=[0, 2, 4],
                    help="rc1pass samples per lane per memory round trip (0 = auto: 4, 2 with Phong)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -176,6 +233,9 @@ def parse():
                    help="dos/ebs flat shading: 64-job chunks per XCD turn (0: library default)")
     p.add_argument("--postpass", action="store_true",
                    help="also time the multiscaling post-pass filters on this workload's frame")
+    p.add_argument("--no-cadence", action="store_true",
+                   help="rc1pass, 1 GPU: skip the plugin-cadence lines (one frame per call on one "
+                        "stream: the static view and the 24-state orbit)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_rc1pass.json"))
     p.add_argument("--orbit", action="store_true",
                    help="move the camera every frame through the reference's camera states "
@@ -189,7 +249,29 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="launcher rehearsal without a GPU: the ranks join a gloo group and "
                         "rank 0 prints the world size (tests/test_bench_launch.py)")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+def split_defaults(a, world):
+    """The screen split bench.py runs for these arguments at this world size (the
+    defaults of --frames-per-launch, --streams, --buffer-sets, --exchange-frames,
+    --root-renders), as ScreenTileSplit keyword arguments.  Shared with the world-8
+    control-flow test (tests/test_distributed_cpu.py), so the test runs exactly the
+    N = 8 default path."""
+    fpl = a.frames_per_launch if a.frames_per_launch > 0 else (4 if a.renderer == "rc1pass" else 1)
+    streams = a.streams or ((4 if world >= 2 else 3) if fpl > 1 else
+                            (16 if world >= 8 else (12 if world >= 4 else 4)))
+    # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
+    # on rank 0) would otherwise rival a rank's share of the frame (~23 us at N = 8)
+    gx = fpl if fpl > 1 else (a.exchange_frames or (2 if world >= 4 else 1))
+    # rank 0's exchange (receive + unpack of 7/8 of every frame at N = 8) competes
+    # with its own render and stalls it (tools/rank0_probe.py: 0.0295 ms per
+    # frame against 0.0125 for a render-only rank); with 3+ render ranks the root
+    # only gathers (0.0094 ms per frame) and N - 1 ranks render
+    root_renders = (a.root_renders == 1 or world < 4 or a.renderer != "rc1pass"
+                    or a.transport != "rccl") if a.root_renders != 0 else False
+    return {"streams": streams, "frames_per_exchange": gx, "frames_per_launch": fpl,
+            "buffer_sets": a.buffer_sets or 4 * streams, "root_renders": root_renders}
 
 
 def dry_run(world, rank, a):
@@ -374,6 +456,67 @@ def load_pmc(path, workload_key, kernel, sha):
     return {}
 
 
+def cadence_lines(r, dev, W, H, fmt, cam, S_static, reps=100):
+    """The plugin's own cadence: ONE frame per cvr_render_rc1pass call
+    on ONE stream, as HipRayCasting1Pass::Redraw issues it once per
+    RenderingManager::Display (renderingmanager.cpp:199-208, rc1prenderer.cpp:140-151),
+    each frame RGBA16F into a device buffer.  Two lines: the static headline view
+    (the launch order learned on it) and an orbit through the reference's 24 camera
+    states (data/#list_camera_states), one state per frame, so no frame's order was
+    learned on its own view.  Host wall time between synchronisations over `reps`
+    frames; kernel times from the library's HIP events on the same stream."""
+    L = N.lib()
+    h = r.device.handle
+    s = torch.cuda.Stream(dev)
+    r.device.set_stream(s.cuda_stream)
+    img = torch.zeros((H, W, 4), dtype=torch.float16 if fmt == N.FORMAT_RGBA16F else torch.float32,
+                      device=dev)
+    total = torch.zeros((1,), dtype=torch.int64, device=dev)
+    out = N.Output(img.data_ptr(), None, None, 1, fmt)
+    out_cnt = N.Output(img.data_ptr(), None, total.data_ptr(), 1, fmt)
+    path = os.path.join(ROOT, "tests", "golden", "list_camera_states")
+    ncam = ctypes.c_int()
+    N.check(L.cvr_read_camera_state(path.encode(), 0, N.Camera(), None, 0, ncam), "camera list")
+    orbit = [make_frame(read_camera_state(path, i), W, H) for i in range(ncam.value)]
+    S_orbit = []
+    for f in orbit:                  # samples of each state, counted by the kernel
+        total.zero_()
+        r.render_to(f, out_cnt)
+        torch.cuda.synchronize(dev)
+        S_orbit.append(int(total.item()))
+    res = {}
+    for name, frames, S in (("static", [make_frame(cam, W, H)], [S_static]), ("orbit", orbit, S_orbit)):
+        n = reps if name == "static" else 2 * len(frames)
+        for i in range(max(20, len(frames))):          # warm: clocks, the slot's launch order
+            r.render_to(frames[i % len(frames)], out)
+        torch.cuda.synchronize(dev)
+        N.check(L.cvr_set_option(h, b"kernel_timing", n), "kernel_timing", h)
+        t0 = time.perf_counter()
+        for i in range(n):
+            r.render_to(frames[i % len(frames)], out)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        kt = (ctypes.c_float * n)()
+        nkt = ctypes.c_int()
+        N.check(L.cvr_read_kernel_times(h, kt, n, ctypes.byref(nkt)), "kernel times", h)
+        N.check(L.cvr_set_option(h, b"kernel_timing", 0), "kernel_timing", h)
+        Sn = sum(S[i % len(S)] for i in range(n))
+        kms = float(np.mean(kt[:nkt.value]))
+        res[name] = {"frames": n, "ms_per_frame": round(dt / n * 1e3, 4),
+                     "fps": round(n / dt, 1),
+                     "Msamples_s": round(Sn / dt / 1e6, 2),
+                     "kernel_ms_mean": round(kms, 4),
+                     "kernel_Msamples_s": round(Sn / n / (kms * 1e-3) / 1e6, 2),
+                     "samples_per_frame_mean": int(round(Sn / n))}
+        if name == "orbit":
+            res[name]["samples_per_state"] = S_orbit
+    res["what"] = ("one cvr_render_rc1pass call per frame on one stream, RGBA16F device output "
+                   "(the plugin's Redraw cadence; the adapter's HIP-GL interop copy of the "
+                   "frame is not included: no GL here); static = camera 'Initial State', orbit "
+                   "= the reference's camera states in order, one per frame")
+    return res
+
+
 def postpass_bench(r, dev, W, H, reps):
     """The step after the march: RenderFrameToScreen's multiscaling
     filters, timed with HIP events on the context stream.  Modes 1-2 filter a (2W, 2H)
@@ -504,15 +647,13 @@ def main():
     # the driver's 20-frame command at N = 1, 0.0808 ms per frame (1 frame per launch,
     # 4 streams) -> 0.0778 (4 per launch, 3 streams); rank shares at N = 8 over 20
     # frames 0.0254 -> 0.0154 ms, in steady state 0.0224 -> 0.0122-0.0131 ms
-    if a.frames_per_launch <= 0:
-        a.frames_per_launch = 4 if a.renderer == "rc1pass" else 1
-    if a.renderer != "rc1pass" and a.frames_per_launch != 1:
+    if a.renderer != "rc1pass" and a.frames_per_launch > 1:
         sys.exit("bench.py: --frames-per-launch > 1 needs --renderer rc1pass")
-    if not 1 <= a.frames_per_launch <= 8:
+    if a.frames_per_launch > 8:
         sys.exit("bench.py: --frames-per-launch must be in 1..8")
-    FPL = a.frames_per_launch
-    a.streams = a.streams or ((4 if world >= 2 else 3) if FPL > 1 else
-                              (16 if world >= 8 else (12 if world >= 4 else 4)))
+    SD = split_defaults(a, world)
+    FPL = a.frames_per_launch = SD["frames_per_launch"]
+    a.streams = SD["streams"]
     if a.renderer == "rc1pass":
         N.check(N.lib().cvr_set_option(r.device.handle, b"quad", quad), "quad", r.device.handle)
         if a.batch:
@@ -536,22 +677,14 @@ def main():
         N.check(N.lib().cvr_set_option(r.device.handle, b"flat_group", a.flat_group), "flat_group",
                 r.device.handle)
     try:
-        # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
-        # on rank 0) would otherwise rival a rank's share of the frame (~23 us at N = 8)
-        gx = FPL if FPL > 1 else (a.exchange_frames or (2 if world >= 4 else 1))
-        # rank 0's exchange (receive + unpack of 7/8 of every frame at N = 8) competes
-        # with its own render and stalls it (tools/rank0_probe.py: 0.0295 ms per
-        # frame against 0.0125 for a render-only rank); with 3+ render ranks the root
-        # only gathers (0.0094 ms per frame) and N - 1 ranks render
-        root_renders = (a.root_renders == 1 or world < 4 or a.renderer != "rc1pass"
-                        or a.transport != "rccl") if a.root_renders != 0 else False
+        root_renders = SD["root_renders"]
 
         def make_split(root):
             return T.ScreenTileSplit(r, W, H, tile=tile, fmt=fmt, device=dev,
                                      transport=a.transport if world > 1 else None,
-                                     streams=a.streams, frames_per_exchange=gx,
-                                     frames_per_launch=FPL,
-                                     buffer_sets=a.buffer_sets or 4 * a.streams,
+                                     streams=SD["streams"],
+                                     frames_per_exchange=SD["frames_per_exchange"],
+                                     frames_per_launch=FPL, buffer_sets=SD["buffer_sets"],
                                      root_renders=root)
         split = make_split(root_renders)
         if world > 1 and not root_renders:
@@ -572,7 +705,9 @@ def main():
                 split.close()
                 root_renders = True
                 split = make_split(True)
-    except N.CvrError as e:     # no native communicator: torch's dist.gather instead
+    except T.CommUnavailable as e:     # no native communicator: torch's dist.gather instead
+        # (only cvr_comm_init failures land here: an option the library rejects is a
+        # configuration error and ends the bench)
         if world == 1 or a.transport != "rccl":
             raise
         print(f"rank {rank}: native RCCL gather unavailable ({e}); using dist.gather",
@@ -826,6 +961,28 @@ def main():
                          "bytes_fetched_per_launch": b_fetch,
                          "achieved_fetched": round(b_fetch / (kern_ms * 1e-3) / 1e9, 1),
                          "frac_fetched": round(b_fetch / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+            # SURVEY §8(d)'s figure (B_alg over the launch time against the HBM peak) is an
+            # effective bandwidth, not a roofline: most of B_alg is served by L1/L2 and
+            # it exceeds 1 on cache-friendly views.  Kept as effective_frac; the roofline
+            # proper is the busier of the vmem and VALU pipes (pipe_roofline)
+            eff = roof["frac"]
+            live_wl = None
+            if not a.phong and shade[2]:
+                ntiles_frame = pixels // 64
+                tf_loads = -(-(len(tf) + 2) // 64)
+                live_wl = FPL * (batch * int(shade[2]) + ntiles_frame * tf_loads)
+            pr = pipe_roofline(kern_ms, FPL, pmc, live_wl)
+            if pr:
+                roof.update(pr)
+                roof["effective_bound"] = "hbm (SURVEY 8d effective bandwidth)"
+                roof["effective_achieved"] = round(achieved, 1)
+                roof["effective_frac"] = eff
+                roof["effective_frac_frame"] = roof.pop("frac_frame")
+                roof["definition"] = ("frac: the busier pipe of the march (vmem: wave-loads x 1 KiB "
+                                      "vs 64 B/clk/CU; valu: wave-instructions x 2 clk per SIMD), "
+                                      "at the 2.4 GHz peak clock; effective_frac: B_alg / launch "
+                                      "time / 8 TB/s (SURVEY 8d, not a roofline when > 1); "
+                                      "traffic_frac: PMC HBM bytes / launch time / 8 TB/s")
         if dos:
             roof.update({"shaded_samples": shade[0], "shadow_lit_samples": shade[1],
                          "cone_fetches_per_shaded": [f_occ, f_sdw],
@@ -923,6 +1080,8 @@ def main():
                                          "of the build + cell4 expansion kernels"}
         if a.postpass and world == 1:
             res["postpass"] = postpass_bench(r, dev, W, H, a.steps)
+        if world == 1 and a.renderer == "rc1pass" and not a.orbit and not a.no_cadence:
+            res["plugin_cadence"] = cadence_lines(r, dev, W, H, fmt, cam, S_cam[0])
         if world == 1 and not a.no_cpu_baseline:
             dos_cfg = None
             if dos:

@@ -44,6 +44,7 @@ SINGLE_RAY_PER_PIXEL, MULTIPLE_RAYS_PER_PIXEL, DOWN_SCALING_RENDER, UP_SCALING_R
 (FILTER_BOX, FILTER_HAT, FILTER_CATMULL_ROM, FILTER_MITCHELL_NETRAVALI, FILTER_CARDINAL_BSPLINE_3,
  FILTER_CARDINAL_OMOMS3) = range(6)
 COMM_ID_BYTES = 128
+MAX_GATHER_SETS = 64   # cvr.h CVR_MAX_GATHER_SETS
 
 
 class CvrError(RuntimeError):

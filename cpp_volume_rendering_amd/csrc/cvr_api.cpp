@@ -44,6 +44,18 @@ void free_dev(void*& p) {
   p = nullptr;
 }
 
+// Before a state change writes or frees device state that frames read (volume
+// cells, TF, gradient, occupancy, cone tables, extinction pyramid, SAT): frames
+// may be in flight on any render stream the caller rotates (non-blocking
+// streams do not wait for the null-stream copies below), so the whole device
+// drains first.  The reference's equivalent is the GL pipeline's implicit
+// ordering on Init after a TF change (renderingmanager.cpp:1050-1127).
+#define QUIESCE(c)                             \
+  do {                                         \
+    HIP_TRY(c, hipSetDevice((c)->device));     \
+    HIP_TRY(c, hipDeviceSynchronize());        \
+  } while (0)
+
 // float -> binary16 bits, round to nearest even (the GL driver's conversion of
 // GL_FLOAT client data to a 16F internal format).
 uint16_t to_half_bits(float f) {
@@ -432,7 +444,10 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     return CVR_OK;
   }
   if (!std::strcmp(key, "gather_sets")) {
-    if (value < 0 || value > 48) return fail(c, CVR_ERR_ARG, "gather_sets must be 0..48");
+    // exchange g waits for exchange g + D - B, which the 64-event ring still holds
+    // while B - D < 64 (cvr_comm.cpp): any B <= 64 with D >= 1 render streams
+    if (value < 0 || value > CVR_MAX_GATHER_SETS)
+      return fail(c, CVR_ERR_ARG, "gather_sets must be 0..%d", CVR_MAX_GATHER_SETS);
     c->gather_sets = value;
     return CVR_OK;
   }
@@ -550,8 +565,7 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
     return fail(c, CVR_ERR_ARG, "cvr_set_volume: volume too large for 32-bit cell indexing");
   if ((size_t)(w + 1) * (h + 1) >= (size_t)1 << 23)
     return fail(c, CVR_ERR_ARG, "cvr_set_volume: slice too large for 24-bit cell addressing");
-  HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  QUIESCE(c);   // frames in flight on any stream read the state replaced below
   free_dev(c->d_vox); c->vox_bytes = 0;
   free_dev(c->d_cells); c->cells_bytes = 0;
   free_dev(c->d_grad); c->grad_bytes = 0; c->grad_mode = 0;
@@ -575,6 +589,7 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
   c->occ_valid = 0;
   c->cell_flags_valid = 0;   // the cells are rebuilt without flags
   c->cell_flags_set = 0;
+  c->cell_flags_oom = 0;
   { void* p = c->d_ext; free_dev(p); c->d_ext = nullptr; c->ext_levels = 0; }
   { void* p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr; }
   { void* p = c->d_sat; free_dev(p); c->d_sat = nullptr; }
@@ -625,8 +640,7 @@ cvr_status cvr_set_transfer_function(cvr_ctx* ctx, const float* rgbt, int n) {
     q[i] = half_round(rgbt[i]);   // GL_RGBA16F
     if (i % 4 == 3) amax = std::isfinite(q[i]) ? std::max(amax, q[i]) : NAN;
   }
-  HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  QUIESCE(c);   // frames in flight on any stream read the state replaced below
   if (n != c->tf_n) {
     void* p = c->d_tf; free_dev(p); c->d_tf = nullptr;
     HIP_TRY(c, hipMalloc((void**)&c->d_tf, (size_t)n * 16));
@@ -647,6 +661,7 @@ cvr_status cvr_set_transfer_function(cvr_ctx* ctx, const float* rgbt, int n) {
                        hipMemcpyHostToDevice));
   c->occ_valid = 0;
   c->cell_flags_valid = 0;
+  c->cell_flags_oom = 0;
   return CVR_OK;
 }
 
@@ -655,8 +670,7 @@ cvr_status cvr_set_gradient(cvr_ctx* ctx, int mode) {
   if (!c) return CVR_ERR_ARG;
   if (mode < 0 || mode > 2) return fail(c, CVR_ERR_ARG, "cvr_set_gradient: bad mode %d", mode);
   if (mode != 0 && !c->d_vox) return fail(c, CVR_ERR_STATE, "cvr_set_gradient: no volume");
-  HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  QUIESCE(c);   // frames in flight on any stream read the state replaced below
   free_dev(c->d_grad); c->grad_bytes = 0; c->grad_mode = 0;
   if (mode == 0) return CVR_OK;
   c->grad_bytes = cvr::cell_count(c->cells) * 48;
@@ -716,7 +730,7 @@ static cvr_status ensure_scratch(Ctx* c, size_t bytes) {
 static cvr_status ensure_occupancy(Ctx* c) {
   if (c->occ_valid) return CVR_OK;
   if (!c->d_lut || !c->d_tf_prefix) return fail(c, CVR_ERR_STATE, "occupancy: no volume or TF");
-  HIP_TRY(c, hipSetDevice(c->device));
+  QUIESCE(c);   // frames in flight on other streams may still read d_occ
   const int sh = c->macro_shift;
   if (c->mm_shift != sh) {
     for (int i = 0; i < 3; i++) c->mdim[i] = ((c->N[i] - 1) >> sh) + 1;
@@ -763,6 +777,21 @@ static cvr_status ensure_cell_flags(Ctx* c) {
   c->cell_flags_valid = 1;
   c->cell_flags_set = 1;
   return CVR_OK;
+}
+
+// The per-cell skip is a bit-exact optimisation, so a frame must not fail for
+// want of its 2 bytes of scratch per cell (2.1 GB at 1024^3, next to the EBS
+// SAT): on OOM the frame renders without it (every density read takes |corner|,
+// so stale flags in the sign bits are ignored) and the build is retried on the
+// next frame.  Any other error is returned.
+static cvr_status cell_flags_or_off(Ctx* c) {
+  if (c->cell_flags_oom && !c->cell_flags_valid) return CVR_ERR_OOM;
+  const cvr_status st = ensure_cell_flags(c);
+  if (st == CVR_ERR_OOM) {
+    (void)hipGetLastError();   // clear the failed allocation's error
+    c->cell_flags_oom = 1;
+  }
+  return st;
 }
 
 // Camera, volume and tiling constants of one frame (shared by every renderer):
@@ -885,10 +914,13 @@ static cvr_status render_rc1pass_frames(Ctx* c, const cvr_frame* frames, int nf,
   A.occ = nullptr;
   A.cell_skip = 0;
   if (c->cell_skip > 0) {   // (the quad march ignores it)
-    cvr_status st = ensure_cell_flags(c);
-    if (st != CVR_OK) return st;
-    A.cell_skip = c->cell_skip;
-    A.inv_step = 1.0f / A.step;
+    const cvr_status st = cell_flags_or_off(c);
+    if (st == CVR_OK) {
+      A.cell_skip = c->cell_skip;
+      A.inv_step = 1.0f / A.step;
+    } else if (st != CVR_ERR_OOM) {
+      return st;
+    }
   }
   if (c->macro_shift > 0 && A.cell_skip == 0) {
     cvr_status st = ensure_occupancy(c);
@@ -1358,8 +1390,7 @@ cvr_status cvr_set_extinction_volume(cvr_ctx* ctx, const float* tf_rgba, int n, 
   // the RGBA16F opacity TF (GenerateTexture_1D_RGBA, transferfunction1d.cpp:58-87)
   std::vector<float> q((size_t)n * 4);
   for (size_t i = 0; i < q.size(); i++) q[i] = half_round(tf_rgba[i]);
-  HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  QUIESCE(c);   // frames in flight on any stream read the state replaced below
   { void* p = c->d_ext; free_dev(p); c->d_ext = nullptr; c->ext_levels = 0; }
   { void* p = c->d_ext_cells; free_dev(p); c->d_ext_cells = nullptr; }
   // cell8 texels are addressed with 32-bit byte offsets (16 B each)
@@ -1453,7 +1484,6 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   if (f->nranks > 1 && (f->tile_size < 16 || f->tile_size % 16 != 0 || f->rank < 0 || f->rank >= f->nranks))
     return fail(c, CVR_ERR_ARG, "cvr_render_dosct: bad tiling");
   HIP_TRY(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
 
   // cone tables: covered distance <= 0 -> the volume diagonal * 0.50 / 0.75
   // (GetDiagonal in double, dosrcrenderer.cpp:112-113)
@@ -1477,7 +1507,7 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
         for (int j = 0; j < 4; j++)   // GetConeSectionsInfoTex uploads RGBA16F
           up[((size_t)k * CVR_MAX_CONE_SECTIONS + i) * 4 + j] = half_round(c->cone_tab[k].sections[i][j]);
     if (!c->d_cones) HIP_TRY(c, hipMalloc((void**)&c->d_cones, up.size() * sizeof(float)));
-    HIP_TRY(c, hipStreamSynchronize(s));
+    QUIESCE(c);   // DOS frames in flight on other streams read d_cones
     HIP_TRY(c, hipMemcpy(c->d_cones, up.data(), up.size() * sizeof(float), hipMemcpyHostToDevice));
     c->cone_key[0] = cp[0];
     c->cone_key[1] = cp[1];
@@ -1490,10 +1520,13 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
   fill_frame_args(c, f, p->step, Q.a, ntiles, npix);
   Q.a.filter_bits = c->filter_bits;   // GL_LINEAR weights of every fetch (CVR-SPEC-8 at 8)
   if (c->cell_skip > 0) {   // the per-cell skip flags in the count / emit march
-    cvr_status st = ensure_cell_flags(c);
-    if (st != CVR_OK) return st;
-    Q.a.cell_skip = 1;
-    Q.a.inv_step = 1.0f / Q.a.step;
+    const cvr_status st = cell_flags_or_off(c);
+    if (st == CVR_OK) {
+      Q.a.cell_skip = 1;
+      Q.a.inv_step = 1.0f / Q.a.step;
+    } else if (st != CVR_ERR_OOM) {
+      return st;
+    }
   }
   Q.a.out_half = o->format == CVR_FORMAT_RGBA16F;
   Q.a.ka = p->ka;   // Phong ambient/diffuse/specular weights of the surface term
@@ -1584,8 +1617,7 @@ cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n)
   // the shader indexes texels (plus one cell4 plane) with 32-bit / 24-bit products
   if (w > 4096 || h > 4096 || d > 4096 || cells >= ((size_t)1 << 31))
     return fail(c, CVR_ERR_ARG, "cvr_set_extinction_sat: volume too large for the SAT");
-  HIP_TRY(c, hipSetDevice(c->device));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  QUIESCE(c);   // frames in flight on any stream read the state replaced below
   // Same grid as the last build (a TF change): rebuild into the existing buffers.
   // Freeing and re-allocating the ~30 GB of a 1024^3 SAT costs seconds.
   const bool same = c->d_sat && c->sat_dims[0] == w && c->sat_dims[1] == h && c->sat_dims[2] == d;
@@ -1717,7 +1749,11 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
     const int w = c->sat_dims[0], h = c->sat_dims[1], d = c->sat_dims[2];
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipMalloc((void**)&c->d_sat_cells, cvr::sat_cells_float4s(w, h, d) * sizeof(float4)));
-    HIP_TRY(c, cvr::launch_sat_cells(*c, c->d_sat, c->d_sat_cells, c->stream));
+    const hipError_t e = cvr::launch_sat_cells(*c, c->d_sat, c->d_sat_cells, c->stream);
+    if (e != hipSuccess) {   // never leave an unbuilt copy behind for the next frame to read
+      void* q = c->d_sat_cells; free_dev(q); c->d_sat_cells = nullptr;
+      return fail(c, CVR_ERR_HIP, "cvr_render_extbsd: cell4 SAT build: %s", hipGetErrorString(e));
+    }
   }
   const bool phong = p->apply_gradient_shading != 0;
   if (phong && !c->d_grad) return fail(c, CVR_ERR_STATE, "cvr_render_extbsd: Phong needs cvr_set_gradient");
@@ -1736,10 +1772,13 @@ cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_par
   fill_frame_args(c, f, p->step, Q.a, ntiles, npix);
   Q.a.filter_bits = c->filter_bits;   // GL_LINEAR weights of every fetch (CVR-SPEC-8 at 8)
   if (c->cell_skip > 0) {   // the per-cell skip flags in the count / emit march
-    cvr_status st = ensure_cell_flags(c);
-    if (st != CVR_OK) return st;
-    Q.a.cell_skip = 1;
-    Q.a.inv_step = 1.0f / Q.a.step;
+    const cvr_status st = cell_flags_or_off(c);
+    if (st == CVR_OK) {
+      Q.a.cell_skip = 1;
+      Q.a.inv_step = 1.0f / Q.a.step;
+    } else if (st != CVR_ERR_OOM) {
+      return st;
+    }
   }
   Q.a.out_half = o->format == CVR_FORMAT_RGBA16F;
   Q.a.ka = p->ka; Q.a.kd = p->kd; Q.a.ks = p->ks;

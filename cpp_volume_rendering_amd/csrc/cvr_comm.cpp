@@ -133,12 +133,14 @@ cvr_status cvr_gather_tiles_n(cvr_ctx* ctx, const cvr_frame* f, int nframes, con
   if (!c) return CVR_ERR_ARG;
   Comm* m = comm_of(c);
   if (!m) return cfail(c, CVR_ERR_STATE, "cvr_gather_tiles: cvr_comm_init not called");
-  if (!f || !d_packed || nframes < 1 || tpr_max < 0 || (f->nranks > 1 && f->tile_size < 16) ||
+  // gather_root_idle: rank 0 renders nothing; communicator ranks 1..N-1 render the
+  // split over N-1 render ranks (frame rank = communicator rank - 1).  An idle
+  // root sends nothing, so it needs no packed buffer.
+  const bool idle_root = c->gather_root_idle && m->nranks > 2;
+  if (!f || (!d_packed && !(idle_root && m->rank == 0)) || nframes < 1 || tpr_max < 0 ||
+      (f->nranks > 1 && f->tile_size < 16) ||
       (format != CVR_FORMAT_RGBA32F && format != CVR_FORMAT_RGBA16F))
     return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: bad arguments");
-  // gather_root_idle: rank 0 renders nothing; communicator ranks 1..N-1 render the
-  // split over N-1 render ranks (frame rank = communicator rank - 1)
-  const bool idle_root = c->gather_root_idle && m->nranks > 2;
   const int want_nranks = idle_root ? m->nranks - 1 : m->nranks;
   const int want_rank = idle_root ? m->rank - 1 : m->rank;
   if (f->nranks != want_nranks || (f->rank != want_rank && !(idle_root && m->rank == 0)))

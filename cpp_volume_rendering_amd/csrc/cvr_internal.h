@@ -272,6 +272,7 @@ struct Ctx {
   int cell_skip = 3;
   int cell_flags_valid = 0;       // the cells' flags match the current TF
   int cell_flags_set = 0;         // the cells carry flags (of some TF)
+  int cell_flags_oom = 0;         // the last flag build ran out of memory (retried after a volume / TF change)
   // transfer function (RGBA16F values as float)
   float* d_tf = nullptr;
   int tf_n = 0;

@@ -565,6 +565,10 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
       const unsigned long long v = wave_sum(nskip);
       if (lane == 0 && v) atomicAdd(&A.shade_ctr[1], v);
     }
+    if (CS > 0 && !PHONG) {   // the wave's march rounds (K cell loads each): bench.py's vmem roofline
+      const uint32_t r = wave_max(nbatch);
+      if (lane == 0 && r) atomicAdd(&A.shade_ctr[2], (unsigned long long)r);
+    }
   }
   if (tile_samples) {   // per-tile sample count; summed by tile_order_kernel (no hot atomic)
     unsigned long long v = wave_sum(cnt);

@@ -102,6 +102,12 @@ def _copy_frame(f):
     return g
 
 
+class CommUnavailable(N.CvrError):
+    """The library's RCCL communicator could not be created (cvr_comm_init failed):
+    the only error a caller may answer by falling back to torch's dist.gather.
+    Option and argument errors are CvrError and mean a wrong configuration."""
+
+
 class ScreenTileSplit:
     """One renderer's frames split over the ranks of a process group.
 
@@ -207,6 +213,10 @@ class ScreenTileSplit:
             # waits for the exchange that used its next set rounds earlier, not for
             # its own last one (library option gather_sets)
             self.nbuf = -(-int(buffer_sets) // streams) * streams
+            # the library holds the end events of the last MAX_GATHER_SETS exchanges
+            # (cvr.h CVR_MAX_GATHER_SETS): the most whole multiples of the streams
+            if self.nbuf > N.MAX_GATHER_SETS:
+                self.nbuf = max(streams, N.MAX_GATHER_SETS // streams * streams)
         self.G = max(1, int(frames_per_exchange)) if (self.transport == "rccl" and
                                                        self.streams is not None) else 1
         if self.split and self.G == 1:
@@ -278,7 +288,10 @@ class ScreenTileSplit:
         dist.broadcast(t, src=0, group=self.group)
         uid = bytes(t.cpu().tolist())
         h = self.r.device.handle
-        N.check(L.cvr_comm_init(h, self.world, self.rank, uid), "cvr_comm_init", h)
+        try:
+            N.check(L.cvr_comm_init(h, self.world, self.rank, uid), "cvr_comm_init", h)
+        except N.CvrError as e:
+            raise CommUnavailable(e.status, "cvr_comm_init", str(e)) from e
         self._comm = True
         N.check(L.cvr_set_option(h, b"split_streams", self.nstreams), "split_streams", h)
         N.check(L.cvr_set_option(h, b"gather_sets", self.nbuf), "gather_sets", h)

@@ -305,7 +305,8 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *   "gather_sets" buffer sets the caller rotates over those calls (a multiple of
  *                split_streams; 0 = one per stream): exchange g uses set g % B on
  *                stream g % D, and the stream's next render waits for exchange
- *                g + D - B, the last user of the set it writes next (0..48)
+ *                g + D - B, the last user of the set it writes next
+ *                (0..CVR_MAX_GATHER_SETS)
  *   "gather_root_idle" 1 (communicators of N >= 3 ranks): rank 0 renders nothing and
  *                only gathers and unpacks; ranks 1..N-1 render the split over N-1
  *                render ranks (their cvr_frame: rank = communicator rank - 1,
@@ -508,6 +509,9 @@ cvr_status  cvr_screenshot_rgb8(cvr_ctx* ctx, const void* d_frame, int format, i
  * -------------------------------------------------------------------------- */
 
 #define CVR_COMM_ID_BYTES 128
+/* The most exchange buffer sets (option "gather_sets"): the library keeps the
+ * end events of the last 64 exchanges. */
+#define CVR_MAX_GATHER_SETS 64
 
 /* Rank 0 creates the communicator id (ncclGetUniqueId) and hands it to every
  * rank out of band (e.g. torch.distributed broadcast). */
@@ -576,8 +580,10 @@ cvr_status  cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* 
 cvr_status  cvr_selftest_arith(cvr_ctx* ctx, uint64_t out[3]);
 
 /* Measurement (shade_counters option), for the last shaded frame
- * (cvr_render_dosct / cvr_render_extbsd; cvr_render_rc1pass with Blinn-Phong
- * fills out[0] only): out[0] samples that ran the shading
+ * (cvr_render_dosct / cvr_render_extbsd; cvr_render_rc1pass: out[0] the
+ * Blinn-Phong shaded samples, out[1] the samples the per-cell skip stepped over
+ * without a load, out[2] (emission-absorption, cell_skip > 0) the waves' march
+ * rounds, each K = 4 cell loads per wave): out[0] samples that ran the shading
  * (alpha > 0), out[1] those whose shadow was traced (spot cut-off excluded),
  * out[2] the secondary trilinear fetches actually issued (extinction pyramid /
  * SAT): the secondary traffic of the roofline.  For DOS the reference's own tap

@@ -392,14 +392,130 @@ def _native_idle_root_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("worker", ["flow", "batch", "idle_root"])
+def _native_bench8_worker(rank, world, port, q):
+    """Exactly `bench.py --gpus 8`'s default split (bench.split_defaults): 1024^2, 16^2
+    tiles, 4 frames per launch and per exchange, 4 render streams, 16 buffer sets,
+    an idle root (ranks 1..7 render the split over 7 render ranks), 32 HW queues.
+    Every rank must issue the same gathers; each render rank renders its 4-frame
+    groups as its own split rank into the group's buffer set, rotated over the 16."""
+    os.environ["WORLD_SIZE"] = str(world)       # bench.py reads it at import (HW queues)
+    import bench
+    from cpp_volume_rendering_amd import _native as N
+    from cpp_volume_rendering_amd.renderer import Camera
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fake = _FakeLib()
+        N._lib = fake
+
+        class R:
+            _ENTRY = "cvr_render_rc1pass"
+            _params = N.Rc1passParams()
+
+            class device:
+                handle = 1
+
+                @staticmethod
+                def set_stream(s):
+                    fake.stream = s
+
+        a = bench.parse(["--gpus", str(world)])
+        kw = bench.split_defaults(a, world)
+        assert kw == {"streams": 4, "frames_per_exchange": 4, "frames_per_launch": 4,
+                      "buffer_sets": 16, "root_renders": False}, kw
+        assert bench.HW_QUEUES == 32 and a.tile == 16 and a.transport == "rccl"
+        W = H = 1024
+        sp = T.ScreenTileSplit(R(), W, H, tile=a.tile, fmt=N.FORMAT_RGBA16F, device="cpu",
+                               transport=a.transport, stream_factory=_FakeStream,
+                               count_samples=True, **kw)
+        assert sp.idle_root and sp.renders == (rank != 0)
+        assert sp.sworld == world - 1 and sp.srank == max(rank - 1, 0)
+        assert sp.nbuf == 16 and sp.G == 4 and sp.L == 4 and sp.nstreams == 4
+        assert sp.k == (0 if rank == 0 else T.tiles_for_rank(W, H, 16, rank - 1, world - 1))
+        cam = Camera(**D.INITIAL_STATE_CAMERA)
+        nframes = 4 * 16 + 6            # every buffer set used, then reused, and a partial group
+        for _ in range(nframes):
+            sp.submit(cam)
+        sp.flush()
+        renders = [c for c in fake.calls if c[0] == "render_n"]
+        gathers = [c for c in fake.calls if c[0] == "gather"]
+        sizes = [4] * (nframes // 4) + ([nframes % 4] if nframes % 4 else [])
+        assert [g[2] for g in gathers] == sizes
+        streams = [s.cuda_stream for s in sp.streams]
+        bufs = set()
+        for grp, g in enumerate(gathers):
+            assert g[1] == streams[grp % 4]
+            assert g[4] == (rank == 0)
+            bufs.add(g[3])
+        if rank == 0:
+            assert renders == []
+        else:
+            assert [r[2] for r in renders] == sizes
+            assert all(fr == (rank - 1, world - 1) for r in renders for fr in r[5])
+            for grp, rc in enumerate(renders):
+                assert rc[1] == streams[grp % 4]
+            assert len(bufs) == 16          # the 16 sets rotate
+        for opt in (("opt", b"gather_root_idle", 1), ("opt", b"gather_sets", 16),
+                    ("opt", b"split_streams", 4)):
+            assert opt in fake.calls, opt
+        sp.close()
+        q.put(("ok", rank, len(gathers)))
+    except Exception as e:   # noqa: BLE001  (reported to the parent)
+        q.put(("fail", rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _buffer_sets_worker(rank, world, port, q):
+    """Buffer sets above the library's limit (CVR_MAX_GATHER_SETS = 64) are clamped to
+    the most whole multiples of the streams, never passed on."""
+    from cpp_volume_rendering_amd import _native as N
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fake = _FakeLib()
+        N._lib = fake
+
+        class R:
+            _ENTRY = "cvr_render_rc1pass"
+            _params = N.Rc1passParams()
+
+            class device:
+                handle = 1
+
+                @staticmethod
+                def set_stream(s):
+                    fake.stream = s
+
+        for streams, sets, want in ((16, 64, 64), (16, 80, 64), (13, 52, 52), (20, 80, 60),
+                                    (3, 200, 63)):
+            fake.calls.clear()
+            sp = T.ScreenTileSplit(R(), 64, 64, tile=16, fmt=N.FORMAT_RGBA16F, device="cpu",
+                                   transport="rccl", streams=streams, stream_factory=_FakeStream,
+                                   buffer_sets=sets)
+            assert sp.nbuf == want, (streams, sets, sp.nbuf)
+            assert ("opt", b"gather_sets", want) in fake.calls
+            sp.close()
+        q.put(("ok", rank, 0))
+    except Exception as e:   # noqa: BLE001  (reported to the parent)
+        q.put(("fail", rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("worker", ["flow", "batch", "idle_root", "bench8", "buffer_sets"])
 def test_native_split_control_flow_gloo(worker):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     target = {"flow": _native_flow_worker, "batch": _native_batch_worker,
-              "idle_root": _native_idle_root_worker}[worker]
-    world = 3 if worker == "idle_root" else 2
+              "idle_root": _native_idle_root_worker, "bench8": _native_bench8_worker,
+              "buffer_sets": _buffer_sets_worker}[worker]
+    world = {"idle_root": 3, "bench8": 8}.get(worker, 2)
     procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()

@@ -14,7 +14,7 @@ WRITE_SIZE are KiB per dispatch; on gfx950 FETCH_SIZE counts 128-B requests at 6
 so it is doubled.  Both are the L2's fabric-side requests (Infinity-Cache hits
 included): an upper bound of the bytes HBM served.  busy = counter / 256 CUs /
 (kernel ns x 2.4 GHz); VALU issue = SQ_INSTS_VALU x 2 cycles / 1024 SIMDs / kernel
-cycles; VALU per sample = SQ_INSTS_VALU x 64 / samples; scratch estimate = write
+cycles (a wave64 VALU instruction issues over 2 cycles, the guide's constants table); VALU per sample = SQ_INSTS_VALU x 64 / samples; scratch estimate = write
 bytes - the frame's algorithmic stores."""
 import json
 import sys
@@ -53,10 +53,29 @@ if "SQ_INSTS_VALU" in summ and samples and bench["metric"].startswith("Msamples/
 for k in ("SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"):
     if k in summ:
         rec[k.lower()] = summ[k]
+# the vector-memory pipe (DESIGN §5 "what a wave-load costs"): TD busy splits into
+# cycles stalled on the cache (TD_TC_STALL: L1 misses in flight) and its own work;
+# TCP accesses count (lane quad, 128-B line) pairs, 16 per coalesced dwordx4 wave-load
+if cyc and "TD_TC_STALL" in summ:
+    rec["td_tc_stall_frac_per_cu"] = summ["TD_TC_STALL"] / 256.0 / cyc
+vm = summ.get("SQ_INSTS_VMEM_RD")
+if vm:
+    if "TD_TD_BUSY" in summ and "TD_TC_STALL" in summ:
+        rec["td_work_cycles_per_wave_load"] = (summ["TD_TD_BUSY"] - summ["TD_TC_STALL"]) / vm
+        rec["td_busy_cycles_per_wave_load"] = summ["TD_TD_BUSY"] / vm
+    if "TCP_TOTAL_CACHE_ACCESSES_sum" in summ:
+        rec["tcp_accesses_per_wave_load"] = summ["TCP_TOTAL_CACHE_ACCESSES_sum"] / vm
+    if "TCP_TCC_READ_REQ_sum" in summ:
+        rec["l1_miss_requests_per_wave_load"] = summ["TCP_TCC_READ_REQ_sum"] / vm
+if ns and "GRBM_GUI_ACTIVE" in summ:
+    # the guide's effective clock: GRBM_GUI_ACTIVE summed over the 8 XCDs / kernel time
+    rec["effective_clock_ghz_under_pmc"] = summ["GRBM_GUI_ACTIVE"] / 8.0 / ns
+rec["frames_per_launch"] = bench["config"].get("frames_per_launch", 1)
+rec["counters"] = {k: v for k, v in summ.items() if not k.startswith("_")}
 rec["dispatches"] = summ.get("_dispatches_per_counter", {})
 rec["method"] = ("rocprofv3 --kernel-trace --pmc, one pass per counter group (tools/pmc_bench.sh); "
                  "tools/pmc_summary.py averages the dominant kernel's dispatches; "
                  "tools/pmc_record.py (corrections in its docstring)")
-rec["round"] = 4
+rec["round"] = 5
 json.dump(rec, open(out, "w"), indent=1)
 print(json.dumps(rec, indent=1))
