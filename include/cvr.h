@@ -327,6 +327,18 @@ cvr_status  cvr_set_option(cvr_ctx* ctx, const char* key, int value);
 int         cvr_get_option(const cvr_ctx* ctx, const char* key);
 cvr_status  cvr_synchronize(cvr_ctx* ctx);
 
+/* State setters (cvr_set_volume*, cvr_set_transfer_function, cvr_set_gradient,
+ * cvr_set_extinction_volume, cvr_set_extinction_sat, and the cone-table upload
+ * inside cvr_render_dosct when its cone parameters change) first drain the
+ * WHOLE device (hipDeviceSynchronize): frames already issued on any stream --
+ * the caller may rotate several non-blocking streams -- finish with the old
+ * state, and frames issued after the call see the new one (the ordering GL
+ * gives the reference's Init after a TF change, renderingmanager.cpp:1050-1127).
+ * The per-cell skip flags a new volume or TF needs are rebuilt lazily by the
+ * next frame; if their scratch (2 B per cell) cannot be allocated, that frame
+ * and the following ones render without the skip (the same pixels) until the
+ * next state change. */
+
 /* Volume: x-fastest voxels (i + j*w + k*w*h), 1 byte (u8) or 2 bytes (u16)
  * per voxel, normalised as v/255 or v/65535 (structuredgridvolume.cpp:121-151)
  * and stored with GL_R16F semantics.  The data is copied (host pointer). */
