@@ -927,6 +927,21 @@ def main():
             roof["vmem_dwordx4_per_s"] = round(vm, 1)
             roof["vmem_peak_dwordx4_per_s"] = vm_peak
             roof["vmem_frac"] = round(vm / vm_peak, 4)
+        if shaded and pmc.get("kernel_ns_avg_under_pmc") and pmc.get("valu_wave_insts"):
+            # the shade kernel's own pipes (the counters and the duration of the same
+            # dispatches under PMC; the frame's other kernels are ~15 % of it): the
+            # roofline on the pipe that binds, beside the L2 figure
+            t_pmc = pmc["kernel_ns_avg_under_pmc"] * 1e-9
+            pipes = {"valu": {"frac": round(pmc["valu_wave_insts"] / t_pmc / 1e9 / VALU_PEAK_GWIPS, 4),
+                              "count": "PMC SQ_INSTS_VALU of flat_shade_kernel"}}
+            if pmc.get("sq_insts_vmem_rd"):
+                pipes["vmem"] = {"frac": round(pmc["sq_insts_vmem_rd"] * 1024 / t_pmc / 1e9 / VMEM_PEAK_GBS, 4),
+                                 "count": "PMC SQ_INSTS_VMEM_RD of flat_shade_kernel"}
+            if pmc.get("td_tc_stall_frac_per_cu") is not None:
+                pipes["vmem"]["td_busy_per_cu"] = round(pmc["td_busy_frac_per_cu"], 3)
+                pipes["vmem"]["td_stalled_on_cache_per_cu"] = round(pmc["td_tc_stall_frac_per_cu"], 3)
+            roof["shade_kernel_pipes"] = pipes
+            roof["shade_kernel_bound"] = max(pipes, key=lambda k: pipes[k]["frac"])
         # the counters of the same workload's dominant kernel on this library build
         # (rocprofv3 --pmc, committed under profiles/): which pipe is busy, VALU per
         # sample, the bytes written

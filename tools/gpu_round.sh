@@ -17,6 +17,6 @@ if [ "$STEP" = "all" ] || [ "$STEP" = "bench" ]; then
   timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err && cat gpurun_out/bench.json || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
 fi
 if [ "$STEP" = "all" ] || [ "$STEP" = "prof" ]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o trace --output-format csv -- python3 bench.py --no-cpu-baseline --streams 1 --steps 20 > gpurun_out/prof_bench.json 2> gpurun_out/prof.err || { echo "prof failed"; tail -20 gpurun_out/prof.err; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o trace --output-format csv -- python3 bench.py --no-cpu-baseline --no-cadence --streams 1 --steps 20 > gpurun_out/prof_bench.json 2> gpurun_out/prof.err || { echo "prof failed"; tail -20 gpurun_out/prof.err; exit 1; }
   find gpurun_out/prof -name "*stats*" | head
 fi

@@ -1,28 +1,32 @@
 #!/bin/bash
 # One GPU session of the current round (edited per session; the committed copy is
 # the last one run).  Each GPU step has its own limit; the first failure ends the call.
+# Round 5, s05: the round's final library -- GPU suite, smoke, PMC records of every
+# workload (bench.py uses a record only on the build it was counted on), bench lines,
+# and the one-stream kernel trace of the headline.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=${TAG:-r05_s04}
+T=${TAG:-r05_s05}
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest_gpu_all.log 2>&1 || { tail -30 gpurun_out/${T}_pytest_gpu_all.log; exit 1; }
 tail -2 gpurun_out/${T}_pytest_gpu_all.log
-# A/B: the x-lerps as one asm block (no s_nop hazard waits) vs four (round 4)
-timeout -k 10 900 bash tools/ab_bench.sh tri_old ea "--steps 200 --warmup 20 --no-cadence" 3 > gpurun_out/${T}_ab_tri_ea.log 2>&1 || { tail -5 gpurun_out/${T}_ab_tri_ea.log; exit 1; }
-tail -2 gpurun_out/${T}_ab_tri_ea.log
-timeout -k 10 900 bash tools/ab_bench.sh tri_old ea1 "--steps 200 --warmup 20 --no-cadence --frames-per-launch 1 --streams 1" 2 > gpurun_out/${T}_ab_tri_ea1.log 2>&1 || { tail -5 gpurun_out/${T}_ab_tri_ea1.log; exit 1; }
-tail -2 gpurun_out/${T}_ab_tri_ea1.log
-timeout -k 10 900 bash tools/ab_bench.sh tri_old phong "--phong --no-cadence" 2 > gpurun_out/${T}_ab_tri_phong.log 2>&1 || { tail -5 gpurun_out/${T}_ab_tri_phong.log; exit 1; }
-tail -2 gpurun_out/${T}_ab_tri_phong.log
-timeout -k 10 900 bash tools/ab_bench.sh tri_old dos "--renderer dos --steps 5" 2 > gpurun_out/${T}_ab_tri_dos.log 2>&1 || { tail -5 gpurun_out/${T}_ab_tri_dos.log; exit 1; }
-tail -2 gpurun_out/${T}_ab_tri_dos.log
-# per-view kernel times over the 24 reference camera states (static vs orbit, LPT vs interleaved)
-timeout -k 10 400 python tools/orbit_views.py --orders 1,2 --smooth 0,3,10 > gpurun_out/${T}_orbit_views.json 2> gpurun_out/${T}_orbit_views.err || { tail -5 gpurun_out/${T}_orbit_views.err; exit 1; }
-python3 -c "import json; d=json.load(open('gpurun_out/${T}_orbit_views.json')); print(d['modes'], d.get('smooth'))"
-# plugin cadence (one frame per call, one stream) with the quad march for the longest
-# tiles: a lone frame lasts as long as its longest tile (~110 us at ~0.28 us per batch)
-for q in 0 1 3 6; do
-  timeout -k 10 300 python bench.py --quad $q --steps 40 --warmup 10 --no-cpu-baseline > gpurun_out/${T}_cad_quad$q.json 2> gpurun_out/${T}_cad_quad$q.err || { tail -5 gpurun_out/${T}_cad_quad$q.err; exit 1; }
-  python3 -c "import json; d=json.load(open('gpurun_out/${T}_cad_quad$q.json')); c=d['plugin_cadence']; print('quad $q', d['ms_per_step'], c['static']['ms_per_frame'], c['static']['kernel_ms_mean'], c['orbit']['ms_per_frame'], c['orbit']['kernel_ms_mean'], d.get('parity', {}).get('bit_exact'))"
-done
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || { tail -10 gpurun_out/${T}_smoke.log; exit 1; }
+tail -1 gpurun_out/${T}_smoke.log
+timeout -k 10 2400 bash tools/pmc_session.sh rc1pass phong longray dos ebs > gpurun_out/${T}_pmc_session.log 2>&1 || { tail -20 gpurun_out/${T}_pmc_session.log; exit 1; }
+tail -5 gpurun_out/${T}_pmc_session.log
+for w in rc1pass rc1pass_phong rc1pass_longray dos ebs; do cp gpurun_out/pmc_$w.json profiles/pmc_$w.json; done
+run() {   # name, bench args
+  local name=$1; shift
+  timeout -k 10 400 python bench.py "$@" > gpurun_out/${T}_$name.json 2> gpurun_out/${T}_$name.err || { tail -20 gpurun_out/${T}_$name.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/${T}_$name.json')); r=d['roofline']; print('$name', d['ms_per_step'], r['kernel_ms'], r.get('bound'), r['frac'], r.get('effective_frac'), d['value'], json.dumps({k: (v['ms_per_frame'], v['kernel_ms_mean']) for k, v in d.get('plugin_cadence', {}).items() if isinstance(v, dict)}))"
+}
+run driver --gpus 1 --steps 20 --warmup 5
+run driver200
+run phong --phong --no-cadence
+run longray --tf-alpha 0.02 --no-cadence
+run orbit --orbit --steps 96 --warmup 24 --no-cpu-baseline
+run dos --renderer dos
+run ebs --renderer ebs
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o trace --output-format csv -- python3 bench.py --no-cpu-baseline --no-cadence --streams 1 --steps 20 > gpurun_out/${T}_prof_bench.json 2> gpurun_out/${T}_prof.err || { echo "prof failed"; tail -20 gpurun_out/${T}_prof.err; exit 1; }
+find gpurun_out/${T}_prof -name "*kernel_stats.csv" | head -1
