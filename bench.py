@@ -193,9 +193,6 @@ def parse(argv=None):
     p.add_argument("--skip-min-pct", type=int, default=-1,
                    help="empty-space skipping when >= this %% of macro cells are empty (101: off; "
                         "-1: the library default)")
-    p.add_argument("--prefetch", type=int, default=-1, choices=[-1, 0, 1],
-                   help="rc1pass: 1 = the software-pipelined march (next batch's loads as LDS-DMA "
-                        "during the composite), 0 = the plain march (-1: library default)")
     p.add_argument("--cell-skip", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4],
                    help="rc1pass per-cell skip: 0 off, 1 empty-sample flags, 2 + distance skip "
                         "(-1: the library default, 3: + the distance skip when every lane can)")
@@ -666,9 +663,6 @@ def main():
                     r.device.handle)
         if a.cell_skip >= 0:
             N.check(N.lib().cvr_set_option(r.device.handle, b"cell_skip", a.cell_skip), "cell_skip",
-                    r.device.handle)
-        if a.prefetch >= 0:
-            N.check(N.lib().cvr_set_option(r.device.handle, b"prefetch", a.prefetch), "prefetch",
                     r.device.handle)
         if a.launch_interleave >= 0:
             N.check(N.lib().cvr_set_option(r.device.handle, b"launch_interleave", a.launch_interleave),

@@ -433,11 +433,6 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->max_waves_cu = value;
     return CVR_OK;
   }
-  if (!std::strcmp(key, "prefetch")) {
-    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "prefetch must be 0 or 1");
-    c->prefetch = value;
-    return CVR_OK;
-  }
   if (!std::strcmp(key, "launch_interleave")) {
     if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "launch_interleave must be 0 or 1");
     c->launch_interleave = value;
@@ -507,7 +502,6 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "gather_sets")) return c->gather_sets;
   if (!std::strcmp(key, "gather_root_idle")) return c->gather_root_idle;
   if (!std::strcmp(key, "launch_interleave")) return c->launch_interleave;
-  if (!std::strcmp(key, "prefetch")) return c->prefetch;
   if (!std::strcmp(key, "sat_build_us")) return c->sat_build_us;   // read-only
   if (!std::strcmp(key, "order_interval")) return c->order_interval;
   if (!std::strcmp(key, "skip_min_pct")) return c->skip_min_pct;

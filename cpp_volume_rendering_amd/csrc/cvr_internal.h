@@ -377,7 +377,6 @@ struct Ctx {
   void* comm = nullptr;
   int split_streams = 1;           // option "split_streams": render streams the caller rotates
   int gather_sets = 0;             // option "gather_sets": buffer sets the caller rotates (>= split_streams)
-  int prefetch = 0;                // option "prefetch": the software-pipelined (LDS-DMA) EA march (raymarch.hip)
   int launch_interleave = 1;       // option "launch_interleave": multi-frame launches deal the frames'
                                    // launch-order entries interleaved (LaunchFrames::interleave)
   int gather_root_idle = 0;        // option "gather_root_idle": rank 0 only gathers (renders nothing)

@@ -320,203 +320,6 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
   }
 }
 
-// ---------------------------------------------------------------------------
-// Prefetched march (option "prefetch", round 5)
-// ---------------------------------------------------------------------------
-// march_ray<4, false, false, XF, 2, 0, CS> software-pipelined through LDS.  The
-// march is latency-bound (§5′): per SIMD 8 waves each issue a batch of four
-// 16-B cell loads and wait for them, and VALU is busy 62 % of the time.  Here
-// the NEXT batch's loads are issued as LDS-DMA (buffer_load_dwordx4 ... lds)
-// before the current batch's composite, so they are in flight while it runs,
-// and they hold no VGPRs while in flight (the data lands in a 4 KiB staging
-// buffer; the batch reads it back with four ds_read_b128).  The TF moves to LDS
-// as RGBA16F (8 B per padded entry; its values are RGBA16F already, so the lerps
-// read the halves exactly, as the cells' x-lerps do), leaving room for the
-// staging buffer.  Images and per-pixel counts are march_ray's bit for bit: the
-// only reordering is that the distance skip of a batch is decided before its
-// composite, i.e. a lane that the composite stops (ERT) may still count as able
-// to skip -- a skip is exact for every lane that keeps marching, and a stopped
-// lane counts none of it, so only the wave's round structure changes.
-constexpr int kPfK = 4;
-
-// Padded RGBA16F TF: tfh[k] = T[clamp(k - 1, 0, n - 1)] as (r | g << 16, b | a << 16).
-__device__ __forceinline__ void load_tf_lds_half(uint2* tfh, const float4* __restrict__ tf_g, int n) {
-  for (int i = threadIdx.x; i < n + 2; i += blockDim.x) {
-    const float4 v = tf_g[min(max(i - 1, 0), n - 1)];
-    tfh[i] = make_uint2(f32_to_h16(v.x) | (f32_to_h16(v.y) << 16), f32_to_h16(v.z) | (f32_to_h16(v.w) << 16));
-  }
-  __syncthreads();
-}
-
-// lerpf(a, b, t) of fp16 values held in the low (LO) or high halves of the words
-// wa, wb: (b - a) as one mixed-precision FMA (b * 1 - a, one rounding = the f32
-// subtraction of the exactly converted halves), then fmaf(t, b - a, a).
-template <bool HI>
-__device__ __forceinline__ float half_lerp(uint32_t wa, uint32_t wb, float t) {
-  float d, r;
-  if (HI) {
-    asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(wb), "v"(wa));
-    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r) : "v"(t), "v"(d), "v"(wa));
-  } else {
-    asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[1,0,1]" : "=v"(d) : "v"(wb), "v"(wa));
-    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(t), "v"(d), "v"(wa));
-  }
-  return r;
-}
-
-template <bool XF, int CS>
-__device__ __forceinline__ void march_ray_pf(const Rc1passArgs& A, const uint4* __restrict__ cells,
-                                             const uint2* __restrict__ tfh, uint4* __restrict__ stage,
-                                             int px, int py, float4& dst, uint32_t& cnt,
-                                             uint32_t& nbatch, uint32_t& nskip) {
-  constexpr int K = kPfK;
-  dst = make_float4(0.f, 0.f, 0.f, 0.f);
-  cnt = 0;
-  Ray r;
-  if (!ray_setup(A, px, py, r)) return;   // misses keep (0,0,0,0)
-  const float step = A.step, D = r.D, fn = (float)A.tf_n;
-  float s = 0.0f;
-  bool done = !(s < D);
-  const bool wave_in_box = __ballot(r.outside) == 0;
-  const __amdgpu_buffer_rsrc_t crs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)cells, 0, -1, kBufferConfigDword);
-  const int lane = (int)__lane_id();
-  typedef __attribute__((address_space(3))) void* lds_ptr;
-  // stage 1 of the batch starting at s0: its steps, validity and trilinear
-  // weights; its four cell loads go to the staging buffer (slot j * 64 + lane)
-  auto stage1 = [&](float s0, float (&h)[K], bool (&v)[K], float (&wx)[K], float (&wy)[K],
-                    float (&wz)[K], float& ss_out) {
-    float c[K + 1];
-    float t[K];
-    c[0] = s0;
-#pragma unroll
-    for (int j = 0; j < K; j++) c[j + 1] = c[j] + step;
-    if (__ballot(!(D - c[K - 1] >= step)) == 0) {
-#pragma unroll
-      for (int j = 0; j < K; j++) {
-        v[j] = true;
-        h[j] = step;
-        t[j] = fmaf(step, 0.5f, c[j]);
-      }
-      ss_out = c[K];
-    } else {
-      float ss = s0;
-#pragma unroll
-      for (int j = 0; j < K; j++) {
-        v[j] = ss < D;
-        h[j] = fminf(step, D - ss);
-        t[j] = v[j] ? fmaf(h[j], 0.5f, ss) : 0.0f;
-        ss = ss + h[j];
-      }
-      ss_out = ss;
-    }
-#pragma unroll
-    for (int j = 0; j < K; j++) {
-      const float x = fmaf(r.dt.x, t[j], r.o.x), y = fmaf(r.dt.y, t[j], r.o.y), z = fmaf(r.dt.z, t[j], r.o.z);
-      const SamplePos p = wave_in_box ? sample_pos(x, y, z, A) : sample_pos_clamped(x, y, z, A);
-      wx[j] = p.ax;
-      wy[j] = p.ay;
-      wz[j] = p.az;
-      const uint32_t off = mad_i24(p.iz, A.cells.bpitch_z,
-                                   mad_i24(p.iy, A.cells.bpitch_y, ((uint32_t)p.ix << 4) + A.cells.borigin));
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)(stage + j * 64), 16, (int)off, 0, 0, 0);
-    }
-  };
-  float hc[K], axc[K], ayc[K], azc[K], ssc;
-  bool vc[K];
-  if (!done) stage1(s, hc, vc, axc, ayc, azc, ssc);
-  while (!done) {
-    if (CS > 0) nbatch++;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this batch's cells are in LDS
-    uint4 raw[K];
-#pragma unroll
-    for (int j = 0; j < K; j++) raw[j] = stage[j * 64 + lane];
-    // stage 2: alpha first, as march_ray (the rgb lerps only for visible samples)
-    bool we[K];
-    int tfi[K];
-    float tfa[K], sw[K];
-    int qlast = 0;
-#pragma unroll
-    for (int j = 0; j < K; j++) {
-      we[j] = CS > 0 && __ballot(!cell_empty(raw[j])) == 0;
-      if (CS >= 2 && j == K - 1) qlast = cell_empty(raw[j]) ? cell_skip_q(raw[j]) : 0;
-      if (CS > 0 && we[j]) {
-        tfa[j] = 0.0f; tfi[j] = 0; sw[j] = 0.0f;
-      } else {
-        const float xd = fmaf(trilerp_cell<true>(raw[j], axc[j], ayc[j], azc[j]), fn, -0.5f);
-        tfa[j] = __builtin_amdgcn_fractf(xd);
-        tfi[j] = cvt_flr(xd);   // padded entries tfi + 1, tfi + 2
-        sw[j] = half_lerp<true>(tfh[tfi[j] + 1].y, tfh[tfi[j] + 2].y, tfa[j]);
-      }
-    }
-    // the batch's end, and the distance skip decided before its composite
-    s = ssc;
-    const bool end_i = !(s < D);
-    uint32_t iskip = 0;
-    if (CS >= 2 && wave_in_box) {
-      const bool ok = !end_i && qlast > 0 && vc[K - 1];
-      if ((CS != 3 || __ballot(!ok) == 0) && ok) {
-        float dx = r.dt.x, dy = r.dt.y, dz = r.dt.z;
-        asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
-        const float kinv = __builtin_amdgcn_rcpf(step * fmaxf(fmaxf(fabsf(dx), fabsf(dy)), fabsf(dz)));
-        int m = min(cvt_flr(((float)qlast - kSkipMarginTexels) * kinv), cvt_flr((D - s) * A.inv_step) - 2);
-        if (CS == 2) {
-          if (m > 0) {
-            iskip = (uint32_t)m;
-            for (; m > 0; m--) s = s + step;
-          }
-        } else {
-          int i = 0;
-          for (; __all(i < m); i++) s = s + step;
-          iskip = (uint32_t)i;
-        }
-      }
-    }
-    // the next batch's loads: in flight during this batch's composite
-    float hn[K], axn[K], ayn[K], azn[K], ssn = s;
-    bool vn[K];
-    if (!end_i) stage1(s, hn, vn, axn, ayn, azn, ssn);
-    // stage 3: front-to-back composite + ERT, in sample order (march_ray's)
-#pragma unroll
-    for (int j = 0; j < K; j++) {
-      if (!done) {
-        if (!vc[j]) {
-          done = true;
-        } else {
-          cnt++;
-          if (!(CS > 0 && we[j]) && sw[j] > 0.0f) {
-            const uint2 e1 = tfh[tfi[j] + 1], e2 = tfh[tfi[j] + 2];
-            const float cr = half_lerp<false>(e1.x, e2.x, tfa[j]);
-            const float cg = half_lerp<true>(e1.x, e2.x, tfa[j]);
-            const float cb = half_lerp<false>(e1.y, e2.y, tfa[j]);
-            const float x = -(sw[j] * hc[j]);
-            const float a = 1.0f - (XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
-            const float om = 1.0f - dst.w;
-            dst.x = fmaf(om, cr * a, dst.x);
-            dst.y = fmaf(om, cg * a, dst.y);
-            dst.z = fmaf(om, cb * a, dst.z);
-            dst.w = fmaf(om, a, dst.w);
-            if (dst.w > 0.99f) done = true;
-          }
-        }
-      }
-    }
-    if (!done) {
-      cnt += iskip;
-      nskip += iskip;
-    }
-    if (end_i) done = true;
-#pragma unroll
-    for (int j = 0; j < K; j++) {
-      hc[j] = hn[j]; vc[j] = vn[j];
-      axc[j] = axn[j]; ayc[j] = ayn[j]; azc[j] = azn[j];
-    }
-    ssc = ssn;
-  }
-  // no LDS-DMA write may land after the wave (and its LDS) is gone
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // Value of `v` in lane L of this lane's quad (DPP quad_perm broadcast).
 template <int L>
 __device__ __forceinline__ float quad_bcast(float v) {
@@ -659,8 +462,8 @@ constexpr int rc1_waves_per_eu() {
   return (K == 4 && !PHONG && !SKIP && !QUAD) ? 8 : 1;
 #endif
 }
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB, int CS, bool PF = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF ? 1 : rc1_waves_per_eu<K, PHONG, SKIP, QUAD>())))
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB, int CS>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rc1_waves_per_eu<K, PHONG, SKIP, QUAD>())))
 rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
                     float4* __restrict__ out0, uint32_t* __restrict__ samples0,
@@ -712,14 +515,7 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
   } else {
     t = b;
   }
-  static_assert(!PF || (K == kPfK && !PHONG && !SKIP && !QUAD && BUF == 2 && FB == 0 && CS > 0),
-                "the prefetched march is the emission-absorption headline variant only");
-  // PF: a static LDS staging buffer (its address folds into M0 at compile time)
-  // and the TF as RGBA16F in the dynamic LDS
-  __shared__ uint4 pf_stage[PF ? kPfK * 64 : 1];
-  uint2* tfh = reinterpret_cast<uint2*>(tfp);
-  if (PF) load_tf_lds_half(tfh, tf_g, A.tf_n);
-  else load_tf_lds(tfp, tf_g, A.tf_n);
+  load_tf_lds(tfp, tf_g, A.tf_n);
   const int lane = threadIdx.x;
   unsigned long long t_start = 0;
   if (A.tile_stats || A.cost_time) t_start = __builtin_amdgcn_s_memrealtime();
@@ -736,11 +532,8 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
     const bool inside = px < A.W && py < A.H;
     dst = make_float4(0.f, 0.f, 0.f, 0.f);
     cnt = 0;
-    if (PF) {
-      if (inside) march_ray_pf<XF, CS>(A, cells, tfh, pf_stage, px, py, dst, cnt, nbatch, nskip);
-    } else if (inside) {
-      march_ray<K, PHONG, SKIP, XF, BUF, FB, CS>(A, cells, grad, tfp, px, py, dst, cnt, nshade, nbatch, nskip);
-    }
+    if (inside) march_ray<K, PHONG, SKIP, XF, BUF, FB, CS>(A, cells, grad, tfp, px, py, dst, cnt, nshade,
+                                                          nbatch, nskip);
     writer = inside || A.packed;
     if (CS > 0) {
       // the output index again, from the lane id (v_mbcnt) and the wave's tile
@@ -1023,11 +816,11 @@ __global__ void clear_u32_kernel(uint32_t* __restrict__ p, int n) {
 // Kernel variant: K (batch), PHONG, SKIP (empty-space skipping compiled in),
 // QUAD (quad path compiled in), XF (range-free exp).  Paths a frame does not
 // use are compiled out: they would cost the hot loop registers (occupancy).
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB = 0, int CS = 0, bool PF = false>
+template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB = 0, int CS = 0>
 static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                                  unsigned long long* tile_samples, const int* order,
                                  uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
-  size_t lds = PF ? (size_t)(a.tf_n + 2) * sizeof(uint2) : (size_t)(a.tf_n + 2) * sizeof(float4);
+  size_t lds = (size_t)(a.tf_n + 2) * sizeof(float4);
   if (c.max_waves_cu > 0) lds = std::max(lds, (size_t)(160 * 1024 / c.max_waves_cu) & ~(size_t)255);
   // cell (1,1,1) <-> texel (0,0,0)
   const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
@@ -1041,7 +834,7 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
     lf.interleave = (order && (grid & 7) == 0 && c.launch_interleave) ? 1 : 0;
     grid *= lf.n;
   }
-  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF, FB, CS, PF>), dim3(grid), dim3(64), lds, s,
+  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF, FB, CS>), dim3(grid), dim3(64), lds, s,
                      a, cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, out, samples,
                      tile_samples, order, tile_cost, order ? plan.boost : 0, lf);
   return hipGetLastError();
@@ -1066,19 +859,6 @@ static hipError_t launch_kps(const Ctx& c, const Rc1passArgs& a, float4* out, ui
                       : launch_variant<K, PHONG, SKIP, false, false, 0, 8>(c, a, out, samples, ts, order, tile_cost, plan, s);
   }
   const bool quad = order && plan.quad_pct > 0;
-  if constexpr (K == kPfK && !PHONG && !SKIP) {
-    if (!quad && a.cell_skip > 0 && buf == 2 && c.prefetch) {
-      // the prefetched march (option "prefetch"): the emission-absorption variants
-#define CVR_PF_LAUNCH(CSV)                                                                                 \
-      return a.exp_fast ? launch_variant<K, PHONG, false, false, true, 2, 0, CSV, true>(c, a, out, samples, ts, order, tile_cost, plan, s) \
-                        : launch_variant<K, PHONG, false, false, false, 2, 0, CSV, true>(c, a, out, samples, ts, order, tile_cost, plan, s);
-      if (a.cell_skip == 1) { CVR_PF_LAUNCH(1) }
-      if (a.cell_skip == 2) { CVR_PF_LAUNCH(2) }
-      if (a.cell_skip == 4) { CVR_PF_LAUNCH(4) }
-      CVR_PF_LAUNCH(3)
-#undef CVR_PF_LAUNCH
-    }
-  }
   if (!SKIP && !quad && a.cell_skip > 0) {   // per-cell skip flags (a.occ is null then)
 #define CVR_CS_LAUNCH(CSV)                                                                                 \
     if (buf == 2)                                                                                          \
