@@ -246,6 +246,9 @@ def parse(argv=None):
     p.add_argument("--settle-ms", type=float, default=150.0,
                    help="untimed frames before the warmup until this much wall time has passed "
                         "(GPU clocks ramp over the first ~100 ms of load)")
+    p.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                   help="extra cvr_set_option (repeatable; e.g. band_cap=150), recorded in "
+                        "config.options")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher rehearsal without a GPU: the ranks join a gloo group and "
                         "rank 0 prints the world size (tests/test_bench_launch.py)")
@@ -670,6 +673,9 @@ def main():
         if a.skip_min_pct >= 0:
             N.check(N.lib().cvr_set_option(r.device.handle, b"skip_min_pct", a.skip_min_pct),
                     "skip_min_pct", r.device.handle)
+    for kv in a.opt:
+        k, _, v = kv.partition("=")
+        N.check(N.lib().cvr_set_option(r.device.handle, k.encode(), int(v)), k, r.device.handle)
     if shaded and a.shade_flat >= 0:
         N.check(N.lib().cvr_set_option(r.device.handle, b"shade_flat", a.shade_flat), "shade_flat",
                 r.device.handle)
@@ -1054,6 +1060,7 @@ def main():
                                    + (", Blinn-Phong FD gradient" if a.phong else ""),
                        "volume": n, "viewport": [W, H], "samples_per_frame": S_all,
                        "workload_key": wkey, "lib_sha16": sha,
+                       **({"options": dict(kv.partition("=")[::2] for kv in a.opt)} if a.opt else {}),
                        "settle_frames": settle,
                        "parallelism": f"screen tiles {tile}x{tile} over {world} GPU(s)"
                                       if world > 1 else "1 GPU",

@@ -482,6 +482,13 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->boost_pct = value;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "band_cap")) {
+    if (value < 100 || value > 200) return fail(c, CVR_ERR_ARG, "band_cap must be 100..200");
+    if (value != c->band_cap_pct)
+      for (auto& o : c->oslot) o.valid = 0;   // the learned orders are laid out for the old cap
+    c->band_cap_pct = value;
+    return CVR_OK;
+  }
   return fail(c, CVR_ERR_ARG, "unknown option '%s'", key);
 }
 
@@ -492,6 +499,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "tile_order")) return c->use_order;
   if (!std::strcmp(key, "stale_deg")) return c->stale_deg;
   if (!std::strcmp(key, "boost")) return c->boost_pct;
+  if (!std::strcmp(key, "band_cap")) return c->band_cap_pct;
   if (!std::strcmp(key, "tile_cost")) return c->cost_time;
   if (!std::strcmp(key, "macro")) return c->macro_shift;
   if (!std::strcmp(key, "max_waves_cu")) return c->max_waves_cu;
@@ -955,10 +963,12 @@ static cvr_status render_rc1pass_frames(Ctx* c, const cvr_frame* frames, int nf,
   plan.quad_pct = c->filter_bits ? 0 : c->quad_pct;   // the quad march has no filter_bits variant
   {
     // Bands are cut by predicted work, so one may hold more than 1/8 of the
-    // tiles: up to 2x the even share (the epilogue falls back to even bands
-    // past that); every band gets that many slots (+3 per quad-split tile).
+    // tiles: up to band_cap % of the even share (default 2x; the epilogue falls
+    // back to even bands past that); every band gets that many slots (+3 per
+    // quad-split tile), and the slots past a band's entries are empty workgroups.
     const int seg_avg = (plan.ntiles + 7) / 8;
-    plan.max_seg = std::min(std::min(plan.ntiles, 2 * seg_avg), cvr::kMaxBandTiles);
+    const int cap = (int)(((long long)seg_avg * c->band_cap_pct + 99) / 100);
+    plan.max_seg = std::min(std::min(plan.ntiles, cap), cvr::kMaxBandTiles);
     if (plan.max_seg < seg_avg) plan.max_seg = seg_avg;   // (too large to order; see can_order)
     const int per_band = plan.max_seg + 3 * (int)(((long long)plan.max_seg * plan.quad_pct) / 100);
     plan.order_slots = 8 * per_band;

@@ -288,6 +288,7 @@ struct Ctx {
   int max_waves_cu = 0;            // experiment (option "max_waves_cu"): cap residency via LDS
   int epi_stop = 0;                // diagnostics (option "debug_epi_stop")
   int debug_keep = 0;              // diagnostics (option "debug_keep"): render only the longest entries
+  int band_cap_pct = 130;           // option "band_cap": most tiles a work-balanced XCD band may take, % of 1/8
   int boost_pct = 5;               // % of every band's longest entries run at raised priority
   int filter_bits = 0;             // GL_LINEAR weights at this many fraction bits (0 = exact; rc1pass)
   int quad_pct = 0;                // % of every band's longest tiles marched 4 lanes per ray

@@ -620,8 +620,8 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
 //    (row-major wave tiles) is cut into 8 contiguous bands of equal predicted
 //    work — weight = the tile's critical path + kTileWeightBias, prefix-summed
 //    over the whole frame — so every XCD finishes together while keeping a
-//    compact screen region (L2 locality).  If a band would exceed `max_seg`
-//    tiles the split falls back to equal tile counts.  Each band is ordered by
+//    compact screen region (L2 locality).  A band that would exceed `max_seg`
+//    tiles (option band_cap) has its boundaries moved the least that fits.  Each band is ordered by
 //    descending critical path (bucketed into 256 cost levels: O(n), ties in any
 //    order — the order never changes a pixel), its longest `nquad` tiles are
 //    expanded into four quad quarters, and the entries are dealt to physical
@@ -730,6 +730,16 @@ tile_epilogue_kernel(uint32_t* __restrict__ tile_cost, unsigned long long* __res
     if (bounds[k] < 0) balanced = false;
   }
   if (balanced) {
+    // Held to the cap (max_seg >= ceil(ntiles / 8), so this is always feasible):
+    // each boundary moves the least that leaves its band <= max_seg tiles and
+    // the bands after it room for the rest.
+    if (tid == 0) {
+      for (int k = 1; k < 8; k++) {
+        const int lo = max(bounds[k - 1], ntiles - (8 - k) * max_seg);
+        bounds[k] = min(max(bounds[k], lo), bounds[k - 1] + max_seg);
+      }
+    }
+    __syncthreads();
     for (int k = 0; k < 8; k++)
       if (bounds[k + 1] < bounds[k] || bounds[k + 1] - bounds[k] > max_seg) balanced = false;
   }

@@ -265,6 +265,9 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                order is relearned (default 5; 0 = always use it)
  *   "boost"      percent of each band's longest entries launched at raised wave
  *                priority (with tile_order 1; default 5)
+ *   "band_cap"   most tiles a work-balanced XCD band may take, in percent of an
+ *                even eighth (100..200, default 130); the launch has 8 x that many
+ *                slots, the ones past a band's tiles exit at once
  *   "quad"       percent of each band's longest tiles marched sample-parallel, four
  *                lanes per ray (with tile_order 1; default 0)
  *   "order_interval" rebuild the LPT order every n-th frame (default 8; costs

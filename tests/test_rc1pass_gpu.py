@@ -251,6 +251,10 @@ SCHEDULES = [
     dict(tile_order=1, batch=2, order_interval=1, boost=0),
     # screen order interleaved over the XCDs (the fallback of a stale order)
     dict(tile_order=2, batch=4),
+    # XCD bands capped near the even share (fewer empty slots; past the cap the
+    # bands fall back to even tile counts)
+    dict(tile_order=1, batch=4, band_cap=100),
+    dict(tile_order=1, batch=4, band_cap=125, quad=10),
 ]
 
 
@@ -273,7 +277,7 @@ def test_schedules_bitexact(oracle, bonsai_tf, name, sched):
     d = Device(0)
     try:
         for k in ("tile_order", "quad", "boost", "batch", "macro", "skip_min_pct", "async_order",
-                  "order_interval", "cell_skip"):
+                  "order_interval", "cell_skip", "band_cap"):
             if k in opts:
                 N.check(N.lib().cvr_set_option(d.handle, k.encode(), opts[k]), k)
         for frame in range(5):
