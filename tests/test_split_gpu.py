@@ -139,7 +139,7 @@ CAMS = [dict(INITIAL), dict(INITIAL, eye=(-300.0, 120.0, 380.0)),
         dict(INITIAL, eye=(0.0, -400.0, 200.0))]
 
 
-def _rccl_worker(rank, world, port, q):
+def _rccl_worker(rank, world, port, q, root_renders=True):
     import torch
     import torch.distributed as dist
     from cpp_volume_rendering_amd.renderer import (DataManager, RayCasting1Pass,
@@ -158,7 +158,8 @@ def _rccl_worker(rank, world, port, q):
         assert r.Init(W, H)
         r.PrepareRender(Camera(**INITIAL))
         try:
-            sp = T.ScreenTileSplit(r, tile=32, fmt=N.FORMAT_RGBA16F, transport="rccl")
+            sp = T.ScreenTileSplit(r, tile=32, fmt=N.FORMAT_RGBA16F, transport="rccl",
+                                   root_renders=root_renders)
         except N.CvrError as e:
             if rank == 0:
                 q.put(("skip", str(e)))
@@ -182,14 +183,20 @@ def _rccl_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_rccl_gather_two_ranks_one_gpu():
+@pytest.mark.parametrize("world,root_renders", [(2, True), (3, False)])
+def test_rccl_gather_ranks_one_gpu(world, root_renders):
+    """world ranks on one GPU through the native RCCL gather; (3, False) is the idle
+    root of bench.py --gpus 8 (rank 0 gathers only, ranks 1..2 render the split
+    over 2): rank 0's image equals its own full render bit for bit.  Skipped where
+    RCCL refuses several ranks on one device."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    procs = [ctx.Process(target=_rccl_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rccl_worker, args=(r, world, port, q, root_renders))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -200,10 +207,10 @@ def test_rccl_gather_two_ranks_one_gpu():
         p.join(5)
     status, detail = q.get(timeout=10) if not q.empty() or not alive else ("hung", "")
     if status == "skip":
-        pytest.skip(f"RCCL refused two ranks on one GPU: {detail}")
+        pytest.skip(f"RCCL refused {world} ranks on one GPU: {detail}")
     assert not alive, "RCCL gather workers hung"
     assert status == "ok"
-    assert [p.exitcode for p in procs] == [0, 0]
+    assert [p.exitcode for p in procs] == [0] * world
 
 
 @pytest.mark.parametrize("nstreams", [4, 16])
