@@ -99,7 +99,8 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
                                           const uint4* __restrict__ grad,
                                           const float4* __restrict__ tfp, int px, int py,
                                           float4& dst, uint32_t& cnt, uint32_t& nshade,
-                                          uint32_t& nbatch, uint32_t& nskip) {
+                                          uint32_t& nbatch, uint32_t& nskip, uint32_t& npm,
+                                          uint32_t& npc) {
   dst = make_float4(0.f, 0.f, 0.f, 0.f);
   cnt = 0;
   Ray r;
@@ -243,6 +244,20 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       }
     }
     bool visible = false;
+#ifdef CVR_PROBE_SHADE_PASSES   // cost probe (tools/phong_pass_probe.py): shading passes per batch
+    bool shj[K];
+    if (PHONG) {
+      int nv = 0;
+#pragma unroll
+      for (int j = 0; j < K; j++) {
+        shj[j] = false;
+        nv += (!done && vj[j] && !(CS > 0 && we[j]) && src[j].w > 0.0f) ? 1 : 0;
+      }
+      // one pass per sample the busiest lane must shade (ballots: active lanes only)
+#pragma unroll
+      for (int q = 1; q <= K; q++) npm += __ballot(nv >= q) != 0 ? 1u : 0u;
+    }
+#endif
     // stage 3: front-to-back composite + ERT, in sample order.  The branches
     // matter: a wave whose samples are all transparent (empty space) skips
     // the exp and the composite together (a branch-free select form measured
@@ -266,6 +281,9 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
             if (PHONG) {
               shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
               nshade++;
+#ifdef CVR_PROBE_SHADE_PASSES
+              shj[j] = true;
+#endif
             }
             const float x = -(sc.w * hj[j]);
             const float a = 1.0f - (XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
@@ -279,6 +297,12 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
         }
       }
     }
+#ifdef CVR_PROBE_SHADE_PASSES
+    if (PHONG) {
+#pragma unroll
+      for (int j = 0; j < K; j++) npc += __ballot(shj[j]) != 0 ? 1u : 0u;   // passes run today
+    }
+#endif
     s = ss;
     if (!(s < D)) done = true;
     probe = !visible;
@@ -524,7 +548,7 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
   float4 dst;
   // nskip: samples stepped over without a load (measurement); the EA march has
   // no shaded-sample count, so it shares that register
-  uint32_t cnt, nshade = 0, nbatch = 0, nskip_own = 0;
+  uint32_t cnt, nshade = 0, nbatch = 0, nskip_own = 0, npm = 0, npc = 0;
   uint32_t& nskip = PHONG ? nskip_own : nshade;
   bool writer;
   if (!QUAD || quarter < 0) {   // whole tile, one lane per ray
@@ -533,7 +557,7 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
     dst = make_float4(0.f, 0.f, 0.f, 0.f);
     cnt = 0;
     if (inside) march_ray<K, PHONG, SKIP, XF, BUF, FB, CS>(A, cells, grad, tfp, px, py, dst, cnt, nshade,
-                                                          nbatch, nskip);
+                                                          nbatch, nskip, npm, npc);
     writer = inside || A.packed;
     if (CS > 0) {
       // the output index again, from the lane id (v_mbcnt) and the wave's tile
@@ -561,6 +585,16 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
       const unsigned long long v = wave_sum(nshade);
       if (lane == 0 && v) atomicAdd(&A.shade_ctr[0], v);
     }
+#ifdef CVR_PROBE_SHADE_PASSES
+    if (PHONG) {   // [1] passes if each lane shaded its visible samples in turn, [2] passes today
+      // every active lane adds each batch's wave-wide count: the longest-lived lane has it all
+      const uint32_t pm = wave_max(npm), pc = wave_max(npc);
+      if (lane == 0) {
+        atomicAdd(&A.shade_ctr[1], (unsigned long long)pm);
+        atomicAdd(&A.shade_ctr[2], (unsigned long long)pc);
+      }
+    }
+#else
     if (CS >= 2) {
       const unsigned long long v = wave_sum(nskip);
       if (lane == 0 && v) atomicAdd(&A.shade_ctr[1], v);
@@ -569,6 +603,7 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
       const uint32_t r = wave_max(nbatch);
       if (lane == 0 && r) atomicAdd(&A.shade_ctr[2], (unsigned long long)r);
     }
+#endif
   }
   if (tile_samples) {   // per-tile sample count; summed by tile_order_kernel (no hot atomic)
     unsigned long long v = wave_sum(cnt);
