@@ -41,7 +41,7 @@ def split_shift(nranks: int) -> int:
 def split_tile(rank: int, nranks: int, k: int, ntx: int) -> tuple[int, int]:
     """(tx, ty) of rank's k-th tile: virtual row-major tile v = rank + k*nranks, whose
     row ty is rotated by split_shift*ty tiles (mirror of cvr::split_tile, cvr_internal.h;
-    tools/split_balance.py measures the balance)."""
+    tests/models/split_balance.py measures the balance)."""
     v = rank + k * nranks
     ty = v // ntx
     tx = (v - ty * ntx - split_shift(nranks) * ty) % ntx

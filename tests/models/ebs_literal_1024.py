@@ -16,7 +16,7 @@ them counted:
 Three cases: SAT ambient occlusion only, SAT box-chain shadow only, both (the bench's
 workload).  Writes profiles/r05/ebs_literal_1024.json.
 
-  python tools/ebs_literal_1024.py [--rows 0:32,496:528] [--threads 8]
+  python tests/models/ebs_literal_1024.py [--rows 0:32,496:528] [--threads 8]
 """
 import argparse
 import json
@@ -26,7 +26,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import oracle as O  # noqa: E402

@@ -10,7 +10,7 @@ line (8 x 1 x 1 = today's x-fastest cell8 grid).  Ray lengths come from the
 oracle's per-pixel sample counts (ERT included).  Positions are float32 numpy,
 approximate to ~1e-4 texels: a statistic, not a parity claim.
 
-  python tools/line_sim.py [--res 1024] [--size 512] [--camera N]
+  python tests/models/line_sim.py [--res 1024] [--size 512] [--camera N]
 """
 from __future__ import annotations
 
@@ -21,7 +21,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

@@ -14,7 +14,7 @@ slots (the GPU's 8192 at 8 waves/SIMD) in several orders:
                step, alpha-only composite to ERT), i.e. a probe kernel's estimate
 Reports the makespan of each (in "samples" of critical path) relative to lpt.
 
-  python tools/order_predict_sim.py [--res 1024] [--size 512] [--cams 0,4,11,14]
+  python tests/models/order_predict_sim.py [--res 1024] [--size 512] [--cams 0,4,11,14]
 """
 import argparse
 import json
@@ -23,7 +23,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

@@ -4,14 +4,14 @@
 data/#list_camera_states): samples per rank, max/mean over ranks, for the tile -> rank
 assignments 'mod' (tile t -> t mod N, row-major) and 'rot s' (row ty rotated by s*ty
 tiles before t mod N; with N | tiles-per-row that is rank (tx + s*ty) mod N).  CPU only.
-Usage: python tools/split_balance.py [--tile 32,16] [--ranks 2,4,8] [--views 0,3,7]"""
+Usage: python tests/models/split_balance.py [--tile 32,16] [--ranks 2,4,8] [--views 0,3,7]"""
 import argparse
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from cpp_volume_rendering_amd import datasets as D  # noqa: E402
 from cpp_volume_rendering_amd.renderer import read_camera_state  # noqa: E402
