@@ -970,7 +970,8 @@ static cvr_status render_rc1pass_frames(Ctx* c, const cvr_frame* frames, int nf,
     const int cap = (int)(((long long)seg_avg * c->band_cap_pct + 99) / 100);
     plan.max_seg = std::min(std::min(plan.ntiles, cap), cvr::kMaxBandTiles);
     if (plan.max_seg < seg_avg) plan.max_seg = seg_avg;   // (too large to order; see can_order)
-    const int per_band = plan.max_seg + 3 * (int)(((long long)plan.max_seg * plan.quad_pct) / 100);
+    int per_band = plan.max_seg + 3 * (int)(((long long)plan.max_seg * plan.quad_pct) / 100);
+    per_band = (per_band + 3) & ~3;   // whole groups of 4 waves per workgroup (raymarch.hip)
     plan.order_slots = 8 * per_band;
     plan.boost = (int)(((long long)seg_avg * c->boost_pct) / 100);
     plan.keep = c->debug_keep;

@@ -486,8 +486,19 @@ constexpr int rc1_waves_per_eu() {
   return (K == 4 && !PHONG && !SKIP && !QUAD) ? 8 : 1;
 #endif
 }
+// Waves (8x8 tiles) per workgroup: they share one TF copy in LDS and one
+// dispatch.  Slot b of the launch (launch order, bands, frames: as with one wave
+// per workgroup) is wave w of workgroup B = 8 q + x with b = 8 (W q + w) + x, so
+// it still runs on XCD b % 8.  (The quad march keeps one wave per workgroup.)
+#ifndef CVR_RC1_WPG
+#define CVR_RC1_WPG 1
+#endif
+template <bool QUAD>
+constexpr int rc1_waves_per_group() { return QUAD ? 1 : CVR_RC1_WPG; }
+
 template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB, int CS>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rc1_waves_per_eu<K, PHONG, SKIP, QUAD>())))
+__global__ void __launch_bounds__(64 * rc1_waves_per_group<QUAD>())
+__attribute__((amdgpu_waves_per_eu(rc1_waves_per_eu<K, PHONG, SKIP, QUAD>())))
 rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
                     const uint4* __restrict__ grad, const float4* __restrict__ tf_g,
                     float4* __restrict__ out0, uint32_t* __restrict__ samples0,
@@ -501,7 +512,10 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
   Rc1passArgs A = A0;
   float4* __restrict__ out = out0;
   uint32_t* __restrict__ samples = samples0;
-  int b = blockIdx.x, f = 0;
+  constexpr int WG = rc1_waves_per_group<QUAD>();
+  int b = WG > 1 ? (((WG * ((int)blockIdx.x >> 3) + (int)(threadIdx.x >> 6)) << 3) | ((int)blockIdx.x & 7))
+                 : (int)blockIdx.x;
+  int f = 0;
   const int nt = A.ntiles;
   if (LF.n > 1) {
     if (LF.interleave) {          // b = 8 (n e + f) + x -> frame f, block 8 e + x
@@ -527,20 +541,25 @@ rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
     samples = LF.samples[f];
     if (f != 0) tile_cost = nullptr;
   }
-  int t, quarter = -1;
+  int t = 0, quarter = -1;
+  bool pad = false;   // a slot past a band's entries (or past the tiles): the wave exits
   if (order) {
     const int e = order[b];
-    if (e < 0) return;                      // padding slot of a shorter band (whole workgroup)
+    pad = e < 0;
     t = e & (kQuadFlag - 1);
     if (QUAD) quarter = (e >> 28) - 1;
-    if ((b >> 3) < boost) __builtin_amdgcn_s_setprio(2);
+    if (!pad && (b >> 3) < boost) __builtin_amdgcn_s_setprio(2);
+  } else if (b >= nt) {
+    pad = true;
   } else if ((nt & 7) == 0 && !A.interleave) {
     t = (b & 7) * (nt >> 3) + (b >> 3);
   } else {
     t = b;
   }
-  load_tf_lds(tfp, tf_g, A.tf_n);
-  const int lane = threadIdx.x;
+  if (WG == 1 && pad) return;               // (whole workgroup)
+  load_tf_lds(tfp, tf_g, A.tf_n);           // every wave of the workgroup takes part (barrier)
+  if (pad) return;
+  const int lane = (int)(threadIdx.x & 63);
   unsigned long long t_start = 0;
   if (A.tile_stats || A.cost_time) t_start = __builtin_amdgcn_s_memrealtime();
   int px, py;
@@ -869,7 +888,12 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
   if (c.max_waves_cu > 0) lds = std::max(lds, (size_t)(160 * 1024 / c.max_waves_cu) & ~(size_t)255);
   // cell (1,1,1) <-> texel (0,0,0)
   const uint4* cells = (const uint4*)c.d_cells;   // sample_pos indexes from the first cell
+  constexpr int WG = rc1_waves_per_group<QUAD>();
+  // slots: a multiple of 8 x WG (the order's bands hold a multiple of 4 slots,
+  // cvr_api.cpp; the slots past the tiles exit at once)
   int grid = order ? plan.order_slots : plan.ntiles;
+  grid = (grid + 8 * WG - 1) / (8 * WG) * (8 * WG);
+  if (order && grid != plan.order_slots) return hipErrorInvalidValue;
   LaunchFrames lf;
   lf.n = 1;
   lf.interleave = 0;
@@ -879,7 +903,7 @@ static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out
     lf.interleave = (order && (grid & 7) == 0 && c.launch_interleave) ? 1 : 0;
     grid *= lf.n;
   }
-  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF, FB, CS>), dim3(grid), dim3(64), lds, s,
+  hipLaunchKernelGGL((rc1pass_tile_kernel<K, PHONG, SKIP, QUAD, XF, BUF, FB, CS>), dim3(grid / WG), dim3(64 * WG), lds, s,
                      a, cells, (const uint4*)c.d_grad, (const float4*)c.d_tf, out, samples,
                      tile_samples, order, tile_cost, order ? plan.boost : 0, lf);
   return hipGetLastError();

@@ -10,9 +10,9 @@ export TMPDIR=/tmp
 GRPS="FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum;SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_INST_ANY;TD_TD_BUSY TD_TC_STALL TA_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES;TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE"
 for w in "$@"; do
   case $w in
-    rc1pass) ARGS="--streams 1 --no-cadence"; K=rc1pass_tile_kernel; export PMC_GRID=5453824 PMC_STEPS=8; OUT=pmc_rc1pass.json;;   # 4 frames per launch x 21304 ordered slots (band_cap 130) x 64
-    phong)   ARGS="--streams 1 --phong --no-cadence"; K=rc1pass_tile_kernel; export PMC_GRID=5453824 PMC_STEPS=8; OUT=pmc_rc1pass_phong.json;;
-    longray) ARGS="--streams 1 --tf-alpha 0.02 --no-cadence"; K=rc1pass_tile_kernel; export PMC_GRID=5453824 PMC_STEPS=8; OUT=pmc_rc1pass_longray.json;;
+    rc1pass) ARGS="--streams 1 --no-cadence"; K=rc1pass_tile_kernel; export PMC_GRID=5455872 PMC_STEPS=8; OUT=pmc_rc1pass.json;;   # 4 frames per launch x 21312 ordered slots (band_cap 130, bands of whole 4-slot groups) x 64
+    phong)   ARGS="--streams 1 --phong --no-cadence"; K=rc1pass_tile_kernel; export PMC_GRID=5455872 PMC_STEPS=8; OUT=pmc_rc1pass_phong.json;;
+    longray) ARGS="--streams 1 --tf-alpha 0.02 --no-cadence"; K=rc1pass_tile_kernel; export PMC_GRID=5455872 PMC_STEPS=8; OUT=pmc_rc1pass_longray.json;;
     dos)     ARGS="--renderer dos --streams 1"; K=flat_shade_kernel; unset PMC_GRID; export PMC_STEPS=3; OUT=pmc_dos.json;;
     ebs)     ARGS="--renderer ebs --streams 1"; K=flat_shade_kernel; unset PMC_GRID; export PMC_STEPS=3; OUT=pmc_ebs.json;;
   esac
