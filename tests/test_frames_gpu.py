@@ -156,7 +156,8 @@ def test_frames_screen_tile_share(dev, bonsai_tf, nranks, tile):
 
 @pytest.mark.parametrize("opt,val", [("tile_order", 0), ("tile_order", 2), ("cell_skip", 0),
                                      ("cell_skip", 2), ("quad", 10), ("filter_bits", 8),
-                                     ("batch", 2), ("launch_interleave", 0)])
+                                     ("batch", 2), ("launch_interleave", 0), ("band_cap", 100),
+                                     ("band_cap", 200)])
 def test_frames_options(bonsai_tf, opt, val):
     d = Device(0)
     try:
