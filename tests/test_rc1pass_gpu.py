@@ -439,3 +439,44 @@ def test_kernel_timing_ring(dev, bonsai_tf):
     finally:
         N.check(L.cvr_set_option(dev.handle, b"kernel_timing", 0), "kernel_timing")
     assert L.cvr_read_kernel_times(dev.handle, ms, 8, ctypes.byref(n)) == N.CVR_ERR_STATE
+
+
+@pytest.mark.parametrize("cap", [100, 130, 200])
+def test_band_cap_holds(bonsai_tf, cap):
+    """Under the learned launch order every XCD band holds at most band_cap % of an
+    even eighth of the tiles (tile_epilogue_kernel moves a balanced boundary the
+    least that fits), and every tile runs in exactly one slot: the slots the
+    tiles report (tile_stats: block index b -> band b % 8, entry b / 8) are
+    distinct and within the band's entries.  The image stays that of the first
+    (unordered) frame."""
+    W = H = 256
+    ntiles = (W // 8) * (H // 8)
+    seg_avg = (ntiles + 7) // 8
+    cap_tiles = (seg_avg * cap + 99) // 100
+    d = Device(0)
+    try:
+        for k, v in (("tile_order", 1), ("band_cap", cap), ("tile_stats", 1), ("order_interval", 1)):
+            N.check(N.lib().cvr_set_option(d.handle, k.encode(), v), k, d.handle)
+        vol = D.marschner_lobb_u8(128)
+        first = None
+        for frame in range(4):
+            rgba, cnt, _ = gpu_render(d, vol, D.voxel_scale(128), bonsai_tf, INITIAL, W, H,
+                                      set_data=(frame == 0))
+            if first is None:
+                first = (rgba, cnt)
+        assert_bitexact(rgba, first[0], f"cap {cap} ordered rgba")
+        assert_bitexact(cnt, first[1], f"cap {cap} ordered counts")
+        st = np.zeros(ntiles * 4, np.uint64)
+        nt = ctypes.c_int()
+        N.check(N.lib().cvr_copy_tile_stats(d.handle, st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                            ntiles, ctypes.byref(nt)), "stats", d.handle)
+        slots = (st.reshape(-1, 4)[:, 3] >> np.uint64(32)).astype(np.int64)
+        assert len(np.unique(slots)) == ntiles
+        assert not np.array_equal(slots, np.arange(ntiles)), "the learned order was not in use"
+        band, entry = slots & 7, slots >> 3
+        per_band = np.bincount(band, minlength=8)
+        assert per_band.sum() == ntiles and per_band.max() <= cap_tiles, per_band
+        for x in range(8):   # a band's entries are 0 .. n-1, each once
+            assert np.array_equal(np.sort(entry[band == x]), np.arange(per_band[x]))
+    finally:
+        d.close()
