@@ -36,7 +36,8 @@ EXPORTED_SYMBOLS = (
     "cvr_set_extinction_volume", "cvr_copy_extinction_level", "cvr_render_dosct",
     "cvr_tf1d_ext_lut", "cvr_set_extinction_sat", "cvr_copy_extinction_sat", "cvr_sat_layout_check", "cvr_render_extbsd",
     "cvr_comm_unique_id", "cvr_comm_init", "cvr_comm_destroy", "cvr_gather_tiles",
-    "cvr_gather_tiles_n", "cvr_unpack_tiles_device_n",
+    "cvr_gather_tiles_n", "cvr_unpack_tiles_device_n", "cvr_tile_code_bound", "cvr_encode_tiles",
+    "cvr_decode_tiles",
     "cvr_gather_sync", "cvr_multiscale_resolution", "cvr_multiscale_filter",
     "cvr_screenshot_rgb8", "cvr_iso_params_default", "cvr_render_iso", "cvr_iso_block_ranges",
 )
@@ -185,6 +186,9 @@ def lib() -> ctypes.CDLL:
         "cvr_gather_tiles": ([P, ctypes.POINTER(Frame), P, I, I, P, P], I),
         "cvr_gather_sync": ([P], I),
         "cvr_unpack_tiles_device_n": ([P, ctypes.POINTER(Frame), P, I, I, I, I, P], I),
+        "cvr_tile_code_bound": ([I, I], ctypes.c_size_t),
+        "cvr_encode_tiles": ([P, P, I, I, P, P], I),
+        "cvr_decode_tiles": ([P, P, I, I, P], I),
         "cvr_gather_tiles_n": ([P, ctypes.POINTER(Frame), I, P, I, I, P,
                                 ctypes.POINTER(ctypes.c_void_p)], I),
         "cvr_multiscale_resolution": ([I, I, I, IP, IP], I),

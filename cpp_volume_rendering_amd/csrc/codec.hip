@@ -1,0 +1,211 @@
+// Lossless per-tile code of RGBA16F screen tiles: the bytes of the
+// multi-GPU exchange.  At every world size the frame is bound by rank 0's xGMI
+// inbound, 8 B per pixel; rendered tiles are smooth, so each tile's channels
+// are stored as differences from the tile's minimum bit pattern at the bit
+// width of the largest difference.
+//
+// Stream (32-bit words): [0, ntiles] the word where tile t's code starts (entry
+// ntiles: the stream's end), then per tile 3 header words -- the four channel
+// bases (16 bits each, R | G << 16, B | A << 16) and the four widths (5 bits
+// each) -- and per channel with width w > 0 the npx differences packed
+// little-endian at w bits each (8 w words for a 16 x 16 tile).  Any bit
+// pattern round-trips (the differences are of unsigned 16-bit patterns, so
+// signs, NaNs and infinities are just patterns).
+//
+// Three launches: per-tile sizes, one workgroup's scan into the start table,
+// and the packing; the decode is one launch.  A wave per tile throughout (64
+// lanes over the tile's pixels; the packing reads its pixels from LDS).
+#include "cvr_internal.h"
+
+namespace cvr {
+
+namespace {
+
+constexpr int kCodecHeaderWords = 3;
+constexpr int kScanThreads = 1024;
+
+__device__ __forceinline__ uint32_t chan(uint2 v, int c) {
+  const uint32_t w = (c < 2) ? v.x : v.y;
+  return (c & 1) ? (w >> 16) : (w & 0xffffu);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+  return v;
+}
+
+// The tile's per-channel bases and widths (every lane gets them).
+__device__ __forceinline__ void tile_stats(const uint2* __restrict__ px, int npx, uint32_t (&base)[4],
+                                           uint32_t (&width)[4]) {
+  const int lane = (int)threadIdx.x;
+  uint32_t mn[4] = {0xffffu, 0xffffu, 0xffffu, 0xffffu}, mx[4] = {0u, 0u, 0u, 0u};
+  for (int p = lane; p < npx; p += 64) {
+    const uint2 v = px[p];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t x = chan(v, c);
+      mn[c] = min(mn[c], x);
+      mx[c] = max(mx[c], x);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    base[c] = wave_min_u32(mn[c]);
+    const uint32_t span = wave_max_u32(mx[c]) - base[c];
+    width[c] = span ? 32u - (uint32_t)__builtin_clz(span) : 0u;
+  }
+}
+
+__device__ __forceinline__ uint32_t code_words(int npx, const uint32_t (&width)[4]) {
+  uint32_t n = kCodecHeaderWords;
+#pragma unroll
+  for (int c = 0; c < 4; c++) n += ((uint32_t)npx * width[c] + 31u) >> 5;
+  return n;
+}
+
+__global__ void __launch_bounds__(64) tile_code_size_kernel(const uint2* __restrict__ tiles, int npx,
+                                                            int ntiles, uint32_t* __restrict__ stream) {
+  const int t = blockIdx.x;
+  if (t >= ntiles) return;
+  uint32_t base[4], width[4];
+  tile_stats(tiles + (size_t)t * npx, npx, base, width);
+  if (threadIdx.x == 0) stream[t] = code_words(npx, width);
+}
+
+// In place: stream[0..ntiles) holds the tiles' word counts; afterwards stream[t] =
+// (ntiles + 1) + the exclusive sum, stream[ntiles] = the total, *bytes = 4 x total.
+__global__ void __launch_bounds__(kScanThreads) tile_code_scan_kernel(uint32_t* __restrict__ stream, int ntiles,
+                                                                      unsigned long long* __restrict__ bytes) {
+  __shared__ uint32_t part[kScanThreads];
+  const int tid = (int)threadIdx.x;
+  const int per = (ntiles + kScanThreads - 1) / kScanThreads;
+  const int b0 = min(tid * per, ntiles), b1 = min(b0 + per, ntiles);
+  uint32_t s = 0;
+  for (int i = b0; i < b1; i++) s += stream[i];
+  part[tid] = s;
+  __syncthreads();
+  for (int off = 1; off < kScanThreads; off <<= 1) {   // inclusive scan of the partial sums
+    const uint32_t v = tid >= off ? part[tid - off] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = (uint32_t)(ntiles + 1) + (tid ? part[tid - 1] : 0u);
+  for (int i = b0; i < b1; i++) {
+    const uint32_t n = stream[i];
+    stream[i] = run;
+    run += n;
+  }
+  if (tid == kScanThreads - 1) {
+    const uint32_t end = (uint32_t)(ntiles + 1) + part[kScanThreads - 1];
+    stream[ntiles] = end;
+    *bytes = 4ull * end;
+  }
+}
+
+__global__ void __launch_bounds__(64) tile_encode_kernel(const uint2* __restrict__ tiles, int npx, int ntiles,
+                                                         uint32_t* __restrict__ stream) {
+  extern __shared__ uint2 pxl[];
+  const int t = blockIdx.x;
+  if (t >= ntiles) return;
+  const int lane = (int)threadIdx.x;
+  const uint2* src = tiles + (size_t)t * npx;
+  for (int p = lane; p < npx; p += 64) pxl[p] = src[p];
+  __syncthreads();
+  uint32_t base[4], width[4];
+  tile_stats(pxl, npx, base, width);
+  uint32_t* out = stream + stream[t];
+  if (lane == 0) {
+    out[0] = base[0] | (base[1] << 16);
+    out[1] = base[2] | (base[3] << 16);
+    out[2] = width[0] | (width[1] << 5) | (width[2] << 10) | (width[3] << 15);
+  }
+  uint32_t pos = kCodecHeaderWords;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint32_t w = width[c];
+    const uint32_t nw = ((uint32_t)npx * w + 31u) >> 5;
+    for (uint32_t j = (uint32_t)lane; j < nw; j += 64) {
+      const uint32_t bit0 = j << 5;
+      const uint32_t p0 = bit0 / w, p1 = min((bit0 + 31u) / w, (uint32_t)npx - 1u);
+      uint32_t acc = 0;
+      for (uint32_t p = p0; p <= p1; p++) {
+        const uint32_t d = chan(pxl[p], c) - base[c];
+        const int sh = (int)(p * w) - (int)bit0;   // < 32: p <= (bit0 + 31) / w
+        acc |= sh >= 0 ? (d << sh) : (d >> -sh);
+      }
+      out[pos + j] = acc;
+    }
+    pos += nw;
+  }
+}
+
+__global__ void __launch_bounds__(64) tile_decode_kernel(const uint32_t* __restrict__ stream, int npx, int ntiles,
+                                                         uint2* __restrict__ tiles) {
+  const int t = blockIdx.x;
+  if (t >= ntiles) return;
+  const uint32_t* in = stream + stream[t];
+  const uint32_t h0 = in[0], h1 = in[1], h2 = in[2];
+  const uint32_t base[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
+  const uint32_t width[4] = {h2 & 31u, (h2 >> 5) & 31u, (h2 >> 10) & 31u, (h2 >> 15) & 31u};
+  uint32_t start[4];
+  uint32_t pos = kCodecHeaderWords;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    start[c] = pos;
+    pos += ((uint32_t)npx * width[c] + 31u) >> 5;
+  }
+  uint2* dst = tiles + (size_t)t * npx;
+  for (int p = (int)threadIdx.x; p < npx; p += 64) {
+    uint32_t v[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t w = width[c];
+      uint32_t d = 0;
+      if (w) {
+        const uint32_t bit = (uint32_t)p * w, j = bit >> 5, b = bit & 31u;
+        uint32_t x = in[start[c] + j] >> b;
+        if (b + w > 32u) x |= in[start[c] + j + 1] << (32u - b);
+        d = x & ((1u << w) - 1u);
+      }
+      v[c] = base[c] + d;
+    }
+    dst[p] = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+  }
+}
+
+}  // namespace
+
+size_t tile_code_bound_bytes(int tile, int ntiles) {
+  const size_t npx = (size_t)tile * tile;
+  return 4 * ((size_t)ntiles + 1 + (size_t)ntiles * (kCodecHeaderWords + 4 * ((npx * 16 + 31) / 32)));
+}
+
+hipError_t launch_tile_encode(const void* d_tiles, int tile, int ntiles, void* d_stream,
+                              unsigned long long* d_bytes, hipStream_t s) {
+  const int npx = tile * tile;
+  uint32_t* stream = static_cast<uint32_t*>(d_stream);
+  const uint2* tiles = static_cast<const uint2*>(d_tiles);
+  if (ntiles > 0)
+    hipLaunchKernelGGL(tile_code_size_kernel, dim3(ntiles), dim3(64), 0, s, tiles, npx, ntiles, stream);
+  hipLaunchKernelGGL(tile_code_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, stream, ntiles, d_bytes);
+  if (ntiles > 0)
+    hipLaunchKernelGGL(tile_encode_kernel, dim3(ntiles), dim3(64), (size_t)npx * sizeof(uint2), s, tiles, npx,
+                       ntiles, stream);
+  return hipGetLastError();
+}
+
+hipError_t launch_tile_decode(const void* d_stream, int tile, int ntiles, void* d_tiles, hipStream_t s) {
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tile_decode_kernel, dim3(ntiles), dim3(64), 0, s, static_cast<const uint32_t*>(d_stream),
+                     tile * tile, ntiles, static_cast<uint2*>(d_tiles));
+  return hipGetLastError();
+}
+
+}  // namespace cvr

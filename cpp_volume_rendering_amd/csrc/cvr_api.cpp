@@ -1296,6 +1296,32 @@ cvr_status cvr_unpack_tiles_device(cvr_ctx* ctx, const cvr_frame* f, const void*
   return cvr_unpack_tiles_device_n(ctx, f, d_packed, tpr_max, 1, 0, format, d_rgba);
 }
 
+size_t cvr_tile_code_bound(int tile, int ntiles) {
+  if (tile < 16 || tile % 16 != 0 || tile > 64 || ntiles < 0) return 0;
+  return cvr::tile_code_bound_bytes(tile, ntiles);
+}
+
+cvr_status cvr_encode_tiles(cvr_ctx* ctx, const void* d_tiles, int tile, int ntiles, void* d_stream,
+                            unsigned long long* d_bytes) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if ((!d_tiles && ntiles > 0) || !d_stream || !d_bytes || !cvr_tile_code_bound(tile, ntiles))
+    return fail(c, CVR_ERR_ARG, "cvr_encode_tiles: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, cvr::launch_tile_encode(d_tiles, tile, ntiles, d_stream, d_bytes, c->stream));
+  return CVR_OK;
+}
+
+cvr_status cvr_decode_tiles(cvr_ctx* ctx, const void* d_stream, int tile, int ntiles, void* d_tiles) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return CVR_ERR_ARG;
+  if (!d_stream || (!d_tiles && ntiles > 0) || !cvr_tile_code_bound(tile, ntiles))
+    return fail(c, CVR_ERR_ARG, "cvr_decode_tiles: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, cvr::launch_tile_decode(d_stream, tile, ntiles, d_tiles, c->stream));
+  return CVR_OK;
+}
+
 
 
 // Output handling shared by the shaded renderers (device or host buffers, the

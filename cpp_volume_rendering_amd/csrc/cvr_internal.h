@@ -438,6 +438,11 @@ hipError_t launch_block_minmax(const void* vox, int bpv, const int N[3], const i
 hipError_t launch_iso(const Ctx& c, const IsoArgs& q, int variant, bool phong, const float2* mm,
                       float4* out, uint32_t* samples, unsigned long long* tile_samples,
                       hipStream_t s);
+// codec.hip: the lossless per-tile code of RGBA16F tiles (cvr_encode_tiles)
+size_t tile_code_bound_bytes(int tile, int ntiles);
+hipError_t launch_tile_encode(const void* d_tiles, int tile, int ntiles, void* d_stream,
+                              unsigned long long* d_bytes, hipStream_t s);
+hipError_t launch_tile_decode(const void* d_stream, int tile, int ntiles, void* d_tiles, hipStream_t s);
 hipError_t launch_unpack_tiles(const void* packed, void* out, int half, int W, int H, int tile,
                                int nranks, int tpr_max, hipStream_t s, size_t rank_stride = 0);
 
