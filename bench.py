@@ -222,6 +222,10 @@ def parse(argv=None):
                         "(-1: 0 for rc1pass at >= 4 GPUs, else 1; DESIGN §7a)")
     p.add_argument("--quad", type=int, default=-1,
                    help="quad (4 lanes per ray) share of the longest tiles, %% (default 0)")
+    p.add_argument("--exchange-code", type=int, default=1, choices=[0, 1],
+                   help="N > 1, RGBA16F: 1 = the exchange moves the lossless per-tile code "
+                        "(one encode launch per group on the render ranks, one fused decode "
+                        "on rank 0; DESIGN §7b), 0 = raw tiles (one ncclGather)")
     p.add_argument("--transport", choices=["rccl", "torch"], default="rccl",
                    help="N > 1 gather: the library's RCCL communicator or dist.gather")
     p.add_argument("--shade-flat", type=int, default=-1, choices=[-1, 0, 1],
@@ -691,7 +695,7 @@ def main():
                                      streams=SD["streams"],
                                      frames_per_exchange=SD["frames_per_exchange"],
                                      frames_per_launch=FPL, buffer_sets=SD["buffer_sets"],
-                                     root_renders=root)
+                                     root_renders=root, code=bool(a.exchange_code))
         split = make_split(root_renders)
         if world > 1 and not root_renders:
             # pre-flight: one frame through the idle-root exchange must equal rank 0's
@@ -943,7 +947,8 @@ def main():
             if pmc.get("sq_insts_vmem_rd"):
                 pipes["vmem"] = {"frac": round(pmc["sq_insts_vmem_rd"] * 1024 / t_pmc / 1e9 / VMEM_PEAK_GBS, 4),
                                  "count": "PMC SQ_INSTS_VMEM_RD of flat_shade_kernel"}
-            if pmc.get("td_tc_stall_frac_per_cu") is not None:
+            if ("vmem" in pipes and pmc.get("td_tc_stall_frac_per_cu") is not None
+                    and pmc.get("td_busy_frac_per_cu") is not None):
                 pipes["vmem"]["td_busy_per_cu"] = round(pmc["td_busy_frac_per_cu"], 3)
                 pipes["vmem"]["td_stalled_on_cache_per_cu"] = round(pmc["td_tc_stall_frac_per_cu"], 3)
             roof["shade_kernel_pipes"] = pipes

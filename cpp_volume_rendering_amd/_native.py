@@ -37,7 +37,8 @@ EXPORTED_SYMBOLS = (
     "cvr_tf1d_ext_lut", "cvr_set_extinction_sat", "cvr_copy_extinction_sat", "cvr_sat_layout_check", "cvr_render_extbsd",
     "cvr_comm_unique_id", "cvr_comm_init", "cvr_comm_destroy", "cvr_gather_tiles",
     "cvr_gather_tiles_n", "cvr_unpack_tiles_device_n", "cvr_tile_code_bound", "cvr_encode_tiles",
-    "cvr_decode_tiles",
+    "cvr_decode_tiles", "cvr_comm_init_local", "cvr_create_group", "cvr_group_size",
+    "cvr_group_member",
     "cvr_gather_sync", "cvr_multiscale_resolution", "cvr_multiscale_filter",
     "cvr_screenshot_rgb8", "cvr_iso_params_default", "cvr_render_iso", "cvr_iso_block_ranges",
 )
@@ -183,6 +184,10 @@ def lib() -> ctypes.CDLL:
         "cvr_comm_unique_id": ([ctypes.c_char_p], I),
         "cvr_comm_init": ([P, I, I, ctypes.c_char_p], I),
         "cvr_comm_destroy": ([P], I),
+        "cvr_comm_init_local": ([ctypes.POINTER(P), I], I),
+        "cvr_create_group": ([IP, I, ctypes.POINTER(P)], I),
+        "cvr_group_size": ([P], I),
+        "cvr_group_member": ([P, I], P),
         "cvr_gather_tiles": ([P, ctypes.POINTER(Frame), P, I, I, P, P], I),
         "cvr_gather_sync": ([P], I),
         "cvr_unpack_tiles_device_n": ([P, ctypes.POINTER(Frame), P, I, I, I, I, P], I),

@@ -180,7 +180,170 @@ __global__ void __launch_bounds__(64) tile_decode_kernel(const uint32_t* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// The exchange's form of the code (cvr_comm.cpp): ONE launch per exchange group.
+// Tile t of the group is frame f = t / k, the rank's tile i = t % k, read from slot
+// f * tpr + i of the packed buffer.  Each tile claims its words with one atomic on
+// ctr[0] (so tiles land in claim order, not in t order: the start table makes the
+// order irrelevant to the decode), and the last workgroup to finish (ticket on
+// ctr[1]) writes the stream's end word and its length in bytes, then zeroes the
+// counters for the next launch on the same buffer set.  The stream is written to
+// `dst`, which may be a peer device's memory (the in-process transport pushes it
+// there); the counters stay on the encoding device.
+__global__ void __launch_bounds__(64) exchange_encode_kernel(const uint2* __restrict__ packed, int npx, int k,
+                                                             int tpr, int ntiles, uint32_t* __restrict__ dst,
+                                                             unsigned int* __restrict__ ctr,
+                                                             unsigned long long* __restrict__ d_bytes) {
+  extern __shared__ uint2 pxl[];
+  __shared__ uint32_t s_off;
+  const int lane = (int)threadIdx.x;
+  if (ntiles == 0) {   // a rank without tiles: the empty stream
+    if (lane == 0) {
+      dst[0] = 1u;
+      if (d_bytes) *d_bytes = 4ull;
+    }
+    return;
+  }
+  const int t = blockIdx.x;
+  const int f = t / k, i = t - f * k;
+  const uint2* src = packed + ((size_t)f * tpr + i) * npx;
+  for (int p = lane; p < npx; p += 64) pxl[p] = src[p];
+  __syncthreads();
+  uint32_t base[4], width[4];
+  tile_stats(pxl, npx, base, width);
+  if (lane == 0) s_off = atomicAdd(&ctr[0], code_words(npx, width));
+  __syncthreads();
+  const uint32_t start = (uint32_t)ntiles + 1u + s_off;
+  uint32_t* out = dst + start;
+  if (lane == 0) {
+    dst[t] = start;
+    out[0] = base[0] | (base[1] << 16);
+    out[1] = base[2] | (base[3] << 16);
+    out[2] = width[0] | (width[1] << 5) | (width[2] << 10) | (width[3] << 15);
+  }
+  uint32_t pos = kCodecHeaderWords;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint32_t w = width[c];
+    const uint32_t nw = ((uint32_t)npx * w + 31u) >> 5;
+    for (uint32_t j = (uint32_t)lane; j < nw; j += 64) {
+      const uint32_t bit0 = j << 5;
+      const uint32_t p0 = bit0 / w, p1 = min((bit0 + 31u) / w, (uint32_t)npx - 1u);
+      uint32_t acc = 0;
+      for (uint32_t p = p0; p <= p1; p++) {
+        const uint32_t d = chan(pxl[p], c) - base[c];
+        const int sh = (int)(p * w) - (int)bit0;
+        acc |= sh >= 0 ? (d << sh) : (d >> -sh);
+      }
+      out[pos + j] = acc;
+    }
+    pos += nw;
+  }
+  // every lane's words are issued before the ticket: the last workgroup's end word
+  // and the stream length then cover all of them (kernel end publishes the rest)
+  __threadfence();
+  __syncthreads();
+  if (lane == 0) {
+    const unsigned int ticket = atomicAdd(&ctr[1], 1u);
+    if (ticket == (unsigned int)ntiles - 1u) {
+      const uint32_t total = atomicAdd(&ctr[0], 0u);
+      const uint32_t end = (uint32_t)ntiles + 1u + total;
+      dst[ntiles] = end;
+      if (d_bytes) *d_bytes = 4ull * end;
+      atomicExch(&ctr[0], 0u);
+      atomicExch(&ctr[1], 0u);
+    }
+  }
+}
+
+// Rank 0's half, fused: decode every source's stream of the group and write its
+// pixels straight into the frames' images (the unpack of unpack_tiles_kernel, the
+// tile's screen position from split_tile).  Workgroup = (source r, frame f, slot i)
+// over nsrc x nframes x tpr slots; slots past the source's tiles exit.  Source r is
+// frame rank r of the split; its stream is at src + r * slot_words, or, for r = 0
+// with raw0 set (a rendering root), its raw packed tiles at raw0 (frame f at
+// f * raw0_fstride tiles).  A tile's code is staged in LDS (one coalesced read of
+// its words) before 64 lanes unpack 4 pixels each.
+__global__ void __launch_bounds__(64) exchange_decode_kernel(ExchangeDecode a) {
+  extern __shared__ uint32_t code[];
+  const int lane = (int)threadIdx.x;
+  const int per_src = a.nframes * a.tpr;
+  const int r = (int)blockIdx.x / per_src;
+  const int rem = (int)blockIdx.x - r * per_src;
+  const int f = rem / a.tpr, i = rem - f * a.tpr;
+  const int nt = a.tile_grid_n;
+  const int k = nt > r ? (nt - r + a.nsplit - 1) / a.nsplit : 0;   // cvr_tiles_for_rank
+  if (i >= k) return;
+  uint2* __restrict__ img = a.img[f];
+  if (!img) return;
+  int tx, ty;
+  split_tile(r, a.nsplit, i, a.ntx, tx, ty);
+  const int npx = a.tile * a.tile;
+  const int x0 = tx * a.tile, y0 = ty * a.tile;
+  if (r == 0 && a.raw0) {
+    const uint2* src = a.raw0 + ((size_t)f * a.raw0_fstride + i) * npx;
+    for (int p = lane; p < npx; p += 64) {
+      const int px = x0 + p % a.tile, py = y0 + p / a.tile;
+      if (px < a.W && py < a.H) img[(size_t)py * a.W + px] = src[p];
+    }
+    return;
+  }
+  const uint32_t* in = a.src + (size_t)r * a.slot_words;
+  const uint32_t* tc = in + in[f * k + i];
+  const uint32_t h0 = tc[0], h1 = tc[1], h2 = tc[2];
+  const uint32_t base[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
+  const uint32_t width[4] = {h2 & 31u, (h2 >> 5) & 31u, (h2 >> 10) & 31u, (h2 >> 15) & 31u};
+  uint32_t start[4];
+  uint32_t nw = kCodecHeaderWords;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    start[c] = nw;
+    nw += ((uint32_t)npx * width[c] + 31u) >> 5;
+  }
+  for (uint32_t j = (uint32_t)lane; j < nw; j += 64) code[j] = tc[j];
+  code[nw] = 0u;   // the word after the last one a straddling read may touch (weight 0)
+  __syncthreads();
+  for (int p = lane; p < npx; p += 64) {
+    uint32_t v[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t w = width[c];
+      uint32_t d = 0;
+      if (w) {
+        const uint32_t bit = (uint32_t)p * w, j = bit >> 5, b = bit & 31u;
+        uint32_t x = code[start[c] + j] >> b;
+        if (b + w > 32u) x |= code[start[c] + j + 1] << (32u - b);
+        d = x & ((1u << w) - 1u);
+      }
+      v[c] = base[c] + d;
+    }
+    const int px = x0 + p % a.tile, py = y0 + p / a.tile;
+    if (px < a.W && py < a.H) img[(size_t)py * a.W + px] = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+  }
+}
+
 }  // namespace
+
+hipError_t launch_exchange_encode(const void* d_packed, int tile, int k, int tpr, int nframes, void* d_dst,
+                                  unsigned int* d_ctr, unsigned long long* d_bytes, hipStream_t s) {
+  const int npx = tile * tile;
+  const long long nt = (long long)k * nframes;
+  if (nt > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(exchange_encode_kernel, dim3(nt > 0 ? (unsigned)nt : 1u), dim3(64),
+                     (size_t)npx * sizeof(uint2), s, static_cast<const uint2*>(d_packed), npx, k > 0 ? k : 1,
+                     tpr, (int)nt, static_cast<uint32_t*>(d_dst), d_ctr, d_bytes);
+  return hipGetLastError();
+}
+
+hipError_t launch_exchange_decode(const ExchangeDecode& a, hipStream_t s) {
+  const long long slots = (long long)a.nsrc * a.nframes * a.tpr;
+  if (slots <= 0) return hipSuccess;
+  if (slots > 0x7fffffffLL) return hipErrorInvalidValue;
+  // a tile's words: 3 + 4 channels x (npx x 16 bits) at most, + the guard word
+  const size_t lds = 4 * ((size_t)kCodecHeaderWords + 4 * ((size_t)a.tile * a.tile / 2) + 1);
+  hipLaunchKernelGGL(exchange_decode_kernel, dim3((unsigned)slots), dim3(64), lds, s, a);
+  return hipGetLastError();
+}
 
 size_t tile_code_bound_bytes(int tile, int ntiles) {
   const size_t npx = (size_t)tile * tile;

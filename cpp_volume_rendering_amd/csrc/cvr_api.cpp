@@ -248,6 +248,7 @@ cvr_status cvr_create(int device, cvr_ctx** out_ctx) {
 void cvr_destroy(cvr_ctx* ctx) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return;
+  cvr::group_release(c);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   cvr::comm_release(c);
@@ -306,6 +307,12 @@ cvr_status cvr_set_stream(cvr_ctx* ctx, void* stream) {
 cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c || !key) return CVR_ERR_ARG;
+  if (c->group) {
+    for (const char* k : {"split_streams", "gather_sets", "gather_root_idle", "exchange_lag"})
+      if (!std::strcmp(key, k))
+        return fail(c, CVR_ERR_ARG, "option '%s' belongs to the group's own exchange", key);
+    return cvr::group_each(c, [&](cvr_ctx* _m) { return cvr_set_option(_m, key, value); });
+  }
   if (!std::strcmp(key, "batch")) {
     if (value != 0 && value != 2 && value != 4)
       return fail(c, CVR_ERR_ARG, "batch must be 0 (auto), 2 or 4");
@@ -451,6 +458,17 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->gather_sets = value;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "exchange_code")) {
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "exchange_code must be 0 or 1");
+    c->exchange_code = value;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "exchange_lag")) {
+    if (value < -1 || value >= CVR_MAX_GATHER_SETS)
+      return fail(c, CVR_ERR_ARG, "exchange_lag must be -1 (auto) .. %d", CVR_MAX_GATHER_SETS - 1);
+    c->exchange_lag = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "split_streams")) {
     if (value < 1 || value > 32) return fail(c, CVR_ERR_ARG, "split_streams must be 1..32");
     c->split_streams = value;
@@ -470,6 +488,11 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
   }
   if (!std::strcmp(key, "debug_epi_stop")) {   // diagnostics: truncated order builds
     c->epi_stop = value;
+    return CVR_OK;
+  }
+  if (!std::strcmp(key, "debug_cell_flags_oom")) {   // tests: the skip flags' scratch "fails"
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "debug_cell_flags_oom must be 0 or 1");
+    c->debug_flags_oom = value;
     return CVR_OK;
   }
   if (!std::strcmp(key, "debug_keep")) {   // diagnostics only: the image is incomplete
@@ -495,6 +518,7 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
 int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
   if (!c || !key) return -1;
+  if (c->group) return cvr_get_option(cvr_group_member(const_cast<cvr_ctx*>(ctx), 0), key);
   if (!std::strcmp(key, "batch")) return c->batch;
   if (!std::strcmp(key, "tile_order")) return c->use_order;
   if (!std::strcmp(key, "stale_deg")) return c->stale_deg;
@@ -504,11 +528,15 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "macro")) return c->macro_shift;
   if (!std::strcmp(key, "max_waves_cu")) return c->max_waves_cu;
   if (!std::strcmp(key, "debug_keep")) return c->debug_keep;
+  if (!std::strcmp(key, "debug_cell_flags_oom")) return c->debug_flags_oom;
+  if (!std::strcmp(key, "cell_flags_active")) return c->cell_flags_valid && !c->cell_flags_oom;   // read-only
   if (!std::strcmp(key, "debug_epi_stop")) return c->epi_stop;
   if (!std::strcmp(key, "async_order")) return c->async_order;
   if (!std::strcmp(key, "split_streams")) return c->split_streams;
   if (!std::strcmp(key, "gather_sets")) return c->gather_sets;
   if (!std::strcmp(key, "gather_root_idle")) return c->gather_root_idle;
+  if (!std::strcmp(key, "exchange_code")) return c->exchange_code;
+  if (!std::strcmp(key, "exchange_lag")) return c->exchange_lag;
   if (!std::strcmp(key, "launch_interleave")) return c->launch_interleave;
   if (!std::strcmp(key, "sat_build_us")) return c->sat_build_us;   // read-only
   if (!std::strcmp(key, "order_interval")) return c->order_interval;
@@ -539,6 +567,10 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
 cvr_status cvr_synchronize(cvr_ctx* ctx) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c) return CVR_ERR_ARG;
+  if (c->group) {
+    cvr_status st = cvr::group_each(c, [&](cvr_ctx* _m) { return cvr_synchronize(_m); });
+    if (st != CVR_OK) return st;
+  }
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (c->side) HIP_TRY(c, hipStreamSynchronize(c->side));
@@ -548,11 +580,18 @@ cvr_status cvr_synchronize(cvr_ctx* ctx) {
 size_t cvr_device_bytes(const cvr_ctx* ctx) {
   const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
   if (!c) return 0;
+  if (c->group) {
+    size_t b = 0;
+    for (int i = 0; i < cvr_group_size(ctx); i++)
+      b += cvr_device_bytes(cvr_group_member(const_cast<cvr_ctx*>(ctx), i));
+    return b;
+  }
   return c->vox_bytes + c->cells_bytes + c->grad_bytes + (size_t)c->tf_n * 16 + c->scratch_bytes;
 }
 
 cvr_status cvr_copy_cells(cvr_ctx* ctx, void* out, size_t capacity) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_copy_cells(_m, out, capacity); });
   if (!c || !out) return CVR_ERR_ARG;
   if (!c->d_cells) return fail(c, CVR_ERR_STATE, "cvr_copy_cells: no volume set");
   if (capacity < c->cells_bytes)
@@ -626,6 +665,7 @@ static cvr_status set_volume_common(Ctx* c, const void* src, bool src_device, in
 cvr_status cvr_set_volume(cvr_ctx* ctx, const void* voxels, int bpv, int w, int h, int d,
                           const float scale[3]) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_each(c, [&](cvr_ctx* _m) { return cvr_set_volume(_m, voxels, bpv, w, h, d, scale); });
   if (!c) return CVR_ERR_ARG;
   return set_volume_common(c, voxels, false, bpv, w, h, d, scale);
 }
@@ -633,12 +673,14 @@ cvr_status cvr_set_volume(cvr_ctx* ctx, const void* voxels, int bpv, int w, int 
 cvr_status cvr_set_volume_device(cvr_ctx* ctx, const void* d_voxels, int bpv, int w, int h,
                                  int d, const float scale[3]) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_each(c, [&](cvr_ctx* _m) { return cvr_set_volume_device(_m, d_voxels, bpv, w, h, d, scale); });
   if (!c) return CVR_ERR_ARG;
   return set_volume_common(c, d_voxels, true, bpv, w, h, d, scale);
 }
 
 cvr_status cvr_set_transfer_function(cvr_ctx* ctx, const float* rgbt, int n) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_each(c, [&](cvr_ctx* _m) { return cvr_set_transfer_function(_m, rgbt, n); });
   if (!c) return CVR_ERR_ARG;
   if (!rgbt || n < 2 || n > 4096)
     return fail(c, CVR_ERR_ARG, "cvr_set_transfer_function: need 2 <= n <= 4096 entries");
@@ -675,6 +717,7 @@ cvr_status cvr_set_transfer_function(cvr_ctx* ctx, const float* rgbt, int n) {
 
 cvr_status cvr_set_gradient(cvr_ctx* ctx, int mode) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_each(c, [&](cvr_ctx* _m) { return cvr_set_gradient(_m, mode); });
   if (!c) return CVR_ERR_ARG;
   if (mode < 0 || mode > 2) return fail(c, CVR_ERR_ARG, "cvr_set_gradient: bad mode %d", mode);
   if (mode != 0 && !c->d_vox) return fail(c, CVR_ERR_STATE, "cvr_set_gradient: no volume");
@@ -774,6 +817,8 @@ static cvr_status ensure_cell_flags(Ctx* c) {
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipDeviceSynchronize());
   const size_t n = cvr::cell_count(c->cells);
+  if (c->debug_flags_oom)   // tests: the scratch allocation fails
+    return fail(c, CVR_ERR_OOM, "cell flags: scratch allocation failed (debug_cell_flags_oom)");
   uint8_t* t = nullptr;
   HIP_TRY(c, hipMalloc((void**)&t, 2 * n));
   hipError_t e = cvr::launch_cell_flags(*c, false, t, t + n, c->stream);
@@ -790,14 +835,17 @@ static cvr_status ensure_cell_flags(Ctx* c) {
 // The per-cell skip is a bit-exact optimisation, so a frame must not fail for
 // want of its 2 bytes of scratch per cell (2.1 GB at 1024^3, next to the EBS
 // SAT): on OOM the frame renders without it (every density read takes |corner|,
-// so stale flags in the sign bits are ignored) and the build is retried on the
-// next frame.  Any other error is returned.
+// so stale flags in the sign bits are ignored) until the next volume or TF
+// change, which clears cell_flags_oom and retries the build.  The frame itself
+// succeeds, so the OOM message is not left in cvr_last_error.  Any other error is
+// returned.
 static cvr_status cell_flags_or_off(Ctx* c) {
   if (c->cell_flags_oom && !c->cell_flags_valid) return CVR_ERR_OOM;
   const cvr_status st = ensure_cell_flags(c);
   if (st == CVR_ERR_OOM) {
     (void)hipGetLastError();   // clear the failed allocation's error
     c->cell_flags_oom = 1;
+    c->err.clear();
   }
   return st;
 }
@@ -963,9 +1011,10 @@ static cvr_status render_rc1pass_frames(Ctx* c, const cvr_frame* frames, int nf,
   plan.quad_pct = c->filter_bits ? 0 : c->quad_pct;   // the quad march has no filter_bits variant
   {
     // Bands are cut by predicted work, so one may hold more than 1/8 of the
-    // tiles: up to band_cap % of the even share (default 2x; the epilogue falls
-    // back to even bands past that); every band gets that many slots (+3 per
-    // quad-split tile), and the slots past a band's entries are empty workgroups.
+    // tiles: up to band_cap % of the even share (default 130;
+    // tile_epilogue_kernel moves the band boundaries the least that fits the
+    // cap); every band gets that many slots (+3 per quad-split tile), and the
+    // slots past a band's entries are empty workgroups.
     const int seg_avg = (plan.ntiles + 7) / 8;
     const int cap = (int)(((long long)seg_avg * c->band_cap_pct + 99) / 100);
     plan.max_seg = std::min(std::min(plan.ntiles, cap), cvr::kMaxBandTiles);
@@ -1165,6 +1214,10 @@ static cvr_status render_rc1pass_frames(Ctx* c, const cvr_frame* frames, int nf,
 cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pass_params* p,
                               const cvr_output* o) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group)
+    return cvr::group_render(c, f, 1, o, [&](cvr_ctx* _m, const cvr_frame* mf, int, const cvr_output* mo) {
+      return cvr_render_rc1pass(_m, mf, p, mo);
+    });
   if (!c) return CVR_ERR_ARG;
   return render_rc1pass_frames(c, f, 1, p, o);
 }
@@ -1172,12 +1225,17 @@ cvr_status cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* f, const cvr_rc1pas
 cvr_status cvr_render_rc1pass_frames(cvr_ctx* ctx, const cvr_frame* frames, int nframes,
                                      const cvr_rc1pass_params* p, const cvr_output* outs) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group)
+    return cvr::group_render(c, frames, nframes, outs, [&](cvr_ctx* _m, const cvr_frame* mf, int nf, const cvr_output* mo) {
+      return cvr_render_rc1pass_frames(_m, mf, nf, p, mo);
+    });
   if (!c) return CVR_ERR_ARG;
   return render_rc1pass_frames(c, frames, nframes, p, outs);
 }
 
 cvr_status cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int* out_tiles) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_copy_tile_stats(_m, out, max_tiles, out_tiles); });
   if (!c || !out_tiles) return CVR_ERR_ARG;
   *out_tiles = c->tile_stats_n;
   if (!out) return CVR_OK;
@@ -1191,6 +1249,7 @@ cvr_status cvr_copy_tile_stats(cvr_ctx* ctx, uint64_t* out, int max_tiles, int* 
 
 cvr_status cvr_selftest_arith(cvr_ctx* ctx, uint64_t out[3]) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_selftest_arith(_m, out); });
   if (!c || !out) return CVR_ERR_ARG;
   HIP_TRY(c, hipSetDevice(c->device));
   unsigned long long* d = nullptr;
@@ -1207,6 +1266,17 @@ cvr_status cvr_selftest_arith(cvr_ctx* ctx, uint64_t out[3]) {
 cvr_status cvr_read_shade_counters(cvr_ctx* ctx, uint64_t out[3]) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c || !out) return CVR_ERR_ARG;
+  if (c->group) {
+    uint64_t sum[3] = {0, 0, 0};
+    cvr_status st = cvr::group_each(c, [&](cvr_ctx* _m) {
+      uint64_t v[3];
+      cvr_status e = cvr_read_shade_counters(_m, v);
+      for (int i = 0; i < 3; i++) sum[i] += v[i];
+      return e;
+    });
+    for (int i = 0; i < 3; i++) out[i] = sum[i];
+    return st;
+  }
   if (!c->d_shade) return fail(c, CVR_ERR_STATE, "shade_counters option was not enabled");
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1216,6 +1286,7 @@ cvr_status cvr_read_shade_counters(cvr_ctx* ctx, uint64_t out[3]) {
 
 cvr_status cvr_read_kernel_times(cvr_ctx* ctx, float* ms, int max_frames, int* out_frames) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_read_kernel_times(_m, ms, max_frames, out_frames); });
   if (!c || !out_frames || max_frames < 0 || (max_frames > 0 && !ms)) return CVR_ERR_ARG;
   const long long nev = (long long)c->ev_start.size();
   if (!nev) return fail(c, CVR_ERR_STATE, "kernel_timing option was not enabled");
@@ -1245,6 +1316,7 @@ cvr_status cvr_multiscale_resolution(int mode, int sw, int sh, int* rw, int* rh)
 cvr_status cvr_multiscale_filter(cvr_ctx* ctx, int mode, int kernel, void* d_frame, int fw, int fh,
                                  void* d_screen, int sw, int sh) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_multiscale_filter(_m, mode, kernel, d_frame, fw, fh, d_screen, sw, sh); });
   if (!c) return CVR_ERR_ARG;
   if (!d_frame || !d_screen || mode < 1 || mode > 3 || kernel < 0 || kernel > 5 || fw < 1 ||
       fh < 1 || sw < 1 || sh < 1 || d_frame == d_screen)
@@ -1262,6 +1334,7 @@ cvr_status cvr_multiscale_filter(cvr_ctx* ctx, int mode, int kernel, void* d_fra
 cvr_status cvr_screenshot_rgb8(cvr_ctx* ctx, const void* d_frame, int format, int w, int h,
                                void* d_rgb) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_screenshot_rgb8(_m, d_frame, format, w, h, d_rgb); });
   if (!c) return CVR_ERR_ARG;
   if (!d_frame || !d_rgb || w < 1 || h < 1 ||
       (format != CVR_FORMAT_RGBA32F && format != CVR_FORMAT_RGBA16F))
@@ -1276,6 +1349,7 @@ cvr_status cvr_unpack_tiles_device_n(cvr_ctx* ctx, const cvr_frame* f, const voi
                                      int tpr_max, int nframes, int frame_index, int format,
                                      void* d_rgba) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_unpack_tiles_device_n(_m, f, d_gathered, tpr_max, nframes, frame_index, format, d_rgba); });
   if (!c) return CVR_ERR_ARG;
   if (!f || !d_gathered || !d_rgba || f->nranks < 1 || f->tile_size < 16 || tpr_max < 0 ||
       nframes < 1 || frame_index < 0 || frame_index >= nframes ||
@@ -1304,6 +1378,7 @@ size_t cvr_tile_code_bound(int tile, int ntiles) {
 cvr_status cvr_encode_tiles(cvr_ctx* ctx, const void* d_tiles, int tile, int ntiles, void* d_stream,
                             unsigned long long* d_bytes) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_encode_tiles(_m, d_tiles, tile, ntiles, d_stream, d_bytes); });
   if (!c) return CVR_ERR_ARG;
   if ((!d_tiles && ntiles > 0) || !d_stream || !d_bytes || !cvr_tile_code_bound(tile, ntiles))
     return fail(c, CVR_ERR_ARG, "cvr_encode_tiles: bad arguments");
@@ -1314,6 +1389,7 @@ cvr_status cvr_encode_tiles(cvr_ctx* ctx, const void* d_tiles, int tile, int nti
 
 cvr_status cvr_decode_tiles(cvr_ctx* ctx, const void* d_stream, int tile, int ntiles, void* d_tiles) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_decode_tiles(_m, d_stream, tile, ntiles, d_tiles); });
   if (!c) return CVR_ERR_ARG;
   if (!d_stream || (!d_tiles && ntiles > 0) || !cvr_tile_code_bound(tile, ntiles))
     return fail(c, CVR_ERR_ARG, "cvr_decode_tiles: bad arguments");
@@ -1405,6 +1481,7 @@ static cvr_status render_shaded(Ctx* c, const cvr_output* o, int ntiles, size_t 
 cvr_status cvr_set_extinction_volume(cvr_ctx* ctx, const float* tf_rgba, int n, const int res_in[3],
                                      float sigma0) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_each(c, [&](cvr_ctx* _m) { return cvr_set_extinction_volume(_m, tf_rgba, n, res_in, sigma0); });
   if (!c) return CVR_ERR_ARG;
   if (!tf_rgba || n < 2 || n > cvr::kMaxTfLds)
     return fail(c, CVR_ERR_ARG, "cvr_set_extinction_volume: need 2 <= n <= 4096 TF entries");
@@ -1482,6 +1559,7 @@ cvr_status cvr_set_extinction_volume(cvr_ctx* ctx, const float* tf_rgba, int n, 
 cvr_status cvr_copy_extinction_level(cvr_ctx* ctx, int level, float* out, int dims[3],
                                      int* n_levels) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_copy_extinction_level(_m, level, out, dims, n_levels); });
   if (!c) return CVR_ERR_ARG;
   if (n_levels) *n_levels = c->ext_levels;
   if (!c->d_ext) return fail(c, CVR_ERR_STATE, "cvr_copy_extinction_level: no extinction volume");
@@ -1506,6 +1584,10 @@ static bool same_cone(const cvr_cone_params& a, const cvr_cone_params& b) {
 cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_params* p,
                             const cvr_output* o) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group)
+    return cvr::group_render(c, f, 1, o, [&](cvr_ctx* _m, const cvr_frame* mf, int, const cvr_output* mo) {
+      return cvr_render_dosct(_m, mf, p, mo);
+    });
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_dosct: null argument");
 
@@ -1644,6 +1726,7 @@ cvr_status cvr_render_dosct(cvr_ctx* ctx, const cvr_frame* f, const cvr_dos_para
 
 cvr_status cvr_set_extinction_sat(cvr_ctx* ctx, const float* ext_lut, int lut_n) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_each(c, [&](cvr_ctx* _m) { return cvr_set_extinction_sat(_m, ext_lut, lut_n); });
   if (!c) return CVR_ERR_ARG;
   if (!c->d_vox) return fail(c, CVR_ERR_STATE, "cvr_set_extinction_sat: no volume set");
   const int nv = c->bpv == 1 ? 256 : 65536;
@@ -1756,6 +1839,7 @@ cvr_status cvr_sat_layout_check(const int dims[3], int layout, int pad_planes, u
 
 cvr_status cvr_copy_extinction_sat(cvr_ctx* ctx, float* out, size_t capacity, int dims[3]) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_copy_extinction_sat(_m, out, capacity, dims); });
   if (!c) return CVR_ERR_ARG;
   if (!c->d_sat) return fail(c, CVR_ERR_STATE, "cvr_copy_extinction_sat: no SAT built");
   if (dims) for (int i = 0; i < 3; i++) dims[i] = c->sat_dims[i];
@@ -1771,6 +1855,10 @@ cvr_status cvr_copy_extinction_sat(cvr_ctx* ctx, float* out, size_t capacity, in
 cvr_status cvr_render_extbsd(cvr_ctx* ctx, const cvr_frame* f, const cvr_ebs_params* p,
                              const cvr_output* o) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group)
+    return cvr::group_render(c, f, 1, o, [&](cvr_ctx* _m, const cvr_frame* mf, int, const cvr_output* mo) {
+      return cvr_render_extbsd(_m, mf, p, mo);
+    });
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_extbsd: null argument");
   if (c->filter_bits && c->sat_layout != 0)
@@ -1941,6 +2029,7 @@ static void iso_blocks_of(const cvr_iso_params* p, int nb[3]) {
 
 cvr_status cvr_iso_block_ranges(cvr_ctx* ctx, const int num_blocks[3], float* out_min, float* out_max) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group) return cvr::group_call_root(c, [&](cvr_ctx* _m) { return cvr_iso_block_ranges(_m, num_blocks, out_min, out_max); });
   if (!c) return CVR_ERR_ARG;
   if (!num_blocks || !out_min || !out_max) return fail(c, CVR_ERR_ARG, "cvr_iso_block_ranges: null argument");
   if (!c->d_vox) return fail(c, CVR_ERR_STATE, "cvr_iso_block_ranges: no volume set");
@@ -1961,6 +2050,10 @@ cvr_status cvr_iso_block_ranges(cvr_ctx* ctx, const int num_blocks[3], float* ou
 cvr_status cvr_render_iso(cvr_ctx* ctx, const cvr_frame* f, const cvr_iso_params* p,
                           const cvr_output* o) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->group)
+    return cvr::group_render(c, f, 1, o, [&](cvr_ctx* _m, const cvr_frame* mf, int, const cvr_output* mo) {
+      return cvr_render_iso(_m, mf, p, mo);
+    });
   if (!c) return CVR_ERR_ARG;
   if (!f || !p || !o || !o->rgba) return fail(c, CVR_ERR_ARG, "cvr_render_iso: null argument");
   if (c->filter_bits)

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -273,6 +274,7 @@ struct Ctx {
   int cell_flags_valid = 0;       // the cells' flags match the current TF
   int cell_flags_set = 0;         // the cells carry flags (of some TF)
   int cell_flags_oom = 0;         // the last flag build ran out of memory (retried after a volume / TF change)
+  int debug_flags_oom = 0;        // tests (option "debug_cell_flags_oom"): the flag build reports OOM
   // transfer function (RGBA16F values as float)
   float* d_tf = nullptr;
   int tf_n = 0;
@@ -381,6 +383,11 @@ struct Ctx {
   int launch_interleave = 1;       // option "launch_interleave": multi-frame launches deal the frames'
                                    // launch-order entries interleaved (LaunchFrames::interleave)
   int gather_root_idle = 0;        // option "gather_root_idle": rank 0 only gathers (renders nothing)
+  int exchange_code = 1;           // option "exchange_code": RGBA16F exchanges move the per-tile code
+  int exchange_lag = -1;           // option "exchange_lag": data phase trails by this many exchanges
+                                   // (-1 = split_streams - 1, bounded by the buffer sets)
+  // single-process group (cvr_create_group, cvr_group.cpp): the members this context fans out to
+  struct Group* group = nullptr;
   // scratch
   unsigned long long* d_total = nullptr;
   void* d_scratch = nullptr;      // host-output staging
@@ -388,6 +395,15 @@ struct Ctx {
 };
 
 void comm_release(Ctx* c);   // cvr_comm.cpp
+// cvr_group.cpp: a group context's members
+struct Group;
+using MemberRender = std::function<cvr_status(cvr_ctx*, const cvr_frame*, int, const cvr_output*)>;
+void group_release(Ctx* g);
+cvr_status group_each(Ctx* g, const std::function<cvr_status(cvr_ctx*)>& fn);
+cvr_status group_call_root(Ctx* g, const std::function<cvr_status(cvr_ctx*)>& fn);
+Ctx* group_root(Ctx* g);
+cvr_status group_render(Ctx* g, const cvr_frame* frames, int nf, const cvr_output* outs,
+                        const MemberRender& render);
 void flat_release(FlatJobs& J);   // flat.hip
 
 // postpass.hip: multiscaling filters (mode 1-3, kernel 0-5) and the screenshot
@@ -445,6 +461,25 @@ hipError_t launch_tile_encode(const void* d_tiles, int tile, int ntiles, void* d
 hipError_t launch_tile_decode(const void* d_stream, int tile, int ntiles, void* d_tiles, hipStream_t s);
 hipError_t launch_unpack_tiles(const void* packed, void* out, int half, int W, int H, int tile,
                                int nranks, int tpr_max, hipStream_t s, size_t rank_stride = 0);
+hipError_t launch_unpack_tiles_u32(const uint32_t* packed, uint32_t* out, int W, int H, int tile,
+                                   int nranks, int tpr_max, hipStream_t s, size_t rank_stride);
+// the exchange's one-launch encode of a group (nframes x k tiles at slot stride tpr)
+// into d_dst (any device's memory); d_ctr: two zeroed words on this device, left zero
+hipError_t launch_exchange_encode(const void* d_packed, int tile, int k, int tpr, int nframes, void* d_dst,
+                                  unsigned int* d_ctr, unsigned long long* d_bytes, hipStream_t s);
+// rank 0: every source's stream (or raw tiles) of a group decoded into the frames' images
+struct ExchangeDecode {
+  const uint32_t* src;               // source r's stream at src + r * slot_words
+  size_t slot_words;
+  const uint2* raw0;                 // source 0 as raw packed tiles (a rendering root), or null
+  size_t raw0_fstride;               // tiles between frames of raw0
+  int nsrc;                          // sources = the split's ranks
+  int nsplit;                        // the split's nranks (split_tile)
+  int nframes, tpr;                  // frames of the group, tile slots per frame and source
+  int tile, W, H, ntx, tile_grid_n;  // tile size, image, tiles per row, tiles per frame
+  uint2* img[kMaxLaunchFrames];      // frame f's RGBA16F image (null: skipped)
+};
+hipError_t launch_exchange_decode(const ExchangeDecode& a, hipStream_t s);
 
 inline CellGrid make_cell_grid(const int N[3]) {
   CellGrid g;

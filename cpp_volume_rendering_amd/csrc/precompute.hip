@@ -200,6 +200,19 @@ unpack_tiles_kernel(const PX* __restrict__ packed, PX* __restrict__ out, int W, 
   }
 }
 
+// per-pixel sample counts (uint32) of packed tiles, for the single-process group
+hipError_t launch_unpack_tiles_u32(const uint32_t* packed, uint32_t* out, int W, int H, int tile,
+                                   int nranks, int tpr_max, hipStream_t s, size_t rank_stride) {
+  const int ntx = (W + tile - 1) / tile;
+  const long long nslots = (long long)nranks * tpr_max;
+  if (nslots == 0) return hipSuccess;
+  if (nslots > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (rank_stride == 0) rank_stride = (size_t)tpr_max;
+  hipLaunchKernelGGL(unpack_tiles_kernel<uint32_t>, dim3((unsigned)nslots), dim3(256), 0, s, packed, out, W,
+                     H, tile, nranks, tpr_max, rank_stride, ntx);
+  return hipGetLastError();
+}
+
 hipError_t launch_unpack_tiles(const void* packed, void* out, int half, int W, int H, int tile,
                                int nranks, int tpr_max, hipStream_t s, size_t rank_stride) {
   int ntx = (W + tile - 1) / tile;

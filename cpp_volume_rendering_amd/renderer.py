@@ -227,10 +227,24 @@ def read_light_position(path: str, list_index: int = 0, light: int = 0):
 class Device:
     """One libcvr context (cvr_ctx) bound to a HIP device; owns all device data."""
 
-    def __init__(self, device: int = 0):
-        self.device = device
+    def __init__(self, device: int = 0, devices=None):
+        """devices (a list of device indices): one context over all of them in this
+        process (cvr_create_group: every frame split over the devices and gathered
+        on devices[0], which is also `device`)."""
         self._h = ctypes.c_void_p()
-        N.check(N.lib().cvr_create(device, ctypes.byref(self._h)), "cvr_create")
+        if devices is not None:
+            devs = [int(d) for d in devices]
+            self.device = devs[0]
+            arr = (ctypes.c_int * len(devs))(*devs)
+            N.check(N.lib().cvr_create_group(arr, len(devs), ctypes.byref(self._h)),
+                    "cvr_create_group")
+        else:
+            self.device = device
+            N.check(N.lib().cvr_create(device, ctypes.byref(self._h)), "cvr_create")
+
+    @property
+    def group_size(self) -> int:
+        return int(N.lib().cvr_group_size(self.handle))
 
     @property
     def handle(self):
@@ -396,10 +410,17 @@ class BaseVolumeRenderer:
 
 
 class RayCasting1Pass(BaseVolumeRenderer):
-    """HIP implementation of RayCasting1Pass (cppvolrend/structured/rc1pass/rc1prenderer.cpp)."""
+    """HIP implementation of RayCasting1Pass (cppvolrend/structured/rc1pass/rc1prenderer.cpp).
 
-    def __init__(self, device: int = 0):
+    ``devices`` (a list of GPU indices): the renderer runs on all of them from this one
+    process (cvr_create_group: each frame split into screen tiles over the devices and
+    gathered on devices[0]; same pixels as one GPU)."""
+
+    def __init__(self, device: int = 0, devices=None):
         super().__init__()
+        self._devices = list(devices) if devices is not None else None
+        if self._devices:
+            device = self._devices[0]
         self.m_u_step_size = 0.5                    # rc1prenderer.cpp:21
         self.m_apply_gradient_shading = False       # :22
         self._device_index = device
@@ -431,7 +452,7 @@ class RayCasting1Pass(BaseVolumeRenderer):
         dm = self.m_ext_data_manager
         if dm is None or dm.volume is None or dm.tf_rgbt is None:
             return False                            # rc1prenderer.cpp:54
-        self._dev = Device(self._device_index)
+        self._dev = Device(self._device_index, devices=self._devices)
         self._dev.set_volume(dm.volume, dm.scale)
         self._dev.set_transfer_function(dm.tf_rgbt)
         if dm.gradient_type != N.GRADIENT_NONE:
@@ -598,8 +619,8 @@ class RC1PConeTracingDirOcclusionShading(RayCasting1Pass):
 
     POINT_LIGHT, SPOT_LIGHT, DIRECTIONAL_LIGHT = 0, 1, 2   # type_of_shadow combo (:543)
 
-    def __init__(self, device: int = 0):
-        super().__init__(device)
+    def __init__(self, device: int = 0, devices=None):
+        super().__init__(device, devices)
         self.glsl_apply_occlusion = True            # dosrcrenderer.cpp:44
         self.glsl_apply_shadow = False              # :53
         self.type_of_shadow = self.POINT_LIGHT      # :59
@@ -659,8 +680,8 @@ class RC1PExtinctionBasedShading(RayCasting1Pass):
 
     POINT_LIGHT, DIRECTIONAL_LIGHT = 0, 1
 
-    def __init__(self, device: int = 0):
-        super().__init__(device)
+    def __init__(self, device: int = 0, devices=None):
+        super().__init__(device, devices)
         self.apply_ambient_occlusion = True          # ebsrenderer.cpp:27-31
         self.ambient_occlusion_shells = 15
         self.ambient_occlusion_radius = 1.0
@@ -720,8 +741,8 @@ class RayCasting1PassIsoAdapt(RayCasting1Pass):
 
     VARIANT = 2
 
-    def __init__(self, device: int = 0):
-        super().__init__(device)
+    def __init__(self, device: int = 0, devices=None):
+        super().__init__(device, devices)
         self._params = N.IsoParams()
         N.lib().cvr_iso_params_default(self.VARIANT, ctypes.byref(self._params))
         d = self._params
@@ -742,7 +763,7 @@ class RayCasting1PassIsoAdapt(RayCasting1Pass):
         dm = self.m_ext_data_manager
         if dm is None or dm.volume is None:
             return False                            # GetCurrentVolumeTexture() == nullptr
-        self._dev = Device(self._device_index)
+        self._dev = Device(self._device_index, devices=self._devices)
         self._dev.set_volume(dm.volume, dm.scale)
         if dm.gradient_type != N.GRADIENT_NONE:
             self._dev.set_gradient(dm.gradient_type)

@@ -140,7 +140,9 @@ class ScreenTileSplit:
     Transport ``"rccl"`` (default on GPUs at world > 1): the library's own
     communicator (cvr_comm_init, id broadcast over the process group) and
     cvr_gather_tiles, two C calls per frame; rank 0 renders straight into its block
-    of the gather buffer.  ``"torch"``: ``dist.gather`` of the process group (any
+    of the gather buffer.  ``code`` (default): RGBA16F exchanges move the lossless
+    per-tile code instead of raw tiles (library option exchange_code),
+    and every frame of an exchange group gets its own image on rank 0.  ``"torch"``: ``dist.gather`` of the process group (any
     backend; the gloo tests), one stream, with ``render_fn(frame, out_tensor,
     total_tensor_or_None)`` and ``unpack_fn(frame, gathered, image)`` defaulting to
     the library (renderer.render_to, cvr_unpack_tiles_device); the CPU tests pass
@@ -150,8 +152,10 @@ class ScreenTileSplit:
                  fmt: int = N.FORMAT_RGBA16F, group=None, device=None, render_fn=None,
                  unpack_fn=None, count_samples: bool = False, transport: str = None,
                  streams: int = None, frames_per_exchange: int = 1, stream_factory=None,
-                 frames_per_launch: int = 1, buffer_sets: int = 0, root_renders: bool = True):
+                 frames_per_launch: int = 1, buffer_sets: int = 0, root_renders: bool = True,
+                 code: bool = True):
         self.r = renderer
+        self.code = bool(code)      # native transport: RGBA16F exchanges move the per-tile code
         self.width = width if width is not None else renderer.width
         self.height = height if height is not None else renderer.height
         self.tile = tile
@@ -201,9 +205,6 @@ class ScreenTileSplit:
             self.L = 1
         if self.split and self.L > 1:
             frames_per_exchange = self.L
-        nimg = streams * self.L if not self.split else 1
-        self._images = ([torch.zeros((h, w, 4), dtype=dtype, device=self.device)
-                         for _ in range(nimg)] if self.rank == 0 else None)
         # buffer sets: frame n uses set n % nbuf (one per stream; two for one stream).
         # With the native transport, G = frames_per_exchange consecutive frames share
         # one set (one slot each), render on its stream and travel in ONE gather.
@@ -221,6 +222,13 @@ class ScreenTileSplit:
                                                        self.streams is not None) else 1
         if self.split and self.G == 1:
             self.L = 1
+        # rank 0's images: world 1 rotates D x L; a native split gives every frame of an
+        # exchange group its own image (the coded exchange decodes the group's frames in
+        # one launch, so they cannot share one), the torch transport one
+        nimg = (streams * self.L if not self.split else
+                (self.G if self.transport == "rccl" and self.streams is not None else 1))
+        self._images = ([torch.zeros((h, w, 4), dtype=dtype, device=self.device)
+                         for _ in range(nimg)] if self.rank == 0 else None)
         self._batch = []            # frames of the open launch (L > 1)
         if self.split:
             # padded to tpr_max tiles (gather needs equal sizes); padding stays zero
@@ -256,11 +264,13 @@ class ScreenTileSplit:
                                  fmt) for j in range(self.G)]
                 slots.append((self.streams[i % self.nstreams].cuda_stream, outs, blk.data_ptr(),
                               g.data_ptr() if g is not None else None))
-            img = self._images[0].data_ptr() if self.rank == 0 else None
-            imgs = (ctypes.c_void_p * self.G)(*([img] * self.G))
+            imgs = (ctypes.c_void_p * self.G)(*([self._images[j].data_ptr() for j in range(self.G)]
+                                                 if self.rank == 0 else [None] * self.G))
             self._fast = (L, h, getattr(L, self.r._ENTRY), ctypes.byref(self.r._params), imgs,
                           slots)
             self._group = 0      # frames rendered into the open exchange group
+        self._xg = 0             # exchange groups issued (the library's exchange count)
+        self._last_j = 0         # rank 0: image of the last exchanged frame
 
     def _image_index(self, n):
         """World 1: the image of frame n (launch group g = n // L on stream g % D)."""
@@ -274,7 +284,7 @@ class ScreenTileSplit:
         if self._images is None:
             return None
         if self.split:
-            return self._images[0]
+            return self._images[self._last_j if self._fast is not None else 0]
         return self._images[self._image_index(max(self.completed, 0))]
 
     def _init_comm(self):
@@ -296,6 +306,7 @@ class ScreenTileSplit:
         N.check(L.cvr_set_option(h, b"split_streams", self.nstreams), "split_streams", h)
         N.check(L.cvr_set_option(h, b"gather_sets", self.nbuf), "gather_sets", h)
         N.check(L.cvr_set_option(h, b"gather_root_idle", int(self.idle_root)), "gather_root_idle", h)
+        N.check(L.cvr_set_option(h, b"exchange_code", int(self.code)), "exchange_code", h)
 
     def close(self):
         if self._comm:
@@ -310,7 +321,7 @@ class ScreenTileSplit:
                        total.data_ptr() if total is not None else None, 1, self.fmt)
         self.r.render_to(frame, out)
 
-    def _unpack_lib(self, frame, gathered, image):
+    def _unpack_lib(self, frame, gathered, image):  # torch transport
         N.check(N.lib().cvr_unpack_tiles_device(self.r.device.handle, ctypes.byref(frame),
                                                 gathered.data_ptr(), self.tpr_max, self.fmt,
                                                 image.data_ptr()),
@@ -355,8 +366,11 @@ class ScreenTileSplit:
             if self._fresh:
                 self._stream_for(n)
             G = self.G
-            sptr, outs, buf, g = slots[(n // G) % self.nbuf]
-            j = n % G
+            # the open exchange group: its buffer set (and stream) follow the library's
+            # own exchange count, its frames fill slots 0, 1, ... (a flush may close a
+            # group early, so frame numbers need not align with groups)
+            sptr, outs, buf, g = slots[self._xg % self.nbuf]
+            j = self._group
             L.cvr_set_stream(h, sptr)
             if self.renders:
                 st = entry(h, ctypes.byref(frame), params, ctypes.byref(outs[j]))
@@ -400,7 +414,7 @@ class ScreenTileSplit:
         frames, self._batch = self._batch, []
         nb = len(frames)
         n0 = self.submitted - nb
-        g = n0 // self.L
+        g = self._xg if self.split else n0 // self.L
         self._stream_for(g)
         if not self.split:
             outs = [N.Output(self._images[self._image_index(n0 + j)].data_ptr(), None,
@@ -426,14 +440,15 @@ class ScreenTileSplit:
         """Gather the open group's `nframes` frames, the last of which is frame
         `n_last`, in one ncclGather on the group's stream."""
         L, h, entry, params, imgs, slots = self._fast
-        n0 = n_last - nframes + 1                        # first frame of the group
-        sptr, outs, buf, g = slots[(n0 // self.G) % self.nbuf]
+        sptr, outs, buf, g = slots[self._xg % self.nbuf]
         L.cvr_set_stream(h, sptr)
         st = L.cvr_gather_tiles_n(h, ctypes.byref(self._frame), nframes, buf, self.tpr_max,
                                   self.fmt, g, imgs if self.rank == 0 else None)
         if st:
             N.check(st, "cvr_gather_tiles_n", h)
         self._group = 0
+        self._xg += 1
+        self._last_j = nframes - 1       # the image of the group's last frame
 
     def _frame_for(self, camera):
         """This rank's cvr_frame for `camera` (cached while the camera is unchanged)."""

@@ -553,6 +553,16 @@ cvr_status  cvr_comm_init(cvr_ctx* ctx, int nranks, int rank,
                           const unsigned char id[CVR_COMM_ID_BYTES]);
 cvr_status  cvr_comm_destroy(cvr_ctx* ctx);
 
+/* The same protocol without RCCL, for n contexts of THIS process (rank i =
+ * ctxs[i]; the devices may repeat, e.g. n contexts on one GPU): the bytes move
+ * as device copies (over xGMI between GPUs).  Every exchange call
+ * (cvr_gather_tiles_n) must be made by ranks 1..n-1 before rank 0 makes it, and
+ * the buffer sets must exceed the render streams (gather_sets > split_streams):
+ * a rank's next render waits for rank 0's completed exchange of its buffers.
+ * cvr_create_group uses it; tests use it to run the multi-rank exchange on one
+ * GPU (RCCL refuses several ranks per device). */
+cvr_status  cvr_comm_init_local(cvr_ctx* const* ctxs, int n);
+
 /* Gather one frame's packed tiles on rank 0 (one ncclGather) and unpack them
  * into the image.
  * Every rank calls it right after rendering its tiles (frame->rank/nranks
@@ -587,8 +597,47 @@ cvr_status  cvr_gather_tiles_n(cvr_ctx* ctx, const cvr_frame* frame, int nframes
                                const void* d_packed, int tiles_per_rank_max, int format,
                                void* d_gathered, void* const* d_images);
 
-/* The context stream waits for every gather issued so far. */
+/* The context stream waits for every gather issued so far (posting any whose
+ * data phase still trails, see exchange_lag). */
 cvr_status  cvr_gather_sync(cvr_ctx* ctx);
+
+/* Exchange form (options, set on every rank alike):
+ *   "exchange_code" 1 (default): RGBA16F exchanges of N > 1 ranks move the lossless
+ *                per-tile code (cvr_encode_tiles' stream, encoded in one launch per
+ *                exchange on the render stream) instead of raw tiles, and rank 0
+ *                decodes every rank's stream straight into the images in one
+ *                launch; 0: raw tiles (one ncclGather, then the unpack).  RGBA32F
+ *                always moves raw tiles.  The images are identical either way.
+ *   "exchange_lag" the coded exchange's sizes vary, so they travel first (an 8-byte
+ *                gather on a second communicator, right after the encode) and
+ *                exchange g's data is posted when a later call reads g's sizes on
+ *                the host: at most this many exchanges later (-1, the default:
+ *                split_streams - 1; bounded by gather_sets - split_streams so a
+ *                render stream never waits for an unposted exchange; 0: at once,
+ *                which blocks the host until this rank's encode is done). */
+
+/* ----------------------------------------------------------------------------
+ * One context over several GPUs of this process (SURVEY.md §8b threading row:
+ * multi-GPU inside cvr_render when ndev > 1).  The reference app is one GLUT
+ * process with one GL thread (app_freeglut.cpp:125,174), so its plugin cannot be
+ * one process per GPU.  cvr_create_group returns a context whose state setters
+ * (volume, TF, gradient, extinction pyramid, SAT, options) apply to one member
+ * context per device, and whose render calls (rc1pass, rc1pass_frames, dosct,
+ * extbsd, iso; whole frames, nranks <= 1) split the frame into 16 x 16 screen
+ * tiles on the diagonal lattice over the members, render every share on its own
+ * device concurrently, and gather the tiles on devices[0] (the in-process
+ * transport of cvr_comm_init_local; RGBA16F as the per-tile code) into the
+ * caller's outputs, which live on devices[0] (or the host).  Same pixels, counts
+ * and totals as one context.  Devices may repeat.  The group's stream
+ * (cvr_set_stream) is devices[0]'s; member 0 renders on it.  Host outputs block;
+ * device outputs are queued on the group's stream.  Options split_streams,
+ * gather_sets, gather_root_idle and exchange_lag belong to the group's own
+ * exchange and are refused. */
+cvr_status  cvr_create_group(const int* devices, int n, cvr_ctx** out_ctx);
+/* Members of a group (1 for a plain context) and member i's context (NULL if none;
+ * owned by the group: for inspection, not for cvr_destroy). */
+int         cvr_group_size(const cvr_ctx* ctx);
+cvr_ctx*    cvr_group_member(cvr_ctx* ctx, int i);
 
 /* Diagnostics (tile_stats option): for each 8x8 tile of the last frame, four
  * uint64: start and end stamp (s_memrealtime, 100 MHz), its longest ray's

@@ -212,7 +212,8 @@ class _FakeLib:
         return 0
 
     def cvr_gather_tiles_n(self, h, fr, nframes, buf, tpr, fmt, g, imgs):
-        self.calls.append(("gather", self.stream, nframes, buf, g is not None))
+        self.calls.append(("gather", self.stream, nframes, buf, g is not None,
+                           [imgs[j] for j in range(nframes)] if imgs is not None else None))
         return 0
 
     def cvr_gather_sync(self, h):
@@ -457,8 +458,17 @@ def _native_bench8_worker(rank, world, port, q):
                 assert rc[1] == streams[grp % 4]
             assert len(bufs) == 16          # the 16 sets rotate
         for opt in (("opt", b"gather_root_idle", 1), ("opt", b"gather_sets", 16),
-                    ("opt", b"split_streams", 4)):
+                    ("opt", b"split_streams", 4), ("opt", b"exchange_code", 1)):
             assert opt in fake.calls, opt
+        # the coded exchange decodes a group's frames in one launch: rank 0 hands every
+        # frame of a group its own image (4 distinct), the same 4 for every group
+        if rank == 0:
+            imgs = [tuple(g[5]) for g in gathers]
+            assert all(len(set(i)) == len(i) for i in imgs)
+            assert imgs[0] == tuple(im.data_ptr() for im in sp._images[:4])
+            assert all(i == imgs[0][:len(i)] for i in imgs)
+        else:
+            assert all(g[5] is None for g in gathers)
         sp.close()
         q.put(("ok", rank, len(gathers)))
     except Exception as e:   # noqa: BLE001  (reported to the parent)
