@@ -265,17 +265,26 @@ def split_defaults(a, world):
     --root-renders), as ScreenTileSplit keyword arguments.  Shared with the world-8
     control-flow test (tests/test_distributed_cpu.py), so the test runs exactly the
     N = 8 default path."""
-    fpl = a.frames_per_launch if a.frames_per_launch > 0 else (4 if a.renderer == "rc1pass" else 1)
+    # 8 frames per launch (and per exchange) from 8 GPUs: a 7-way share of one frame
+    # is ~2300 wave tiles, so a 4-frame launch is about one residency of the GPU and
+    # lasts as long as its longest rays; 8 frames amortise that tail (7-way share with
+    # the encode 0.0135 -> 0.0124 ms per frame, tools/exchange_probe.py,
+    # profiles/r06/s10_*) and halve the host calls per frame (DESIGN §7b)
+    fpl = (a.frames_per_launch if a.frames_per_launch > 0 else
+           ((8 if world >= 8 else 4) if a.renderer == "rc1pass" else 1))
     streams = a.streams or ((4 if world >= 2 else 3) if fpl > 1 else
                             (16 if world >= 8 else (12 if world >= 4 else 4)))
     # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
     # on rank 0) would otherwise rival a rank's share of the frame (~23 us at N = 8)
     gx = fpl if fpl > 1 else (a.exchange_frames or (2 if world >= 4 else 1))
-    # rank 0's exchange (receive + unpack of 7/8 of every frame at N = 8) competes
-    # with its own render and stalls it (tools/rank0_probe.py: 0.0295 ms per
-    # frame against 0.0125 for a render-only rank); with 3+ render ranks the root
-    # only gathers (0.0094 ms per frame) and N - 1 ranks render
-    root_renders = (a.root_renders == 1 or world < 4 or a.renderer != "rc1pass"
+    # Rank 0's share of the exchange is one fused decode per group of every render
+    # rank's coded tiles (DESIGN §7b, tools/exchange_probe.py: ~14-19 us per 4-frame
+    # group at N = 4 and 8).  At N = 8 an idle root leaves 7 render ranks whose
+    # share (0.0124-0.0135 ms per frame with the encode) beats an 8-way share plus
+    # the decode on rank 0 (~0.0128 + ~0.004); at N = 4 three render ranks lose a
+    # quarter of the GPUs (0.0289 ms) against 4-way + decode (~0.022 + ~0.0035), so
+    # the root renders below 8 ranks and only gathers from 8 on
+    root_renders = (a.root_renders == 1 or world < 8 or a.renderer != "rc1pass"
                     or a.transport != "rccl") if a.root_renders != 0 else False
     return {"streams": streams, "frames_per_exchange": gx, "frames_per_launch": fpl,
             "buffer_sets": a.buffer_sets or 4 * streams, "root_renders": root_renders}

@@ -15,6 +15,8 @@
 // Three launches: per-tile sizes, one workgroup's scan into the start table,
 // and the packing; the decode is one launch.  A wave per tile throughout (64
 // lanes over the tile's pixels; the packing reads its pixels from LDS).
+#include <algorithm>
+
 #include "cvr_internal.h"
 
 namespace cvr {
@@ -40,10 +42,11 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return v;
 }
 
-// The tile's per-channel bases and widths (every lane gets them).
+// The tile's per-channel bases and widths (every lane of the calling wave gets them;
+// a wave codes one tile, so the lane is the thread's index within its wave).
 __device__ __forceinline__ void tile_stats(const uint2* __restrict__ px, int npx, uint32_t (&base)[4],
                                            uint32_t (&width)[4]) {
-  const int lane = (int)threadIdx.x;
+  const int lane = (int)threadIdx.x & 63;
   uint32_t mn[4] = {0xffffu, 0xffffu, 0xffffu, 0xffffu}, mx[4] = {0u, 0u, 0u, 0u};
   for (int p = lane; p < npx; p += 64) {
     const uint2 v = px[p];
@@ -147,13 +150,17 @@ __global__ void __launch_bounds__(64) tile_encode_kernel(const uint2* __restrict
 }
 
 __global__ void __launch_bounds__(64) tile_decode_kernel(const uint32_t* __restrict__ stream, int npx, int ntiles,
-                                                         uint2* __restrict__ tiles) {
+                                                         size_t max_words, uint2* __restrict__ tiles) {
   const int t = blockIdx.x;
   if (t >= ntiles) return;
-  const uint32_t* in = stream + stream[t];
+  // a stream that does not parse is skipped rather than followed past its bound
+  const uint32_t t0 = stream[t];
+  if ((size_t)t0 + kCodecHeaderWords > max_words) return;
+  const uint32_t* in = stream + t0;
   const uint32_t h0 = in[0], h1 = in[1], h2 = in[2];
   const uint32_t base[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
   const uint32_t width[4] = {h2 & 31u, (h2 >> 5) & 31u, (h2 >> 10) & 31u, (h2 >> 15) & 31u};
+  if (max(max(width[0], width[1]), max(width[2], width[3])) > 16u) return;
   uint32_t start[4];
   uint32_t pos = kCodecHeaderWords;
 #pragma unroll
@@ -161,6 +168,7 @@ __global__ void __launch_bounds__(64) tile_decode_kernel(const uint32_t* __restr
     start[c] = pos;
     pos += ((uint32_t)npx * width[c] + 31u) >> 5;
   }
+  if ((size_t)t0 + pos > max_words) return;
   uint2* dst = tiles + (size_t)t * npx;
   for (int p = (int)threadIdx.x; p < npx; p += 64) {
     uint32_t v[4];
@@ -183,37 +191,70 @@ __global__ void __launch_bounds__(64) tile_decode_kernel(const uint32_t* __restr
 // ---------------------------------------------------------------------------
 // The exchange's form of the code (cvr_comm.cpp): ONE launch per exchange group.
 // Tile t of the group is frame f = t / k, the rank's tile i = t % k, read from slot
-// f * tpr + i of the packed buffer.  Each tile claims its words with one atomic on
-// ctr[0] (so tiles land in claim order, not in t order: the start table makes the
-// order irrelevant to the decode), and the last workgroup to finish (ticket on
-// ctr[1]) writes the stream's end word and its length in bytes, then zeroes the
-// counters for the next launch on the same buffer set.  The stream is written to
-// `dst`, which may be a peer device's memory (the in-process transport pushes it
-// there); the counters stay on the encoding device.
-__global__ void __launch_bounds__(64) exchange_encode_kernel(const uint2* __restrict__ packed, int npx, int k,
-                                                             int tpr, int ntiles, uint32_t* __restrict__ dst,
-                                                             unsigned int* __restrict__ ctr,
-                                                             unsigned long long* __restrict__ d_bytes) {
-  extern __shared__ uint2 pxl[];
+// f * tpr + i of the packed buffer.  A workgroup codes kEncTiles tiles, one per wave,
+// and claims their words with ONE 64-bit atomic on *ctr: the low half counts words
+// (the old value is the workgroup's offset, so codes land in claim order, not in t
+// order -- the start table makes the order irrelevant to the decode), the high half
+// counts tiles, so the claim that completes ntiles knows the total: it zeroes the
+// counter for the next launch that uses it and writes the stream's end word and its
+// length in bytes (cvr_encode_tiles passes the length itself as the counter).
+// Measured forms before this one: an atomic per tile (2048 claims on one address
+// serialise, ~20 us per 4-frame share at N = 8), and a __threadfence per workgroup
+// (it writes back the XCD's L2 every time, 55-160 us).  No fence is needed: nothing
+// in the kernel reads another tile's words, and the kernel's end publishes them.
+// Two launches in flight must not share a counter (each exchange buffer set has its
+// own).
+constexpr int kEncTiles = 8;
+__global__ void __launch_bounds__(64 * kEncTiles) exchange_encode_kernel(
+    const uint2* __restrict__ packed, int npx, int k, int tpr, int ntiles, uint32_t* __restrict__ dst,
+    unsigned long long* ctr, unsigned long long* d_bytes, unsigned long long* h_bytes) {
+  extern __shared__ uint2 pxl_all[];
+  __shared__ uint32_t s_words[kEncTiles];
   __shared__ uint32_t s_off;
-  const int lane = (int)threadIdx.x;
+  const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
   if (ntiles == 0) {   // a rank without tiles: the empty stream
-    if (lane == 0) {
+    if (threadIdx.x == 0) {
       dst[0] = 1u;
       if (d_bytes) *d_bytes = 4ull;
+      if (h_bytes) *h_bytes = 4ull;
     }
     return;
   }
-  const int t = blockIdx.x;
-  const int f = t / k, i = t - f * k;
-  const uint2* src = packed + ((size_t)f * tpr + i) * npx;
-  for (int p = lane; p < npx; p += 64) pxl[p] = src[p];
+  const int tpb = (int)(blockDim.x >> 6);   // tiles (waves) per workgroup, <= kEncTiles
+  const int t0 = blockIdx.x * tpb;
+  const int nvalid = min(tpb, ntiles - t0);
+  const int t = t0 + wv;
+  const bool live = wv < nvalid;
+  uint2* pxl = pxl_all + (size_t)wv * npx;
+  uint32_t base[4] = {0, 0, 0, 0}, width[4] = {0, 0, 0, 0};
+  if (live) {
+    const int f = t / k, i = t - f * k;
+    const uint2* src = packed + ((size_t)f * tpr + i) * npx;
+    for (int p = lane; p < npx; p += 64) pxl[p] = src[p];
+    // (a wave reads only its own tile from LDS: the wave's own program order suffices)
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    tile_stats(pxl, npx, base, width);
+    if (lane == 0) s_words[wv] = code_words(npx, width);
+  }
   __syncthreads();
-  uint32_t base[4], width[4];
-  tile_stats(pxl, npx, base, width);
-  if (lane == 0) s_off = atomicAdd(&ctr[0], code_words(npx, width));
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int w = 0; w < nvalid; w++) tot += s_words[w];
+    const unsigned long long old = atomicAdd(ctr, ((unsigned long long)nvalid << 32) | tot);
+    s_off = (uint32_t)old;
+    if ((uint32_t)(old >> 32) + (uint32_t)nvalid == (uint32_t)ntiles) {   // the last claim
+      const uint32_t end = (uint32_t)ntiles + 1u + (uint32_t)old + tot;
+      atomicExch(ctr, 0ull);
+      dst[ntiles] = end;
+      if (d_bytes) *d_bytes = 4ull * end;
+      if (h_bytes) *h_bytes = 4ull * end;   // mapped host memory: the host reads it after the launch
+    }
+  }
   __syncthreads();
-  const uint32_t start = (uint32_t)ntiles + 1u + s_off;
+  if (!live) return;
+  uint32_t start = (uint32_t)ntiles + 1u + s_off;
+  for (int w = 0; w < wv; w++) start += s_words[w];
   uint32_t* out = dst + start;
   if (lane == 0) {
     dst[t] = start;
@@ -238,21 +279,6 @@ __global__ void __launch_bounds__(64) exchange_encode_kernel(const uint2* __rest
       out[pos + j] = acc;
     }
     pos += nw;
-  }
-  // every lane's words are issued before the ticket: the last workgroup's end word
-  // and the stream length then cover all of them (kernel end publishes the rest)
-  __threadfence();
-  __syncthreads();
-  if (lane == 0) {
-    const unsigned int ticket = atomicAdd(&ctr[1], 1u);
-    if (ticket == (unsigned int)ntiles - 1u) {
-      const uint32_t total = atomicAdd(&ctr[0], 0u);
-      const uint32_t end = (uint32_t)ntiles + 1u + total;
-      dst[ntiles] = end;
-      if (d_bytes) *d_bytes = 4ull * end;
-      atomicExch(&ctr[0], 0u);
-      atomicExch(&ctr[1], 0u);
-    }
   }
 }
 
@@ -289,10 +315,15 @@ __global__ void __launch_bounds__(64) exchange_decode_kernel(ExchangeDecode a) {
     return;
   }
   const uint32_t* in = a.src + (size_t)r * a.slot_words;
-  const uint32_t* tc = in + in[f * k + i];
+  // a stream that does not parse (never produced by the encode) is skipped rather than
+  // followed out of its slot: the tile stays as it was
+  const uint32_t t0 = in[f * k + i];
+  if ((size_t)t0 + kCodecHeaderWords > a.slot_words) return;
+  const uint32_t* tc = in + t0;
   const uint32_t h0 = tc[0], h1 = tc[1], h2 = tc[2];
   const uint32_t base[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
   const uint32_t width[4] = {h2 & 31u, (h2 >> 5) & 31u, (h2 >> 10) & 31u, (h2 >> 15) & 31u};
+  if (max(max(width[0], width[1]), max(width[2], width[3])) > 16u) return;
   uint32_t start[4];
   uint32_t nw = kCodecHeaderWords;
 #pragma unroll
@@ -300,6 +331,7 @@ __global__ void __launch_bounds__(64) exchange_decode_kernel(ExchangeDecode a) {
     start[c] = nw;
     nw += ((uint32_t)npx * width[c] + 31u) >> 5;
   }
+  if ((size_t)t0 + nw > a.slot_words) return;
   for (uint32_t j = (uint32_t)lane; j < nw; j += 64) code[j] = tc[j];
   code[nw] = 0u;   // the word after the last one a straddling read may touch (weight 0)
   __syncthreads();
@@ -325,13 +357,16 @@ __global__ void __launch_bounds__(64) exchange_decode_kernel(ExchangeDecode a) {
 }  // namespace
 
 hipError_t launch_exchange_encode(const void* d_packed, int tile, int k, int tpr, int nframes, void* d_dst,
-                                  unsigned int* d_ctr, unsigned long long* d_bytes, hipStream_t s) {
+                                  unsigned long long* ctr, unsigned long long* d_bytes, unsigned long long* h_bytes,
+                                  hipStream_t s) {
   const int npx = tile * tile;
   const long long nt = (long long)k * nframes;
-  if (nt > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(exchange_encode_kernel, dim3(nt > 0 ? (unsigned)nt : 1u), dim3(64),
-                     (size_t)npx * sizeof(uint2), s, static_cast<const uint2*>(d_packed), npx, k > 0 ? k : 1,
-                     tpr, (int)nt, static_cast<uint32_t*>(d_dst), d_ctr, d_bytes);
+  if (nt > 0x7fffffffLL || k > tpr) return hipErrorInvalidValue;
+  // 16 KB of LDS per workgroup: 8 tiles of 16 x 16, 2 of 32 x 32
+  const int tpb = std::max(1, std::min(kEncTiles, 2048 / npx));
+  const unsigned nblk = nt > 0 ? (unsigned)((nt + tpb - 1) / tpb) : 1u;
+  hipLaunchKernelGGL(exchange_encode_kernel, dim3(nblk), dim3(64 * tpb), (size_t)tpb * npx * sizeof(uint2), s, static_cast<const uint2*>(d_packed), npx, k > 0 ? k : 1,
+                     tpr, (int)nt, static_cast<uint32_t*>(d_dst), ctr, d_bytes, h_bytes);
   return hipGetLastError();
 }
 
@@ -367,7 +402,7 @@ hipError_t launch_tile_encode(const void* d_tiles, int tile, int ntiles, void* d
 hipError_t launch_tile_decode(const void* d_stream, int tile, int ntiles, void* d_tiles, hipStream_t s) {
   if (ntiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(tile_decode_kernel, dim3(ntiles), dim3(64), 0, s, static_cast<const uint32_t*>(d_stream),
-                     tile * tile, ntiles, static_cast<uint2*>(d_tiles));
+                     tile * tile, ntiles, tile_code_bound_bytes(tile, ntiles) / 4, static_cast<uint2*>(d_tiles));
   return hipGetLastError();
 }
 

@@ -463,6 +463,11 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->exchange_code = value;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "encode_onepass")) {
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "encode_onepass must be 0 or 1");
+    c->encode_onepass = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "exchange_lag")) {
     if (value < -1 || value >= CVR_MAX_GATHER_SETS)
       return fail(c, CVR_ERR_ARG, "exchange_lag must be -1 (auto) .. %d", CVR_MAX_GATHER_SETS - 1);
@@ -537,6 +542,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "gather_root_idle")) return c->gather_root_idle;
   if (!std::strcmp(key, "exchange_code")) return c->exchange_code;
   if (!std::strcmp(key, "exchange_lag")) return c->exchange_lag;
+  if (!std::strcmp(key, "encode_onepass")) return c->encode_onepass;
   if (!std::strcmp(key, "launch_interleave")) return c->launch_interleave;
   if (!std::strcmp(key, "sat_build_us")) return c->sat_build_us;   // read-only
   if (!std::strcmp(key, "order_interval")) return c->order_interval;
@@ -1383,6 +1389,15 @@ cvr_status cvr_encode_tiles(cvr_ctx* ctx, const void* d_tiles, int tile, int nti
   if ((!d_tiles && ntiles > 0) || !d_stream || !d_bytes || !cvr_tile_code_bound(tile, ntiles))
     return fail(c, CVR_ERR_ARG, "cvr_encode_tiles: bad arguments");
   HIP_TRY(c, hipSetDevice(c->device));
+  if (c->encode_onepass && tile <= 32) {   // (8 tiles staged in LDS per workgroup)
+    // the exchange's one-launch form: tiles in claim order (the start table says where).
+    // Its counter is the caller's own length word, zeroed first, so encodes on several
+    // streams never share one.
+    HIP_TRY(c, hipMemsetAsync(d_bytes, 0, sizeof(unsigned long long), c->stream));
+    HIP_TRY(c, cvr::launch_exchange_encode(d_tiles, tile, ntiles, ntiles, 1, d_stream, d_bytes, d_bytes,
+                                           nullptr, c->stream));
+    return CVR_OK;
+  }
   HIP_TRY(c, cvr::launch_tile_encode(d_tiles, tile, ntiles, d_stream, d_bytes, c->stream));
   return CVR_OK;
 }

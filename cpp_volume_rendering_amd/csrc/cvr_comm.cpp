@@ -16,8 +16,9 @@
 //     stream straight into the images in ONE launch.
 //
 // The coded exchange has variable sizes.  RCCL has no gatherv and a send's count
-// must equal its receive's, so the sizes travel first (an 8-byte ncclGather on a
-// second communicator and stream, right after the encode) and the data of
+// must equal its receive's, so the sizes travel first (the encode writes its
+// length to mapped host memory and to the device; an 8-byte ncclGather on a
+// second communicator and stream brings them to rank 0) and the data of
 // exchange g is posted `lag` exchanges later, when the host reads g's sizes
 // (option exchange_lag): by then the sizes have normally long arrived, and the
 // render streams hold the groups in between, so the device never waits for the
@@ -64,12 +65,13 @@ struct Pending {
 struct CodeSet {
   void* send = nullptr;                  // this rank's stream
   size_t send_cap = 0;
-  unsigned int* ctr = nullptr;           // the encode's two counters (left zero)
+  unsigned long long* ctr = nullptr;     // the encode's claim counter (left zero)
   unsigned long long* d_size = nullptr;  // [1] this rank's stream bytes
   void* recv = nullptr;                  // rank 0: nsrc slots of recv_slot bytes
   size_t recv_slot = 0, recv_cap = 0;
-  unsigned long long* d_sizes = nullptr; // rank 0: [nranks] gathered sizes (RCCL)
+  unsigned long long* d_sizes = nullptr; // rank 0: [nranks] gathered sizes (RCCL; its own slot stays 0)
   unsigned long long* h_sizes = nullptr; // pinned: rank 0 all sizes, others its own at [0]
+  unsigned long long* h_sizes_dev = nullptr;   // the device pointer of h_sizes (mapped)
 };
 
 struct Comm {
@@ -82,7 +84,7 @@ struct Comm {
   hipEvent_t ev_render = nullptr;   // end of the render whose tiles are exchanged
   hipEvent_t ev_gather[kRing] = {}; // exchange g done (rank 0: decoded; others: sent)
   hipEvent_t ev_enc[kRing] = {};    // exchange g's tiles ready (encoded, or rendered when raw)
-  hipEvent_t ev_sz[kRing] = {};     // exchange g's sizes in h_sizes
+  hipEvent_t ev_sz[kRing] = {};     // rank 0 (RCCL): exchange g's gathered sizes in h_sizes
   long long ngather = 0;            // exchanges issued (phase A)
   long long nposted = 0;            // exchanges whose data phase is issued
   Pending pend[kRing];
@@ -171,12 +173,15 @@ cvr_status ensure_set(Ctx* c, Comm* m, int set, size_t send_bytes, size_t recv_s
   if ((int)m->sets.size() <= set) m->sets.resize((size_t)set + 1);
   CodeSet& S = m->sets[(size_t)set];
   if (!S.ctr) {
-    CHIP(c, hipMalloc((void**)&S.ctr, 2 * sizeof(unsigned int) + sizeof(unsigned long long)));
-    CHIP(c, hipMemset(S.ctr, 0, 2 * sizeof(unsigned int) + sizeof(unsigned long long)));
-    S.d_size = reinterpret_cast<unsigned long long*>(S.ctr + 2);
+    CHIP(c, hipMalloc((void**)&S.ctr, 2 * sizeof(unsigned long long)));
+    CHIP(c, hipMemset(S.ctr, 0, 2 * sizeof(unsigned long long)));
+    S.d_size = S.ctr + 1;
+    // mapped, coherent: a render rank's encode writes its stream length here itself,
+    // so the host reads it after the launch without a copy
     CHIP(c, hipHostMalloc((void**)&S.h_sizes, sizeof(unsigned long long) * (size_t)m->nranks,
-                          hipHostMallocDefault));
+                          hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(S.h_sizes, 0, sizeof(unsigned long long) * (size_t)m->nranks);
+    CHIP(c, hipHostGetDevicePointer((void**)&S.h_sizes_dev, S.h_sizes, 0));
     if (m->rank == 0 && m->comm_sz) {
       CHIP(c, hipMalloc((void**)&S.d_sizes, sizeof(unsigned long long) * (size_t)m->nranks));
       CHIP(c, hipMemset(S.d_sizes, 0, sizeof(unsigned long long) * (size_t)m->nranks));
@@ -258,6 +263,8 @@ cvr_status post_data(Ctx* c, Comm* m, long long e) {
     // in-process transport: rank 0 pulls every rank's bytes (device copies); the
     // other ranks only make sure they issued the exchange (they call first)
     if (m->rank == 0) {
+      // its own tiles (raw block 0) come from its own render
+      CHIP(c, hipStreamWaitEvent(m->stream, m->ev_enc[e % kRing], 0));
       for (int r = 1; r < m->nranks; r++) {
         const Comm* mr = comm_of(m->hub->ctxs[(size_t)r]);
         if (mr->ngather <= e)
@@ -272,7 +279,7 @@ cvr_status post_data(Ctx* c, Comm* m, long long e) {
           Comm* mr = comm_of(cr);
           const Pending& Pr = mr->pend[e % kRing];
           const CodeSet& Sr = mr->sets[(size_t)Pr.set];
-          CHIP(c, hipEventSynchronize(mr->ev_sz[e % kRing]));
+          CHIP(c, hipEventSynchronize(mr->ev_enc[e % kRing]));   // its encode wrote the length
           const size_t nb = (size_t)Sr.h_sizes[0];
           const int src = idle ? r - 1 : r;
           if (nb > P.recv_slot)
@@ -298,8 +305,9 @@ cvr_status post_data(Ctx* c, Comm* m, long long e) {
       }
     }
   } else if (P.code) {
-    // RCCL: exact sizes, grouped point-to-point
-    CHIP(c, hipEventSynchronize(m->ev_sz[e % kRing]));
+    // RCCL: exact sizes, grouped point-to-point.  Rank 0 has every size once its
+    // gather's copy is done; a render rank has its own once its encode is.
+    CHIP(c, hipEventSynchronize(m->rank == 0 ? m->ev_sz[e % kRing] : m->ev_enc[e % kRing]));
     const CodeSet& S = m->sets[(size_t)P.set];
     if (m->rank == 0) {
       CNCCL(c, ncclGroupStart());
@@ -314,6 +322,7 @@ cvr_status post_data(Ctx* c, Comm* m, long long e) {
                           m->comm, m->stream));
       }
       CNCCL(c, ncclGroupEnd());
+      CHIP(c, hipStreamWaitEvent(m->stream, m->ev_enc[e % kRing], 0));   // its own raw tiles
       const int nsrc = idle ? m->nranks - 1 : m->nranks;
       CTRY(decode_group(c, m, P, nsrc, !idle));
     } else {
@@ -543,7 +552,7 @@ cvr_status cvr_gather_tiles_n(cvr_ctx* ctx, const cvr_frame* f, int nframes, con
   const size_t fbytes = m->nranks == 1 ? (size_t)f->width * f->height * px
                                        : (size_t)tpr_max * f->tile_size * f->tile_size * px;
   const bool code = c->exchange_code && m->nranks > 1 && format == CVR_FORMAT_RGBA16F &&
-                    f->tile_size <= 64;
+                    f->tile_size <= 32;   // (the encode stages 8 tiles in LDS)
   if (code && nframes > cvr::kMaxLaunchFrames)
     return cfail(c, CVR_ERR_ARG, "cvr_gather_tiles: the coded exchange takes at most %d frames",
                  cvr::kMaxLaunchFrames);
@@ -577,30 +586,25 @@ cvr_status cvr_gather_tiles_n(cvr_ctx* ctx, const cvr_frame* f, int nframes, con
     P.recv_slot = bound;
     CodeSet& S = m->sets[(size_t)set];
     if (!(m->rank == 0)) {
+      // the length lands in d_size (for the sizes' gather) and in mapped host memory
       CHIP(c, cvr::launch_exchange_encode(d_packed, f->tile_size, k, tpr_max, nframes, S.send, S.ctr,
-                                          S.d_size, s));
+                                          S.d_size, S.h_sizes_dev, s));
     }
     CHIP(c, hipEventRecord(m->ev_enc[ki], s));
-    CHIP(c, hipStreamWaitEvent(rs, m->ev_enc[ki], 0));
     if (m->comm_sz) {
-      // rank 0 contributes a zero (its own tiles, if any, stay raw in block 0)
+      CHIP(c, hipStreamWaitEvent(rs, m->ev_enc[ki], 0));
       if (m->rank == 0) {
-        CHIP(c, hipMemsetAsync(S.d_sizes, 0, sizeof(unsigned long long), rs));
+        // rank 0 contributes its slot's zero (its own tiles, if any, stay raw in block 0)
         CNCCL(c, ncclGather(S.d_sizes, S.d_sizes, sizeof(unsigned long long), ncclChar, 0,
                             m->comm_sz, rs));
         CHIP(c, hipMemcpyAsync(S.h_sizes, S.d_sizes, sizeof(unsigned long long) * (size_t)m->nranks,
                                hipMemcpyDeviceToHost, rs));
+        CHIP(c, hipEventRecord(m->ev_sz[ki], rs));
       } else {
         CNCCL(c, ncclGather(S.d_size, nullptr, sizeof(unsigned long long), ncclChar, 0, m->comm_sz,
                             rs));
-        CHIP(c, hipMemcpyAsync(S.h_sizes, S.d_size, sizeof(unsigned long long),
-                               hipMemcpyDeviceToHost, rs));
       }
-    } else if (m->rank != 0) {
-      CHIP(c, hipMemcpyAsync(S.h_sizes, S.d_size, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                             rs));
     }
-    CHIP(c, hipEventRecord(m->ev_sz[ki], rs));
   } else {
     CHIP(c, hipEventRecord(m->ev_enc[ki], s));
   }

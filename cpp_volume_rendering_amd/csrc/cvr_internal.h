@@ -384,6 +384,8 @@ struct Ctx {
                                    // launch-order entries interleaved (LaunchFrames::interleave)
   int gather_root_idle = 0;        // option "gather_root_idle": rank 0 only gathers (renders nothing)
   int exchange_code = 1;           // option "exchange_code": RGBA16F exchanges move the per-tile code
+  int encode_onepass = 0;          // option "encode_onepass": cvr_encode_tiles uses the exchange's
+                                   // one-launch encode (tiles in claim order)
   int exchange_lag = -1;           // option "exchange_lag": data phase trails by this many exchanges
                                    // (-1 = split_streams - 1, bounded by the buffer sets)
   // single-process group (cvr_create_group, cvr_group.cpp): the members this context fans out to
@@ -464,9 +466,12 @@ hipError_t launch_unpack_tiles(const void* packed, void* out, int half, int W, i
 hipError_t launch_unpack_tiles_u32(const uint32_t* packed, uint32_t* out, int W, int H, int tile,
                                    int nranks, int tpr_max, hipStream_t s, size_t rank_stride);
 // the exchange's one-launch encode of a group (nframes x k tiles at slot stride tpr)
-// into d_dst (any device's memory); d_ctr: two zeroed words on this device, left zero
+// into d_dst; ctr: a zeroed 64-bit counter on this device that no other launch in
+// flight uses, left zero (it may be d_bytes itself); h_bytes (may be null): the same
+// length into mapped host memory (its device pointer)
 hipError_t launch_exchange_encode(const void* d_packed, int tile, int k, int tpr, int nframes, void* d_dst,
-                                  unsigned int* d_ctr, unsigned long long* d_bytes, hipStream_t s);
+                                  unsigned long long* ctr, unsigned long long* d_bytes, unsigned long long* h_bytes,
+                                  hipStream_t s);
 // rank 0: every source's stream (or raw tiles) of a group decoded into the frames' images
 struct ExchangeDecode {
   const uint32_t* src;               // source r's stream at src + r * slot_words

@@ -475,9 +475,9 @@ cvr_status  cvr_unpack_tiles_device_n(cvr_ctx* ctx, const cvr_frame* frame,
                                       const void* d_gathered, int tiles_per_rank_max,
                                       int nframes, int frame_index, int format, void* d_rgba);
 
-/* Lossless per-tile code of RGBA16F screen tiles (round 5; not yet used by the
- * exchange -- DESIGN.md §7a: every world size is bound by rank 0's inbound bytes,
- * and a rendered tile's channels span few bits).  d_tiles: ntiles tiles of
+/* Lossless per-tile code of RGBA16F screen tiles (every world
+ * size was bound by rank 0's inbound bytes, and a rendered tile's channels span few
+ * bits; the exchange moves this code since round 6).  d_tiles: ntiles tiles of
  * tile x tile RGBA16F pixels, each row-major (the packed layout of a screen-tile
  * share).  The stream, 32-bit words: ntiles + 1 tile starts (the last = the
  * stream's end), then per tile 3 header words (four 16-bit channel bases, four
@@ -485,7 +485,11 @@ cvr_status  cvr_unpack_tiles_device_n(cvr_ctx* ctx, const cvr_frame* frame,
  * Every bit pattern round-trips.  cvr_tile_code_bound: the largest stream
  * (bytes) for these sizes (tile 16..64, a multiple of 16; 0 = invalid);
  * cvr_encode_tiles writes the stream and its length (bytes, a device u64) on
- * the context stream; cvr_decode_tiles restores the tiles. */
+ * the context stream; cvr_decode_tiles restores the tiles.  Option "encode_onepass"
+ * 1: cvr_encode_tiles runs the exchange's ONE-launch encode instead of three (each
+ * tile claims its words with an atomic, so the codes follow in claim order, not
+ * tile order; the start table says where each is, the length and the decode are
+ * the same).  The multi-rank exchange uses the code (option exchange_code). */
 size_t      cvr_tile_code_bound(int tile, int ntiles);
 cvr_status  cvr_encode_tiles(cvr_ctx* ctx, const void* d_tiles, int tile, int ntiles,
                              void* d_stream, unsigned long long* d_bytes);

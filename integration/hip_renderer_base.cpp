@@ -21,7 +21,18 @@ HipRendererBase::HipRendererBase (int hip_device)
   , m_gl_h(0)
   , m_dev_rgba16f(nullptr)
 {
-  if (cvr_create(hip_device, &m_cvr) != CVR_OK) m_cvr = nullptr;
+  // One GL thread drives the renderer (app_freeglut.cpp:125,174), so the node's GPUs
+  // are used from this process: with more than one visible device (and no device
+  // named) the context is a group over all of them (cvr_create_group), which splits
+  // every frame into screen tiles over the GPUs and gathers it on device 0.
+  int ndev = 0;
+  if (hip_device < 0 && hipGetDeviceCount(&ndev) == hipSuccess && ndev > 1) {
+    std::vector<int> devs((size_t)ndev);
+    for (int i = 0; i < ndev; i++) devs[(size_t)i] = i;
+    if (cvr_create_group(devs.data(), ndev, &m_cvr) != CVR_OK) m_cvr = nullptr;
+  } else if (cvr_create(hip_device < 0 ? 0 : hip_device, &m_cvr) != CVR_OK) {
+    m_cvr = nullptr;
+  }
 #ifdef MULTISAMPLE_AVAILABLE
   vr_pixel_multiscaling_support = true;        // as the GLSL renderers (rc1prenderer.cpp:27-29)
 #endif

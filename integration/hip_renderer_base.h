@@ -5,7 +5,9 @@
  * in cppvolrend/main.cpp:62-79 (see register_hip_renderers.cpp).
  *
  * HipRendererBase holds what every adapter shares:
- *   - the cvr context (one per renderer object, device 0 unless told otherwise);
+ *   - the cvr context (one per renderer object): every visible GPU by default -- a
+ *     group context (cvr_create_group) that splits each frame over the GPUs of this
+ *     process and gathers it on device 0 -- or the one device it is given;
  *   - the upload of the current structured volume (DataManager, datamanager.h:82-84;
  *     StructuredGridVolume::GetArrayData / m_data_storage_size, structuredgridvolume.h:67-76)
  *     and of the transfer function tables GenerateTexture_1D_RGBt / _RGBA build
@@ -41,7 +43,9 @@
 class HipRendererBase : public BaseVolumeRenderer
 {
 public:
-  explicit HipRendererBase (int hip_device = 0);
+  // hip_device >= 0: that GPU; -1 (default): every visible GPU (a cvr_create_group
+  // context when there are several, SURVEY.md §8b threading row)
+  explicit HipRendererBase (int hip_device = -1);
   virtual ~HipRendererBase ();
 
   vis::GRID_VOLUME_DATA_TYPE GetDataTypeSupport () override

@@ -189,3 +189,74 @@ def test_gpu_code_bad_arguments(dev):
     L = N.lib()
     assert L.cvr_encode_tiles(dev.handle, None, 16, 4, None, None) == N.CVR_ERR_ARG
     assert L.cvr_decode_tiles(dev.handle, None, 8, 4, None) == N.CVR_ERR_ARG
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["rendered16", "rendered32", "random", "constant", "empty"])
+def test_gpu_code_onepass(dev, bonsai_tf, kind):
+    """The exchange's one-launch encode (option encode_onepass): tiles claim
+    their words with an atomic, so codes follow in claim order, but the stream has the
+    same length as the three-launch form, every tile's code is the same words wherever
+    it lies, and cvr_decode_tiles restores the tiles bit for bit.  Twice in a row: the
+    launch leaves its counters zero for the next one."""
+    rng = np.random.default_rng(11)
+    tile = 32 if kind == "rendered32" else 16
+    npx = tile * tile
+    if kind.startswith("rendered"):
+        tiles = _rendered_tiles(dev, bonsai_tf, 200, 168, tile, 1, 3)
+    elif kind == "random":
+        tiles = rng.integers(0, 65536, (29, npx, 4)).astype(np.uint16)
+    elif kind == "constant":
+        tiles = np.broadcast_to(rng.integers(0, 65536, (29, 1, 4)), (29, npx, 4)).astype(np.uint16)
+    else:
+        tiles = np.zeros((0, npx, 4), np.uint16)
+    want = np_encode(tiles)
+    n = tiles.shape[0]
+    L = N.lib()
+    N.check(L.cvr_set_option(dev.handle, b"encode_onepass", 1), "opt", dev.handle)
+    try:
+        for _ in range(2):
+            stream, back, nbytes = _gpu_round_trip(dev, tiles, tile)
+            assert np.array_equal(back, tiles)
+            assert nbytes == want.nbytes and int(stream[n]) == len(want)
+            for t in range(n):          # tile t's code, wherever it was placed
+                s, s0 = int(stream[t]), int(want[t])
+                ln = int(want[t + 1]) - s0
+                assert np.array_equal(stream[s:s + ln], want[s0:s0 + ln]), t
+    finally:
+        N.check(L.cvr_set_option(dev.handle, b"encode_onepass", 0), "opt", dev.handle)
+
+
+@pytest.mark.gpu
+def test_gpu_code_onepass_concurrent_streams(dev, bonsai_tf):
+    """One-launch encodes on four streams at once: each keeps its counters in its own
+    stream's end word and length (an earlier form shared one counter pair per context,
+    so concurrent launches claimed each other's words and wrote past their streams)."""
+    import torch
+    tiles = _rendered_tiles(dev, bonsai_tf, 256, 256, 16, 0, 2)
+    n = tiles.shape[0]
+    want = np_encode(tiles)
+    L = N.lib()
+    d_tiles = torch.from_numpy(tiles.view(np.int16).copy()).cuda()
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    bound = L.cvr_tile_code_bound(16, n)
+    outs = [torch.zeros(bound // 4, dtype=torch.int32, device="cuda") for _ in streams]
+    lens = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in streams]
+    torch.cuda.synchronize()
+    N.check(L.cvr_set_option(dev.handle, b"encode_onepass", 1), "opt", dev.handle)
+    try:
+        for rep in range(8):
+            for s, o, ln in zip(streams, outs, lens):
+                dev.set_stream(s.cuda_stream)
+                N.check(L.cvr_encode_tiles(dev.handle, d_tiles.data_ptr(), 16, n, o.data_ptr(),
+                                           ln.data_ptr()), "encode", dev.handle)
+        torch.cuda.synchronize()
+    finally:
+        dev.set_stream(None)
+        N.check(L.cvr_set_option(dev.handle, b"encode_onepass", 0), "opt", dev.handle)
+    for o, ln in zip(outs, lens):
+        assert int(ln.item()) == want.nbytes
+        back = torch.zeros_like(d_tiles)
+        N.check(L.cvr_decode_tiles(dev.handle, o.data_ptr(), 16, n, back.data_ptr()), "decode", dev.handle)
+        torch.cuda.synchronize()
+        assert np.array_equal(back.cpu().numpy().view(np.uint16), tiles)

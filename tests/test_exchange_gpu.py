@@ -142,7 +142,7 @@ def test_local_exchange_equals_full_frames(bonsai_tf, name):
                         "cvr_gather_tiles_n", c.handle)
             g += 1
         cur = torch.cuda.current_stream(dev)
-        for r in order:
+        for r in range(world):           # rank 0 first: it posts the exchanges still trailing
             N.check(L_.cvr_set_stream(ctxs[r].handle, cur.cuda_stream), "stream", ctxs[r].handle)
             N.check(L_.cvr_gather_sync(ctxs[r].handle), "cvr_gather_sync", ctxs[r].handle)
         torch.cuda.synchronize()
@@ -317,8 +317,16 @@ def test_group_dos_ebs_iso_equal_one_context(bonsai_tf, bonsai_tf_rgba):
             assert np.array_equal(a[1], b[1]), name
             assert a[2] == b[2], name
             assert (a[0][..., 3] > 0).mean() > 0.2, name
-        sh = (ctypes.c_uint64 * 3)()
-        N.check(L_.cvr_read_shade_counters(devs[1].handle, sh), "shade", devs[1].handle)
+        # the group's shade counters are its members' sums: equal to one context's
+        shs = []
+        fr = make_frame(Camera(**INITIAL), W, H)
+        for d in devs:
+            N.check(L_.cvr_set_option(d.handle, b"shade_counters", 1), "opt", d.handle)
+            _render_host(d, "cvr_render_extbsd", fr, ebs_params(), N.FORMAT_RGBA32F, W, H)
+            sh = (ctypes.c_uint64 * 3)()
+            N.check(L_.cvr_read_shade_counters(d.handle, sh), "shade", d.handle)
+            shs.append(list(sh))
+        assert shs[0] == shs[1] and shs[0][0] > 0
         assert L_.cvr_device_bytes(devs[1].handle) > 3 * L_.cvr_device_bytes(devs[0].handle) // 2
     finally:
         for d in devs:
