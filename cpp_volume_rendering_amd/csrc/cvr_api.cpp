@@ -463,6 +463,12 @@ cvr_status cvr_set_option(cvr_ctx* ctx, const char* key, int value) {
     c->exchange_code = value;
     return CVR_OK;
   }
+  if (!std::strcmp(key, "native_exp")) {
+    // tolerance mode: NOT bit-exact with the oracle (DESIGN §5‴)
+    if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "native_exp must be 0 or 1");
+    c->native_exp = value;
+    return CVR_OK;
+  }
   if (!std::strcmp(key, "encode_onepass")) {
     if (value < 0 || value > 1) return fail(c, CVR_ERR_ARG, "encode_onepass must be 0 or 1");
     c->encode_onepass = value;
@@ -543,6 +549,7 @@ int cvr_get_option(const cvr_ctx* ctx, const char* key) {
   if (!std::strcmp(key, "exchange_code")) return c->exchange_code;
   if (!std::strcmp(key, "exchange_lag")) return c->exchange_lag;
   if (!std::strcmp(key, "encode_onepass")) return c->encode_onepass;
+  if (!std::strcmp(key, "native_exp")) return c->native_exp;
   if (!std::strcmp(key, "launch_interleave")) return c->launch_interleave;
   if (!std::strcmp(key, "sat_build_us")) return c->sat_build_us;   // read-only
   if (!std::strcmp(key, "order_interval")) return c->order_interval;
@@ -888,6 +895,7 @@ static void fill_frame_args(Ctx* c, const cvr_frame* f, float step, cvr::Rc1pass
   // Sample opacity: a TF lerp lies within [0, max alpha] up to an ulp, and h <= step.
   const double ext = (double)c->tf_max_alpha * (double)A.step * (1.0 + 1.0 / 1024.0);
   A.exp_fast = (ext >= 0.0 && ext <= 86.0) ? 1 : 0;
+  A.exp_native = c->native_exp;
   if (f->nranks <= 1) {
     A.packed = 0;
     ntiles = ((f->width + 7) / 8) * ((f->height + 7) / 8);

@@ -224,6 +224,14 @@ __device__ __forceinline__ f3 normalize3(f3 v) {
 
 
 
+// Tolerance mode only (option native_exp, NOT CVR-SPEC): the hardware exp2 of
+// x * log2(e), two instructions (v_mul, v_exp_f32) against the polynomial's ~14.
+// Its error against cvr_expf is ~|x| * 2^-24 relative; parity is then the
+// tolerance gate of SURVEY §8(c), not bit equality (tests/test_tolerance_gpu.py).
+__device__ __forceinline__ float cvr_expf_native(float x) {
+  return __builtin_amdgcn_exp2f(x * 1.44269504088896341f);
+}
+
 // cvr_expf for x in [-86, 0]: the same value without the range selects (the
 // host enables it only when every sample's -(alpha*h) is known to lie there).
 __device__ __forceinline__ float cvr_expf_neg(float x) {

@@ -59,6 +59,7 @@ struct Rc1passArgs {
   float step;
   int tf_n;
   int exp_fast;                      // 1: every -(alpha*h) lies in [-86, 0] (no exp range checks)
+  int exp_native;                    // tolerance mode (option native_exp): v_exp_f32, not CVR-SPEC
   // Blinn-Phong (ray_marching_1p.comp:48-81)
   float ka, kd, ks, shininess;
   float ispec[3];
@@ -384,6 +385,7 @@ struct Ctx {
                                    // launch-order entries interleaved (LaunchFrames::interleave)
   int gather_root_idle = 0;        // option "gather_root_idle": rank 0 only gathers (renders nothing)
   int exchange_code = 1;           // option "exchange_code": RGBA16F exchanges move the per-tile code
+  int native_exp = 0;               // option "native_exp": tolerance mode (v_exp_f32 in the EA composite)
   int encode_onepass = 0;          // option "encode_onepass": cvr_encode_tiles uses the exchange's
                                    // one-launch encode (tiles in claim order)
   int exchange_lag = -1;           // option "exchange_lag": data phase trails by this many exchanges

@@ -94,7 +94,14 @@ __device__ __forceinline__ bool skip_empty(const Rc1passArgs& A, const Ray& r, f
 //    every skipped h is the full step.
 // Both leave the image and the sample count bit for bit as the plain march.
 
-template <int K, bool PHONG, bool SKIP, bool XF, int BUF, int FB, int CS>
+// (A/B switch: -DCVR_NO_PAIR_EXP builds the scalar exp inside the composite)
+#ifdef CVR_NO_PAIR_EXP
+constexpr bool kNoPairExp = true;
+#else
+constexpr bool kNoPairExp = false;
+#endif
+
+template <int K, bool PHONG, bool SKIP, int XF, int BUF, int FB, int CS>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
                                           const uint4* __restrict__ grad,
                                           const float4* __restrict__ tfp, int px, int py,
@@ -244,6 +251,26 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       }
     }
     bool visible = false;
+    // The batch's alphas up front, two samples per packed exp (cvr_expf_neg2, the
+    // same bits as the composite's scalar cvr_expf_neg): a_j depends on sample j's
+    // extinction only, not on the composite before it.  Only when some lane of the
+    // wave has a sample to composite (empty space skips it, as the composite's
+    // branches do); the lanes and samples that do not composite discard theirs.
+    constexpr bool kPairExp = XF == 1 && kAlphaFirst && (K % 2 == 0) && !kNoPairExp;
+    float aj[K];
+    if (kPairExp) {
+      bool any = false;
+#pragma unroll
+      for (int j = 0; j < K; j++) any |= !done && vj[j] && !(CS > 0 && we[j]) && src[j].w > 0.0f;
+      if (__ballot(any) != 0) {
+#pragma unroll
+        for (int j = 0; j < K; j += 2) {
+          const f2v e = cvr_expf_neg2(f2v{-(src[j].w * hj[j]), -(src[j + 1].w * hj[j + 1])});
+          aj[j] = 1.0f - e.x;
+          aj[j + 1] = 1.0f - e.y;
+        }
+      }
+    }
 #ifdef CVR_PROBE_SHADE_PASSES   // cost probe (tools/phong_pass_probe.py): shading passes per batch
     bool shj[K];
     if (PHONG) {
@@ -286,7 +313,8 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
 #endif
             }
             const float x = -(sc.w * hj[j]);
-            const float a = 1.0f - (XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
+            const float a = kPairExp ? aj[j]
+                                     : 1.0f - (XF == 2 ? cvr_expf_native(x) : XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
             const float om = 1.0f - dst.w;
             dst.x = fmaf(om, sc.x * a, dst.x);
             dst.y = fmaf(om, sc.y * a, dst.y);
@@ -385,7 +413,7 @@ __device__ __forceinline__ void quad_composite(const QSample& q, bool valid, boo
 // reference skipping it (:142).  One memory round trip advances a ray 4K
 // samples instead of K: the longest tiles' critical path shrinks ~4x.
 // Must be called by all 64 lanes (DPP reads neighbours); `active` = lane's ray is live.
-template <int K, bool PHONG, bool XF>
+template <int K, bool PHONG, int XF>
 __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
                                                const uint4* __restrict__ cells,
                                                const uint4* __restrict__ grad,
@@ -437,7 +465,7 @@ __device__ __forceinline__ void march_ray_quad(const Rc1passArgs& A,
       if (vj && sc.w > 0.0f) {
         if (PHONG) shade_phong(A, grad, sp[k], r.dir, tj[k], r.tpos, hg, eye, sc);
         const float x = -(sc.w * hj[k]);
-        const float a = 1.0f - (XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
+        const float a = 1.0f - (XF == 2 ? cvr_expf_native(x) : XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
         q[k] = QSample{a, sc.x * a, sc.y * a, sc.z * a};
       }
       qv[k] = (unsigned)(__ballot(vj) >> qshift) & 0xfu;
@@ -496,7 +524,7 @@ constexpr int rc1_waves_per_eu() {
 template <bool QUAD>
 constexpr int rc1_waves_per_group() { return QUAD ? 1 : CVR_RC1_WPG; }
 
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB, int CS>
+template <int K, bool PHONG, bool SKIP, bool QUAD, int XF, int BUF, int FB, int CS>
 __global__ void __launch_bounds__(64 * rc1_waves_per_group<QUAD>())
 __attribute__((amdgpu_waves_per_eu(rc1_waves_per_eu<K, PHONG, SKIP, QUAD>())))
 rc1pass_tile_kernel(Rc1passArgs A0, const uint4* __restrict__ cells,
@@ -878,9 +906,10 @@ __global__ void clear_u32_kernel(uint32_t* __restrict__ p, int n) {
 // ---------------------------------------------------------------------------
 
 // Kernel variant: K (batch), PHONG, SKIP (empty-space skipping compiled in),
-// QUAD (quad path compiled in), XF (range-free exp).  Paths a frame does not
+// QUAD (quad path compiled in), XF (exp: 0 CVR-SPEC, 1 CVR-SPEC without range
+// selects, 2 the native v_exp_f32 -- tolerance mode, option native_exp).  Paths a frame does not
 // use are compiled out: they would cost the hot loop registers (occupancy).
-template <int K, bool PHONG, bool SKIP, bool QUAD, bool XF, int BUF, int FB = 0, int CS = 0>
+template <int K, bool PHONG, bool SKIP, bool QUAD, int XF, int BUF, int FB = 0, int CS = 0>
 static hipError_t launch_variant(const Ctx& c, const Rc1passArgs& a, float4* out, uint32_t* samples,
                                  unsigned long long* tile_samples, const int* order,
                                  uint32_t* tile_cost, const RenderPlan& plan, hipStream_t s) {
@@ -938,6 +967,10 @@ static hipError_t launch_kps(const Ctx& c, const Rc1passArgs& a, float4* out, ui
                         : launch_variant<K, PHONG, false, false, false, 1, 0, CSV>(c, a, out, samples, ts, order, tile_cost, plan, s); \
     return a.exp_fast ? launch_variant<K, PHONG, false, false, true, 0, 0, CSV>(c, a, out, samples, ts, order, tile_cost, plan, s) \
                       : launch_variant<K, PHONG, false, false, false, 0, 0, CSV>(c, a, out, samples, ts, order, tile_cost, plan, s);
+    // tolerance mode (option native_exp): the headline's variants only (buffer
+    // addressing, exact weights, cell skip 3, either shading) -- DESIGN §5‴
+    if (a.exp_native && buf == 2 && a.cell_skip == 3)
+      return launch_variant<K, PHONG, false, false, 2, 2, 0, 3>(c, a, out, samples, ts, order, tile_cost, plan, s);
     if (a.cell_skip == 1) { CVR_CS_LAUNCH(1) }
     if (a.cell_skip == 3) { CVR_CS_LAUNCH(3) }
     if (a.cell_skip == 4) { CVR_CS_LAUNCH(4) }

@@ -319,6 +319,12 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                1/2): 1 (default) = the launch deals entry e of every frame's XCD
  *                bands before entry e + 1 of any (the longest tiles of all frames
  *                first); 0 = frame after frame.  Images identical either way.
+ *   "native_exp" 1: TOLERANCE MODE, not bit-exact: the emission-absorption march
+ *                (cvr_render_rc1pass[_frames] with cell_skip 3, buffer addressing)
+ *                takes alpha = 1 - exp through the hardware v_exp_f32 instead of the
+ *                CVR-SPEC polynomial; parity is SURVEY §8(c)'s gate (|dRGBA| <= 2e-3 for
+ *                99.9 % of pixels, max 2e-2, SSIM >= 0.99), measured in DESIGN §5‴.
+ *                Default 0.
  * One option changes the arithmetic (and so the image) rather than the speed:
  *   "filter_bits" 0: exact float GL_LINEAR weights (CVR-SPEC, the default);
  *                8: every GL_LINEAR weight (volume, gradient, TF; ray_marching_1p.comp:133,
