@@ -94,12 +94,22 @@ __device__ __forceinline__ bool skip_empty(const Rc1passArgs& A, const Ray& r, f
 //    every skipped h is the full step.
 // Both leave the image and the sample count bit for bit as the plain march.
 
-// (A/B switch: -DCVR_NO_PAIR_EXP builds the scalar exp inside the composite)
-#ifdef CVR_NO_PAIR_EXP
-constexpr bool kNoPairExp = true;
-#else
+// The composite's exp two samples per packed instruction (-DCVR_PAIR_EXP; DESIGN
+// §5‴): bit-exact and 45.7 -> 38.7 VALU per sample on the headline, but 4.7 %
+// slower (0.0731 -> 0.0765 ms per frame, A/B in one session, profiles/r06/s12-s13):
+// the march waits on dependencies, not on VALU issue.  Off by default.
+#ifdef CVR_PAIR_EXP
 constexpr bool kNoPairExp = false;
+#else
+constexpr bool kNoPairExp = true;
 #endif
+#ifndef CVR_PAIR_FROM
+#define CVR_PAIR_FROM 2
+#endif
+#ifndef CVR_RECOMPUTE_TF
+#define CVR_RECOMPUTE_TF 1
+#endif
+constexpr bool kRecomputeTf = CVR_RECOMPUTE_TF != 0;
 
 template <int K, bool PHONG, bool SKIP, int XF, int BUF, int FB, int CS>
 __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __restrict__ cells,
@@ -219,6 +229,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
     // 16-B reads) only for visible samples, ~1 in 5 on the headline frame
     int tfi[K];
     float tfa[K];
+    float txd[K];   // kPairExp: the TF coordinate, its index and weight recomputed at the rgb lerps
     // we[j], wave-uniform: sample j of every marching lane lies in an empty cell.
     // Each is tested right before its sample's math, so the loads of the later
     // samples stay in flight behind it (testing all four first waited for all).
@@ -233,11 +244,12 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
         we[j] = CS > 0 && __ballot(!cell_empty(raw[j])) == 0;
         if (CS >= 2 && j == K - 1) qlast = cell_empty(raw[j]) ? cell_skip_q(raw[j]) : 0;
         if (CS > 0 && we[j]) {
-          tfa[j] = 0.0f; tfi[j] = 0; src[j].w = 0.0f;
+          tfa[j] = 0.0f; tfi[j] = 0; txd[j] = 0.0f; src[j].w = 0.0f;
         } else {
           const float xd = fmaf(trilerp_cell<!PHONG>(raw[j], sp[j].ax, sp[j].ay, sp[j].az), fn, -0.5f);
           tfa[j] = filter_weight<FB>(__builtin_amdgcn_fractf(xd));   // see classify
           tfi[j] = cvt_flr(xd) + 1;
+          txd[j] = xd;
           src[j].w = lerpf(tfp[tfi[j]].w, tfp[tfi[j] + 1].w, tfa[j]);
         }
       }
@@ -251,26 +263,18 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
       }
     }
     bool visible = false;
-    // The batch's alphas up front, two samples per packed exp (cvr_expf_neg2, the
-    // same bits as the composite's scalar cvr_expf_neg): a_j depends on sample j's
-    // extinction only, not on the composite before it.  Only when some lane of the
-    // wave has a sample to composite (empty space skips it, as the composite's
-    // branches do); the lanes and samples that do not composite discard theirs.
+    // Alphas two samples per packed exp (cvr_expf_neg2, the same bits as the scalar
+    // cvr_expf_neg): a_j depends on sample j's extinction only, not on the
+    // composite before it, so at each even j the pair (j, j+1) is computed when some
+    // lane of the wave may composite either of them (empty space skips it, as the
+    // composite's branches do).  Computed at the pair rather than for the whole
+    // batch up front, which held four more registers across the composite and
+    // spilled (13 VGPRs, 0.073 -> 0.080 ms per frame).
     constexpr bool kPairExp = XF == 1 && kAlphaFirst && (K % 2 == 0) && !kNoPairExp;
-    float aj[K];
-    if (kPairExp) {
-      bool any = false;
-#pragma unroll
-      for (int j = 0; j < K; j++) any |= !done && vj[j] && !(CS > 0 && we[j]) && src[j].w > 0.0f;
-      if (__ballot(any) != 0) {
-#pragma unroll
-        for (int j = 0; j < K; j += 2) {
-          const f2v e = cvr_expf_neg2(f2v{-(src[j].w * hj[j]), -(src[j + 1].w * hj[j + 1])});
-          aj[j] = 1.0f - e.x;
-          aj[j + 1] = 1.0f - e.y;
-        }
-      }
-    }
+    float a_odd = 0.0f;   // the pair's second alpha, used by the next sample
+    // the samples from kPairFrom on go in pairs (the first ones keep the scalar exp:
+    // at j = 0 the batch's registers peak)
+    constexpr int kPairFrom = CVR_PAIR_FROM;
 #ifdef CVR_PROBE_SHADE_PASSES   // cost probe (tools/phong_pass_probe.py): shading passes per batch
     bool shj[K];
     if (PHONG) {
@@ -291,6 +295,16 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
     // 1.4x slower on the headline frame).
 #pragma unroll
     for (int j = 0; j < K; j++) {
+      float a_even = 0.0f;
+      if (kPairExp && j >= kPairFrom && ((j - kPairFrom) & 1) == 0) {
+        const bool may = !done && ((vj[j] && !(CS > 0 && we[j]) && src[j].w > 0.0f) ||
+                                   (vj[j + 1] && !(CS > 0 && we[j + 1]) && src[j + 1].w > 0.0f));
+        if (__ballot(may) != 0) {
+          const f2v e = cvr_expf_neg2(f2v{-(src[j].w * hj[j]), -(src[j + 1].w * hj[j + 1])});
+          a_even = 1.0f - e.x;
+          a_odd = 1.0f - e.y;
+        }
+      }
       if (!done) {
         if (!vj[j]) {
           done = true;
@@ -300,10 +314,14 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
           if (!(CS > 0 && we[j]) && sc.w > 0.0f) {
             visible = true;
             if (kAlphaFirst) {   // classify's rgb, same lerps
-              const float4 t0 = tfp[tfi[j]], t1 = tfp[tfi[j] + 1];
-              sc.x = lerpf(t0.x, t1.x, tfa[j]);
-              sc.y = lerpf(t0.y, t1.y, tfa[j]);
-              sc.z = lerpf(t0.z, t1.z, tfa[j]);
+              // (kPairExp: index and weight again from the coordinate -- two VALU per
+              // visible sample for two registers fewer per batch sample across the composite)
+              const int ti = kPairExp && kRecomputeTf ? cvt_flr(txd[j]) + 1 : tfi[j];
+              const float ta = kPairExp && kRecomputeTf ? filter_weight<FB>(__builtin_amdgcn_fractf(txd[j])) : tfa[j];
+              const float4 t0 = tfp[ti], t1 = tfp[ti + 1];
+              sc.x = lerpf(t0.x, t1.x, ta);
+              sc.y = lerpf(t0.y, t1.y, ta);
+              sc.z = lerpf(t0.z, t1.z, ta);
             }
             if (PHONG) {
               shade_phong(A, grad, sp[j], r.dir, tj[j], r.tpos, hg, eye, sc);
@@ -313,7 +331,7 @@ __device__ __forceinline__ void march_ray(const Rc1passArgs& A, const uint4* __r
 #endif
             }
             const float x = -(sc.w * hj[j]);
-            const float a = kPairExp ? aj[j]
+            const float a = (kPairExp && j >= kPairFrom) ? (((j - kPairFrom) & 1) ? a_odd : a_even)
                                      : 1.0f - (XF == 2 ? cvr_expf_native(x) : XF ? cvr_expf_neg(x) : cvr_expf_nb(x));
             const float om = 1.0f - dst.w;
             dst.x = fmaf(om, sc.x * a, dst.x);
