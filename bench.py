@@ -419,7 +419,10 @@ def cpu_baseline(vol, scale, tf, cam, W, H, seconds, dos=None, ebs=None, gpu_rgb
             "kind": "port",
             "sample": f"{rows} image rows ({rows / H:.1f} frames, centre band outward) of the "
                       f"same {W}x{H} frame, {S} samples in {dt:.1f} s on {threads} threads; "
-                      f"C++/OpenMP oracle (no CPU ray-caster exists in the reference)"
+                      f"C++/OpenMP oracle (no CPU ray-caster exists in the reference), built "
+                      f"g++ -O2 -march=x86-64-v3 -ffp-contract=off (oracle/Makefile; not BASELINE.md's "
+                      f"-O3 -march=native: GCC -O3 vectorisation drops a float narrowing the "
+                      f"CVR-SPEC table build needs)"
                       + ("; extinction pyramid built outside the timed sample" if dos else "")
                       + ("; shading only, on the GPU-built SAT (bit-identical to the oracle's, "
                          "tests/test_ebs_gpu.py)" if ebs else ""),
