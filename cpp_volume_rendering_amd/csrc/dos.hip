@@ -454,7 +454,7 @@ __device__ __forceinline__ void cone_stage(const DosArgs& Q, const DosCone& C,
 // visibility exp(-sum) of a cone from `pos` along k, split 1 -> 3 -> 7 rays.
 // Every lane walks the same section table (wave-uniform loads and levels).
 template <int FB>
-__device__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __restrict__ ext,
+__device__ __forceinline__ float cone_trace(const DosArgs& Q, const DosCone& C, const uint4* __restrict__ ext,
                             f3 pos, f3 k, f3 u, f3 v, uint32_t& nf) {
   float rays[7], last[7];
   float track = C.initial_step;
@@ -523,7 +523,10 @@ struct DosShaderT {
   // Shaded colour of one job; `lit` counts the shadow cones traced, `fetches`
   // the extinction taps actually fetched (Q.count_taps; taps whose border factor
   // is exactly 0 are skipped and not counted).
-  __device__ static f3 shade(const DosArgs& Q, const uint4* __restrict__ ext, f3 tx, f3 wp,
+  // Forced inline: as a call (the inliner's choice for filter_bits 8, or after small
+  // changes to the taps) the kernel-argument block Q is copied to scratch, ~1.9 KB
+  // per lane, and the frame runs ~7x slower (72 -> 11 ms)
+  __device__ static __forceinline__ f3 shade(const DosArgs& Q, const uint4* __restrict__ ext, f3 tx, f3 wp,
                              f3 cam, f3 rgb, const f3* g, uint32_t& lit, uint32_t& fetches) {
     const Rc1passArgs& A = Q.a;
     const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
