@@ -520,26 +520,41 @@ struct DosShaderT {
   static constexpr int kFlatWavesPerEU = CVR_DOS_FLAT_WAVES;   // flat_shade_kernel
   using Data = const uint4*;   // the cell8 extinction pyramid
 
-  // Shaded colour of one job; `lit` counts the shadow cones traced, `fetches`
-  // the extinction taps actually fetched (Q.count_taps; taps whose border factor
-  // is exactly 0 are skipped and not counted).
-  // Forced inline: as a call (the inliner's choice for filter_bits 8, or after small
-  // changes to the taps) the kernel-argument block Q is copied to scratch, ~1.9 KB
-  // per lane, and the frame runs ~7x slower (72 -> 11 ms, DESIGN §6)
-  __device__ static __forceinline__ f3 shade(const DosArgs& Q, const uint4* __restrict__ ext, f3 tx, f3 wp,
-                             f3 cam, f3 rgb, const f3* g, uint32_t& lit, uint32_t& fetches) {
+  // The two halves of ShadeSample (:607-656), so that flat shading keeps only the
+  // job's position live across the cone traces (its colour, opacity and gradient
+  // are read back from the job list afterwards, shaded_march.h flat_shade_kernel):
+  //   visibility: the occlusion and shadow cones' transmittances (iocc, isdw);
+  //     `lit` counts the shadow cones traced, `fetches` the extinction taps
+  //     actually fetched (Q.count_taps; taps whose border factor is exactly 0
+  //     are skipped and not counted);
+  //   combine: the shaded colour from them.
+  // shade = combine(visibility), the per-wave kernel's single call.
+  static constexpr bool kSplit = true;
+  struct Vis {
+    float iocc, isdw;
+  };
+  // wp = tx - half_grid, recomputed from an opaque copy of tx where needed so that
+  // the compiler does not keep it live across a cone trace (96-VGPR budget)
+  __device__ static __forceinline__ f3 world_pos(const DosArgs& Q, f3 tx) {
+    asm volatile("" : "+v"(tx.x), "+v"(tx.y), "+v"(tx.z));
     const Rc1passArgs& A = Q.a;
-    const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
-    const f3 light{A.light[0], A.light[1], A.light[2]};
-    float iocc = 0.0f, isdw = 0.0f;
+    return f3{tx.x - A.half_grid[0], tx.y - A.half_grid[1], tx.z - A.half_grid[2]};
+  }
+  __device__ static __forceinline__ Vis visibility(const DosArgs& Q, const uint4* __restrict__ ext, f3 tx,
+                                                   f3 wp, f3 cam, uint32_t& lit, uint32_t& fetches) {
+    const Rc1passArgs& A = Q.a;
+    Vis r{0.0f, 0.0f};
     if (Q.apply_occlusion) {
+      const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
       // eye-space frame of the occlusion cones (:681-684)
       const f3 v_right = normalize3(cross3(cam, f3{0.0f, 1.0f, 0.0f}));
       const f3 v_up = normalize3(cross3(f3{-cam.x, -cam.y, -cam.z}, v_right));
       const f3 k = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
-      iocc = cone_trace<FB>(Q, Q.occ, ext, tx, k, v_up, v_right, fetches);
+      r.iocc = cone_trace<FB>(Q, Q.occ, ext, tx, k, v_up, v_right, fetches);
+      wp = world_pos(Q, tx);
     }
     if (Q.apply_shadow) {
+      const f3 light{A.light[0], A.light[1], A.light[2]};
       f3 k, u, v;
       bool on = true;
       const f3 lf{Q.lfwd[0], Q.lfwd[1], Q.lfwd[2]};
@@ -555,29 +570,43 @@ struct DosShaderT {
       }
       // Cone1RayShadow(pos, k, v, u) is called as (pos, k, u, v): swapped (:559-561)
       if (on) {
-        isdw = cone_trace<FB>(Q, Q.sdw, ext, tx, k, v, u, fetches);
+        r.isdw = cone_trace<FB>(Q, Q.sdw, ext, tx, k, v, u, fetches);
         lit++;
       }
     }
+    return r;
+  }
+  __device__ static __forceinline__ f3 combine(const DosArgs& Q, Vis r, f3 wp, f3 rgb, const f3* g) {
+    const Rc1passArgs& A = Q.a;
     const float inv_k = 1.0f / (Q.ka + Q.kd);
     if (g) {   // ApplyPhongShading
       if (g->x != 0.0f || g->y != 0.0f || g->z != 0.0f) {
+        const f3 eye{A.eye[0], A.eye[1], A.eye[2]};
+        const f3 light{A.light[0], A.light[1], A.light[2]};
         const f3 nrm = normalize3(*g);
         const f3 L = normalize3(f3{light.x - wp.x, light.y - wp.y, light.z - wp.z});
         const f3 Ve = normalize3(f3{eye.x - wp.x, eye.y - wp.y, eye.z - wp.z});
         const f3 Hv = normalize3(f3{Ve.x + L.x, Ve.y + L.y, Ve.z + L.z});
         const float dd = fmaxf(0.0f, dot3(nrm, L));
         const float ds = fmaxf(0.0f, dot3(Hv, nrm));
-        const float diff = inv_k * (iocc * Q.ka + (isdw * Q.kd) * dd);
-        const float spec = (isdw * Q.ks) * cvr_powf_nb(ds, A.shininess);
+        const float diff = inv_k * (r.iocc * Q.ka + (r.isdw * Q.kd) * dd);
+        const float spec = (r.isdw * Q.ks) * cvr_powf_nb(ds, A.shininess);
         return f3{fmaf(A.ispec[0], spec, rgb.x * diff), fmaf(A.ispec[1], spec, rgb.y * diff),
                   fmaf(A.ispec[2], spec, rgb.z * diff)};
       }
       return rgb;
     }
-    return f3{inv_k * ((rgb.x * iocc) * Q.ka + (rgb.x * isdw) * Q.kd),
-              inv_k * ((rgb.y * iocc) * Q.ka + (rgb.y * isdw) * Q.kd),
-              inv_k * ((rgb.z * iocc) * Q.ka + (rgb.z * isdw) * Q.kd)};
+    return f3{inv_k * ((rgb.x * r.iocc) * Q.ka + (rgb.x * r.isdw) * Q.kd),
+              inv_k * ((rgb.y * r.iocc) * Q.ka + (rgb.y * r.isdw) * Q.kd),
+              inv_k * ((rgb.z * r.iocc) * Q.ka + (rgb.z * r.isdw) * Q.kd)};
+  }
+  // Forced inline: as a call (the inliner's choice for filter_bits 8, or after small
+  // changes to the taps) the kernel-argument block Q is copied to scratch, ~1.9 KB
+  // per lane, and the frame runs ~7x slower (72 -> 11 ms, DESIGN §5b)
+  __device__ static __forceinline__ f3 shade(const DosArgs& Q, const uint4* __restrict__ ext, f3 tx, f3 wp,
+                                             f3 cam, f3 rgb, const f3* g, uint32_t& lit, uint32_t& fetches) {
+    const Vis r = visibility(Q, ext, tx, wp, cam, lit, fetches);
+    return combine(Q, r, wp, rgb, g);
   }
 };
 

@@ -413,6 +413,7 @@ struct EbsShaderT {
   using Args = EbsArgs;
   static constexpr int kMinWavesPerEU = CVR_EBS_WAVES;   // register budget (1: compiler's choice)
   static constexpr int kFlatWavesPerEU = CVR_EBS_FLAT_WAVES;   // flat_shade_kernel
+  static constexpr bool kSplit = false;   // flat_shade_kernel calls shade() whole
   using Data = typename LY::Ptr;   // the float SAT, cell4 or plain
   static constexpr int kFB = LY::kFB;   // GL_LINEAR weights of every fetch (filter_bits)
 

@@ -369,7 +369,31 @@ flat_shade_kernel(typename SH::Args Q, typename SH::Data data, FlatJobs J, int n
   const int lane = threadIdx.x;
   const unsigned long long i = (unsigned long long)chunk * 64 + lane;
   uint32_t nlit = 0, nfetch = 0;
-  if (i < total) {
+  if constexpr (SH::kSplit) {
+    if (i < total) {
+      // Only the position (and the pixel slot, for the camera ray) is live across
+      // the cone traces; opacity, colour and gradient are read after them, and the
+      // job index is rebuilt from the block (the shader's visibility / combine
+      // halves: 32 B of spills per lane at the 96-VGPR budget instead of 72)
+      const float* jf = (const float*)(J.jobs + i * (PHONG ? 3 : 2));
+      const f3 tx{jf[0], jf[1], jf[2]};
+      const float4 cm = J.cam[__float_as_int(jf[7])];
+      const typename SH::Vis vis =
+          SH::visibility(Q, data, tx, SH::world_pos(Q, tx), f3{cm.x, cm.y, cm.z}, nlit, nfetch);
+      // (the lane from mbcnt, which the compiler does not equate with the thread
+      // index: the first index and address are not kept live or spilled)
+      const unsigned long long i2 =
+          (unsigned long long)chunk * 64 + __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      const float* jf2 = (const float*)(J.jobs + i2 * (PHONG ? 3 : 2));
+      f3 g;
+      if (PHONG) g = f3{jf2[8], jf2[9], jf2[10]};
+      const f3 tx2{jf2[0], jf2[1], jf2[2]};
+      const f3 c = SH::combine(Q, vis, SH::world_pos(Q, tx2), f3{jf2[4], jf2[5], jf2[6]},
+                               PHONG ? &g : nullptr);
+      const float a = jf2[3];
+      J.res[i2] = make_float4(c.x * a, c.y * a, c.z * a, a);
+    }
+  } else if (i < total) {
     const float4* jp = J.jobs + i * (PHONG ? 3 : 2);
     const float4 q0 = jp[0], q1 = jp[1];
     const f3 tx{q0.x, q0.y, q0.z};
