@@ -1,4 +1,4 @@
-# round 6, session s24: checkpoint of the current library: full GPU suite, smoke, bench, kernel trace
+# round 6, session s25: PMC records of the current library (all five workloads)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-bash tools/gpu_round.sh all
+bash tools/pmc_session.sh rc1pass phong longray dos ebs
