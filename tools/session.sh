@@ -1,13 +1,17 @@
-# round 6, session s28: final bench lines of lib a3ef5d07 (PMC records installed): every workload
+# round 6, session s29: several launch-order slots per one-wave workgroup (CVR_RC1_TPW 2 / 4) vs 1
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06_s28; mkdir -p $O
-run() { n=$1; shift; timeout -k 10 300 python3 bench.py "$@" > $O/$n.json 2>$O/$n.err || { tail -5 $O/$n.err; exit 1; }
-  python3 -c "import json; d=json.loads(open('$O/$n.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$n', d['ms_per_step'], d['value'], r.get('bound'), r.get('frac'), r.get('traffic'))"; }
-run driver --gpus 1 --steps 20 --warmup 5
-run driver200 --no-cpu-baseline --no-cadence --steps 200 --warmup 10
-run orbit --no-cpu-baseline --no-cadence --orbit --steps 200 --warmup 10
-run phong --no-cpu-baseline --no-cadence --phong --steps 100 --warmup 10
-run longray --no-cpu-baseline --no-cadence --tf-alpha 0.02 --steps 40 --warmup 4
-run dos --renderer dos --steps 10 --warmup 2
-run ebs --renderer ebs --steps 4 --warmup 1
+O=gpurun_out/r06_s29; mkdir -p $O
+export CVR_LIB_OVERRIDE=ablib/t2/libcvr.so
+timeout -k 10 400 python -u -m pytest tests/test_rc1pass_gpu.py tests/test_frames_gpu.py tests/test_split_gpu.py -x -q -rf --timeout 200 --timeout-method thread > $O/pytest_t2.log 2>&1 || { tail -20 $O/pytest_t2.log; exit 1; }
+tail -1 $O/pytest_t2.log
+for rep in 1 2; do
+  for lib in cur t2 t4; do
+    if [ $lib = cur ]; then unset CVR_LIB_OVERRIDE; else export CVR_LIB_OVERRIDE=ablib/$lib/libcvr.so; fi
+    for mode in static orbit; do
+      X=""; [ $mode = orbit ] && X="--orbit"
+      timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 200 --warmup 10 $X > $O/${mode}_${lib}_r$rep.json 2>$O/${mode}_${lib}_r$rep.err || exit 1
+      python3 -c "import json; d=json.loads(open('$O/${mode}_${lib}_r$rep.json').read().strip().splitlines()[-1]); pc=d.get('plugin_cadence') or {}; print('$mode $lib', d['ms_per_step'], d['value'], (pc.get('static') or {}).get('ms_per_frame'), (pc.get('orbit') or {}).get('ms_per_frame'))"
+    done
+  done
+done
