@@ -183,6 +183,8 @@ cvr_status group_render(Ctx* g, const cvr_frame* frames, int nf, const cvr_outpu
     if (j > 0 && outs[j].total)
       return gfail(g, CVR_ERR_ARG, "group render: only output 0 may carry a total");
   }
+  if (nf > 1 && !o0.on_device)
+    return gfail(g, CVR_ERR_ARG, "group render: several frames need device outputs");
   const bool half = o0.format == CVR_FORMAT_RGBA16F;
   const size_t px = half ? 8 : 16;
   const int T = 16;
@@ -230,7 +232,7 @@ cvr_status group_render(Ctx* g, const cvr_frame* frames, int nf, const cvr_outpu
     if (o0.on_device) {
       images[j] = outs[j].rgba;
       smp_dst[j] = static_cast<uint32_t*>(outs[j].samples);
-    } else {   // host outputs: one frame (nf = 1 is checked by the member render)
+    } else {   // host outputs: one frame (checked above)
       images[j] = G->stage;
       smp_dst[j] = outs[j].samples ? reinterpret_cast<uint32_t*>(static_cast<char*>(G->stage) + npx_img * px)
                                    : nullptr;
@@ -368,9 +370,9 @@ cvr_status cvr_create_group(const int* devices, int n, cvr_ctx** out_ctx) {
       return st;
     }
     G->members.push_back(reinterpret_cast<Ctx*>(m));
+    G->mb.emplace_back();   // (kept the same length as members: a failed creation releases both)
     hs.push_back(m);
   }
-  G->mb.resize((size_t)n);
   // members on other devices write nothing remote, but the exchange's device copies
   // and the counts' gathers use the xGMI path directly when peer access is on
   for (int i = 0; i < n; i++)

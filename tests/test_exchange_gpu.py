@@ -278,6 +278,31 @@ def test_group_frames_device_outputs(bonsai_tf):
         one.close()
 
 
+def test_group_errors(bonsai_tf):
+    """A member that cannot be created (device 99) fails the group's creation
+    cleanly, releasing the members made so far; several frames with host outputs
+    are refused (a multi-frame launch writes device buffers, as for one context)."""
+    L = N.lib()
+    h = ctypes.c_void_p()
+    devs = (ctypes.c_int * 3)(0, 0, 99)
+    assert L.cvr_create_group(devs, 3, ctypes.byref(h)) != N.CVR_OK
+    assert not h.value
+    vol, scale = D.marschner_lobb_u8(32), D.voxel_scale(32)
+    grp = Device(devices=[0, 0])
+    try:
+        grp.set_volume(vol, scale)
+        grp.set_transfer_function(bonsai_tf)
+        W, H = 64, 48
+        imgs = [np.zeros((H, W, 4), np.float32) for _ in range(2)]
+        fa = (N.Frame * 2)(*[make_frame(Camera(**c), W, H) for c in CAMS[:2]])
+        oa = (N.Output * 2)(*[N.Output(im.ctypes.data, None, None, 0, N.FORMAT_RGBA32F) for im in imgs])
+        st = L.cvr_render_rc1pass_frames(grp.handle, fa, 2, ctypes.byref(_params()), oa)
+        assert st == N.CVR_ERR_ARG
+        assert b"device outputs" in N.lib().cvr_last_error(grp.handle)
+    finally:
+        grp.close()
+
+
 def test_group_dos_ebs_iso_equal_one_context(bonsai_tf, bonsai_tf_rgba):
     """The shaded renderers and the isosurface renderer on a group of 3 equal one
     context (DOS with AO + point-light shadow, EBS defaults, iso variant 0)."""
