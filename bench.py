@@ -709,24 +709,35 @@ def main():
                                      frames_per_launch=FPL, buffer_sets=SD["buffer_sets"],
                                      root_renders=root, code=bool(a.exchange_code))
         split = make_split(root_renders)
-        if world > 1 and not root_renders:
-            # pre-flight: one frame through the idle-root exchange must equal rank 0's
-            # own render of the whole frame, else the bench falls back to a rendering root
-            split.render(cam)
+
+        def preflight(sp):
+            # one frame through the exchange must equal rank 0's own render of the
+            # whole frame (the N > 1 paths have not run on hardware before the
+            # driver's multi-GPU run)
+            sp.render(cam)
             ok = torch.ones((1,), dtype=torch.int32, device=dev)
             if rank == 0:
-                full = torch.zeros_like(split.image)
+                full = torch.zeros_like(sp.image)
                 r.render_to(make_frame(cam, W, H), N.Output(full.data_ptr(), None, None, 1, fmt))
                 torch.cuda.synchronize(dev)
                 view = torch.int16 if fmt else torch.int32
-                ok[0] = int(torch.equal(full.view(view), split.image.view(view)))
+                ok[0] = int(torch.equal(full.view(view), sp.image.view(view)))
             dist.broadcast(ok, src=0)
-            if not int(ok.item()):
-                print(f"rank {rank}: the idle-root exchange did not reproduce the frame; "
-                      f"rank 0 renders its share instead", file=sys.stderr)
+            return bool(int(ok.item()))
+
+        if world > 1 and a.transport == "rccl":
+            # fall back one step at a time: a rendering root, then raw tiles
+            while not preflight(split):
+                if not root_renders:
+                    what, instead, root_renders = "the idle-root exchange", "a rendering root", True
+                elif a.exchange_code:
+                    what, instead, a.exchange_code = "the coded exchange", "raw tiles", 0
+                else:
+                    raise RuntimeError("the multi-GPU exchange does not reproduce the frame")
+                print(f"rank {rank}: {what} did not reproduce the frame; using {instead}",
+                      file=sys.stderr)
                 split.close()
-                root_renders = True
-                split = make_split(True)
+                split = make_split(root_renders)
     except T.CommUnavailable as e:     # no native communicator: torch's dist.gather instead
         # (only cvr_comm_init failures land here: an option the library rejects is a
         # configuration error and ends the bench)
@@ -1099,9 +1110,15 @@ def main():
         }
         res["frame_latency_ms_approx"] = round(kern_ms, 4)
         if world > 1:
-            res["config"]["gather"] = (f"{a.transport}: packed {a.format} tiles to rank 0 "
-                                       f"({split.G} frame(s) per ncclGather) + unpack of every "
-                                       f"frame, {split.nstreams} render streams, {split.nbuf} "
+            coded = a.transport == "rccl" and a.exchange_code and a.format == "rgba16f"
+            res["config"]["gather"] = ((f"{a.transport}: per-tile code of each rank's {a.format} tiles "
+                                        f"({split.G} frame(s) per exchange: one encode launch, sizes "
+                                        f"first, grouped ncclSend/ncclRecv, one decode launch into "
+                                        f"the images on rank 0), " if coded else
+                                        f"{a.transport}: packed {a.format} tiles to rank 0 "
+                                        f"({split.G} frame(s) per ncclGather) + unpack of every "
+                                        f"frame, ")
+                                       + f"{split.nstreams} render streams, {split.nbuf} "
                                        f"buffer sets, "
                                        + ("rank 0 only gathers (N - 1 render ranks)"
                                           if split.idle_root else "every rank renders"))

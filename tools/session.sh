@@ -1,6 +1,12 @@
-# round 6, session s30: group context error paths (member creation failure, host multi-frame)
+# round 6, session s31: render streams for the driver's 20-frame command (3 = default) and 200 frames
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06_s30; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_exchange_gpu.py -x -q -rf --timeout 200 --timeout-method thread > $O/pytest_exchange.log 2>&1 || { tail -30 $O/pytest_exchange.log; exit 1; }
-tail -1 $O/pytest_exchange.log
+O=gpurun_out/r06_s31; mkdir -p $O
+for rep in 1 2; do
+  for st in 3 4 5 6; do
+    for K in 20 200; do
+      timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-cadence --steps $K --warmup 5 --streams $st > $O/s${st}_k${K}_r$rep.json 2>$O/s${st}_k${K}_r$rep.err || exit 1
+      python3 -c "import json; d=json.loads(open('$O/s${st}_k${K}_r$rep.json').read().strip().splitlines()[-1]); print('streams $st K $K', d['ms_per_step'])"
+    done
+  done
+done
