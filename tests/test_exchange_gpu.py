@@ -69,9 +69,11 @@ def _bits(a):
     return a.view(np.uint16 if a.dtype == np.float16 else np.uint32)
 
 
-# world, idle root, coded exchange, format, frames per group, streams, buffer sets, lag
+# world, idle root, coded exchange, format, frames per group, streams, buffer sets, lag[, tile]
 PROTOCOL = {
     "w3_code": (3, False, 1, N.FORMAT_RGBA16F, 4, 2, 4, -1),
+    "w3_code_tile32": (3, False, 1, N.FORMAT_RGBA16F, 4, 2, 4, -1, 32),
+    "w8_idle_code_8frames": (8, True, 1, N.FORMAT_RGBA16F, 8, 4, 16, -1),   # the N >= 8 default (8 per launch)
     "w3_idle_code": (3, True, 1, N.FORMAT_RGBA16F, 4, 2, 4, -1),
     "w8_idle_code": (8, True, 1, N.FORMAT_RGBA16F, 4, 4, 16, -1),   # bench.py --gpus 8's layout
     "w8_code_lag0": (8, False, 1, N.FORMAT_RGBA16F, 4, 4, 16, 0),
@@ -88,7 +90,8 @@ def test_local_exchange_equals_full_frames(bonsai_tf, name):
     as 4-frame launches of different cameras on rotated streams, arrives in its own
     image on rank 0 equal to the one-context frame bit for bit."""
     import torch
-    world, idle, code, fmt, L, D_, B, lag = PROTOCOL[name]
+    world, idle, code, fmt, L, D_, B, lag = PROTOCOL[name][:8]
+    tile = PROTOCOL[name][8] if len(PROTOCOL[name]) > 8 else 16
     n = 64
     vol, scale = D.marschner_lobb_u8(n), D.voxel_scale(n)
     W, H = 272, 208                         # 17 x 13 tiles of 16: ragged shares
@@ -105,7 +108,6 @@ def test_local_exchange_equals_full_frames(bonsai_tf, name):
                          ("exchange_code", code), ("exchange_lag", lag)):
                 N.check(L_.cvr_set_option(c.handle, k.encode(), v), k, c.handle)
         sworld = world - 1 if idle else world
-        tile = 16
         tpr = T.max_tiles_per_rank(W, H, tile, sworld)
         dt = torch.float16 if fmt == N.FORMAT_RGBA16F else torch.float32
         dev = torch.device("cuda", 0)

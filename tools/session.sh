@@ -1,6 +1,6 @@
-# round 6, session s33: the driver's command on the final library with its PMC records installed
+# round 6, session s34: exchange protocol at tile 32 and at 8-frame groups (the N >= 8 default)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06_s33; mkdir -p $O
-timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
-python3 -c "import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]); r=d['roofline']; print(d['ms_per_step'], d['value'], r['bound'], r['frac'], r['traffic'], d['config']['lib_sha16'])"
+O=gpurun_out/r06_s34; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_exchange_gpu.py -x -v -rf --timeout 200 --timeout-method thread > $O/pytest_exchange.log 2>&1 || { tail -30 $O/pytest_exchange.log; exit 1; }
+grep -c PASSED $O/pytest_exchange.log; tail -1 $O/pytest_exchange.log
