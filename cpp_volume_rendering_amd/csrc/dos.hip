@@ -261,7 +261,11 @@ __device__ __forceinline__ float ext_value(const DosArgs& Q, uint4 raw, const Ex
 #ifdef CVR_DOS_EXPERIMENT_NO_BORDER   // cost probes only (tools/build_variant.sh): wrong images
   return rg;
 #endif
+#ifdef CVR_DOS_PROBE_NATIVE_EXP   // cost probe only (tools/build_variant.sh): not CVR-SPEC
+  if (outside) rg = rg * cvr_expf_native(xb);
+#else
   if (outside) rg = rg * cvr_expf_nonpos(xb);
+#endif
   return rg;
 }
 
