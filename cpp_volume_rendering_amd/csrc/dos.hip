@@ -222,6 +222,11 @@ __device__ __forceinline__ ExtLevel load_level(const ExtLevel* lv, int L) {
 #endif
 }
 
+// The cone code's template int M: bits 0-7 the GL_LINEAR weights' fraction bits
+// (filter_bits; 0 = exact), bit 8 (kDosNativeExp) the border attenuation's exp as
+// v_exp_f32 (option native_exp: tolerance mode, not CVR-SPEC).
+constexpr int kDosNativeExp = 0x100;
+
 template <int FB>   // FB: GL_LINEAR weights at FB fraction bits (filter_bits; 0 = exact)
 __device__ __forceinline__ ExtTap ext_tap(const ExtLevel& l, f3 p) {
   const float x = __builtin_amdgcn_fmed3f(fmaf(p.x, l.sx, -0.5f), 0.0f, l.mx);
@@ -231,9 +236,9 @@ __device__ __forceinline__ ExtTap ext_tap(const ExtLevel& l, f3 p) {
   // dims <= 2^12 and < 2^28 cells in all (checked on the host): 24-bit multiplies
   const uint32_t row = __umul24((uint32_t)z, (uint32_t)l.dy) + (uint32_t)y;
   t.off = (__umul24(row, (uint32_t)l.dx) + (uint32_t)x + (uint32_t)l.off) << 4;
-  t.ax = filter_weight<FB>(__builtin_amdgcn_fractf(x));
-  t.ay = filter_weight<FB>(__builtin_amdgcn_fractf(y));
-  t.az = filter_weight<FB>(__builtin_amdgcn_fractf(z));
+  t.ax = filter_weight<(FB & 0xff)>(__builtin_amdgcn_fractf(x));
+  t.ay = filter_weight<(FB & 0xff)>(__builtin_amdgcn_fractf(y));
+  t.az = filter_weight<(FB & 0xff)>(__builtin_amdgcn_fractf(z));
   return t;
 }
 
@@ -255,17 +260,16 @@ __device__ __forceinline__ bool outside_box(const DosArgs& Q, f3 p) {
          (p.z > Q.G[2]);
 }
 
+template <int M>
 __device__ __forceinline__ float ext_value(const DosArgs& Q, uint4 raw, const ExtTap& t,
                                            bool outside, float xb) {
   float rg = trilerp_cell<false, false>(raw, t.ax, t.ay, t.az);   // extinction cells: no flags
 #ifdef CVR_DOS_EXPERIMENT_NO_BORDER   // cost probes only (tools/build_variant.sh): wrong images
   return rg;
 #endif
-#ifdef CVR_DOS_PROBE_NATIVE_EXP   // cost probe only (tools/build_variant.sh): not CVR-SPEC
-  if (outside) rg = rg * cvr_expf_native(xb);
-#else
-  if (outside) rg = rg * cvr_expf_nonpos(xb);
-#endif
+  // tolerance mode (native_exp): v_exp_f32 of the border exponent (~6 % of the C4
+  // frame); the CVR-SPEC exp otherwise
+  if (outside) rg = rg * ((M & kDosNativeExp) ? cvr_expf_native(xb) : cvr_expf_nonpos(xb));
   return rg;
 }
 
@@ -347,7 +351,7 @@ __device__ __forceinline__ void cone_sections(const DosArgs& Q, const DosCone& C
 #pragma unroll
     for (int j = 0; j < JN; j++) {
       const float v =
-          zero[q][j] ? 0.0f : ext_value(Q, raw[q][j], tap[q][j], out[q][j], xb[q][j]) * e[q].w;
+          zero[q][j] ? 0.0f : ext_value<FB>(Q, raw[q][j], tap[q][j], out[q][j], xb[q][j]) * e[q].w;
       rays[J0 + j] += ((last[J0 + j] + v) * e[q].z) * C.ui_weight;
       last[J0 + j] = v;
     }
@@ -517,7 +521,7 @@ __device__ __forceinline__ float cone_trace(const DosArgs& Q, const DosCone& C, 
 template <int FB>
 struct DosShaderT {
   using Args = DosArgs;
-  static constexpr int kFB = FB;   // GL_LINEAR weights of every fetch (filter_bits)
+  static constexpr int kFB = FB & 0xff;   // GL_LINEAR weights of every fetch (filter_bits)
   // register budget: 3 waves/SIMD (168 VGPRs; the compiler alone takes 172 -> 2 waves):
   // kernel 21.1 -> 18.0 ms, 4 waves 18.8 ms (spills)
   static constexpr int kMinWavesPerEU = CVR_DOS_WAVES;
@@ -626,6 +630,8 @@ hipError_t launch_dos(const Ctx& c, const DosArgs& q, float4* out, uint32_t* sam
                       unsigned long long* shade, unsigned long long* tile_samples, hipStream_t s) {
   if (q.a.filter_bits == 8)   // GL texture-unit weights (CVR-SPEC-8)
     return launch_dos_fb<DosShaderT<8>>(c, q, out, samples, shade, tile_samples, s);
+  if (q.a.exp_native)         // tolerance mode: the border attenuation's exp in hardware
+    return launch_dos_fb<DosShaderT<kDosNativeExp>>(c, q, out, samples, shade, tile_samples, s);
   return launch_dos_fb<DosShaderT<0>>(c, q, out, samples, shade, tile_samples, s);
 }
 

@@ -324,7 +324,9 @@ cvr_status  cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
  *                takes alpha = 1 - exp through the hardware v_exp_f32 instead of the
  *                CVR-SPEC polynomial; parity is SURVEY §8(c)'s gate (|dRGBA| <= 2e-3 for
  *                99.9 % of pixels, max 2e-2, SSIM >= 0.99), measured in DESIGN §5‴.
- *                Default 0.
+ *                cvr_render_dosct likewise takes the CONSIDER_BORDERS attenuation of
+ *                an outside cone tap through v_exp_f32 (its march, counts and ERT
+ *                stay bit-exact).  Default 0.
  * One option changes the arithmetic (and so the image) rather than the speed:
  *   "filter_bits" 0: exact float GL_LINEAR weights (CVR-SPEC, the default);
  *                8: every GL_LINEAR weight (volume, gradient, TF; ray_marching_1p.comp:133,

@@ -58,3 +58,42 @@ def test_native_exp_meets_the_gate(oracle, bonsai_tf, n, W, cam):
     assert ssim >= GATE_SSIM, ssim
     # the march itself is unchanged up to early-termination flips
     assert abs(f_S - o_S) <= 1e-4 * o_S
+
+
+@pytest.mark.parametrize("case", ["occlusion", "shadow_point", "inside"])
+def test_native_exp_dos_meets_the_gate(oracle, bonsai_tf, bonsai_tf_rgba, case):
+    """DOS under native_exp: the CONSIDER_BORDERS attenuation of an outside tap takes
+    v_exp_f32 (~6 % of the C4 frame).  The march (counts, ERT) is untouched,
+    so the counts stay bit-exact; the colours meet SURVEY §8(c)'s gate against the
+    CVR-SPEC oracle, and the option off is bit-exact."""
+    import math
+    from test_dos_gpu import LIGHT0, cone_tables, gpu_dos, setup
+    from cpp_volume_rendering_amd.renderer import default_cone_params
+    n = 48
+    vol, scale = D.marschner_lobb_u8(n), D.voxel_scale(n)
+    cam = dict(eye=(10.0, -20.0, 30.0), center=(100.0, 50.0, -200.0), up=(0.0, 1.0, 0.0)) \
+        if case == "inside" else D.INITIAL_STATE_CAMERA
+    kw = dict(apply_shadow=case != "occlusion", shadow_type=0)
+    W, H = 96, 80
+    occ, sdw = default_cone_params(True), default_cone_params(False)
+    dev = Device(0)
+    try:
+        setup(dev, vol, scale, bonsai_tf, bonsai_tf_rgba, (64, 64, 64))
+        step = oracle.default_step(scale)
+        exact = gpu_dos(dev, cam, W, H, step, occ, sdw, **kw)
+        N.check(N.lib().cvr_set_option(dev.handle, b"native_exp", 1), "opt", dev.handle)
+        fast = gpu_dos(dev, cam, W, H, step, occ, sdw, **kw)
+    finally:
+        dev.close()
+    diag = math.sqrt(sum((n * s) ** 2 for s in scale))
+    levels = oracle.ext_volume(oracle.volume_r16f(vol), scale, bonsai_tf_rgba, (64, 64, 64))
+    o_rgba, o_cnt, o_total = oracle.render_dos(
+        oracle.volume_r16f(vol), scale, bonsai_tf, levels, cam, W, H, step,
+        cone_tables(occ, diag, 0.50), cone_tables(sdw, diag, 0.75), light=LIGHT0, **kw)
+    assert np.array_equal(exact[0].view(np.uint32), o_rgba.view(np.uint32)), "default: bit-exact"
+    assert np.array_equal(fast[1], o_cnt) and fast[2] == o_total, "the march is unchanged"
+    assert not np.array_equal(fast[0].view(np.uint32), o_rgba.view(np.uint32)), "the variant ran"
+    within, mx, ssim = _gate(fast[0], o_rgba)
+    assert within >= GATE_FRAC, within
+    assert mx <= GATE_MAX, mx
+    assert ssim >= GATE_SSIM, ssim

@@ -1,15 +1,12 @@
-# round 6, session s37: kernel-trace summaries of every workload on the final library (one stream)
+# round 6, session s38: DOS under native_exp (tolerance mode): gate tests and A/B
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06_s37; mkdir -p $O
-export TMPDIR=/tmp
-run() { n=$1; shift; cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/$n -o run -- python3 -u $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --streams 1 "$@" > $GRAFT_REPO_ROOT/$O/$n.json 2> $GRAFT_REPO_ROOT/$O/$n.err || { tail -5 $GRAFT_REPO_ROOT/$O/$n.err; exit 1; }
-  cd $GRAFT_REPO_ROOT; python3 -c "
-import csv
-rows=list(csv.DictReader(open('$O/$n/run_kernel_stats.csv')))
-for r in rows[:3]: print('$n', r['Name'][:70], r['Calls'], round(float(r['AverageNs'])/1e6,4))"; }
-run rc1pass --no-cadence --steps 40 --warmup 4
-run phong --no-cadence --phong --steps 40 --warmup 4
-run longray --no-cadence --tf-alpha 0.02 --steps 16 --warmup 2
-run dos --renderer dos --steps 5 --warmup 1
-run ebs --renderer ebs --steps 2 --warmup 1
+O=gpurun_out/r06_s38; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_tolerance_gpu.py tests/test_dos_gpu.py -x -q -rf --timeout 200 --timeout-method thread > $O/pytest_tol_dos.log 2>&1 || { tail -30 $O/pytest_tol_dos.log; exit 1; }
+tail -1 $O/pytest_tol_dos.log
+for rep in 1 2 3; do
+  for nx in 0 1; do
+    timeout -k 10 200 python3 bench.py --renderer dos --no-cpu-baseline --steps 10 --warmup 2 --opt native_exp=$nx > $O/dos_nx${nx}_r$rep.json 2>$O/dos_nx${nx}_r$rep.err || exit 1
+    python3 -c "import json; d=json.loads(open('$O/dos_nx${nx}_r$rep.json').read().strip().splitlines()[-1]); print('dos native_exp $nx', d['ms_per_step'], d['roofline']['kernel_ms'])"
+  done
+done
