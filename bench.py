@@ -213,7 +213,7 @@ def parse(argv=None):
                         "the launch group with --frames-per-launch > 1)")
     p.add_argument("--frames-per-launch", type=int, default=0,
                    help="rc1pass: consecutive frames rendered in ONE launch "
-                        "(cvr_render_rc1pass_frames, 1..8; default 4, other renderers 1)")
+                        "(cvr_render_rc1pass_frames, 1..16; default 4, other renderers 1)")
     p.add_argument("--buffer-sets", type=int, default=0,
                    help="N > 1: exchange buffer sets rotated over the render streams (default 4 per "
                         "stream: a render waits for the exchange of its set 4 rounds back)")
@@ -265,13 +265,14 @@ def split_defaults(a, world):
     --root-renders), as ScreenTileSplit keyword arguments.  Shared with the world-8
     control-flow test (tests/test_distributed_cpu.py), so the test runs exactly the
     N = 8 default path."""
-    # 8 frames per launch (and per exchange) from 8 GPUs: a 7-way share of one frame
+    # 16 frames per launch (and per exchange) from 8 GPUs: a 7-way share of one frame
     # is ~2300 wave tiles, so a 4-frame launch is about one residency of the GPU and
-    # lasts as long as its longest rays; 8 frames amortise that tail (7-way share with
-    # the encode 0.0135 -> 0.0124 ms per frame, tools/exchange_probe.py,
-    # profiles/r06/s10_*) and halve the host calls per frame (DESIGN §7b)
+    # lasts as long as its longest rays; more frames amortise that tail (7-way share
+    # with the encode 0.0135 / 0.0121-0.0124 / 0.0118-0.0121 ms per frame at 4 / 8 / 16,
+    # tools/exchange_probe.py, profiles/r06/s10_*, s41) and cut the host calls per
+    # frame (DESIGN §7b)
     fpl = (a.frames_per_launch if a.frames_per_launch > 0 else
-           ((8 if world >= 8 else 4) if a.renderer == "rc1pass" else 1))
+           ((16 if world >= 8 else 4) if a.renderer == "rc1pass" else 1))
     streams = a.streams or ((4 if world >= 2 else 3) if fpl > 1 else
                             (16 if world >= 8 else (12 if world >= 4 else 4)))
     # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us
@@ -668,8 +669,8 @@ def main():
     # frames 0.0254 -> 0.0154 ms, in steady state 0.0224 -> 0.0122-0.0131 ms
     if a.renderer != "rc1pass" and a.frames_per_launch > 1:
         sys.exit("bench.py: --frames-per-launch > 1 needs --renderer rc1pass")
-    if a.frames_per_launch > 8:
-        sys.exit("bench.py: --frames-per-launch must be in 1..8")
+    if a.frames_per_launch > 16:
+        sys.exit("bench.py: --frames-per-launch must be in 1..16")
     SD = split_defaults(a, world)
     FPL = a.frames_per_launch = SD["frames_per_launch"]
     a.streams = SD["streams"]

@@ -182,7 +182,7 @@ struct IsoArgs {
 // 8 (n e + f) + x runs entry e of XCD band x of frame f, so the dispatcher hands
 // out entry e of every frame before entry e + 1 of any -- each band's longest
 // tiles of ALL frames start first (LPT over the launch, not per frame).
-constexpr int kMaxLaunchFrames = 8;
+constexpr int kMaxLaunchFrames = 16;
 struct FrameView {
   float eye[3];
   float col0[3], col1[3], col2[3];   // columns of mat3(View)

@@ -391,7 +391,7 @@ int         cvr_tiles_for_rank(const cvr_frame* frame, int rank);
 cvr_status  cvr_render_rc1pass(cvr_ctx* ctx, const cvr_frame* frame,
                                const cvr_rc1pass_params* params, const cvr_output* out);
 
-/* nframes frames (1..8) in ONE ray-march launch: frames[i] is rendered into
+/* nframes frames (1..16) in ONE ray-march launch: frames[i] is rendered into
  * outs[i] exactly as nframes calls of cvr_render_rc1pass would render it (same
  * pixels, same per-pixel counts).  The frames share the viewport and the screen
  * split (width, height, tile_size, rank, nranks) and may differ in camera; the

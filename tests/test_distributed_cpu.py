@@ -395,10 +395,11 @@ def _native_idle_root_worker(rank, world, port, q):
 
 def _native_bench8_worker(rank, world, port, q):
     """Exactly `bench.py --gpus 8`'s default split (bench.split_defaults): 1024^2, 16^2
-    tiles, 8 frames per launch and per exchange (coded), 4 render streams, 16 buffer sets,
-    an idle root (ranks 1..7 render the split over 7 render ranks), 32 HW queues.
-    Every rank must issue the same gathers; each render rank renders its 8-frame
+    tiles, 16 frames per launch and per exchange (coded), 4 render streams, 16 buffer
+    sets, an idle root (ranks 1..7 render the split over 7 render ranks), 32 HW queues.
+    Every rank must issue the same gathers; each render rank renders its 16-frame
     groups as its own split rank into the group's buffer set, rotated over the 16."""
+    G = 16
     os.environ["WORLD_SIZE"] = str(world)       # bench.py reads it at import (HW queues)
     import bench
     from cpp_volume_rendering_amd import _native as N
@@ -423,7 +424,7 @@ def _native_bench8_worker(rank, world, port, q):
 
         a = bench.parse(["--gpus", str(world)])
         kw = bench.split_defaults(a, world)
-        assert kw == {"streams": 4, "frames_per_exchange": 8, "frames_per_launch": 8,
+        assert kw == {"streams": 4, "frames_per_exchange": G, "frames_per_launch": G,
                       "buffer_sets": 16, "root_renders": False}, kw
         assert bench.HW_QUEUES == 32 and a.tile == 16 and a.transport == "rccl"
         W = H = 1024
@@ -432,16 +433,16 @@ def _native_bench8_worker(rank, world, port, q):
                                count_samples=True, **kw)
         assert sp.idle_root and sp.renders == (rank != 0)
         assert sp.sworld == world - 1 and sp.srank == max(rank - 1, 0)
-        assert sp.nbuf == 16 and sp.G == 8 and sp.L == 8 and sp.nstreams == 4
+        assert sp.nbuf == 16 and sp.G == G and sp.L == G and sp.nstreams == 4
         assert sp.k == (0 if rank == 0 else T.tiles_for_rank(W, H, 16, rank - 1, world - 1))
         cam = Camera(**D.INITIAL_STATE_CAMERA)
-        nframes = 8 * 16 + 6            # every buffer set used, then reused, and a partial group
+        nframes = G * 16 + 6            # every buffer set used, then reused, and a partial group
         for _ in range(nframes):
             sp.submit(cam)
         sp.flush()
         renders = [c for c in fake.calls if c[0] == "render_n"]
         gathers = [c for c in fake.calls if c[0] == "gather"]
-        sizes = [8] * (nframes // 8) + ([nframes % 8] if nframes % 8 else [])
+        sizes = [G] * (nframes // G) + ([nframes % G] if nframes % G else [])
         assert [g[2] for g in gathers] == sizes
         streams = [s.cuda_stream for s in sp.streams]
         bufs = set()
@@ -461,11 +462,11 @@ def _native_bench8_worker(rank, world, port, q):
                     ("opt", b"split_streams", 4), ("opt", b"exchange_code", 1)):
             assert opt in fake.calls, opt
         # the coded exchange decodes a group's frames in one launch: rank 0 hands every
-        # frame of a group its own image (8 distinct), the same 8 for every group
+        # frame of a group its own image (G distinct), the same G for every group
         if rank == 0:
             imgs = [tuple(g[5]) for g in gathers]
             assert all(len(set(i)) == len(i) for i in imgs)
-            assert imgs[0] == tuple(im.data_ptr() for im in sp._images[:8])
+            assert imgs[0] == tuple(im.data_ptr() for im in sp._images[:G])
             assert all(i == imgs[0][:len(i)] for i in imgs)
         else:
             assert all(g[5] is None for g in gathers)

@@ -73,7 +73,8 @@ def _bits(a):
 PROTOCOL = {
     "w3_code": (3, False, 1, N.FORMAT_RGBA16F, 4, 2, 4, -1),
     "w3_code_tile32": (3, False, 1, N.FORMAT_RGBA16F, 4, 2, 4, -1, 32),
-    "w8_idle_code_8frames": (8, True, 1, N.FORMAT_RGBA16F, 8, 4, 16, -1),   # the N >= 8 default (8 per launch)
+    "w8_idle_code_8frames": (8, True, 1, N.FORMAT_RGBA16F, 8, 4, 16, -1),
+    "w8_idle_code_16frames": (8, True, 1, N.FORMAT_RGBA16F, 16, 4, 16, -1),  # the N >= 8 default (16 per launch)
     "w3_idle_code": (3, True, 1, N.FORMAT_RGBA16F, 4, 2, 4, -1),
     "w8_idle_code": (8, True, 1, N.FORMAT_RGBA16F, 4, 4, 16, -1),   # bench.py --gpus 8's layout
     "w8_code_lag0": (8, False, 1, N.FORMAT_RGBA16F, 4, 4, 16, 0),

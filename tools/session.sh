@@ -1,8 +1,8 @@
-# round 6, session s40: the driver's command and the DOS line with the final PMC records installed
+# round 6, session s42: 16 frames per launch: exchange protocol (16-frame groups), multi-frame tests; then PMC records and the full round
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06_s40; mkdir -p $O
-timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
-python3 -c "import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]); r=d['roofline']; print(d['ms_per_step'], d['value'], r['bound'], r['frac'], r['traffic'], d['config']['lib_sha16'])"
-timeout -k 10 400 python3 bench.py --renderer dos --steps 10 --warmup 2 > $O/dos.json 2> $O/dos.err || { tail -5 $O/dos.err; exit 1; }
-python3 -c "import json; d=json.loads(open('$O/dos.json').read().strip().splitlines()[-1]); r=d['roofline']; print(d['ms_per_step'], d['value'], r['bound'], r['frac'], r['traffic'])"
+O=gpurun_out/r06_s42; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_exchange_gpu.py tests/test_frames_gpu.py -x -q -rf --timeout 200 --timeout-method thread > $O/pytest_16.log 2>&1 || { tail -30 $O/pytest_16.log; exit 1; }
+tail -1 $O/pytest_16.log
+bash tools/pmc_session.sh rc1pass phong longray dos ebs || exit 1
+bash tools/gpu_round.sh all
