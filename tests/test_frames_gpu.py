@@ -177,11 +177,12 @@ def test_frames_argument_errors(dev, bonsai_tf):
     L = N.lib()
     p = _params()
     W, H = 64, 48
-    buf = [torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") for _ in range(9)]
-    outs = (N.Output * 9)(*[N.Output(b.data_ptr(), None, None, 1, N.FORMAT_RGBA32F) for b in buf])
-    frames = (N.Frame * 9)(*[make_frame(Camera(**INITIAL), W, H) for _ in range(9)])
+    buf = [torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") for _ in range(17)]
+    outs = (N.Output * 17)(*[N.Output(b.data_ptr(), None, None, 1, N.FORMAT_RGBA32F) for b in buf])
+    frames = (N.Frame * 17)(*[make_frame(Camera(**INITIAL), W, H) for _ in range(17)])
     assert L.cvr_render_rc1pass_frames(dev.handle, frames, 0, ctypes.byref(p), outs) == N.CVR_ERR_ARG
-    assert L.cvr_render_rc1pass_frames(dev.handle, frames, 9, ctypes.byref(p), outs) == N.CVR_ERR_ARG
+    # at most 16 frames per launch
+    assert L.cvr_render_rc1pass_frames(dev.handle, frames, 17, ctypes.byref(p), outs) == N.CVR_ERR_ARG
     bad = (N.Frame * 2)(make_frame(Camera(**INITIAL), W, H), make_frame(Camera(**INITIAL), W, H + 1))
     assert L.cvr_render_rc1pass_frames(dev.handle, bad, 2, ctypes.byref(p), outs) == N.CVR_ERR_ARG
     host = np.zeros((H, W, 4), np.float32)
