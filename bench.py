@@ -265,14 +265,22 @@ def split_defaults(a, world):
     --root-renders), as ScreenTileSplit keyword arguments.  Shared with the world-8
     control-flow test (tests/test_distributed_cpu.py), so the test runs exactly the
     N = 8 default path."""
-    # 16 frames per launch (and per exchange) from 8 GPUs: a 7-way share of one frame
-    # is ~2300 wave tiles, so a 4-frame launch is about one residency of the GPU and
-    # lasts as long as its longest rays; more frames amortise that tail (7-way share
-    # with the encode 0.0135 / 0.0121-0.0124 / 0.0118-0.0121 ms per frame at 4 / 8 / 16,
-    # tools/exchange_probe.py, profiles/r06/s10_*, s41) and cut the host calls per
-    # frame (DESIGN §7b)
+    # Frames per launch (and per exchange) at N > 1, from the length of the run: a
+    # share of one frame is a fraction of a GPU residency, so a launch lasts as long
+    # as its longest rays and more frames per launch amortise that tail in a long run
+    # (7-way share with the encode, steady state: 0.0135 / 0.0121-0.0124 /
+    # 0.0118-0.0121 ms per frame at 4 / 8 / 16 frames; N = 2 / 4: -4 / -6 % at 16),
+    # while a short run needs several launches in flight on its streams (a 16-frame
+    # burst: 0.0147 / 0.0161 / 0.0180 ms at 4 / 8 / 16; tools/exchange_probe.py,
+    # profiles/r06/s41, s43, s44; DESIGN §7b).  So: the largest power of two up to 16
+    # that leaves two launches per render stream (4 streams): 4 frames for the
+    # driver's 20-step runs, 16 from 128 steps on.  One GPU keeps 4.
+    steps = a.steps or 200
+    fpl_n = 4
+    while fpl_n < 16 and steps // (2 * 4) >= 2 * fpl_n:
+        fpl_n *= 2
     fpl = (a.frames_per_launch if a.frames_per_launch > 0 else
-           ((16 if world >= 8 else 4) if a.renderer == "rc1pass" else 1))
+           ((fpl_n if world >= 2 else 4) if a.renderer == "rc1pass" else 1))
     streams = a.streams or ((4 if world >= 2 else 3) if fpl > 1 else
                             (16 if world >= 8 else (12 if world >= 4 else 4)))
     # fewer, larger exchanges at high N: one gather's host + launch cost (~18 us

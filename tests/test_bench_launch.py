@@ -72,3 +72,24 @@ def test_hw_queues_rejects_bad_values(bad):
     p = _run(["--dry-run", *bad])
     assert p.returncode != 0
     assert "hw-queues" in p.stderr
+
+
+def test_split_defaults_frames_per_launch_follow_the_run_length():
+    """bench.split_defaults: at N > 1 the rc1pass launch groups grow with the run (two
+    launches per render stream at least: 4 frames for the driver's 20-step runs, 16
+    from 128 steps on); one GPU keeps 4; other renderers 1."""
+    import bench
+    want = {20: 4, 50: 4, 64: 8, 100: 8, 128: 16, 200: 16}
+    for steps, fpl in want.items():
+        for world in (2, 4, 8):
+            a = bench.parse(["--gpus", str(world), "--steps", str(steps)])
+            kw = bench.split_defaults(a, world)
+            assert kw["frames_per_launch"] == fpl == kw["frames_per_exchange"], (steps, world, kw)
+            assert kw["streams"] == 4 and kw["root_renders"] == (world < 8)
+        assert bench.split_defaults(bench.parse(["--steps", str(steps)]), 1)["frames_per_launch"] == 4
+    a = bench.parse(["--gpus", "8"])                 # the default run (200 steps)
+    assert bench.split_defaults(a, 8)["frames_per_launch"] == 16
+    a = bench.parse(["--gpus", "8", "--renderer", "dos", "--steps", "200"])
+    assert bench.split_defaults(a, 8)["frames_per_launch"] == 1
+    a = bench.parse(["--gpus", "8", "--frames-per-launch", "8", "--steps", "20"])
+    assert bench.split_defaults(a, 8)["frames_per_launch"] == 8
